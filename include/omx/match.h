@@ -1,0 +1,203 @@
+/*
+ * omx/match.h — C ABI of the MI355X-native OrientDB SQL MATCH executor.
+ *
+ * This is the drop-in boundary described in SURVEY.md §8(b). Every entry point replaces one piece of
+ * the reference's MATCH execution (OrientDB 2.2.8, paths relative to /root/reference):
+ *
+ *   omx_graph_create        ← the record/ridbag reads the DFS performs lazily:
+ *                             ORidBag.rawIterator      core/.../db/record/ridbag/ORidBag.java:160
+ *                             OrientVertex.getVertices graphdb/.../blueprints/impls/orient/OrientVertex.java:401-460
+ *                             ODocument.field          core/.../record/impl/ODocument.java:820
+ *                             (the snapshot is built once; it is immutable afterwards)
+ *   omx_statement_parse     ← OMatchStatement.parse    core/.../sql/parser/OMatchStatement.java:129-178
+ *                             (assignDefaultAliases :202-218, addAliases :905-948, Pattern.validate Pattern.java:48-65)
+ *   omx_statement_explain   ← estimateRootEntries :874-903 + sortEdges :272-325 (the execution plan, as JSON)
+ *   omx_execute             ← OMatchStatement.execute  :244-267 → calculateMatch :334-386 → processContext :412-568
+ *                             → addResult :661-729 → OBasicCommandContext.addToUniqueResult
+ *                               core/.../command/OBasicCommandContext.java:347-353
+ *   omx_result_*            ← OSQLSynchQuery.getResult core/.../sql/query/OSQLSynchQuery.java:111-113 (the OResultSet)
+ *   omx_last_error          ← the message of OCommandExecutionException / OCommandSQLParsingException
+ *
+ * Conventions: plain C types only; every function returns an int status (OMX_OK = 0) unless it is
+ * a getter; on failure omx_last_error() (thread-local) describes the error. OMX_E_UNSUPPORTED means
+ * "valid MATCH, but not executable by this engine": the host (the Java OMatchStatement strategy) falls
+ * back to the reference executor. Handles are not thread-safe; a graph may be shared read-only by
+ * several statements executed one at a time per host thread.
+ */
+#ifndef OMX_MATCH_H
+#define OMX_MATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------------------- */
+#define OMX_OK            0
+#define OMX_E_UNSUPPORTED 1 /* valid query, not supported by the GPU engine → host falls back        */
+#define OMX_E_INVALID     2 /* bad argument / bad snapshot / unknown class                             */
+#define OMX_E_OOM         3 /* device or host allocation failed                                        */
+#define OMX_E_DEVICE      4 /* HIP runtime error (no device, launch failure, ...)                      */
+#define OMX_E_PARSE       5 /* OCommandSQLParsingException equivalent                                  */
+#define OMX_E_EXECUTION   6 /* OCommandExecutionException equivalent                                   */
+
+/* ---- snapshot description ------------------------------------------------------------------------ */
+#define OMX_PROP_INT32  1 /* values: const int32_t[V]                                                 */
+#define OMX_PROP_INT64  2 /* values: const int64_t[V]                                                 */
+#define OMX_PROP_DOUBLE 3 /* values: const double[V]                                                  */
+#define OMX_PROP_STRING 4 /* values: const int32_t[V] codes into dict (sorted, unique, UTF-8)         */
+#define OMX_PROP_BOOL   5 /* values: const int32_t[V] 0/1                                              */
+
+typedef struct omx_class_desc {
+  const char *name;      /* class name, e.g. "Person"                                              */
+  int32_t superclass;    /* index of the superclass in the class array, -1 for a root class         */
+  int32_t is_edge_class; /* 1 for E and its subclasses                                              */
+  int32_t cluster_id;    /* cluster of the class (RID = cluster:position), informational           */
+} omx_class_desc;
+
+/* Adjacency of one edge class (regular or lightweight edges alike): for every vertex v the multiset of
+ * neighbours of v through out_<Class> (out CSR) and in_<Class> (in CSR). Duplicates (parallel edges)
+ * must be kept: they are the ridbag multiplicity (OSBTreeRidBag.java:292-295). Within a row the order
+ * is free; omx sorts rows it finds unsorted. */
+typedef struct omx_edge_set_desc {
+  int32_t edge_class;           /* index into classes[]                                            */
+  uint64_t n_edges;             /* E                                                               */
+  const uint64_t *out_row_ptr;  /* [V+1]                                                           */
+  const uint32_t *out_col;      /* [E] dense vertex ids                                            */
+  const uint64_t *in_row_ptr;   /* [V+1] (the transpose); may be NULL → built by omx              */
+  const uint32_t *in_col;       /* [E]                                                             */
+} omx_edge_set_desc;
+
+typedef struct omx_property_desc {
+  const char *name;             /* property name (field name)                                      */
+  int32_t type;                 /* OMX_PROP_*                                                      */
+  const void *values;           /* [V]                                                             */
+  const uint8_t *present;       /* [V] 1 = field present, 0 = null/absent; NULL = all present       */
+  int32_t dict_size;            /* OMX_PROP_STRING only                                            */
+  const char *const *dict;      /* OMX_PROP_STRING only: sorted by byte order, unique              */
+} omx_property_desc;
+
+/* A schema index (CREATE INDEX ... ON Class (prop)). Only used for root estimation, exactly as
+ * OWhereClause.estimate uses indexes (OWhereClause.java:57-95). */
+typedef struct omx_index_desc {
+  int32_t class_id;
+  const char *property;
+  int32_t unique; /* 1 = UNIQUE / UNIQUE_HASH_INDEX, 0 = NOTUNIQUE                                   */
+} omx_index_desc;
+
+typedef struct omx_graph_desc {
+  uint32_t n_vertices;                 /* V                                                       */
+  int32_t n_classes;
+  const omx_class_desc *classes;
+  const uint16_t *vertex_class;        /* [V] class index of every vertex                         */
+  const uint64_t *rids;                /* [V] RID packed (cluster << 48) | position               */
+  int32_t n_edge_sets;
+  const omx_edge_set_desc *edge_sets;
+  int32_t n_properties;
+  const omx_property_desc *properties;
+  int32_t n_indexes;
+  const omx_index_desc *indexes;
+  int32_t device;                      /* HIP device ordinal; -1 = host-only (plan/explain only)   */
+} omx_graph_desc;
+
+typedef struct omx_graph omx_graph;
+typedef struct omx_statement omx_statement;
+typedef struct omx_result omx_result;
+
+/* ---- graph snapshot --------------------------------------------------------------------------- */
+int omx_graph_create(const omx_graph_desc *desc, omx_graph **out);
+void omx_graph_destroy(omx_graph *g);
+/* Host-side introspection of a snapshot (counts are the OClassImpl.count(polymorphic) of a class). */
+int omx_graph_class_count(const omx_graph *g, const char *class_name, uint64_t *count);
+uint64_t omx_graph_device_bytes(const omx_graph *g);
+
+/* ---- statement (parse + pattern) -------------------------------------------------------------- */
+int omx_statement_parse(const char *text, omx_statement **out);
+void omx_statement_free(omx_statement *s);
+
+/* Query parameters (OCommandSQL.execute(args...)): positional (name == NULL, index = position) or
+ * named (":name"). */
+#define OMX_VAL_NULL   0
+#define OMX_VAL_INT    1
+#define OMX_VAL_DOUBLE 2
+#define OMX_VAL_STRING 3
+#define OMX_VAL_BOOL   4
+typedef struct omx_value {
+  int32_t type;
+  int32_t index;       /* positional index (0-based) when name == NULL                             */
+  const char *name;    /* named parameter (without ':') or NULL                                    */
+  int64_t i;
+  double d;
+  const char *s;
+} omx_value;
+
+/* Writes the MATCH plan as JSON into buf (NUL-terminated, truncated to len): aliases with classes,
+ * estimates, prefetched aliases, root alias and the sorted edge list. Works on host-only graphs. */
+int omx_statement_explain(omx_statement *s, const omx_graph *g, const omx_value *params, int32_t n_params,
+                          char *buf, size_t len);
+
+/* ---- execution -------------------------------------------------------------------------------- */
+#define OMX_MODE_MATERIALIZE 0 /* distinct RETURN rows (the OResultSet)                            */
+#define OMX_MODE_COUNT       1 /* counts only (edges traversed, bindings, distinct rows if cheap)   */
+
+#define OMX_FLAG_KERNEL_TIMING 1 /* time every kernel with HIP events (omx_result_kernel_stat)     */
+#define OMX_FLAG_NO_RID_MAP    2 /* return dense vertex ids instead of RIDs                         */
+#define OMX_FLAG_KEEP_DEVICE   4 /* do not copy rows to the host (benchmarking; rows stay in HBM)   */
+
+typedef struct omx_exec_options {
+  int32_t mode;          /* OMX_MODE_*                                                            */
+  int32_t flags;         /* OMX_FLAG_*                                                            */
+  int64_t limit;         /* OMatchStatement.setLimit (limitFromProtocol); -1 = none               */
+  int32_t shard_rank;    /* root shard of this process (multi-GPU): roots v with v % world == rank */
+  int32_t shard_world;   /* 1 = no sharding                                                       */
+  const omx_value *params;
+  int32_t n_params;
+} omx_exec_options;
+
+void omx_exec_options_init(omx_exec_options *o);
+int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, omx_result **out);
+
+typedef struct omx_result_info {
+  uint64_t n_rows;           /* distinct RETURN rows (after LIMIT)                                 */
+  int32_t n_cols;            /* RID columns per row (0 for an empty result)                        */
+  int32_t deduplicated;      /* 1 if a dedup pass ran, 0 if rows were distinct by construction     */
+  uint64_t edges_traversed;  /* Σ_h E_t(h), SURVEY §8(d)                                           */
+  uint64_t bindings;         /* complete matches before dedup                                      */
+  uint64_t alg_bytes;        /* algorithmic HBM bytes, SURVEY §8(d)                                */
+  double device_ms;          /* wall time of the device part (root scan → last kernel)             */
+  double total_ms;           /* wall time of omx_execute                                           */
+} omx_result_info;
+
+int omx_result_info_get(const omx_result *r, omx_result_info *info);
+const char *omx_result_column_name(const omx_result *r, int32_t col);
+/* Row-major n_rows × n_cols RIDs ((cluster << 48) | position), or dense ids with NO_RID_MAP.
+ * Library-owned; valid until omx_result_free. NULL with KEEP_DEVICE. */
+const uint64_t *omx_result_rows(const omx_result *r);
+/* Per-kernel device timing (OMX_FLAG_KERNEL_TIMING): i-th kernel name, launches, total ms, and the
+ * algorithmic bytes the launches of that kernel moved. Returns OMX_E_INVALID past the end. */
+int omx_result_kernel_stat(const omx_result *r, int32_t i, const char **name, int64_t *launches, double *total_ms,
+                           uint64_t *alg_bytes);
+void omx_result_free(omx_result *r);
+
+const char *omx_last_error(void);
+const char *omx_version(void);
+
+/* ---- synthetic graphs (benchmark / test inputs) -------------------------------- */
+/* Graph500 RMAT (a=.57,b=.19,c=.19), V = 2^scale, edge_factor·V raw directed edges, deterministic
+ * counter-based RNG (splitmix64), vertex ids scrambled by a bijection. simple != 0 removes self loops
+ * and parallel edges. Outputs are host arrays owned by the library (omx_host_free). */
+int omx_rmat_generate(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t simple, uint64_t **out_row_ptr,
+                      uint32_t **out_col, uint64_t *n_edges);
+/* CSR transpose (host, multi-threaded); rows of the output are sorted. */
+int omx_csr_transpose(uint32_t n_vertices, const uint64_t *row_ptr, const uint32_t *col, uint64_t **t_row_ptr,
+                      uint32_t **t_col);
+/* age property of the synthetic Person vertices: uniform [0,100) from splitmix64(seed ^ v). */
+int omx_synthetic_int_column(uint32_t n_vertices, uint64_t seed, int32_t modulo, int32_t **out);
+void omx_host_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OMX_MATCH_H */
