@@ -1,0 +1,204 @@
+"""ORACLE (test infrastructure only) — drives oracle/dfs_ref.c over a Person/Knows CSR graph.
+
+The plan (estimates, sortEdges, bound/candidate/free per edge) comes from the Python restatement
+(oracle/match_ref.py, MatchOracle); WHERE clauses are evaluated with numpy over the property columns
+(same operator semantics as match_ref.Evaluator for the int/comparison subset: a null-free synthetic
+schema). Supports fixed-length patterns (single-hop out/in/both items) — variable-length items stay
+with the Python oracle.
+"""
+import ctypes as C
+import os
+import time
+
+import numpy as np
+
+from oracle.match_ref import Ctx, MatchContext, MatchOracle, RefDB, THRESHOLD
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "_build", "libdfsref.so")
+MAXP, MAXA = 4, 16
+
+
+class dfs_step(C.Structure):
+    _fields_ = [("src", C.c_int32), ("dst", C.c_int32), ("mode", C.c_int32), ("forward", C.c_int32),
+                ("nparts", C.c_int32), ("rp", C.POINTER(C.c_uint64) * MAXP), ("col", C.POINTER(C.c_uint32) * MAXP),
+                ("where_bm", C.POINTER(C.c_uint64)), ("cand_bm", C.POINTER(C.c_uint64)), ("need_dedup", C.c_int32)]
+
+
+class dfs_plan(C.Structure):
+    _fields_ = [("nsteps", C.c_int32), ("naliases", C.c_int32), ("steps", dfs_step * MAXA)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise ImportError("oracle C library missing: make -C oracle")
+        L = C.CDLL(LIB)
+        L.dfs_run.restype = C.c_int64
+        L.dfs_run.argtypes = [C.POINTER(dfs_plan), C.c_int32, C.POINTER(C.c_uint32), C.c_int64, C.c_int32, C.c_int32,
+                              C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.dfs_free.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+class CsrGraph:
+    """Person/Knows graph as arrays: out CSR, in CSR, property columns (name → numpy array)."""
+
+    def __init__(self, rp, col, columns, trp=None, tcol=None, simple=True):
+        self.V = len(rp) - 1
+        self.rp = np.ascontiguousarray(rp, np.uint64)
+        self.col = np.ascontiguousarray(col, np.uint32)
+        if trp is None:
+            src = np.repeat(np.arange(self.V, dtype=np.uint32), np.diff(self.rp).astype(np.int64))
+            order = np.lexsort((src, self.col))
+            tcol = src[order]
+            cnt = np.bincount(self.col, minlength=self.V)
+            trp = np.zeros(self.V + 1, np.uint64)
+            trp[1:] = np.cumsum(cnt)
+        self.trp = np.ascontiguousarray(trp, np.uint64)
+        self.tcol = np.ascontiguousarray(tcol, np.uint32)
+        self.columns = columns
+        self.simple = simple
+        # a schema-only RefDB for the planner (class counts; no records are traversed through it)
+        db = RefDB()
+        db.create_class("V")
+        db.create_class("E", is_edge=True)
+        db.create_class("Person", "V")
+        db.create_class("Knows", "E", is_edge=True)
+        self._count = self.V
+        db.count = lambda c: self.V if c in ("Person", "V") else 0
+        self.schema = db
+
+
+def np_eval(e, cols, params):
+    """Vectorised restatement of Evaluator.boolean/value for the int subset (null-free columns)."""
+    k = e[0]
+    if k == "and":
+        out = np_eval(e[1][0], cols, params)
+        for x in e[1][1:]:
+            out = out & np_eval(x, cols, params)
+        return out
+    if k == "or":
+        out = np_eval(e[1][0], cols, params)
+        for x in e[1][1:]:
+            out = out | np_eval(x, cols, params)
+        return out
+    if k == "not":
+        return ~np_eval(e[1], cols, params)
+    if k == "paren":
+        return np_eval(e[1], cols, params)
+    if k == "truth":
+        v = np_eval(e[1], cols, params)
+        return v if isinstance(v, np.ndarray) and v.dtype == bool else np.asarray(v is True)
+    if k == "cmp":
+        a, b = np_eval(e[2], cols, params), np_eval(e[3], cols, params)
+        op = e[1]
+        return {"=": np.equal, "==": np.equal, "!=": np.not_equal, "<>": np.not_equal, "<": np.less,
+                "<=": np.less_equal, ">": np.greater, ">=": np.greater_equal}[op](a, b)
+    if k == "lit":
+        return e[1]
+    if k == "param":
+        return params[e[1]]
+    if k == "field":
+        return cols[e[1]]
+    if k == "math":
+        a, b = np_eval(e[2], cols, params), np_eval(e[3], cols, params)
+        return {"+": np.add, "-": np.subtract, "*": np.multiply, "%": np.mod}[e[1]](a, b)
+    raise NotImplementedError("oracle C path: expression %r" % (e,))
+
+
+def _bm_from_mask(mask):
+    words = np.zeros((len(mask) + 63) // 64, np.uint64)
+    idx = np.nonzero(mask)[0]
+    np.bitwise_or.at(words, idx >> 6, np.left_shift(np.uint64(1), (idx & 63).astype(np.uint64)))
+    return words
+
+
+def run(g, query, params=None, nthreads=1, emit=True, root_sample=None):
+    """Returns dict(rows=np.uint32[n, k] (distinct, sorted; None when emit=False), aliases, bindings,
+    edges, seconds, nroots)."""
+    mo = MatchOracle(g.schema, query)
+    pmap = MatchOracle._param_map(params)
+    est = mo.estimate_root_entries(Ctx(pmap))
+    sorted_edges = mo.sort_edges(est)
+    aliases = list(mo.nodes)
+    aidx = {a: i for i, a in enumerate(aliases)}
+    prefetched = [a for a, v in est.items() if v < THRESHOLD] or [mo._next_alias(est, MatchContext())]
+    if sorted_edges:
+        e0, f0 = sorted_edges[0]
+        root = e0.out.alias if f0 else e0.in_.alias
+    else:
+        root = aliases[0]
+    cols = g.columns
+    keep = []
+
+    def where_mask(alias):
+        w = mo.where_of(alias)
+        if w is None:
+            return None
+        m = np_eval(w, cols, pmap)
+        return np.broadcast_to(np.asarray(m, bool), (g.V,))
+
+    def cand_mask(alias):
+        m = where_mask(alias)
+        return np.ones(g.V, bool) if m is None else m  # every vertex is a Person
+
+    plan = dfs_plan()
+    plan.naliases = len(aliases)
+    bound = {root}
+    for i, (e, fwd) in enumerate(sorted_edges):
+        it = e.item
+        if it.multi is not None or it.filter.while_ is not None or it.filter.max_depth is not None:
+            raise NotImplementedError("oracle C path: variable-length / multi items")
+        s_alias, t_alias = (e.out.alias, e.in_.alias) if fwd else (e.in_.alias, e.out.alias)
+        if s_alias not in bound:
+            raise NotImplementedError("oracle C path: disconnected pattern")
+        st = plan.steps[i]
+        st.src, st.dst, st.forward = aidx[s_alias], aidx[t_alias], int(fwd)
+        st.mode = 2 if t_alias in bound else (1 if t_alias in prefetched else 0)
+        m = it.method.lower()
+        if not fwd:
+            m = {"out": "in", "in": "out", "both": "both"}[m]
+        parts = {"out": [(g.rp, g.col)], "in": [(g.trp, g.tcol)], "both": [(g.rp, g.col), (g.trp, g.tcol)]}[m]
+        if it.labels and not any(lab.lower() in ("knows", "e") for lab in it.labels):
+            parts = []
+        st.nparts = len(parts)
+        for q, (rp, col) in enumerate(parts):
+            st.rp[q] = rp.ctypes.data_as(C.POINTER(C.c_uint64))
+            st.col[q] = col.ctypes.data_as(C.POINTER(C.c_uint32))
+        st.need_dedup = int(len(parts) > 1 or not g.simple)
+        wm = where_mask(t_alias)
+        if wm is not None:
+            w = _bm_from_mask(wm)
+            keep.append(w)
+            st.where_bm = w.ctypes.data_as(C.POINTER(C.c_uint64))
+        if st.mode == 1:
+            cb = _bm_from_mask(cand_mask(t_alias))
+            keep.append(cb)
+            st.cand_bm = cb.ctypes.data_as(C.POINTER(C.c_uint64))
+        bound.add(t_alias)
+    plan.nsteps = len(sorted_edges)
+    if len(bound) != len(aliases):
+        raise NotImplementedError("oracle C path: cartesian product")
+    roots = np.nonzero(cand_mask(root))[0].astype(np.uint32)
+    if root_sample is not None:
+        roots = roots[:root_sample]
+    out = C.POINTER(C.c_uint32)()
+    nrows = C.c_uint64()
+    edges = C.c_uint64()
+    t0 = time.perf_counter()
+    b = lib().dfs_run(C.byref(plan), aidx[root], roots.ctypes.data_as(C.POINTER(C.c_uint32)), len(roots), nthreads,
+                      int(emit), C.byref(out), C.byref(nrows), C.byref(edges))
+    dt = time.perf_counter() - t0
+    rows = None
+    if emit:
+        n = nrows.value
+        arr = np.ctypeslib.as_array(out, shape=(max(n, 1) * len(aliases),))[:n * len(aliases)].copy()
+        lib().dfs_free(C.cast(out, C.c_void_p))
+        rows = np.unique(arr.reshape(n, len(aliases)), axis=0) if n else arr.reshape(0, len(aliases))
+    return {"rows": rows, "aliases": aliases, "bindings": b, "edges": edges.value, "seconds": dt, "nroots": len(roots)}

@@ -1,0 +1,24 @@
+// exec.h — runs a compiled Plan on the device and produces the distinct RETURN rows.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "graph.h"
+#include "plan.h"
+
+struct omx_result {
+  omx_result_info info{};
+  std::vector<std::string> names;
+  std::vector<uint64_t> rows;  // row-major n_rows × n_cols
+  struct KStat {
+    std::string name;
+    int64_t launches = 0;
+    double ms = 0;
+    uint64_t bytes = 0;
+  };
+  std::vector<KStat> kstats;
+};
+
+namespace omx {
+omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts);
+}

@@ -1,0 +1,170 @@
+// gen.cpp — deterministic synthetic inputs and host CSR utilities.
+//
+// Graph500 RMAT (A=.57, B=.19, C=.19, D=.05), edge factor 16. Every edge is a pure function of
+// (seed, edge index) through splitmix64, so the same graph is produced by any thread count and by
+// the numpy restatement in the tests; vertex ids are scrambled by a seeded bijection of [0, 2^scale)
+// so hubs are spread over the id space (and over GPUs under a modulo partition).
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+template <class F>
+void par(uint64_t n, F f) {
+  unsigned nt = std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+  if (n < (1u << 16)) nt = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back([=] { f(n * t / nt, n * (t + 1) / nt); });
+  for (auto &x : th) x.join();
+}
+
+struct Rmat {
+  int scale;
+  uint64_t seed, mask, m1, m2, c1, c2;
+  // thresholds on a 32-bit uniform: A, A+B, A+B+C
+  static constexpr uint32_t TA = (uint32_t)(0.57 * 4294967296.0);
+  static constexpr uint32_t TB = (uint32_t)(0.76 * 4294967296.0);
+  static constexpr uint32_t TC = (uint32_t)(0.95 * 4294967296.0);
+  Rmat(int s, uint64_t sd) : scale(s), seed(sd) {
+    mask = (scale >= 64) ? ~0ull : ((1ull << scale) - 1);
+    m1 = omx::splitmix64(seed ^ 0x1111) | 1;
+    m2 = omx::splitmix64(seed ^ 0x2222) | 1;
+    c1 = omx::splitmix64(seed ^ 0x3333);
+    c2 = omx::splitmix64(seed ^ 0x4444);
+  }
+  // bijection of [0, 2^scale): odd multiply, add, xor-shift (each invertible mod 2^scale)
+  uint64_t scramble(uint64_t x) const {
+    int h = scale / 2 + 1;
+    x = (x * m1 + c1) & mask;
+    x ^= x >> h;
+    x = (x * m2 + c2) & mask;
+    x ^= x >> h;
+    return x & mask;
+  }
+  void edge(uint64_t i, uint32_t &u, uint32_t &v) const {
+    uint64_t a = 0, b = 0, st = seed * 0x9E3779B97F4A7C15ull + i * 0xD1B54A32D192ED03ull;
+    uint64_t r = 0;
+    for (int lvl = 0; lvl < scale; ++lvl) {
+      if ((lvl & 1) == 0) r = omx::splitmix64(st + (uint64_t)lvl);
+      uint32_t x = (lvl & 1) ? (uint32_t)(r >> 32) : (uint32_t)r;
+      int q = x < TA ? 0 : x < TB ? 1 : x < TC ? 2 : 3;
+      a = (a << 1) | (q >> 1);
+      b = (b << 1) | (q & 1);
+    }
+    u = (uint32_t)scramble(a);
+    v = (uint32_t)scramble(b);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+void omx_host_free(void *p) { std::free(p); }
+
+int omx_csr_transpose(uint32_t V, const uint64_t *rp, const uint32_t *col, uint64_t **trp, uint32_t **tcol) {
+  const uint64_t E = rp[V];
+  std::vector<std::atomic<uint64_t>> deg(V);
+  for (auto &d : deg) d.store(0, std::memory_order_relaxed);
+  par(V, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t v = lo; v < hi; ++v)
+      for (uint64_t e = rp[v]; e < rp[v + 1]; ++e) deg[col[e]].fetch_add(1, std::memory_order_relaxed);
+  });
+  uint64_t *orp = (uint64_t *)std::malloc(sizeof(uint64_t) * ((size_t)V + 1));
+  uint32_t *ocol = (uint32_t *)std::malloc(sizeof(uint32_t) * std::max<uint64_t>(E, 1));
+  if (!orp || !ocol) return OMX_E_OOM;
+  orp[0] = 0;
+  for (uint32_t v = 0; v < V; ++v) orp[v + 1] = orp[v] + deg[v].load(std::memory_order_relaxed);
+  for (uint32_t v = 0; v < V; ++v) deg[v].store(orp[v], std::memory_order_relaxed);
+  par(V, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t v = lo; v < hi; ++v)
+      for (uint64_t e = rp[v]; e < rp[v + 1]; ++e) ocol[deg[col[e]].fetch_add(1, std::memory_order_relaxed)] = (uint32_t)v;
+  });
+  par(V, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t v = lo; v < hi; ++v) std::sort(ocol + orp[v], ocol + orp[v + 1]);
+  });
+  *trp = orp;
+  *tcol = ocol;
+  return OMX_OK;
+}
+
+int omx_rmat_generate(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t simple, uint64_t **out_rp,
+                      uint32_t **out_col, uint64_t *n_edges) {
+  if (scale < 1 || scale > 31 || edge_factor < 1 || !out_rp || !out_col || !n_edges) return OMX_E_INVALID;
+  const uint64_t V = 1ull << scale, M = (uint64_t)edge_factor * V;
+  Rmat g(scale, seed);
+  std::vector<std::atomic<uint64_t>> deg(V);
+  for (auto &d : deg) d.store(0, std::memory_order_relaxed);
+  par(M, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i) {
+      uint32_t u, v;
+      g.edge(i, u, v);
+      deg[u].fetch_add(1, std::memory_order_relaxed);
+    }
+  });
+  std::vector<uint64_t> rp(V + 1, 0);
+  for (uint64_t v = 0; v < V; ++v) rp[v + 1] = rp[v] + deg[v].load(std::memory_order_relaxed);
+  for (uint64_t v = 0; v < V; ++v) deg[v].store(rp[v], std::memory_order_relaxed);
+  uint32_t *col = (uint32_t *)std::malloc(sizeof(uint32_t) * std::max<uint64_t>(M, 1));
+  if (!col) return OMX_E_OOM;
+  par(M, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i) {
+      uint32_t u, v;
+      g.edge(i, u, v);
+      col[deg[u].fetch_add(1, std::memory_order_relaxed)] = v;
+    }
+  });
+  // sort rows; optionally drop self loops and parallel edges (SURVEY §8(d) headline runs)
+  std::vector<uint64_t> keep(V, 0);
+  par(V, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t v = lo; v < hi; ++v) {
+      uint32_t *b = col + rp[v], *e = col + rp[v + 1];
+      std::sort(b, e);
+      if (simple) {
+        uint32_t *w = b;
+        for (uint32_t *x = b; x < e; ++x)
+          if (*x != (uint32_t)v && (w == b || *(w - 1) != *x)) *w++ = *x;
+        keep[v] = (uint64_t)(w - b);
+      } else {
+        keep[v] = (uint64_t)(e - b);
+      }
+    }
+  });
+  uint64_t *orp = (uint64_t *)std::malloc(sizeof(uint64_t) * (V + 1));
+  if (!orp) {
+    std::free(col);
+    return OMX_E_OOM;
+  }
+  orp[0] = 0;
+  for (uint64_t v = 0; v < V; ++v) orp[v + 1] = orp[v] + keep[v];
+  const uint64_t E = orp[V];
+  if (simple) {  // compact in place (destination never passes the source)
+    for (uint64_t v = 0; v < V; ++v)
+      if (orp[v] != rp[v]) std::memmove(col + orp[v], col + rp[v], keep[v] * sizeof(uint32_t));
+    uint32_t *shrunk = (uint32_t *)std::realloc(col, sizeof(uint32_t) * std::max<uint64_t>(E, 1));
+    if (shrunk) col = shrunk;
+  }
+  *out_rp = orp;
+  *out_col = col;
+  *n_edges = E;
+  return OMX_OK;
+}
+
+int omx_synthetic_int_column(uint32_t V, uint64_t seed, int32_t modulo, int32_t **out) {
+  if (modulo <= 0 || !out) return OMX_E_INVALID;
+  int32_t *c = (int32_t *)std::malloc(sizeof(int32_t) * std::max<uint32_t>(V, 1));
+  if (!c) return OMX_E_OOM;
+  par(V, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t v = lo; v < hi; ++v) c[v] = (int32_t)(omx::splitmix64(seed ^ (v * 0xA24BAED4963EE407ull)) % (uint64_t)modulo);
+  });
+  *out = c;
+  return OMX_OK;
+}
+
+}  // extern "C"

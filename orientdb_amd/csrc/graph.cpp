@@ -1,0 +1,343 @@
+// graph.cpp — snapshot validation, host-side statistics and upload to HBM.
+#include "graph.h"
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <cstring>
+#include <thread>
+
+#include "sql.h"
+
+namespace omx {
+
+// ---- device pool -----------------------------------------------------------------------------------
+
+static size_t round_size(size_t b) {
+  if (b <= 4096) return 4096;
+  if (b <= (1u << 20)) {  // power of two up to 1 MiB
+    size_t r = 4096;
+    while (r < b) r <<= 1;
+    return r;
+  }
+  const size_t g = 2u << 20;  // 2 MiB granules above
+  return (b + g - 1) / g * g;
+}
+
+void *DevicePool::alloc(size_t bytes) {
+  size_t sz = round_size(bytes);
+  auto it = free_.lower_bound(sz);
+  if (it != free_.end() && it->first <= sz + sz / 4 + (2u << 20)) {
+    void *p = it->second;
+    live_[p] = it->first;
+    cached_ -= it->first;
+    free_.erase(it);
+    return p;
+  }
+  void *p = nullptr;
+  if (hipMalloc(&p, sz) != hipSuccess) {
+    (void)hipGetLastError();
+    trim();
+    if (hipMalloc(&p, sz) != hipSuccess) {
+      (void)hipGetLastError();
+      fail(OMX_E_OOM, "device allocation of " + std::to_string(sz) + " bytes failed");
+    }
+  }
+  live_[p] = sz;
+  return p;
+}
+
+void DevicePool::release(void *p) {
+  auto it = live_.find(p);
+  if (it == live_.end()) return;
+  free_.emplace(it->second, p);
+  cached_ += it->second;
+  live_.erase(it);
+}
+
+void DevicePool::trim() {
+  for (auto &kv : free_) (void)hipFree(kv.second);
+  free_.clear();
+  cached_ = 0;
+}
+
+DevicePool::~DevicePool() {
+  trim();
+  for (auto &kv : live_) (void)hipFree(kv.first);
+}
+
+// ---- graph -----------------------------------------------------------------------------------------
+
+Graph::~Graph() {
+  if (device >= 0) {
+    (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();
+    auto f = [](void *p) { if (p) (void)hipFree(p); };
+    f(d_vclass);
+    f(d_rids);
+    f(d_cols);
+    for (auto &e : esets) { f(e.d_out_rp); f(e.d_in_rp); f(e.d_out_col); f(e.d_in_col); }
+    for (auto &p : props) { f(p.d_values); f(p.d_present); }
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+}
+
+int Graph::class_id(const std::string &name) const {
+  for (size_t i = 0; i < classes.size(); ++i)
+    if (classes[i].name == name) return (int)i;
+  for (size_t i = 0; i < classes.size(); ++i)
+    if (ieq(classes[i].name, name)) return (int)i;
+  return -1;
+}
+
+int Graph::prop_id(const std::string &name) const {
+  for (size_t i = 0; i < props.size(); ++i)
+    if (props[i].name == name) return (int)i;
+  return -1;
+}
+
+bool Graph::is_subclass_of(int c, int sup) const {
+  while (c >= 0) {
+    if (c == sup) return true;
+    c = classes[c].super;
+  }
+  return false;
+}
+
+uint64_t Graph::count(int c) const {
+  uint64_t n = 0;
+  for (int x : classes[c].poly) n += classes[x].exact_count;
+  return n;
+}
+
+void Graph::class_mask(int c, uint64_t mask[4]) const {
+  mask[0] = mask[1] = mask[2] = mask[3] = 0;
+  for (int x : classes[c].poly) mask[x >> 6] |= 1ull << (x & 63);
+}
+
+int64_t Graph::index_hits(int cls, int prop, const Value &v) const {
+  const Property &p = props[prop];
+  int64_t n = 0;
+  uint64_t mask[4];
+  class_mask(cls, mask);
+  for (uint32_t i = 0; i < V; ++i) {
+    int c = h_vclass[i];
+    if (!((mask[c >> 6] >> (c & 63)) & 1)) continue;
+    if (!p.h_present.empty() && !p.h_present[i]) continue;
+    bool eq = false;
+    if (p.type == OMX_PROP_DOUBLE) {
+      double x = p.h_dbl[i];
+      eq = (v.kind == Value::INT && x == (double)v.i) || (v.kind == Value::DBL && x == v.d);
+    } else if (p.type == OMX_PROP_STRING) {
+      eq = v.kind == Value::STR && p.h_int[i] >= 0 && p.dict[p.h_int[i]] == v.s;
+    } else {
+      int64_t x = p.h_int[i];
+      eq = (v.kind == Value::INT && x == v.i) || (v.kind == Value::DBL && (double)x == v.d) ||
+           (v.kind == Value::BOOL && x == v.i);
+    }
+    n += eq;
+  }
+  return n;
+}
+
+// ---- creation --------------------------------------------------------------------------------------
+
+template <class F>
+static void parallel_for(uint64_t n, F f) {
+  unsigned nt = std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+  if (n < 65536) nt = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([=]() {
+      uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+      f(lo, hi);
+    });
+  for (auto &x : th) x.join();
+}
+
+// Checks row order; returns (sorted, simple).
+static std::pair<bool, bool> scan_rows(uint32_t V, const uint64_t *rp, const uint32_t *col) {
+  std::atomic<bool> sorted{true}, simple{true};
+  parallel_for(V, [&](uint64_t lo, uint64_t hi) {
+    bool so = true, si = true;
+    for (uint64_t v = lo; v < hi; ++v)
+      for (uint64_t e = rp[v] + 1; e < rp[v + 1]; ++e) {
+        if (col[e - 1] > col[e]) so = false;
+        if (col[e - 1] >= col[e]) si = false;
+      }
+    if (!so) sorted = false;
+    if (!si) simple = false;
+  });
+  return {sorted.load(), simple.load()};
+}
+
+static void sort_rows(uint32_t V, const uint64_t *rp, uint32_t *col) {
+  parallel_for(V, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t v = lo; v < hi; ++v) std::sort(col + rp[v], col + rp[v + 1]);
+  });
+}
+
+template <class T>
+static T *upload(const T *h, size_t n, uint64_t &acc) {
+  if (n == 0) n = 1;
+  T *d = nullptr;
+  HIP_CHECK(hipMalloc(&d, n * sizeof(T)));
+  if (h) HIP_CHECK(hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
+  else HIP_CHECK(hipMemset(d, 0, n * sizeof(T)));
+  acc += n * sizeof(T);
+  return d;
+}
+
+extern "C" int omx_csr_transpose(uint32_t, const uint64_t *, const uint32_t *, uint64_t **, uint32_t **);
+
+Graph *graph_create(const omx_graph_desc *d) {
+  if (!d) fail(OMX_E_INVALID, "null graph descriptor");
+  if (d->n_classes <= 0 || d->n_classes > 256) fail(OMX_E_INVALID, "n_classes must be in [1, 256]");
+  if (d->n_vertices > 0 && (!d->vertex_class || !d->rids)) fail(OMX_E_INVALID, "vertex_class and rids required");
+  auto g = std::make_unique<Graph>();
+  g->V = d->n_vertices;
+  g->device = d->device;
+  uint32_t V = g->V;
+
+  for (int i = 0; i < d->n_classes; ++i) {
+    ClassInfo c;
+    c.name = d->classes[i].name ? d->classes[i].name : "";
+    c.super = d->classes[i].superclass;
+    c.is_edge = d->classes[i].is_edge_class != 0;
+    c.cluster = d->classes[i].cluster_id;
+    if (c.super < -1 || c.super >= d->n_classes) fail(OMX_E_INVALID, "bad superclass index for " + c.name);
+    g->classes.push_back(c);
+  }
+  for (int i = 0; i < d->n_classes; ++i)
+    for (int j = 0; j < d->n_classes; ++j)
+      if (g->is_subclass_of(j, i)) g->classes[i].poly.push_back(j);
+  std::vector<uint64_t> counts(d->n_classes, 0);
+  for (uint32_t v = 0; v < V; ++v) {
+    uint16_t c = d->vertex_class[v];
+    if (c >= d->n_classes) fail(OMX_E_INVALID, "vertex_class out of range at vertex " + std::to_string(v));
+    counts[c]++;
+  }
+  for (int i = 0; i < d->n_classes; ++i) g->classes[i].exact_count = counts[i];
+
+  // properties
+  for (int i = 0; i < d->n_properties; ++i) {
+    const omx_property_desc &pd = d->properties[i];
+    Property p;
+    p.name = pd.name ? pd.name : "";
+    p.type = pd.type;
+    if (p.type < OMX_PROP_INT32 || p.type > OMX_PROP_BOOL) fail(OMX_E_INVALID, "bad property type for " + p.name);
+    if (p.type == OMX_PROP_STRING) {
+      for (int k = 0; k < pd.dict_size; ++k) p.dict.push_back(pd.dict[k]);
+      for (int k = 1; k < pd.dict_size; ++k)
+        if (!(p.dict[k - 1] < p.dict[k])) fail(OMX_E_INVALID, "string dictionary of " + p.name + " not sorted/unique");
+    }
+    if (pd.present)
+      for (uint32_t v = 0; v < V && !p.has_nulls; ++v) p.has_nulls = pd.present[v] == 0;
+    g->props.push_back(std::move(p));
+  }
+  for (int i = 0; i < d->n_indexes; ++i) {
+    const omx_index_desc &x = d->indexes[i];
+    int pid = g->prop_id(x.property ? x.property : "");
+    if (x.class_id < 0 || x.class_id >= d->n_classes) fail(OMX_E_INVALID, "bad index class");
+    if (pid < 0) continue;  // index on a property no vertex carries: never matches a condition
+    g->indexes.push_back({x.class_id, pid, x.unique != 0});
+    Property &p = g->props[pid];
+    const omx_property_desc &pd = d->properties[pid];
+    if (p.h_int.empty() && p.h_dbl.empty()) {
+      if (p.type == OMX_PROP_DOUBLE) p.h_dbl.assign((const double *)pd.values, (const double *)pd.values + V);
+      else if (p.type == OMX_PROP_INT64) p.h_int.assign((const int64_t *)pd.values, (const int64_t *)pd.values + V);
+      else {
+        const int32_t *s = (const int32_t *)pd.values;
+        p.h_int.assign(s, s + V);
+      }
+      if (pd.present) p.h_present.assign(pd.present, pd.present + V);
+    }
+  }
+  if (!g->indexes.empty()) g->h_vclass.assign(d->vertex_class, d->vertex_class + V);
+
+  // edge sets: validate, sort rows if needed, build the transpose if absent
+  std::vector<std::vector<uint32_t>> sorted_copies;
+  struct Tmp { const uint64_t *orp, *irp; const uint32_t *ocol, *icol; uint64_t *own_rp = nullptr; uint32_t *own_col = nullptr; };
+  std::vector<Tmp> tmp(d->n_edge_sets);
+  for (int i = 0; i < d->n_edge_sets; ++i) {
+    const omx_edge_set_desc &ed = d->edge_sets[i];
+    EdgeSet es;
+    es.cls = ed.edge_class;
+    es.n_edges = ed.n_edges;
+    if (es.cls < 0 || es.cls >= d->n_classes) fail(OMX_E_INVALID, "bad edge class index");
+    if (!ed.out_row_ptr || (ed.n_edges && !ed.out_col)) fail(OMX_E_INVALID, "edge set without out CSR");
+    if (ed.out_row_ptr[0] != 0 || ed.out_row_ptr[V] != ed.n_edges) fail(OMX_E_INVALID, "out_row_ptr inconsistent");
+    Tmp &t = tmp[i];
+    t.orp = ed.out_row_ptr;
+    t.ocol = ed.out_col;
+    for (uint64_t e = 0; e < ed.n_edges; e += std::max<uint64_t>(1, ed.n_edges / 4096))
+      if (ed.out_col[e] >= V) fail(OMX_E_INVALID, "out_col out of range");
+    auto so = scan_rows(V, t.orp, t.ocol);
+    if (!so.first) {
+      sorted_copies.emplace_back(t.ocol, t.ocol + ed.n_edges);
+      sort_rows(V, t.orp, sorted_copies.back().data());
+      t.ocol = sorted_copies.back().data();
+      so = scan_rows(V, t.orp, t.ocol);
+    }
+    es.out_sorted = so.first;
+    es.out_simple = so.second;
+    if (ed.in_row_ptr && ed.in_col) {
+      if (ed.in_row_ptr[V] != ed.n_edges) fail(OMX_E_INVALID, "in_row_ptr inconsistent");
+      t.irp = ed.in_row_ptr;
+      t.icol = ed.in_col;
+      auto si = scan_rows(V, t.irp, t.icol);
+      if (!si.first) {
+        sorted_copies.emplace_back(t.icol, t.icol + ed.n_edges);
+        sort_rows(V, t.irp, sorted_copies.back().data());
+        t.icol = sorted_copies.back().data();
+        si = scan_rows(V, t.irp, t.icol);
+      }
+      es.in_sorted = si.first;
+      es.in_simple = si.second;
+    } else {
+      omx_csr_transpose(V, t.orp, t.ocol, &t.own_rp, &t.own_col);
+      t.irp = t.own_rp;
+      t.icol = t.own_col;
+      auto si = scan_rows(V, t.irp, t.icol);
+      es.in_sorted = si.first;
+      es.in_simple = si.second;
+    }
+    g->esets.push_back(es);
+  }
+
+  if (g->device >= 0) {
+    HIP_CHECK(hipSetDevice(g->device));
+    HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    uint64_t &acc = g->device_bytes;
+    g->d_vclass = upload(d->vertex_class, V, acc);
+    g->d_rids = upload(d->rids, V, acc);
+    for (int i = 0; i < d->n_edge_sets; ++i) {
+      EdgeSet &es = g->esets[i];
+      es.d_out_rp = upload(tmp[i].orp, (size_t)V + 1, acc);
+      es.d_out_col = upload(tmp[i].ocol, es.n_edges, acc);
+      es.d_in_rp = upload(tmp[i].irp, (size_t)V + 1, acc);
+      es.d_in_col = upload(tmp[i].icol, es.n_edges, acc);
+    }
+    std::vector<DColumn> cols;
+    for (int i = 0; i < d->n_properties; ++i) {
+      Property &p = g->props[i];
+      const omx_property_desc &pd = d->properties[i];
+      size_t w = (p.type == OMX_PROP_INT64 || p.type == OMX_PROP_DOUBLE) ? 8 : 4;
+      void *dv = nullptr;
+      HIP_CHECK(hipMalloc(&dv, std::max<size_t>(1, (size_t)V * w)));
+      if (V) HIP_CHECK(hipMemcpy(dv, pd.values, (size_t)V * w, hipMemcpyHostToDevice));
+      acc += (size_t)V * w;
+      p.d_values = dv;
+      if (p.has_nulls) p.d_present = upload(pd.present, V, acc);
+      cols.push_back({p.d_values, p.d_present, p.type, 0});
+    }
+    if (!cols.empty()) g->d_cols = upload(cols.data(), cols.size(), acc);
+  }
+  for (auto &t : tmp) {
+    omx_host_free(t.own_rp);
+    omx_host_free(t.own_col);
+  }
+  return g.release();
+}
+
+}  // namespace omx

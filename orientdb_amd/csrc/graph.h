@@ -1,0 +1,137 @@
+// graph.h — the immutable HBM snapshot of a database's vertices, ridbags and properties.
+//
+// Replaces the lazy record/ridbag reads of the reference's DFS (ORidBag.rawIterator
+// C/db/record/ridbag/ORidBag.java:160, OrientVertex.getVertices B/OrientVertex.java:401-460,
+// ODocument.field C/record/impl/ODocument.java:820) with one snapshot per database state:
+//   * per edge class: out-CSR and in-CSR (u64 row_ptr, u32 dense vertex ids), rows sorted;
+//   * class_id u16 per vertex, RID u64 per vertex;
+//   * one column per property (int32 / int64 / double / dictionary-coded string) + presence bytes.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+#include "devtypes.h"
+
+#define HIP_CHECK(x)                                                                                    \
+  do {                                                                                                  \
+    hipError_t e_ = (x);                                                                                \
+    if (e_ != hipSuccess) ::omx::fail(OMX_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+namespace omx {
+
+// Caching device allocator: execution buffers are recycled between queries so that a steady-state
+// omx_execute issues no hipMalloc/hipFree (Guideline 9 of the CDNA HIP guide).
+class DevicePool {
+ public:
+  void *alloc(size_t bytes);
+  void release(void *p);
+  void trim();
+  ~DevicePool();
+  size_t cached_bytes() const { return cached_; }
+
+ private:
+  std::multimap<size_t, void *> free_;
+  std::unordered_map<void *, size_t> live_;
+  size_t cached_ = 0;
+};
+
+template <class T>
+struct DBuf {
+  DevicePool *pool = nullptr;
+  T *p = nullptr;
+  size_t n = 0;
+  DBuf() = default;
+  DBuf(DevicePool *pl, size_t count) : pool(pl), n(count) {
+    p = count ? (T *)pool->alloc(count * sizeof(T)) : nullptr;
+  }
+  DBuf(const DBuf &) = delete;
+  DBuf &operator=(const DBuf &) = delete;
+  DBuf(DBuf &&o) noexcept { *this = std::move(o); }
+  DBuf &operator=(DBuf &&o) noexcept {
+    if (this != &o) {
+      reset();
+      pool = o.pool; p = o.p; n = o.n;
+      o.p = nullptr; o.n = 0;
+    }
+    return *this;
+  }
+  ~DBuf() { reset(); }
+  void reset() {
+    if (p && pool) pool->release(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct ClassInfo {
+  std::string name;
+  int super = -1;
+  bool is_edge = false;
+  int cluster = 0;
+  uint64_t exact_count = 0;     // vertices whose class is exactly this one
+  std::vector<int> poly;        // this class and every subclass (polymorphic set)
+};
+
+struct EdgeSet {
+  int cls = -1;
+  uint64_t n_edges = 0;
+  bool out_sorted = true, in_sorted = true;  // rows ascending
+  bool out_simple = true, in_simple = true;  // rows strictly ascending (no parallel edges)
+  uint64_t *d_out_rp = nullptr, *d_in_rp = nullptr;
+  uint32_t *d_out_col = nullptr, *d_in_col = nullptr;
+};
+
+struct Property {
+  std::string name;
+  int type = 0;
+  std::vector<std::string> dict;        // strings, sorted
+  bool has_nulls = false;
+  void *d_values = nullptr;
+  uint8_t *d_present = nullptr;
+  // host copy kept only for indexed properties (root estimation, OWhereClause.estimate)
+  std::vector<int64_t> h_int;
+  std::vector<double> h_dbl;
+  std::vector<uint8_t> h_present;
+};
+
+struct IndexInfo {
+  int cls;
+  int prop;
+  bool unique;
+};
+
+struct Graph {
+  uint32_t V = 0;
+  int device = -1;
+  std::vector<ClassInfo> classes;
+  std::vector<EdgeSet> esets;
+  std::vector<Property> props;
+  std::vector<IndexInfo> indexes;
+  std::vector<uint16_t> h_vclass;  // kept only when indexes exist
+  uint16_t *d_vclass = nullptr;
+  uint64_t *d_rids = nullptr;
+  DColumn *d_cols = nullptr;
+  uint64_t device_bytes = 0;
+  hipStream_t stream = nullptr;
+  DevicePool pool;
+
+  ~Graph();
+  bool on_device() const { return device >= 0; }
+  int class_id(const std::string &name) const;        // case-insensitive, -1 if absent
+  int prop_id(const std::string &name) const;         // exact, -1 if absent
+  bool is_subclass_of(int c, int sup) const;
+  uint64_t count(int c) const;                         // OClassImpl.count() (polymorphic)
+  void class_mask(int c, uint64_t mask[4]) const;      // polymorphic set as a 256-bit mask
+  // index lookup size for prop == value over the polymorphic class (OWhereClause.estimateFromIndex)
+  int64_t index_hits(int cls, int prop, const struct Value &v) const;
+};
+
+Graph *graph_create(const omx_graph_desc *d);
+
+}  // namespace omx

@@ -1,0 +1,645 @@
+// kernels.hip — gfx950 (MI355X / CDNA4) kernels of the MATCH executor.
+//
+// None of this is a dense contraction: every kernel is HBM/L2-bound integer work (no MFMA). The
+// hot one is k_expand, the frontier expansion of one pattern edge over the binding table
+// (OMatchStatement.processContext P/OMatchStatement.java:412-568 → OMatchPathItem.executeTraversal
+// P/OMatchPathItem.java:49-78 → OrientVertex.getVertices B/OrientVertex.java:401-460):
+//   * merge-path load balance over (rows + edges), so RMAT hubs (deg ~1e4-1e5) and degree-1 rows
+//     cost the same per item; tile = 256 threads × 8 items;
+//   * per tile, row ownership of every edge is resolved in LDS (scatter of row starts + block
+//     max-scan), so the col[] loads are coalesced (lane l reads edge j0 + k·256 + l);
+//   * the target filter is a V-bit bitmap probe (L2-resident: 512 KiB at RMAT-22);
+//   * compaction by wave64 ballot + mbcnt, wave totals scanned in LDS; a tile writes its rows
+//     contiguously at its own edge offset ("gapped" output, no global atomics) and its count, which a
+//     scan + k_compact_tiles turns into a dense table. Without a filter the output is already dense.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace omx {
+
+#define KCHECK(name)                                                                                    \
+  do {                                                                                                  \
+    hipError_t e_ = hipGetLastError();                                                                  \
+    if (e_ != hipSuccess) fail(OMX_E_DEVICE, std::string("launch of ") + name + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+static inline unsigned nblocks(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+__device__ __forceinline__ bool bm_test(const uint64_t *bm, uint32_t v) { return (bm[v >> 6] >> (v & 63)) & 1ull; }
+
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// ---- predicate VM (compiled WHERE / while; P/OWhereClause.java:36-41, operators P/O*Operator.java) ----
+
+struct VmVal {
+  int64_t i;
+  double d;
+  int32_t t;  // 0 null, 1 int, 2 double, 3 bool
+};
+
+__device__ __forceinline__ VmVal vm_col(const DColumn &c, uint32_t v) {
+  VmVal x{0, 0.0, 0};
+  if (c.present && !c.present[v]) return x;
+  switch (c.type) {
+    case OMX_PROP_INT64: x.i = ((const int64_t *)c.values)[v]; x.t = 1; break;
+    case OMX_PROP_DOUBLE: x.d = ((const double *)c.values)[v]; x.t = 2; break;
+    case OMX_PROP_BOOL: x.i = ((const int32_t *)c.values)[v] != 0; x.t = 3; break;
+    case OMX_PROP_STRING: {
+      int32_t code = ((const int32_t *)c.values)[v];
+      if (code < 0) return x;
+      x.i = code;
+      x.t = 1;
+      break;
+    }
+    default: x.i = ((const int32_t *)c.values)[v]; x.t = 1; break;
+  }
+  return x;
+}
+
+__device__ __forceinline__ int vm_cmp(const VmVal &a, const VmVal &b) {
+  if (a.t != 2 && b.t != 2) return a.i < b.i ? -1 : (a.i > b.i ? 1 : 0);
+  double x = a.t == 2 ? a.d : (double)a.i, y = b.t == 2 ? b.d : (double)b.i;
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+__device__ __forceinline__ bool vm_truthy(const VmVal &a) { return a.t == 3 && a.i != 0; }
+
+__device__ bool eval_pred(const DPred &P, uint32_t v, int64_t depth) {
+  if (P.use_class) {
+    uint32_t c = P.vclass[v];
+    if (!((P.class_mask[c >> 6] >> (c & 63)) & 1ull)) return false;
+  }
+  if (P.n == 0) return true;
+  VmVal st[16];
+  int sp = 0;
+  for (int pc = 0; pc < P.n; ++pc) {
+    const DPredInstr in = P.code[pc];
+    switch (in.op) {
+      case P_PUSH_COL: st[sp++] = vm_col(P.cols[in.arg], v); break;
+      case P_PUSH_INT: st[sp++] = VmVal{in.i, 0.0, 1}; break;
+      case P_PUSH_DBL: st[sp++] = VmVal{0, in.d, 2}; break;
+      case P_PUSH_NULL: st[sp++] = VmVal{0, 0.0, 0}; break;
+      case P_PUSH_BOOL: st[sp++] = VmVal{in.i != 0, 0.0, 3}; break;
+      case P_PUSH_DEPTH: st[sp++] = VmVal{depth, 0.0, 1}; break;
+      case P_PUSH_DEG: {
+        const DAdj &a = P.deg[in.arg];
+        int64_t d = 0;
+        for (int p = 0; p < a.n; ++p) d += (int64_t)(a.p[p].rp[v + 1] - a.p[p].rp[v]);
+        st[sp++] = VmVal{d, 0.0, 1};
+        break;
+      }
+      case P_ADD: case P_SUB: case P_MUL: case P_DIV: case P_MOD: {
+        VmVal b = st[--sp], a = st[--sp];
+        VmVal r{0, 0.0, 0};
+        if (a.t != 0 && b.t != 0) {
+          if (a.t != 2 && b.t != 2) {
+            r.t = 1;
+            switch (in.op) {
+              case P_ADD: r.i = a.i + b.i; break;
+              case P_SUB: r.i = a.i - b.i; break;
+              case P_MUL: r.i = a.i * b.i; break;
+              case P_DIV: if (b.i) r.i = a.i / b.i; else r.t = 0; break;
+              default: if (b.i) r.i = a.i % b.i; else r.t = 0; break;
+            }
+          } else {
+            double x = a.t == 2 ? a.d : (double)a.i, y = b.t == 2 ? b.d : (double)b.i;
+            r.t = 2;
+            switch (in.op) {
+              case P_ADD: r.d = x + y; break;
+              case P_SUB: r.d = x - y; break;
+              case P_MUL: r.d = x * y; break;
+              case P_DIV: r.d = x / y; break;
+              default: r.d = fmod(x, y); break;
+            }
+          }
+        }
+        st[sp++] = r;
+        break;
+      }
+      case P_EQ: case P_NE: {
+        VmVal b = st[--sp], a = st[--sp];
+        bool eq = a.t != 0 && b.t != 0 && vm_cmp(a, b) == 0;
+        st[sp++] = VmVal{in.op == P_EQ ? eq : !eq, 0.0, 3};
+        break;
+      }
+      case P_LT: case P_LE: case P_GT: case P_GE: {
+        VmVal b = st[--sp], a = st[--sp];
+        bool r = false;
+        if (a.t != 0 && b.t != 0) {
+          int c = vm_cmp(a, b);
+          r = in.op == P_LT ? c < 0 : in.op == P_LE ? c <= 0 : in.op == P_GT ? c > 0 : c >= 0;
+        }
+        st[sp++] = VmVal{r, 0.0, 3};
+        break;
+      }
+      case P_AND: case P_OR: {
+        VmVal b = st[--sp], a = st[--sp];
+        bool r = in.op == P_AND ? (vm_truthy(a) && vm_truthy(b)) : (vm_truthy(a) || vm_truthy(b));
+        st[sp++] = VmVal{r, 0.0, 3};
+        break;
+      }
+      case P_NOT: st[sp - 1] = VmVal{!vm_truthy(st[sp - 1]), 0.0, 3}; break;
+      case P_TRUTH: st[sp - 1] = VmVal{vm_truthy(st[sp - 1]), 0.0, 3}; break;
+      default: break;
+    }
+  }
+  return vm_truthy(st[0]);
+}
+
+// one lane per vertex, 64 vertices per wave → one u64 bitmap word per wave via ballot
+__global__ __launch_bounds__(256) void k_eval_bitmap(DPred P, uint32_t V, int64_t depth, uint64_t *words) {
+  uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool b = v < V && eval_pred(P, (uint32_t)v, depth);
+  uint64_t m = __ballot(b);
+  if ((threadIdx.x & 63) == 0 && v < (uint64_t)V) words[v >> 6] = m;
+}
+
+void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s) {
+  if (!V) return;
+  hipLaunchKernelGGL(k_eval_bitmap, dim3(nblocks(V, 256)), dim3(256), 0, s, pred, V, depth, words);
+  KCHECK("k_eval_bitmap");
+}
+
+__global__ void k_bitmap_and(const uint64_t *a, uint64_t *b, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] &= a[i];
+}
+void launch_bitmap_and(const uint64_t *a, uint64_t *b, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_bitmap_and, dim3(nblocks(n, 256)), dim3(256), 0, s, a, b, n);
+  KCHECK("k_bitmap_and");
+}
+
+__device__ __forceinline__ uint64_t shard_word(uint64_t w, uint64_t word, uint32_t V, int rank, int world) {
+  uint64_t base = word * 64;
+  if (base + 64 > V) w &= (V - base >= 64) ? ~0ull : ((1ull << (V - base)) - 1);
+  if (world > 1) {
+    uint64_t m = 0;
+    for (int b = 0; b < 64; ++b)
+      if ((base + b) % (uint64_t)world == (uint64_t)rank) m |= 1ull << b;
+    w &= m;
+  }
+  return w;
+}
+
+__global__ void k_word_popc(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t *counts) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) counts[i] = __popcll(shard_word(words[i], i, V, rank, world));
+}
+void launch_word_popc(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t *counts,
+                      hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_word_popc, dim3(nblocks(n, 256)), dim3(256), 0, s, words, n, V, rank, world, counts);
+  KCHECK("k_word_popc");
+}
+
+__global__ void k_word_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world,
+                               const uint32_t *offsets, uint32_t *out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t w = shard_word(words[i], i, V, rank, world);
+  uint32_t o = offsets[i];
+  while (w) {
+    int b = __builtin_ctzll(w);
+    out[o++] = (uint32_t)(i * 64 + b);
+    w &= w - 1;
+  }
+}
+void launch_word_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world,
+                         const uint32_t *offsets, uint32_t *out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_word_scatter, dim3(nblocks(n, 256)), dim3(256), 0, s, words, n, V, rank, world, offsets, out);
+  KCHECK("k_word_scatter");
+}
+
+// ---- expansion ------------------------------------------------------------------------------------
+
+__device__ __forceinline__ uint64_t adj_degree(const DAdj &a, uint32_t v) {
+  uint64_t d = 0;
+  for (int p = 0; p < a.n; ++p) d += a.p[p].rp[v + 1] - a.p[p].rp[v];
+  return d;
+}
+
+__global__ void k_row_degree(const uint32_t *src, uint64_t R, DAdj adj, uint64_t *deg) {
+  uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) deg[r] = adj_degree(adj, src[r]);
+  else if (r == R) deg[R] = 0;
+}
+void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t *deg, hipStream_t s) {
+  hipLaunchKernelGGL(k_row_degree, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, R, adj, deg);
+  KCHECK("k_row_degree");
+}
+
+// merge path over A = row ends (offs[r+1]) and B = edge indices 0..E-1; a row end is consumed
+// before edge j when offs[r+1] <= j.
+__global__ void k_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part) {
+  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  uint64_t d = t * (uint64_t)kExpandTile;
+  if (d > R + E) d = R + E;
+  uint64_t lo = d > E ? d - E : 0, hi = d < R ? d : R;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (offs[mid + 1] <= d - 1 - mid) lo = mid + 1;
+    else hi = mid;
+  }
+  part[t] = lo;
+}
+void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_mp_partition, dim3(nblocks(ntiles + 1, 256)), dim3(256), 0, s, offs, R, E, ntiles, part);
+  KCHECK("k_mp_partition");
+}
+
+template <bool SINGLE, bool FILTER, bool WRITE>
+__global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
+  constexpr int B = kExpandBlock, IPT = kExpandIPT, T = kExpandTile, W = B / 64;
+  __shared__ uint64_t s_base[T + 1];  // SINGLE: first col index of the row's remaining edges; else [0] = skip of row 0
+  __shared__ uint32_t s_vtx[SINGLE ? 1 : T + 1];
+  __shared__ uint16_t s_ls[T + 1];    // local start of each row inside the tile
+  __shared__ uint16_t s_seg[T];       // local row owning each tile edge
+  __shared__ uint32_t s_wave[IPT * W];
+  __shared__ uint32_t s_wmax[W];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t t = blockIdx.x;
+  const uint64_t d0 = t * (uint64_t)T;
+  const uint64_t d1 = min(d0 + (uint64_t)T, a.R + a.E);
+  const uint64_t i0 = a.part[t], i1 = a.part[t + 1];
+  const uint64_t j0 = d0 - i0, j1 = d1 - i1;
+  const uint32_t ne = (uint32_t)(j1 - j0);
+  if (ne == 0) {
+    if (tid == 0) a.tile_count[t] = 0;
+    return;
+  }
+  const uint64_t rlast = min(i1, a.R - 1);
+  const uint32_t nr = (uint32_t)(rlast - i0 + 1);
+
+  for (uint32_t x = tid; x < ne; x += B) s_seg[x] = 0;
+  __syncthreads();
+  for (uint32_t lr = tid; lr < nr; lr += B) {
+    const uint64_t r = i0 + lr;
+    const uint64_t rs = a.offs[r], re = a.offs[r + 1];
+    const uint64_t s = rs > j0 ? rs - j0 : 0;
+    const uint64_t e = re < j1 ? (re > j0 ? re - j0 : 0) : ne;
+    s_ls[lr] = (uint16_t)(s < ne ? s : ne);
+    if (e > s && s < ne) s_seg[s] = (uint16_t)lr;
+    const uint32_t v = a.src[r];
+    const uint64_t skip = rs < j0 ? j0 - rs : 0;
+    if (SINGLE) {
+      s_base[lr] = a.adj.p[0].rp[v] + skip;
+    } else {
+      s_vtx[lr] = v;
+      if (lr == 0) s_base[0] = skip;
+    }
+  }
+  __syncthreads();
+  // inclusive max-scan of s_seg (row index of the latest row starting at or before each edge)
+  {
+    uint32_t vals[IPT];
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      uint32_t idx = tid * IPT + i;
+      uint32_t x = idx < ne ? s_seg[idx] : 0;
+      m = m > x ? m : x;
+      vals[i] = m;
+    }
+    uint32_t incl = m;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      uint32_t y = __shfl_up(incl, off, 64);
+      if (lane >= (uint32_t)off) incl = incl > y ? incl : y;
+    }
+    if (lane == 63) s_wmax[wave] = incl;
+    uint32_t excl = __shfl_up(incl, 1, 64);
+    if (lane == 0) excl = 0;
+    __syncthreads();
+    uint32_t wp = 0;
+    for (uint32_t w = 0; w < wave; ++w) wp = wp > s_wmax[w] ? wp : s_wmax[w];
+    uint32_t pre = excl > wp ? excl : wp;
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      uint32_t idx = tid * IPT + i;
+      if (idx < ne) s_seg[idx] = (uint16_t)(pre > vals[i] ? pre : vals[i]);
+    }
+  }
+  __syncthreads();
+
+  uint32_t nb[IPT];
+  uint16_t lrs[IPT];
+  uint32_t passmask = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const uint32_t jl = k * B + tid;
+    nb[k] = 0;
+    lrs[k] = 0;
+    if (jl < ne) {
+      const uint32_t lr = s_seg[jl];
+      uint64_t kk = jl - s_ls[lr];
+      uint32_t n;
+      if (SINGLE) {
+        n = a.adj.p[0].col[s_base[lr] + kk];
+      } else {
+        const uint32_t v = s_vtx[lr];
+        if (lr == 0) kk += s_base[0];
+        n = 0;
+        for (int p = 0; p < a.adj.n; ++p) {
+          const uint64_t b0 = a.adj.p[p].rp[v], dp = a.adj.p[p].rp[v + 1] - b0;
+          if (kk < dp) {
+            n = a.adj.p[p].col[b0 + kk];
+            break;
+          }
+          kk -= dp;
+        }
+      }
+      nb[k] = n;
+      lrs[k] = (uint16_t)lr;
+      bool pass = FILTER ? bm_test(a.filter, n) : true;
+      passmask |= (uint32_t)pass << k;
+    }
+  }
+
+  if (!FILTER) {
+    if (WRITE) {
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        const uint32_t jl = k * B + tid;
+        if (jl < ne) {
+          const uint64_t o = j0 + jl;
+          const uint64_t r = i0 + lrs[k];
+          a.out_dst[o] = nb[k];
+          for (int c = 0; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
+        }
+      }
+    }
+    if (tid == 0) a.tile_count[t] = ne;
+    return;
+  }
+
+  // compaction: wave ballots per item row k, wave totals scanned in LDS (edge order preserved)
+  uint64_t masks[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    masks[k] = __ballot((passmask >> k) & 1u);
+    if (lane == 0) s_wave[k * W + wave] = (uint32_t)__popcll(masks[k]);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t run = 0;
+    for (int x = 0; x < IPT * W; ++x) {
+      uint32_t c = s_wave[x];
+      s_wave[x] = run;
+      run += c;
+    }
+    a.tile_count[t] = run;
+  }
+  __syncthreads();
+  if (WRITE) {
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      if ((passmask >> k) & 1u) {
+        const uint64_t o = j0 + s_wave[k * W + wave] + lane_prefix(masks[k]);
+        const uint64_t r = i0 + lrs[k];
+        a.out_dst[o] = nb[k];
+        for (int c = 0; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
+      }
+    }
+  }
+}
+
+void launch_expand(const ExpandArgs &a, uint64_t ntiles, bool write, hipStream_t s) {
+  if (!ntiles) return;
+  const bool single = a.adj.n == 1, filter = a.filter != nullptr;
+  dim3 g((unsigned)ntiles), b(kExpandBlock);
+#define OMX_EXP(S, F, Wr) hipLaunchKernelGGL((k_expand<S, F, Wr>), g, b, 0, s, a)
+  if (single) {
+    if (filter) { if (write) OMX_EXP(true, true, true); else OMX_EXP(true, true, false); }
+    else { if (write) OMX_EXP(true, false, true); else OMX_EXP(true, false, false); }
+  } else {
+    if (filter) { if (write) OMX_EXP(false, true, true); else OMX_EXP(false, true, false); }
+    else { if (write) OMX_EXP(false, false, true); else OMX_EXP(false, false, false); }
+  }
+#undef OMX_EXP
+  KCHECK("k_expand");
+}
+
+struct ColPtrs {
+  const uint32_t *in[kMaxCols];
+  uint32_t *out[kMaxCols];
+};
+
+__global__ void k_compact_tiles(int ncols, ColPtrs cp, const uint64_t *part, const uint32_t *tile_count,
+                                const uint64_t *tile_offs) {
+  const uint64_t t = blockIdx.x;
+  const uint32_t cnt = tile_count[t];
+  if (!cnt) return;
+  const uint64_t j0 = t * (uint64_t)kExpandTile - part[t];
+  const uint64_t dst = tile_offs[t];
+  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
+    for (int c = 0; c < ncols; ++c) cp.out[c][dst + i] = cp.in[c][j0 + i];
+}
+void launch_compact_tiles(int ncols, uint32_t *const *in, uint32_t *const *out, const uint64_t *part,
+                          const uint32_t *tile_count, const uint64_t *tile_offs, uint64_t ntiles, hipStream_t s) {
+  if (!ntiles) return;
+  ColPtrs cp;
+  for (int c = 0; c < ncols; ++c) {
+    cp.in[c] = in[c];
+    cp.out[c] = out[c];
+  }
+  hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)ntiles), dim3(256), 0, s, ncols, cp, part, tile_count, tile_offs);
+  KCHECK("k_compact_tiles");
+}
+
+// ---- bound-target check (existence of dst[r] in N(src[r]); P/OMatchStatement.java:468-477) ----------
+
+__global__ void k_check(const uint32_t *src, const uint32_t *dst, uint64_t R, DAdj adj, const uint64_t *filter,
+                        uint8_t *flags) {
+  uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint32_t v = src[r], t = dst[r];
+  bool found = false;
+  if (!filter || bm_test(filter, t)) {
+    for (int p = 0; p < adj.n && !found; ++p) {
+      uint64_t lo = adj.p[p].rp[v], hi = adj.p[p].rp[v + 1];
+      const uint32_t *col = adj.p[p].col;
+      if (adj.sorted) {
+        while (lo < hi) {
+          uint64_t mid = (lo + hi) >> 1;
+          uint32_t x = col[mid];
+          if (x < t) lo = mid + 1;
+          else hi = mid;
+        }
+        found = lo < adj.p[p].rp[v + 1] && col[lo] == t;
+      } else {
+        for (uint64_t e = lo; e < hi && !found; ++e) found = col[e] == t;
+      }
+    }
+  }
+  flags[r] = found;
+}
+void launch_check(const uint32_t *src, const uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
+                  uint8_t *flags, hipStream_t s) {
+  if (!R) return;
+  hipLaunchKernelGGL(k_check, dim3(nblocks(R, 256)), dim3(256), 0, s, src, dst, R, adj, filter, flags);
+  KCHECK("k_check");
+}
+
+// ---- helpers ----------------------------------------------------------------------------------------
+
+__global__ void k_gather_cols(const uint32_t *idx, uint64_t n, int ncols, ColPtrs cp) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = idx[i];
+  for (int c = 0; c < ncols; ++c) cp.out[c][i] = cp.in[c][r];
+}
+void launch_gather_cols(const uint32_t *idx, uint64_t n, int ncols, const uint32_t *const *in, uint32_t *const *out,
+                        hipStream_t s) {
+  if (!n || !ncols) return;
+  ColPtrs cp;
+  for (int c = 0; c < ncols; ++c) {
+    cp.in[c] = in[c];
+    cp.out[c] = out[c];
+  }
+  hipLaunchKernelGGL(k_gather_cols, dim3(nblocks(n, 256)), dim3(256), 0, s, idx, n, ncols, cp);
+  KCHECK("k_gather_cols");
+}
+
+__global__ void k_cross(uint64_t R, int ncols, ColPtrs cp, const uint32_t *cand, uint64_t ncand, uint32_t *out_dst) {
+  uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= R * ncand) return;
+  const uint64_t r = o / ncand, c = o % ncand;
+  out_dst[o] = cand[c];
+  for (int k = 0; k < ncols; ++k) cp.out[k][o] = cp.in[k][r];
+}
+void launch_cross(uint64_t R, int ncols, const uint32_t *const *in, uint32_t *const *out, const uint32_t *cand,
+                  uint64_t ncand, uint32_t *out_dst, hipStream_t s) {
+  if (!R || !ncand) return;
+  ColPtrs cp;
+  for (int c = 0; c < ncols; ++c) {
+    cp.in[c] = in[c];
+    cp.out[c] = out[c];
+  }
+  hipLaunchKernelGGL(k_cross, dim3(nblocks(R * ncand, 256)), dim3(256), 0, s, R, ncols, cp, cand, ncand, out_dst);
+  KCHECK("k_cross");
+}
+
+__global__ void k_flag_bitmap(const uint32_t *v, uint64_t n, const uint64_t *bm, uint8_t *flags) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flags[i] = bm_test(bm, v[i]);
+}
+void launch_flag_bitmap(const uint32_t *v, uint64_t n, const uint64_t *bm, uint8_t *flags, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_flag_bitmap, dim3(nblocks(n, 256)), dim3(256), 0, s, v, n, bm, flags);
+  KCHECK("k_flag_bitmap");
+}
+
+__global__ void k_iota(uint32_t *out, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (uint32_t)i;
+}
+void launch_iota(uint32_t *out, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_iota, dim3(nblocks(n, 256)), dim3(256), 0, s, out, n);
+  KCHECK("k_iota");
+}
+
+__global__ void k_pack_pairs(const uint32_t *hi, const uint32_t *lo, uint64_t n, uint64_t *keys) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) keys[i] = ((uint64_t)hi[i] << 32) | lo[i];
+}
+void launch_pack_pairs(const uint32_t *hi, const uint32_t *lo, uint64_t n, uint64_t *keys, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_pack_pairs, dim3(nblocks(n, 256)), dim3(256), 0, s, hi, lo, n, keys);
+  KCHECK("k_pack_pairs");
+}
+
+__global__ void k_unpack_pairs(const uint64_t *keys, uint64_t n, uint32_t *hi, uint32_t *lo) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    hi[i] = (uint32_t)(keys[i] >> 32);
+    lo[i] = (uint32_t)keys[i];
+  }
+}
+void launch_unpack_pairs(const uint64_t *keys, uint64_t n, uint32_t *hi, uint32_t *lo, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_unpack_pairs, dim3(nblocks(n, 256)), dim3(256), 0, s, keys, n, hi, lo);
+  KCHECK("k_unpack_pairs");
+}
+
+__global__ void k_flag_not_in(const uint64_t *sorted, uint64_t ns, const uint64_t *keys, uint64_t n, uint8_t *flags) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = keys[i];
+  uint64_t lo = 0, hi = ns;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (sorted[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  flags[i] = !(lo < ns && sorted[lo] == k);
+}
+void launch_flag_not_in(const uint64_t *sorted, uint64_t ns, const uint64_t *keys, uint64_t n, uint8_t *flags,
+                        hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_flag_not_in, dim3(nblocks(n, 256)), dim3(256), 0, s, sorted, ns, keys, n, flags);
+  KCHECK("k_flag_not_in");
+}
+
+__global__ void k_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicOr((unsigned long long *)&bm[v[i] >> 6], 1ull << (v[i] & 63));
+}
+void launch_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_mark_bitmap, dim3(nblocks(n, 256)), dim3(256), 0, s, v, n, bm);
+  KCHECK("k_mark_bitmap");
+}
+
+__global__ void k_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = src[idx[i]];
+}
+void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_gather_u32, dim3(nblocks(n, 256)), dim3(256), 0, s, src, idx, n, out);
+  KCHECK("k_gather_u32");
+}
+
+__global__ void k_flag_row_change(int ncols, ColPtrs cp, uint64_t n, uint8_t *flags) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool change = i == 0;
+  for (int c = 0; c < ncols && !change; ++c) change = cp.in[c][i] != cp.in[c][i - 1];
+  flags[i] = change;
+}
+void launch_flag_row_change(int ncols, const uint32_t *const *cols, uint64_t n, uint8_t *flags, hipStream_t s) {
+  if (!n) return;
+  ColPtrs cp;
+  for (int c = 0; c < ncols; ++c) cp.in[c] = cols[c];
+  hipLaunchKernelGGL(k_flag_row_change, dim3(nblocks(n, 256)), dim3(256), 0, s, ncols, cp, n, flags);
+  KCHECK("k_flag_row_change");
+}
+
+__global__ void k_map_rids(int ncols, ColPtrs cp, uint64_t n, const uint64_t *rids, uint64_t *out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int c = 0; c < ncols; ++c) {
+    uint32_t v = cp.in[c][i];
+    out[i * ncols + c] = rids ? rids[v] : (uint64_t)v;
+  }
+}
+void launch_map_rids(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, uint64_t *out,
+                     hipStream_t s) {
+  if (!n || !ncols) return;
+  ColPtrs cp;
+  for (int c = 0; c < ncols; ++c) cp.in[c] = cols[c];
+  hipLaunchKernelGGL(k_map_rids, dim3(nblocks(n, 256)), dim3(256), 0, s, ncols, cp, n, rids, out);
+  KCHECK("k_map_rids");
+}
+
+}  // namespace omx

@@ -1,0 +1,834 @@
+// plan.cpp — restates the reference's MATCH planning and compiles it to device steps.
+//
+//   parse-time      OMatchStatement.parse (P/OMatchStatement.java:129-178): assignDefaultAliases
+//                   :202-218, Pattern.addExpression (P/Pattern.java:15-27), addAliases :905-948,
+//                   rebindFilters :185-195, Pattern.validate (P/Pattern.java:48-65)
+//   estimates       estimateRootEntries :874-903, OWhereClause.estimate (P/OWhereClause.java:57-95)
+//   edge order      sortEdges :272-325 (stable sort of OPair by estimate, CM/util/OPair.java:97-99)
+//   candidates      calculateMatch :334-386 (prefetch below threshold 20, getNextAlias :858-872)
+//   per-edge rules  processContext :412-568 — forward: OMatchPathItem.executeTraversal applies the
+//                   target's WHERE (P/OMatchPathItem.java:49-107); reverse: executeReverse, WHERE only
+//                   in the free branch (:553-554); bound target → existence (:468-477); prefetched
+//                   target → candidate membership (:478-490), free → bind (:491-497)
+//   cartesian       expandCartesianProduct :620-650
+//   projection      addResult :661-729 ($elements, $pathElements, $patterns/$matches, $paths, aliases)
+#include "plan.h"
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <optional>
+#include <set>
+#include <sstream>
+
+namespace omx {
+
+const Value *Params::get(const Expr &p) const {
+  if (!p.name.empty()) {
+    for (auto &kv : named)
+      if (kv.first == p.name) return &kv.second;
+    return nullptr;
+  }
+  if (p.param_index >= 0 && (size_t)p.param_index < positional.size()) return &positional[p.param_index];
+  return nullptr;
+}
+
+namespace {
+
+const std::string kDefaultPrefix = "$ORIENT_DEFAULT_ALIAS_";
+const int64_t kThreshold = 20;  // OMatchStatement.threshold (:35)
+const int64_t kLongMax = INT64_MAX;
+
+struct PNode {
+  std::string alias;
+  std::vector<int> out, in;  // edge indices, insertion order (LinkedHashSet)
+  bool optional = false;
+};
+struct PEdge {
+  const PathItem *item;
+  int out, in;
+};
+
+bool is_num(const Value &v) { return v.kind == Value::INT || v.kind == Value::DBL; }
+double as_dbl(const Value &v) { return v.kind == Value::DBL ? v.d : (double)v.i; }
+
+// OQueryOperatorEquals.equals (S/operator/OQueryOperatorEquals.java:67-97) on constants.
+bool const_equals(const Value &a, const Value &b) {
+  if (a.kind == Value::NUL || b.kind == Value::NUL) return false;
+  if (is_num(a) && is_num(b)) {
+    if (a.kind == Value::INT && b.kind == Value::INT) return a.i == b.i;
+    return as_dbl(a) == as_dbl(b);
+  }
+  if (a.kind == Value::STR && b.kind == Value::STR) return a.s == b.s;
+  if (a.kind == Value::BOOL && b.kind == Value::BOOL) return a.i == b.i;
+  if (a.kind == Value::STR && is_num(b)) return a.s == (b.kind == Value::INT ? std::to_string(b.i) : std::to_string(b.d));
+  if (is_num(a) && b.kind == Value::STR) {
+    char *end = nullptr;
+    double x = std::strtod(b.s.c_str(), &end);
+    return end && *end == 0 && !b.s.empty() && x == as_dbl(a);
+  }
+  return false;
+}
+
+class Planner {
+ public:
+  Planner(const Statement &st, const Graph &g, const Params &params) : st_(st), g_(g), params_(params) {}
+
+  std::unique_ptr<Plan> run(bool logical_only) {
+    plan_ = std::make_unique<Plan>();
+    exprs_ = st_.expressions;  // private copy: default aliases / rebound filters are assigned here
+    assign_default_aliases();
+    for (auto &e : exprs_) add_expression(e);
+    for (auto &e : exprs_) {
+      add_aliases(e.origin);
+      for (auto &it : e.items) add_aliases(it.filter);
+    }
+    validate();
+    for (auto &n : nodes_) {
+      plan_->aliases.push_back(n.alias);
+      plan_->explicit_alias.push_back(n.alias.rfind(kDefaultPrefix, 0) != 0);
+    }
+    estimate_root_entries();
+    for (auto &kv : plan_->estimates)
+      if (kv.second == 0) plan_->empty = true;
+    sort_edges();
+    choose_prefetch_and_root();
+    if (logical_only) return std::move(plan_);
+    compile_steps();
+    compile_projection();
+    plan_->limit = st_.has_limit ? st_.limit : -1;
+    return std::move(plan_);
+  }
+
+ private:
+  const Statement &st_;
+  const Graph &g_;
+  const Params &params_;
+  std::unique_ptr<Plan> plan_;
+  std::vector<MatchExpression> exprs_;
+  std::vector<PNode> nodes_;
+  std::map<std::string, int> alias_idx_;
+  std::vector<PEdge> edges_;
+  std::vector<std::string> class_order_, filter_order_;  // LinkedHashMap insertion orders
+  std::map<std::string, std::string> alias_class_;
+  std::map<std::string, std::vector<ExprP>> alias_where_;
+  std::vector<std::pair<int, bool>> sorted_;  // (edge index, forward)
+  std::set<int> prefetched_;
+  int root_ = -1;
+
+  // ---- parse-time -------------------------------------------------------------------------------
+  void assign_default_aliases() {
+    int counter = 0;
+    for (auto &e : exprs_) {
+      if (e.origin.alias.empty()) e.origin.alias = kDefaultPrefix + std::to_string(counter++);
+      for (auto &it : e.items)
+        if (it.filter.alias.empty()) it.filter.alias = kDefaultPrefix + std::to_string(counter++);
+    }
+  }
+  int node(const MatchFilter &f) {
+    auto it = alias_idx_.find(f.alias);
+    int id;
+    if (it == alias_idx_.end()) {
+      id = (int)nodes_.size();
+      nodes_.push_back(PNode{f.alias});
+      alias_idx_[f.alias] = id;
+    } else {
+      id = it->second;
+    }
+    if (f.optional) nodes_[id].optional = true;
+    return id;
+  }
+  void add_expression(const MatchExpression &e) {
+    int origin = node(e.origin);
+    for (auto &it : e.items) {
+      int nxt = node(it.filter);
+      edges_.push_back(PEdge{&it, origin, nxt});
+      nodes_[origin].out.push_back((int)edges_.size() - 1);
+      nodes_[nxt].in.push_back((int)edges_.size() - 1);
+      origin = nxt;
+    }
+  }
+  void add_aliases(const MatchFilter &f) {
+    if (f.where) {
+      if (!alias_where_.count(f.alias)) filter_order_.push_back(f.alias);
+      alias_where_[f.alias].push_back(f.where);
+    }
+    if (!f.class_name.empty()) {
+      auto it = alias_class_.find(f.alias);
+      if (it == alias_class_.end()) {
+        alias_class_[f.alias] = f.class_name;
+        class_order_.push_back(f.alias);
+      } else {
+        int a = g_.class_id(f.class_name), b = g_.class_id(it->second);
+        if (a < 0 || b < 0) fail(OMX_E_EXECUTION, "class not defined: " + (a < 0 ? f.class_name : it->second));
+        if (g_.is_subclass_of(a, b)) it->second = f.class_name;
+        else if (!g_.is_subclass_of(b, a))
+          fail(OMX_E_EXECUTION, "classes defined for alias " + f.alias + " (" + f.class_name + ", " + it->second +
+                                    ") are not in the same hierarchy");
+      }
+    }
+  }
+  void validate() {
+    for (auto &n : nodes_)
+      if (n.optional) {
+        if (!n.out.empty())
+          fail(OMX_E_PARSE, "In current MATCH version, optional nodes are allowed only on right terminal nodes");
+        if (n.in.empty()) fail(OMX_E_PARSE, "In current MATCH version, optional nodes must have at least one incoming pattern edge");
+      }
+  }
+  ExprP where_of(const std::string &alias) const {
+    auto it = alias_where_.find(alias);
+    if (it == alias_where_.end()) return nullptr;
+    auto a = std::make_shared<Expr>();
+    a->kind = Expr::AND;
+    a->kids = it->second;
+    return a;
+  }
+
+  // ---- estimates -------------------------------------------------------------------------------
+  std::optional<Value> fold(const ExprP &e) const {
+    if (!e) return std::nullopt;
+    switch (e->kind) {
+      case Expr::LIT: return e->value;
+      case Expr::PARAM: {
+        const Value *v = params_.get(*e);
+        if (!v) fail(OMX_E_EXECUTION, "missing value for query parameter " + expr_text(e));
+        return *v;
+      }
+      case Expr::MATH: {
+        auto a = fold(e->kids[0]), b = fold(e->kids[1]);
+        if (!a || !b) return std::nullopt;
+        if (e->name == "+" && (a->kind == Value::STR || b->kind == Value::STR)) {
+          auto str = [](const Value &v) {
+            return v.kind == Value::STR ? v.s : v.kind == Value::INT ? std::to_string(v.i)
+                                                : v.kind == Value::NUL ? std::string() : std::to_string(v.d);
+          };
+          return Value::Str(str(*a) + str(*b));
+        }
+        if (!is_num(*a) || !is_num(*b)) return Value();
+        if (a->kind == Value::INT && b->kind == Value::INT) {
+          int64_t x = a->i, y = b->i;
+          if (e->name == "+") return Value::Int(x + y);
+          if (e->name == "-") return Value::Int(x - y);
+          if (e->name == "*") return Value::Int(x * y);
+          if (y == 0) unsupported("integer division by zero in a constant expression");
+          if (e->name == "/") return Value::Int(x / y);
+          return Value::Int(x % y);
+        }
+        double x = as_dbl(*a), y = as_dbl(*b);
+        if (e->name == "+") return Value::Dbl(x + y);
+        if (e->name == "-") return Value::Dbl(x - y);
+        if (e->name == "*") return Value::Dbl(x * y);
+        if (e->name == "/") return Value::Dbl(x / y);
+        return Value::Dbl(std::fmod(x, y));
+      }
+      case Expr::CMP: {
+        auto a = fold(e->kids[0]), b = fold(e->kids[1]);
+        if (!a || !b) return std::nullopt;
+        const std::string &op = e->name;
+        if (op == "=") return Value::Bool(const_equals(*a, *b));
+        if (op == "!=") return Value::Bool(!const_equals(*a, *b));
+        if (a->kind == Value::NUL) {
+          if (op == "<") return Value::Bool(false);
+          unsupported("comparison with a null left operand (NullPointerException in the reference)");
+        }
+        if (b->kind == Value::NUL) return Value::Bool(false);
+        int c;
+        if (is_num(*a) && is_num(*b)) {
+          if (a->kind == Value::INT && b->kind == Value::INT) c = a->i < b->i ? -1 : a->i > b->i;
+          else c = as_dbl(*a) < as_dbl(*b) ? -1 : as_dbl(*a) > as_dbl(*b);
+        } else if (a->kind == Value::STR && b->kind == Value::STR) {
+          c = a->s < b->s ? -1 : a->s > b->s;
+        } else {
+          unsupported("comparison of constants of different types");
+        }
+        if (op == "<") return Value::Bool(c < 0);
+        if (op == "<=") return Value::Bool(c <= 0);
+        if (op == ">") return Value::Bool(c > 0);
+        return Value::Bool(c >= 0);
+      }
+      case Expr::AND:
+      case Expr::OR: {
+        bool all = true, any = false;
+        for (auto &k : e->kids) {
+          auto v = fold(k);
+          if (!v) return std::nullopt;
+          bool b = v->kind == Value::BOOL && v->i;
+          all = all && b;
+          any = any || b;
+        }
+        return Value::Bool(e->kind == Expr::AND ? all : any);
+      }
+      case Expr::NOT: {
+        auto v = fold(e->kids[0]);
+        if (!v) return std::nullopt;
+        return Value::Bool(!(v->kind == Value::BOOL && v->i));
+      }
+      case Expr::TRUTH: {
+        auto v = fold(e->kids[0]);
+        if (!v) return std::nullopt;
+        return Value::Bool(v->kind == Value::BOOL && v->i);
+      }
+      default: return std::nullopt;
+    }
+  }
+
+  // OBooleanExpression.flatten: disjunctive normal form as a list of AND blocks.
+  std::vector<std::vector<ExprP>> flatten(const ExprP &e) const {
+    if (e->kind == Expr::OR) {
+      std::vector<std::vector<ExprP>> out;
+      for (auto &k : e->kids) {
+        auto f = flatten(k);
+        out.insert(out.end(), f.begin(), f.end());
+      }
+      return out;
+    }
+    if (e->kind == Expr::AND) {
+      std::vector<std::vector<ExprP>> blocks{{}};
+      for (auto &k : e->kids) {
+        auto f = flatten(k);
+        std::vector<std::vector<ExprP>> nb;
+        for (auto &b : blocks)
+          for (auto &x : f) {
+            auto y = b;
+            y.insert(y.end(), x.begin(), x.end());
+            nb.push_back(y);
+          }
+        blocks.swap(nb);
+      }
+      return blocks;
+    }
+    return {{e}};
+  }
+
+  int64_t estimate(int cls, const ExprP &where) const {
+    int64_t count = (int64_t)g_.count(cls);
+    if (count > 1) count /= 2;
+    if (count < kThreshold) return count;
+    int64_t indexes_count = 0;
+    for (auto &block : flatten(where)) {
+      std::vector<std::pair<std::string, Value>> conds;  // getEqualityOperations (P/OWhereClause.java:222-236)
+      for (auto &b : block)
+        if (b->kind == Expr::CMP && b->name == "=" && b->kids[0]->kind == Expr::FIELD &&
+            (b->kids[1]->kind == Expr::LIT || b->kids[1]->kind == Expr::PARAM))
+          conds.emplace_back(b->kids[0]->name, *fold(b->kids[1]));
+      int64_t est = kLongMax;
+      for (auto &ix : g_.indexes) {
+        if (!g_.is_subclass_of(cls, ix.cls)) continue;
+        const Value *key = nullptr;
+        for (auto &c : conds)
+          if (c.first == g_.props[ix.prop].name) key = &c.second;
+        if (!key) continue;
+        int64_t hits = g_.index_hits(ix.cls, ix.prop, *key);
+        int64_t n = ix.unique ? (hits > 0 ? 1 : kLongMax) : hits;
+        if (n < est) est = n;
+      }
+      if (est > count) return count;
+      indexes_count += est;
+    }
+    return std::min(indexes_count, count);
+  }
+
+  void estimate_root_entries() {
+    std::vector<std::string> all = class_order_;
+    for (auto &a : filter_order_)
+      if (std::find(all.begin(), all.end(), a) == all.end()) all.push_back(a);
+    for (auto &alias : all) {
+      auto it = alias_class_.find(alias);
+      if (it == alias_class_.end()) continue;
+      int c = g_.class_id(it->second);
+      if (c < 0) fail(OMX_E_EXECUTION, "class not defined: " + it->second);
+      ExprP w = where_of(alias);
+      plan_->estimates.emplace_back(alias, w ? estimate(c, w) : (int64_t)g_.count(c));
+    }
+  }
+
+  void sort_edges() {
+    std::vector<std::pair<int64_t, std::string>> weights;
+    for (auto &kv : plan_->estimates) weights.emplace_back(kv.second, kv.first);
+    std::stable_sort(weights.begin(), weights.end(),
+                     [](const std::pair<int64_t, std::string> &a, const std::pair<int64_t, std::string> &b) {
+                       return a.first < b.first;
+                     });
+    std::set<int> tedges, tnodes;
+    std::vector<int> next;
+    auto in_next = [&](int n) { return std::find(next.begin(), next.end(), n) != next.end(); };
+    while (sorted_.size() < edges_.size()) {
+      for (auto &w : weights) {
+        int root = alias_idx_.at(w.second);
+        if (nodes_[root].optional) continue;
+        if (!tnodes.count(root)) {
+          next.push_back(root);
+          break;
+        }
+      }
+      if (next.empty()) break;
+      while (!next.empty()) {
+        int n = next.front();
+        next.erase(next.begin());
+        tnodes.insert(n);
+        for (int e : nodes_[n].out)
+          if (!tedges.count(e)) {
+            sorted_.emplace_back(e, true);
+            tedges.insert(e);
+            if (!tnodes.count(edges_[e].in) && !in_next(edges_[e].in)) next.push_back(edges_[e].in);
+          }
+        for (int e : nodes_[n].in)
+          if (!tedges.count(e) && edges_[e].item->bidirectional()) {
+            sorted_.emplace_back(e, false);
+            tedges.insert(e);
+            if (!tnodes.count(edges_[e].out) && !in_next(edges_[e].out)) next.push_back(edges_[e].out);
+          }
+      }
+    }
+    for (auto &s : sorted_)
+      plan_->sorted_edges.emplace_back(nodes_[edges_[s.first].out].alias, nodes_[edges_[s.first].in].alias, s.second);
+  }
+
+  void choose_prefetch_and_root() {
+    bool found = false;
+    for (auto &kv : plan_->estimates)
+      if (kv.second < kThreshold) {
+        prefetched_.insert(alias_idx_.at(kv.first));
+        plan_->prefetched.push_back(kv.first);
+        found = true;
+      }
+    if (!found && !plan_->estimates.empty()) {  // getNextAlias (:858-872): first strict minimum
+      const std::pair<std::string, int64_t> *lo = nullptr;
+      for (auto &kv : plan_->estimates)
+        if (!lo || lo->second > kv.second) lo = &kv;
+      prefetched_.insert(alias_idx_.at(lo->first));
+      plan_->prefetched.push_back(lo->first);
+    }
+    if (!sorted_.empty()) {
+      const PEdge &e = edges_[sorted_[0].first];
+      root_ = sorted_[0].second ? e.out : e.in;
+    } else {
+      root_ = 0;
+    }
+    plan_->root = nodes_[root_].alias;
+  }
+
+  // ---- predicate compiler ----------------------------------------------------------------------
+  enum CT { C_NUL, C_INT, C_DBL, C_BOOL };
+  struct ProgBuilder {
+    PredProgram p;
+    int depth = 0, max_depth = 0;
+    void emit(int32_t op, int32_t arg = 0, int64_t i = 0, double d = 0, int dstack = 0) {
+      if (p.code.size() >= (size_t)kMaxPred) unsupported("predicate program too long for the device VM");
+      p.code.push_back(DPredInstr{op, arg, i, d});
+      depth += dstack;
+      max_depth = std::max(max_depth, depth);
+      if (max_depth > 16) unsupported("predicate expression too deep for the device VM");
+    }
+  };
+
+  static bool shadowed(const std::string &n) {
+    std::string l = lower(n);
+    return l == "depth" || l == "matched" || l == "currentmatch" || l == "current" || l == "parent" ||
+           l == "paths" || l == "patterns" || l == "matches" || l == "elements" || l == "pathelements";
+  }
+
+  CT push_const(ProgBuilder &b, const Value &v) {
+    switch (v.kind) {
+      case Value::NUL: b.emit(P_PUSH_NULL, 0, 0, 0, 1); return C_NUL;
+      case Value::INT: b.emit(P_PUSH_INT, 0, v.i, 0, 1); return C_INT;
+      case Value::DBL: b.emit(P_PUSH_DBL, 0, 0, v.d, 1); return C_DBL;
+      case Value::BOOL: b.emit(P_PUSH_BOOL, 0, v.i, 0, 1); return C_BOOL;
+      case Value::STR: unsupported("string value outside a comparison with a string property");
+    }
+    return C_NUL;
+  }
+
+  AdjSpec adjacency(const std::string &method_in, const std::vector<std::string> &labels_in) const {
+    std::string m = lower(method_in);
+    if (m == "oute") m = "out";
+    else if (m == "ine") m = "in";
+    else if (m == "bothe") m = "both";
+    if (m != "out" && m != "in" && m != "both") unsupported("traversal method " + method_in + "() on the device");
+    std::vector<std::string> labels = labels_in;
+    if (labels.size() == 1 && ieq(labels[0], "E")) labels.clear();  // OrientVertex.getFieldNames :1036-1038
+    // the set of edge classes (label + all subclasses; B/OrientVertex.java:1048-1060)
+    std::vector<int> classes;
+    if (labels.empty()) {
+      for (auto &es : g_.esets)
+        if (std::find(classes.begin(), classes.end(), es.cls) == classes.end()) classes.push_back(es.cls);
+    } else {
+      for (auto &l : labels) {
+        int c = g_.class_id(l);
+        if (c < 0) continue;  // no out_<label> field on any vertex
+        for (int s : g_.classes[c].poly)
+          if (std::find(classes.begin(), classes.end(), s) == classes.end()) classes.push_back(s);
+      }
+    }
+    AdjSpec a;
+    for (int c : classes)
+      for (size_t i = 0; i < g_.esets.size(); ++i) {
+        if (g_.esets[i].cls != c) continue;
+        if (m == "out" || m == "both") a.parts.emplace_back((int)i, 0);
+        if (m == "in" || m == "both") a.parts.emplace_back((int)i, 1);
+      }
+    if ((int)a.parts.size() > kMaxAdjParts) unsupported("too many edge classes in one traversal");
+    a.sorted = true;
+    for (auto &p : a.parts) a.sorted = a.sorted && (p.second == 0 ? g_.esets[p.first].out_sorted : g_.esets[p.first].in_sorted);
+    a.dup_free = a.parts.size() <= 1 &&
+                 (a.parts.empty() || (a.parts[0].second == 0 ? g_.esets[a.parts[0].first].out_simple
+                                                             : g_.esets[a.parts[0].first].in_simple));
+    return a;
+  }
+
+  CT compile_value(ProgBuilder &b, const ExprP &e, bool allow_depth) {
+    if (auto v = fold(e)) return push_const(b, *v);
+    switch (e->kind) {
+      case Expr::FIELD: {
+        if (shadowed(e->name)) unsupported("field name shadowed by a context variable: " + e->name);
+        if (e->name[0] == '@') unsupported("record attribute " + e->name + " in a device predicate");
+        int p = g_.prop_id(e->name);
+        if (p < 0) {  // no vertex has the field: always null
+          b.emit(P_PUSH_NULL, 0, 0, 0, 1);
+          return C_NUL;
+        }
+        int t = g_.props[p].type;
+        if (t == OMX_PROP_STRING) unsupported("string property " + e->name + " outside a comparison with a constant");
+        b.emit(P_PUSH_COL, p, 0, 0, 1);
+        return t == OMX_PROP_DOUBLE ? C_DBL : t == OMX_PROP_BOOL ? C_BOOL : C_INT;
+      }
+      case Expr::VAR: {
+        if (ieq(e->name, "$depth") && allow_depth) {
+          b.p.uses_depth = true;
+          b.emit(P_PUSH_DEPTH, 0, 0, 0, 1);
+          return C_INT;
+        }
+        unsupported("context variable " + e->name + " in a device predicate");
+      }
+      case Expr::MATH: {
+        CT l = compile_value(b, e->kids[0], allow_depth);
+        CT r = compile_value(b, e->kids[1], allow_depth);
+        if (l == C_BOOL || r == C_BOOL) unsupported("arithmetic on booleans");
+        int32_t op = e->name == "+" ? P_ADD : e->name == "-" ? P_SUB : e->name == "*" ? P_MUL : e->name == "/" ? P_DIV : P_MOD;
+        b.emit(op, 0, 0, 0, -1);
+        return (l == C_DBL || r == C_DBL) ? C_DBL : C_INT;
+      }
+      case Expr::CHAIN: {
+        // <out|in|both|outE|inE|bothE>('L', ...).size()  →  degree of the current vertex
+        const ExprP &base = e->kids[0];
+        if (base->kind == Expr::CALL && e->suffixes.size() == 1 && e->suffixes[0].kind == Suffix::METHOD &&
+            ieq(e->suffixes[0].name, "size") && e->suffixes[0].args.empty()) {
+          std::vector<std::string> labels;
+          for (auto &a : base->kids) {
+            auto v = fold(a);
+            if (!v || v->kind != Value::STR) unsupported("non-constant edge label");
+            labels.push_back(v->s);
+          }
+          AdjSpec adj = adjacency(base->name, labels);
+          if (b.p.deg.size() >= (size_t)kMaxDegAdj) unsupported("too many degree terms in one predicate");
+          b.p.deg.push_back(adj);
+          b.emit(P_PUSH_DEG, (int)b.p.deg.size() - 1, 0, 0, 1);
+          return C_INT;
+        }
+        unsupported("expression " + expr_text(e) + " in a device predicate");
+      }
+      default: unsupported("expression " + expr_text(e) + " in a device predicate");
+    }
+  }
+
+  static std::string flip(const std::string &op) {
+    if (op == "<") return ">";
+    if (op == ">") return "<";
+    if (op == "<=") return ">=";
+    if (op == ">=") return "<=";
+    return op;
+  }
+
+  bool string_field(const ExprP &e, int *prop) const {
+    if (e->kind != Expr::FIELD || shadowed(e->name)) return false;
+    int p = g_.prop_id(e->name);
+    if (p < 0 || g_.props[p].type != OMX_PROP_STRING) return false;
+    *prop = p;
+    return true;
+  }
+
+  // string property vs string constant → comparison of dictionary codes (the dictionary is sorted)
+  void emit_string_cmp(ProgBuilder &b, int prop, const std::string &op, const std::string &s) {
+    const auto &dict = g_.props[prop].dict;
+    int64_t lb = std::lower_bound(dict.begin(), dict.end(), s) - dict.begin();
+    bool found = (size_t)lb < dict.size() && dict[lb] == s;
+    int64_t ub = lb + (found ? 1 : 0);
+    if (op == "=" || op == "!=") {
+      if (!found) {
+        b.emit(P_PUSH_BOOL, 0, op == "!=", 0, 1);
+        return;
+      }
+      b.emit(P_PUSH_COL, prop, 0, 0, 1);
+      b.emit(P_PUSH_INT, 0, lb, 0, 1);
+      b.emit(op == "=" ? P_EQ : P_NE, 0, 0, 0, -1);
+      return;
+    }
+    b.emit(P_PUSH_COL, prop, 0, 0, 1);
+    if (op == "<") { b.emit(P_PUSH_INT, 0, lb, 0, 1); b.emit(P_LT, 0, 0, 0, -1); }
+    else if (op == "<=") { b.emit(P_PUSH_INT, 0, ub, 0, 1); b.emit(P_LT, 0, 0, 0, -1); }
+    else if (op == ">") { b.emit(P_PUSH_INT, 0, ub, 0, 1); b.emit(P_GE, 0, 0, 0, -1); }
+    else { b.emit(P_PUSH_INT, 0, lb, 0, 1); b.emit(P_GE, 0, 0, 0, -1); }
+  }
+
+  void compile_bool(ProgBuilder &b, const ExprP &e, bool allow_depth) {
+    if (auto v = fold(e)) {
+      b.emit(P_PUSH_BOOL, 0, v->kind == Value::BOOL && v->i, 0, 1);
+      return;
+    }
+    switch (e->kind) {
+      case Expr::OR:
+      case Expr::AND:
+        for (size_t i = 0; i < e->kids.size(); ++i) {
+          compile_bool(b, e->kids[i], allow_depth);
+          if (i) b.emit(e->kind == Expr::OR ? P_OR : P_AND, 0, 0, 0, -1);
+        }
+        return;
+      case Expr::NOT:
+        compile_bool(b, e->kids[0], allow_depth);
+        b.emit(P_NOT);
+        return;
+      case Expr::TRUTH: {
+        CT t = compile_value(b, e->kids[0], allow_depth);
+        if (t != C_BOOL) {  // only a boolean true is "true"
+          b.emit(P_PUSH_BOOL, 0, 0, 0, 1);
+          b.emit(P_AND, 0, 0, 0, -1);
+          return;
+        }
+        b.emit(P_TRUTH);
+        return;
+      }
+      case Expr::CMP: {
+        const ExprP &L = e->kids[0], &R = e->kids[1];
+        std::string op = e->name;
+        int prop;
+        auto fl = fold(L), fr = fold(R);
+        if (string_field(L, &prop) && fr && fr->kind == Value::STR) return emit_string_cmp(b, prop, op, fr->s);
+        if (string_field(R, &prop) && fl && fl->kind == Value::STR) return emit_string_cmp(b, prop, flip(op), fl->s);
+        if (fr && fr->kind == Value::NUL) {
+          b.emit(P_PUSH_BOOL, 0, op == "!=", 0, 1);
+          return;
+        }
+        if (fl && fl->kind == Value::NUL) {
+          if (op == "=" || op == "!=" || op == "<") {
+            b.emit(P_PUSH_BOOL, 0, op == "!=", 0, 1);
+            return;
+          }
+          unsupported("null left operand of " + op);
+        }
+        CT l = compile_value(b, L, allow_depth);
+        CT r = compile_value(b, R, allow_depth);
+        if ((l == C_BOOL) != (r == C_BOOL) && l != C_NUL && r != C_NUL)
+          unsupported("comparison of a boolean with a number");
+        if (l == C_BOOL && op != "=" && op != "!=") unsupported("ordering comparison of booleans");
+        int32_t code = op == "=" ? P_EQ : op == "!=" ? P_NE : op == "<" ? P_LT : op == "<=" ? P_LE : op == ">" ? P_GT : P_GE;
+        b.emit(code, 0, 0, 0, -1);
+        return;
+      }
+      default: unsupported("condition " + expr_text(e) + " in a device predicate");
+    }
+  }
+
+  int add_prog(const ExprP &e, bool allow_depth) {
+    if (!e) return -1;
+    ProgBuilder b;
+    compile_bool(b, e, allow_depth);
+    if (b.p.code.size() == 1 && b.p.code[0].op == P_PUSH_BOOL) {
+      if (b.p.code[0].i) return -1;  // statically true
+      b.p.const_false = true;
+    }
+    plan_->progs.push_back(b.p);
+    return (int)plan_->progs.size() - 1;
+  }
+
+  std::map<std::pair<std::string, int>, int> bm_cache_;  // (alias, kind) → bitmap
+  // kind 0: WHERE of the alias (traversal filter, $currentMatch = neighbour)
+  // kind 1: candidate set = polymorphic class ∧ WHERE (fetchAliasCandidates :401-410)
+  int bitmap(const std::string &alias, int kind) {
+    auto key = std::make_pair(alias, kind);
+    auto it = bm_cache_.find(key);
+    if (it != bm_cache_.end()) return it->second;
+    BitmapSpec s;
+    s.prog = add_prog(where_of(alias), false);
+    if (kind == 1) {
+      auto c = alias_class_.find(alias);
+      if (c == alias_class_.end()) fail(OMX_E_EXECUTION, "Cannot execute MATCH statement on alias " + alias + ": class not defined");
+      s.class_id = g_.class_id(c->second);
+    }
+    int id = -1;
+    if (s.prog >= 0 || s.class_id >= 0) {
+      plan_->bitmaps.push_back(s);
+      id = (int)plan_->bitmaps.size() - 1;
+    }
+    bm_cache_[key] = id;
+    return id;
+  }
+
+  // ---- steps -----------------------------------------------------------------------------------
+  void compile_steps() {
+    for (auto &n : nodes_)
+      if (n.optional) unsupported("optional pattern nodes");
+    for (auto &e : edges_)
+      if (e.item->is_multi) unsupported("multi-step path items .( ... )");
+    // candidate sets that must be non-empty (calculateMatch :340-357, :359-367)
+    for (int a : prefetched_) plan_->must_be_nonempty.push_back(bitmap(nodes_[a].alias, 1));
+    if (!prefetched_.count(root_))
+      fail(OMX_E_EXECUTION, "NullPointerException: no candidates for root alias " + nodes_[root_].alias);
+
+    std::vector<bool> bound(nodes_.size(), false);
+    Step r;
+    r.kind = S_ROOT;
+    r.dst = root_;
+    r.cand_bm = bitmap(nodes_[root_].alias, 1);
+    r.desc = "root " + nodes_[root_].alias;
+    plan_->steps.push_back(r);
+    bound[root_] = true;
+    for (auto &se : sorted_) {
+      const PEdge &pe = edges_[se.first];
+      bool fwd = se.second;
+      const PathItem &it = *pe.item;
+      int s = fwd ? pe.out : pe.in, t = fwd ? pe.in : pe.out;
+      if (!bound[s]) {
+        if (fwd && prefetched_.count(s)) {  // restart from candidates (:434-445)
+          Step n;
+          n.kind = S_NEWROOT;
+          n.dst = s;
+          n.cand_bm = bitmap(nodes_[s].alias, 1);
+          n.desc = "new component root " + nodes_[s].alias;
+          plan_->steps.push_back(n);
+          bound[s] = true;
+        } else {
+          Step k;
+          k.kind = S_KILL;
+          k.desc = "unbound start " + nodes_[s].alias + " without candidates: no results";
+          plan_->steps.push_back(k);
+          return;
+        }
+      }
+      Step st;
+      st.src = s;
+      st.dst = t;
+      st.mode = bound[t] ? T_BOUND : prefetched_.count(t) ? T_CAND : T_FREE;
+      bool varlen = it.filter.while_ || it.filter.has_max_depth;
+      std::string m = lower(it.method);
+      if (m != "out" && m != "in" && m != "both") unsupported("traversal method " + it.method + "() on the device");
+      if (varlen) {
+        st.kind = S_VARLEN;
+        st.adj = adjacency(m, it.labels);
+        st.where_prog = add_prog(where_of(nodes_[t].alias), true);
+        st.while_prog = add_prog(it.filter.while_, true);
+        st.has_max_depth = it.filter.has_max_depth;
+        st.max_depth = it.filter.max_depth;
+        if (st.mode == T_CAND) st.cand_bm = bitmap(nodes_[t].alias, 1);
+      } else {
+        std::string rm = fwd ? m : (m == "out" ? "in" : m == "in" ? "out" : "both");  // executeReverse
+        st.adj = adjacency(rm, it.labels);
+        if (st.mode == T_BOUND) {
+          st.kind = S_CHECK;
+          st.filter_bm = fwd ? bitmap(nodes_[t].alias, 0) : -1;
+        } else {
+          st.kind = S_EXPAND;
+          st.filter_bm = st.mode == T_CAND ? bitmap(nodes_[t].alias, 1) : bitmap(nodes_[t].alias, 0);
+        }
+      }
+      st.desc = std::string(st.kind == S_VARLEN ? "varlen " : st.kind == S_CHECK ? "check " : "expand ") +
+                nodes_[s].alias + (fwd ? " -" : " <-") + it.method + "- " + nodes_[t].alias +
+                (st.mode == T_BOUND ? " [bound]" : st.mode == T_CAND ? " [candidates]" : " [free]");
+      plan_->steps.push_back(st);
+      bound[t] = true;
+    }
+    for (size_t a = 0; a < nodes_.size(); ++a)
+      if (!bound[a]) {  // expandCartesianProduct (:620-650)
+        Step c;
+        c.kind = S_CARTESIAN;
+        c.dst = (int)a;
+        c.cand_bm = bitmap(nodes_[a].alias, 1);
+        c.desc = "cartesian " + nodes_[a].alias;
+        plan_->steps.push_back(c);
+        bound[a] = true;
+      }
+  }
+
+  void compile_projection() {
+    auto has = [&](const char *name) {
+      for (auto &r : st_.returns)
+        if (ieq(r.text, name)) return true;
+      return false;
+    };
+    Plan &p = *plan_;
+    if (has("$elements") || has("$pathElements")) {
+      p.proj = Plan::PROJ_ELEMENTS;
+      bool all = has("$elements") ? false : true;
+      for (size_t a = 0; a < nodes_.size(); ++a)
+        if (all || p.explicit_alias[a]) p.out_aliases.push_back((int)a);
+      p.out_names.push_back(all ? "$pathElements" : "$elements");
+    } else if (has("$patterns") || has("$matches") || has("$paths")) {
+      bool all = !(has("$patterns") || has("$matches"));
+      for (size_t a = 0; a < nodes_.size(); ++a)
+        if (all || p.explicit_alias[a]) {
+          p.out_aliases.push_back((int)a);
+          p.out_names.push_back(nodes_[a].alias);
+        }
+    } else {
+      for (auto &r : st_.returns) {
+        if (r.expr->kind != Expr::FIELD || !alias_idx_.count(r.expr->name))
+          unsupported("RETURN item " + r.text + " (only aliases, $matches, $patterns, $paths, $elements, $pathElements)");
+        p.out_aliases.push_back(alias_idx_.at(r.expr->name));
+        p.out_names.push_back(r.alias.empty() ? r.expr->name : r.alias);
+      }
+    }
+    bool dup_free = true;
+    for (auto &s : p.steps)
+      if (s.kind == S_EXPAND && !s.adj.dup_free) dup_free = false;
+    std::set<int> cover(p.out_aliases.begin(), p.out_aliases.end());
+    p.unique_by_construction = p.proj == Plan::PROJ_ALIASES && dup_free && cover.size() == nodes_.size() &&
+                               p.out_aliases.size() == nodes_.size();
+  }
+};
+
+std::string jstr(const std::string &s) {
+  std::string o = "\"";
+  for (char c : s) {
+    if (c == '"' || c == '\\') o += '\\';
+    o += c;
+  }
+  return o + "\"";
+}
+
+}  // namespace
+
+std::unique_ptr<Plan> build_plan(const Statement &st, const Graph &g, const Params &params, bool logical_only,
+                                 std::string *reason) {
+  if (!logical_only) return Planner(st, g, params).run(false);
+  auto p = Planner(st, g, params).run(true);
+  if (reason) {
+    try {
+      Planner(st, g, params).run(false);
+      reason->clear();
+    } catch (const OmxError &e) {
+      if (e.code != OMX_E_UNSUPPORTED) throw;
+      *reason = e.what();
+    }
+  }
+  return p;
+}
+
+std::string plan_json(const Plan &p, const std::string &reason) {
+  std::ostringstream o;
+  o << "{\"aliases\":[";
+  for (size_t i = 0; i < p.aliases.size(); ++i) o << (i ? "," : "") << jstr(p.aliases[i]);
+  o << "],\"estimates\":{";
+  for (size_t i = 0; i < p.estimates.size(); ++i)
+    o << (i ? "," : "") << jstr(p.estimates[i].first) << ":" << p.estimates[i].second;
+  o << "},\"prefetched\":[";
+  for (size_t i = 0; i < p.prefetched.size(); ++i) o << (i ? "," : "") << jstr(p.prefetched[i]);
+  o << "],\"root\":" << jstr(p.root) << ",\"edges\":[";
+  for (size_t i = 0; i < p.sorted_edges.size(); ++i)
+    o << (i ? "," : "") << "[" << jstr(std::get<0>(p.sorted_edges[i])) << "," << jstr(std::get<1>(p.sorted_edges[i]))
+      << "," << (std::get<2>(p.sorted_edges[i]) ? "true" : "false") << "]";
+  o << "],\"empty\":" << (p.empty ? "true" : "false");
+  o << ",\"supported\":" << (reason.empty() ? "true" : "false") << ",\"unsupported_reason\":" << jstr(reason) << "}";
+  return o.str();
+}
+
+}  // namespace omx

@@ -1,0 +1,86 @@
+// plan.h — logical MATCH plan (the reference's planner) and its compilation to device steps.
+#pragma once
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "devtypes.h"
+#include "graph.h"
+#include "sql.h"
+
+namespace omx {
+
+// Parameters of OCommandSQL.execute(args): positional or named.
+struct Params {
+  std::vector<Value> positional;
+  std::vector<std::pair<std::string, Value>> named;
+  const Value *get(const Expr &p) const;
+};
+
+// Neighbour list of a traversal: concatenation of (edge set, direction) parts.
+struct AdjSpec {
+  std::vector<std::pair<int, int>> parts;  // (edge set index, 0 = out CSR, 1 = in CSR)
+  bool dup_free = false;                   // neighbours of a vertex are distinct
+  bool sorted = true;                      // every part's rows sorted
+};
+
+struct PredProgram {
+  std::vector<DPredInstr> code;  // empty = always true
+  std::vector<AdjSpec> deg;      // adjacency referenced by P_PUSH_DEG
+  bool uses_depth = false;
+  bool const_false = false;      // statically false (e.g. name = 'absent')
+};
+
+struct BitmapSpec {
+  int prog = -1;      // predicate (-1 = none)
+  int class_id = -1;  // polymorphic class test (-1 = none)
+};
+
+enum StepKind { S_ROOT, S_EXPAND, S_CHECK, S_VARLEN, S_NEWROOT, S_CARTESIAN, S_KILL };
+enum TargetMode { T_FREE, T_CAND, T_BOUND };
+
+struct Step {
+  StepKind kind = S_EXPAND;
+  TargetMode mode = T_FREE;
+  int src = -1, dst = -1;  // alias indices (binding-table columns)
+  AdjSpec adj;
+  int filter_bm = -1;      // bitmap applied to a FREE/CAND target, or to the bound target of a forward S_CHECK
+  int cand_bm = -1;        // candidate bitmap (S_ROOT, S_NEWROOT, S_CARTESIAN, S_VARLEN in CAND mode)
+  int where_prog = -1, while_prog = -1;  // S_VARLEN
+  bool has_max_depth = false;
+  int max_depth = 0;
+  std::string desc;
+};
+
+struct Plan {
+  // logical plan (what the reference computes; also reported by omx_statement_explain)
+  std::vector<std::string> aliases;  // pattern nodes, insertion order (Pattern.aliasToNode)
+  std::vector<bool> explicit_alias;
+  std::vector<std::pair<std::string, int64_t>> estimates;  // estimateRootEntries order
+  std::vector<std::string> prefetched;
+  std::string root;
+  std::vector<std::tuple<std::string, std::string, bool>> sorted_edges;  // (out alias, in alias, forward)
+  bool empty = false;  // some estimate is 0 → empty result (OMatchStatement.java:249-251)
+
+  // physical plan
+  std::vector<PredProgram> progs;
+  std::vector<BitmapSpec> bitmaps;
+  std::vector<int> must_be_nonempty;  // candidate bitmaps of prefetched aliases (calculateMatch :340-357)
+  std::vector<Step> steps;
+  enum Projection { PROJ_ALIASES, PROJ_ELEMENTS } proj = PROJ_ALIASES;
+  std::vector<int> out_aliases;
+  std::vector<std::string> out_names;
+  bool unique_by_construction = false;
+  int64_t limit = -1;  // LIMIT clause (-1 = none)
+};
+
+// Builds the plan. Throws OmxError(OMX_E_UNSUPPORTED) when the statement is valid MATCH but outside
+// what the device engine executes (the host then falls back to the reference OMatchStatement);
+// `logical_only` stops after the reference's planning steps (used by explain).
+std::unique_ptr<Plan> build_plan(const Statement &st, const Graph &g, const Params &params, bool logical_only,
+                                 std::string *unsupported_reason = nullptr);
+
+std::string plan_json(const Plan &p, const std::string &unsupported_reason);
+
+}  // namespace omx

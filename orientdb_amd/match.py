@@ -1,0 +1,230 @@
+"""Host mirror of the reference's MATCH command interface, executed on the MI355X.
+
+Reference interface (OrientDB 2.2.8):
+  db.command(new OCommandSQL("MATCH ...")).execute(args...)            → List<ODocument>
+      ODatabaseDocumentTx.command  core/.../db/document/ODatabaseDocumentTx.java:702-714
+  OMatchStatement.parse / execute / setLimit
+      core/.../sql/parser/OMatchStatement.java:129-178, :231-267, :968-971
+  OResultSet (OConcurrentResultSet)  core/.../sql/query/OResultSet.java:33
+
+Here: GraphDatabase(snapshot).command(OCommandSQL("MATCH ...")).execute(*args) → OResultSet of
+ODocument (alias → ORecordId), or of ORecordId for $elements/$pathElements. Errors keep the
+reference's split: OmxParseError ≈ OCommandSQLParsingException, OmxExecutionError ≈
+OCommandExecutionException, OmxUnsupported = "not executable by the device engine" (the Java
+strategy falls back to OMatchStatement).
+"""
+import ctypes as C
+import json
+
+import numpy as np
+
+from . import _native as N
+from .graph import unpack_rid
+
+
+class ORecordId(tuple):
+    """#cluster:position (C/id/ORecordId.java)."""
+
+    def __new__(cls, cluster, position):
+        return super().__new__(cls, (int(cluster), int(position)))
+
+    @classmethod
+    def from_packed(cls, r):
+        return cls(*unpack_rid(r))
+
+    @property
+    def cluster(self):
+        return self[0]
+
+    @property
+    def position(self):
+        return self[1]
+
+    def packed(self):
+        return (self[0] << 48) | self[1]
+
+    def __repr__(self):
+        return "#%d:%d" % self
+
+
+class ODocument(dict):
+    def field(self, name):
+        return self.get(name)
+
+    def fieldNames(self):
+        return list(self.keys())
+
+
+class OResultSet(list):
+    """Distinct result rows + execution statistics (edges traversed, bindings, timings)."""
+    info = None
+    kernel_stats = None
+    columns = None
+    rows = None  # numpy u64 [n, k] of packed RIDs
+
+
+def _values(args, named):
+    vals = []
+    for i, a in enumerate(args):
+        vals.append(_value(a, index=i))
+    for k, a in (named or {}).items():
+        vals.append(_value(a, name=k))
+    arr = (N.omx_value * max(1, len(vals)))(*vals)
+    return arr, len(vals)
+
+
+def _value(a, index=0, name=None):
+    v = N.omx_value()
+    v.index = index
+    v.name = name.encode() if name else None
+    if a is None:
+        v.type = N.OMX_VAL_NULL
+    elif isinstance(a, bool):
+        v.type, v.i = N.OMX_VAL_BOOL, int(a)
+    elif isinstance(a, (int, np.integer)):
+        v.type, v.i = N.OMX_VAL_INT, int(a)
+    elif isinstance(a, (float, np.floating)):
+        v.type, v.d = N.OMX_VAL_DOUBLE, float(a)
+    else:
+        v.type, v.s = N.OMX_VAL_STRING, str(a).encode()
+    return v
+
+
+class OMatchStatement:
+    """OMatchStatement (P/OMatchStatement.java:29) as a drop-in execution strategy."""
+
+    KEYWORD_MATCH = "MATCH"
+
+    def __init__(self, text=None):
+        self._h = None
+        self._limit = -1
+        self.text = None
+        if text is not None:
+            self.parse(text)
+
+    def parse(self, request):
+        text = request.text if isinstance(request, OCommandSQL) else str(request)
+        h = C.c_void_p()
+        N.check(N.lib().omx_statement_parse(text.encode(), C.byref(h)))
+        self.free()
+        self._h = h
+        self.text = text
+        return self
+
+    def setLimit(self, n):
+        """limitFromProtocol (:968-971)."""
+        self._limit = int(n)
+        return self
+
+    def explain(self, graph, *args, **named):
+        arr, n = _values(args, named)
+        buf = C.create_string_buffer(1 << 16)
+        N.check(N.lib().omx_statement_explain(self._h, graph.handle, arr, n, buf, len(buf)))
+        return json.loads(buf.value.decode())
+
+    def execute(self, graph, *args, mode=N.OMX_MODE_MATERIALIZE, flags=0, shard=(0, 1), documents=True, **named):
+        arr, n = _values(args, named)
+        o = N.omx_exec_options()
+        N.lib().omx_exec_options_init(C.byref(o))
+        o.mode = mode
+        o.flags = flags
+        o.limit = self._limit
+        o.shard_rank, o.shard_world = shard
+        o.params = arr
+        o.n_params = n
+        r = C.c_void_p()
+        N.check(N.lib().omx_execute(graph.handle, self._h, C.byref(o), C.byref(r)))
+        try:
+            return self._collect(r, documents)
+        finally:
+            N.lib().omx_result_free(r)
+
+    @staticmethod
+    def _collect(r, documents):
+        L = N.lib()
+        info = N.omx_result_info()
+        N.check(L.omx_result_info_get(r, C.byref(info)))
+        rs = OResultSet()
+        rs.info = {f: getattr(info, f) for f, _ in N.omx_result_info._fields_}
+        cols = []
+        i = 0
+        while True:
+            nm = L.omx_result_column_name(r, i)
+            if nm is None:
+                break
+            cols.append(nm.decode())
+            i += 1
+        rs.columns = cols
+        stats = []
+        i = 0
+        while True:
+            name, launches, ms, by = C.c_char_p(), C.c_int64(), C.c_double(), C.c_uint64()
+            if L.omx_result_kernel_stat(r, i, C.byref(name), C.byref(launches), C.byref(ms), C.byref(by)) != 0:
+                break
+            stats.append({"name": name.value.decode(), "launches": launches.value, "ms": ms.value, "alg_bytes": by.value})
+            i += 1
+        rs.kernel_stats = stats
+        nrows, ncols = info.n_rows, info.n_cols
+        p = L.omx_result_rows(r)
+        if p and nrows and ncols:
+            rs.rows = np.ctypeslib.as_array(p, shape=(nrows * ncols,)).reshape(nrows, ncols).copy()
+        else:
+            rs.rows = np.zeros((0, max(ncols, 0)), np.uint64)
+        if documents and rs.rows.shape[0]:
+            if cols and cols[0] in ("$elements", "$pathElements"):
+                rs.extend(ORecordId.from_packed(x) for x in rs.rows[:, 0])
+            else:
+                for row in rs.rows:
+                    rs.append(ODocument((c, ORecordId.from_packed(x)) for c, x in zip(cols, row)))
+        return rs
+
+    def free(self):
+        if self._h is not None:
+            N.lib().omx_statement_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class OCommandSQL:
+    """OCommandSQL: the text of a command (core/.../sql/OCommandSQL.java)."""
+
+    def __init__(self, text):
+        self.text = text
+
+
+class _BoundCommand:
+    def __init__(self, db, request):
+        self.db = db
+        self.request = request
+        self._limit = -1
+
+    def setLimit(self, n):
+        self._limit = n
+        return self
+
+    def execute(self, *args, **named):
+        text = self.request.text.strip()
+        if not text[:5].upper() == OMatchStatement.KEYWORD_MATCH:
+            raise N.OmxUnsupported(N.OMX_E_UNSUPPORTED, "only MATCH statements run on the device engine")
+        st = OMatchStatement(text).setLimit(self._limit)
+        try:
+            return st.execute(self.db.snapshot, *args, **named)
+        finally:
+            st.free()
+
+
+class GraphDatabase:
+    """`db.command(new OCommandSQL(...)).execute(...)` over a GraphSnapshot."""
+
+    def __init__(self, snapshot):
+        self.snapshot = snapshot
+
+    def command(self, request):
+        if isinstance(request, str):
+            request = OCommandSQL(request)
+        return _BoundCommand(self, request)
