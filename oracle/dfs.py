@@ -22,7 +22,8 @@ MAXP, MAXA = 4, 16
 class dfs_step(C.Structure):
     _fields_ = [("src", C.c_int32), ("dst", C.c_int32), ("mode", C.c_int32), ("forward", C.c_int32),
                 ("nparts", C.c_int32), ("rp", C.POINTER(C.c_uint64) * MAXP), ("col", C.POINTER(C.c_uint32) * MAXP),
-                ("where_bm", C.POINTER(C.c_uint64)), ("cand_bm", C.POINTER(C.c_uint64)), ("need_dedup", C.c_int32)]
+                ("where_bm", C.POINTER(C.c_uint64)), ("cand_bm", C.POINTER(C.c_uint64)), ("need_dedup", C.c_int32),
+                ("sorted", C.c_int32)]
 
 
 class dfs_plan(C.Structure):
@@ -172,6 +173,7 @@ def run(g, query, params=None, nthreads=1, emit=True, root_sample=None):
             st.rp[q] = rp.ctypes.data_as(C.POINTER(C.c_uint64))
             st.col[q] = col.ctypes.data_as(C.POINTER(C.c_uint32))
         st.need_dedup = int(len(parts) > 1 or not g.simple)
+        st.sorted = 1  # CsrGraph rows are sorted (the generator and the transpose sort them)
         wm = where_mask(t_alias)
         if wm is not None:
             w = _bm_from_mask(wm)

@@ -37,6 +37,7 @@ typedef struct {
   const uint64_t *where_bm;   /* target WHERE (NULL = none) */
   const uint64_t *cand_bm;    /* candidate set (class ∧ WHERE) for MODE_CAND */
   int32_t need_dedup;         /* neighbour lists may repeat a vertex (several parts / parallel edges) */
+  int32_t sorted;             /* every part's rows ascending */
 } dfs_step;
 
 typedef struct {
@@ -102,6 +103,21 @@ static void process(const dfs_plan *p, int e, uint32_t *bind, sink *s) {
         seen[nseen++] = r;
       }
       if (st->mode == MODE_BOUND) {
+        if (st->sorted && !dedup) {
+          /* rows sorted: the first match is found by binary search (same branch taken as the
+             linear scan + break of :468-477) */
+          const uint32_t t = bind[st->dst];
+          uint64_t a = lo, b = hi;
+          while (a < b) {
+            uint64_t m = (a + b) >> 1;
+            if (st->col[q][m] < t) a = m + 1; else b = m;
+          }
+          if (a < hi && st->col[q][a] == t && (!st->forward || !st->where_bm || bm(st->where_bm, t))) {
+            process(p, e + 1, bind, s);
+            goto done;
+          }
+          break;
+        }
         if (bind[st->dst] == r) {
           process(p, e + 1, bind, s);
           goto done; /* break (:476) */

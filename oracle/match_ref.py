@@ -77,9 +77,11 @@ class RefDB:
         self._next_cluster = 11
 
     # schema -----------------------------------------------------------------------------------------
-    def create_class(self, name, superclass=None, is_edge=False):
-        self.classes[name] = {"superclass": superclass, "is_edge": is_edge, "cluster": self._next_cluster}
-        self._next_cluster += 1
+    def create_class(self, name, superclass=None, is_edge=False, cluster=None):
+        if cluster is None:
+            cluster = self._next_cluster
+        self.classes[name] = {"superclass": superclass, "is_edge": is_edge, "cluster": cluster}
+        self._next_cluster = max(self._next_cluster, cluster) + 1
         self.by_class[name] = []
 
     def class_name(self, name):

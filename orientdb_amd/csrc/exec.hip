@@ -388,7 +388,7 @@ class Executor {
     ExpandOut o = expand_core(col_[st.src].p, R_, st.adj, bitmap(st.filter_bm), carry, write);
     edges_ += o.E;
     R_ = o.n;
-    if (!write) return;
+    if (!write || R_ == 0) return;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
     col_[st.dst] = std::move(o.dst);
   }

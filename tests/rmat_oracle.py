@@ -7,10 +7,11 @@ from oracle.match_ref import RefDB
 
 def refdb_from_csr(rp, col, age):
     db = RefDB()
-    db.create_class("V")
-    db.create_class("E", is_edge=True)
-    db.create_class("Person", "V")  # cluster 11, as GraphSnapshot.rmat
-    db.create_class("Knows", "E", is_edge=True)
+    # clusters as GraphSnapshot.rmat: V 9, E 10, Person 11 (RID #11:v), Knows 12
+    db.create_class("V", cluster=9)
+    db.create_class("E", is_edge=True, cluster=10)
+    db.create_class("Person", "V", cluster=11)
+    db.create_class("Knows", "E", is_edge=True, cluster=12)
     V = len(rp) - 1
     for v in range(V):
         db.add_vertex("Person", {"uid": v, "age": int(age[v])})

@@ -170,10 +170,11 @@ def test_rmat_parity_multigraph(rmat10_raw, q):
 
 
 RMAT16 = [
-    ("c1_fof", "MATCH {class:Person}-Knows->{}-Knows->{as:fof} RETURN fof", ["fof"]),
+    ("c1_fof_sampled", "MATCH {class:Person,as:a,where:(uid < 512)}-Knows->{}-Knows->{as:fof} RETURN fof", ["fof"]),
     ("c2_both_ends", "MATCH {class:Person,as:a,where:(age < 1)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a,b,c",
      ["a", "b", "c"]),
-    ("c4_triangle", "MATCH {class:Person,as:a}-Knows->{as:b}-Knows->{as:c}-Knows->{as:a} RETURN a,b,c", ["a", "b", "c"]),
+    ("c4_triangle_filtered", "MATCH {class:Person,as:a,where:(age < 10)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:a} RETURN a,b,c",
+     ["a", "b", "c"]),
 ]
 
 
