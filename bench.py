@@ -47,11 +47,20 @@ def cpu_baseline(g, query, target_s=12.0):
     nroots_total = len(np.nonzero(cg.columns["age"] < 1)[0]) if "age < 1" in query else g.V
     per_root = max(probe["seconds"] / max(probe["nroots"], 1), 1e-7)
     sample = int(min(nroots_total, max(64, target_s / per_root)))
-    r = dfs.run(cg, query, nthreads=threads, emit=False, root_sample=sample)
-    return {"value": r["edges"] / r["seconds"] / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
-            "sample": "%d of %d roots (%.1f s, %d edges, %d bindings, oracle/dfs_ref.c DFS, %d threads)" % (
-                r["nroots"], nroots_total, r["seconds"], r["edges"], r["bindings"], threads),
-            "bindings_per_s": r["bindings"] / r["seconds"]}
+    # repeat the bounded sample until ≈ target_s of CPU work has been timed
+    edges = bindings = 0
+    secs = 0.0
+    reps = 0
+    while secs < target_s and reps < 1000:
+        r = dfs.run(cg, query, nthreads=threads, emit=False, root_sample=sample)
+        edges += r["edges"]
+        bindings += r["bindings"]
+        secs += r["seconds"]
+        reps += 1
+    return {"value": edges / secs / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
+            "sample": "%d of %d roots x %d repetitions (%.1f s, %d edges, %d bindings; oracle/dfs_ref.c DFS, %d threads)" % (
+                sample, nroots_total, reps, secs, edges, bindings, threads),
+            "bindings_per_s": bindings / secs}
 
 
 def main():
@@ -124,7 +133,10 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    exp = kst.get("k_expand", {"launches": 1, "ms": 0.0, "alg_bytes": 0})
+    # the dominant kernel: the expansion kernel (heavy-row chunks or light-row merge path) with the most time
+    cands = {k: v for k, v in kst.items() if k in ("k_expand_heavy", "k_expand_light")}
+    dom = max(cands, key=lambda k: cands[k]["ms"]) if cands else "k_expand_heavy"
+    exp = cands.get(dom, {"launches": 1, "ms": 0.0, "alg_bytes": 0})
     achieved = exp["alg_bytes"] / (exp["ms"] / 1e3) / 1e9 if exp["ms"] > 0 else 0.0
     out = {
         "metric": METRIC,
@@ -145,7 +157,7 @@ def main():
                    "parallelism": "roots sharded v%%N across %d GPU(s), graph replicated" % world,
                    "graph_build_s": round(t_build, 2)},
         "bindings_per_s": bindings_all / dt_max,
-        "roofline": {"bound": "hbm", "kernel": "k_expand", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "alg_bytes_per_launch": exp["alg_bytes"] / max(exp["launches"], 1),
                      "avg_launch_ms": exp["ms"] / max(exp["launches"], 1), "traffic": None},

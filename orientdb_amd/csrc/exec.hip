@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -90,6 +91,8 @@ class Executor {
   Executor(Graph &g, const Plan &p, const omx_exec_options &o)
       : g_(g), p_(p), o_(o), s_(g.stream), pool_(g.pool), tm_((o.flags & OMX_FLAG_KERNEL_TIMING) != 0, g.stream) {
     nwords_ = ((uint64_t)g.V + 63) / 64;
+    // rows with at least this many neighbours take the chunked kernel (tests lower it to force the path)
+    if (const char *h = std::getenv("OMX_HEAVY_DEG")) heavy_deg_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
   }
@@ -108,9 +111,13 @@ class Executor {
         const Step &st = p_.steps[i];
         bool last = i + 1 == p_.steps.size();
         bool count_only = last && o_.mode == OMX_MODE_COUNT && p_.unique_by_construction && st.kind == S_EXPAND;
+        // the last expansion of a plan whose rows are distinct by construction may stay block-
+        // segmented in HBM when the rows are not copied to the host
+        bool seg_ok = last && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES &&
+                      (o_.flags & OMX_FLAG_KEEP_DEVICE);
         switch (st.kind) {
           case S_ROOT: root(st); break;
-          case S_EXPAND: expand_step(st, !count_only); counted_only = count_only; break;
+          case S_EXPAND: expand_step(st, !count_only, seg_ok); counted_only = count_only; break;
           case S_CHECK: check_step(st); break;
           case S_VARLEN: varlen_step(st); break;
           case S_NEWROOT:
@@ -177,6 +184,9 @@ class Executor {
   uint64_t R_ = 1;
   uint64_t edges_ = 0, alg_bytes_ = 0, bindings_ = 0;
   int dedup_ran_ = 0;
+  int cus_ = 0;
+  uint64_t heavy_deg_ = kHeavyDeg;
+  bool segmented_ = false;  // the final table is block-segmented (see expand_core)
 
   // ---- helpers -----------------------------------------------------------------------------------
   template <class F>
@@ -293,102 +303,181 @@ class Executor {
     std::vector<DBuf<uint32_t>> carry;
     uint64_t n = 0;
     uint64_t E = 0;
+    // block-segmented result (filtered expansion left un-compacted)
+    bool segmented = false;
+    DBuf<uint64_t> seg_start;
+    DBuf<uint32_t> seg_count;
+    uint32_t nseg = 0;
   };
 
-  // One pattern-edge expansion of R rows (src column) with optional target bitmap; carries the
-  // listed columns. write=false only counts.
+  int cus() {
+    if (!cus_) {
+      hipDeviceProp_t prop;
+      HIP_CHECK(hipGetDeviceProperties(&prop, g_.device));
+      cus_ = prop.multiProcessorCount;
+    }
+    return cus_;
+  }
+
+  // One pattern-edge expansion of R rows (src column) with an optional target bitmap, carrying the
+  // listed columns. write=false only counts. allow_segmented leaves a filtered result as per-block
+  // segments (the final step of a plan whose rows are distinct by construction).
   ExpandOut expand_core(const uint32_t *src, uint64_t R, const AdjSpec &adjs, const uint64_t *filter,
-                        const std::vector<const uint32_t *> &carry, bool write) {
+                        const std::vector<const uint32_t *> &carry, bool write, bool allow_segmented = false) {
     ExpandOut o;
     DAdj adj = make_adj(adjs);
     if (adj.n == 0 || R == 0) return o;
-    DBuf<uint64_t> deg(&pool_, R + 1), offs(&pool_, R + 1);
-    tm_.begin("k_row_degree");
-    launch_row_degree(src, R, adj, deg.p, s_);
-    tm_.end(R * (4 + 16ull * adj.n) + (R + 1) * 8);
+    // 1. degree binning + scans (light edges: merge path; heavy rows: chunks)
+    DBuf<uint64_t> light(&pool_, R + 1), heavy(&pool_, R + 1), loffs(&pool_, R + 1), hoffs(&pool_, R + 1);
+    DBuf<uint32_t> nch(&pool_, R + 1);
+    DBuf<uint64_t> choffs(&pool_, R + 1);
+    tm_.begin("k_row_split");
+    launch_row_split(src, R, adj, heavy_deg_, light.p, heavy.p, nch.p, s_);
+    tm_.end(R * (4 + 16ull * adj.n) + (R + 1) * 20);
     tm_.begin("scan_degrees");
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, deg.p, offs.p, (int64_t)(R + 1), s_); });
-    tm_.end((R + 1) * 16);
-    const uint64_t E = read1(offs.p + R);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, light.p, loffs.p, (int64_t)(R + 1), s_); });
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, heavy.p, hoffs.p, (int64_t)(R + 1), s_); });
+    hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> nit(nch.p, CastU64());
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, nit, choffs.p, (int64_t)(R + 1), s_); });
+    tm_.end((R + 1) * 40);
+    uint64_t tot[3];
+    HIP_CHECK(hipMemcpyAsync(&tot[0], loffs.p + R, 8, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipMemcpyAsync(&tot[1], hoffs.p + R, 8, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipMemcpyAsync(&tot[2], choffs.p + R, 8, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    const uint64_t EL = tot[0], EH = tot[1], nchunks = tot[2];
+    const uint64_t E = EL + EH;
     o.E = E;
     if (E == 0) return o;
-    const uint64_t ntiles = (R + E + kExpandTile - 1) / kExpandTile;
-    DBuf<uint64_t> part(&pool_, ntiles + 1);
-    tm_.begin("k_mp_partition");
-    launch_mp_partition(offs.p, R, E, ntiles, part.p, s_);
-    tm_.end((ntiles + 1) * 8 * 20);
-    DBuf<uint32_t> tcount(&pool_, ntiles);
+    DBuf<ChunkDesc> chunks;
+    if (nchunks) {
+      chunks = DBuf<ChunkDesc>(&pool_, nchunks);
+      tm_.begin("k_fill_chunks");
+      launch_fill_chunks(src, R, adj, choffs.p, hoffs.p, chunks.p, s_);
+      tm_.end(nchunks * sizeof(ChunkDesc));
+    }
+    const uint64_t ntiles = EL ? (R + EL + kExpandTile - 1) / kExpandTile : 0;
+    DBuf<uint64_t> part;
+    if (ntiles) {
+      part = DBuf<uint64_t>(&pool_, ntiles + 1);
+      tm_.begin("k_mp_partition");
+      launch_mp_partition(loffs.p, R, EL, ntiles, part.p, s_);
+      tm_.end((ntiles + 1) * 8 * 20);
+    }
+    // 2. persistent grids and output placement
+    const bool single = adj.n == 1, filt = filter != nullptr;
+    // heavy kernel: a worker is a wave (4 per block); light kernel: a worker is a block
+    constexpr unsigned WPB = kHeavyBlock / 64;
+    const uint64_t hblocks = (nchunks + WPB - 1) / WPB;
+    const unsigned gh = nchunks ? (unsigned)std::min<uint64_t>(hblocks, (uint64_t)cus() * expand_blocks_per_cu(true, single, filt, write)) : 0;
+    const unsigned gl = ntiles ? (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus() * expand_blocks_per_cu(false, single, filt, write)) : 0;
+    const uint64_t wh = (uint64_t)gh * WPB;
+    const uint64_t caph = gh ? (nchunks + wh - 1) / wh * (uint64_t)kChunk : 0;
+    const uint64_t capl = gl ? (ntiles + gl - 1) / gl * (uint64_t)kExpandTile : 0;
+    const uint64_t cap = filt ? wh * caph + gl * capl : E;
     ExpandArgs a{};
     a.src = src;
-    a.offs = offs.p;
+    a.offs = loffs.p;
     a.part = part.p;
     a.R = R;
-    a.E = E;
+    a.E = EL;
+    a.ntiles = ntiles;
     a.adj = adj;
     a.filter = filter;
     a.ncarry = (int32_t)carry.size();
-    a.tile_count = tcount.p;
-    std::vector<DBuf<uint32_t>> gap;
-    DBuf<uint32_t> gdst;
+    a.chunks = chunks.p;
+    a.nchunks = nchunks;
+    a.hoffs = hoffs.p;
+    a.dense_base = EH;
+    std::vector<DBuf<uint32_t>> outc;
+    DBuf<uint32_t> odst;
     if (write) {
-      gdst = DBuf<uint32_t>(&pool_, E);
-      a.out_dst = gdst.p;
+      odst = DBuf<uint32_t>(&pool_, std::max<uint64_t>(cap, 1));
+      a.out_dst = odst.p;
       for (size_t c = 0; c < carry.size(); ++c) {
-        gap.emplace_back(&pool_, E);
+        outc.emplace_back(&pool_, std::max<uint64_t>(cap, 1));
         a.carry_in[c] = carry[c];
-        a.carry_out[c] = gap.back().p;
+        a.carry_out[c] = outc.back().p;
       }
     }
-    tm_.begin("k_expand");
-    launch_expand(a, ntiles, write, s_);
+    if (filt) {
+      o.nseg = (uint32_t)(wh + gl);
+      o.seg_start = DBuf<uint64_t>(&pool_, o.nseg);
+      o.seg_count = DBuf<uint32_t>(&pool_, o.nseg);
+      a.seg_start = o.seg_start.p;
+      a.seg_count = o.seg_count.p;
+    }
     // algorithmic bytes: 8 B row_ptr pair per row + 4 B col per edge (+ 4 B × columns
-    // per emitted row, below)
+    // per emitted row, added below)
     uint64_t kb = 8 * R + 4 * E;
-    if (!filter) {
+    // per-kernel algorithmic bytes: heavy rows carry EH edges, light rows EL (+ 8 B per row each)
+    if (gh) {
+      a.arena_base = 0;
+      a.arena_cap = caph;
+      a.seg_base = 0;
+      tm_.begin("k_expand_heavy");
+      launch_expand_heavy(a, gh, write, s_);
+      tm_.end(4 * EH + 24 * nchunks);
+    }
+    if (gl) {
+      a.arena_base = wh * caph;
+      a.arena_cap = capl;
+      a.seg_base = (uint32_t)wh;
+      tm_.begin("k_expand_light");
+      launch_expand(a, gl, write, s_);
+      tm_.end(8 * R + 4 * EL);
+    }
+    tm_.begin("expand_total");
+    if (!filt) {
       o.n = E;
       if (write) kb += 4ull * (carry.size() + 1) * E;
       tm_.end(kb);
       alg_bytes_ += kb;
       if (write) {
-        o.dst = std::move(gdst);
-        o.carry = std::move(gap);
+        o.dst = std::move(odst);
+        o.carry = std::move(outc);
       }
       return o;
     }
-    // filtered: scan the tile counts, compact the gapped tiles
-    DBuf<uint64_t> toffs(&pool_, ntiles + 1);
-    DBuf<uint32_t> tc1(&pool_, ntiles + 1);
-    HIP_CHECK(hipMemcpyAsync(tc1.p, tcount.p, ntiles * 4, hipMemcpyDeviceToDevice, s_));
-    HIP_CHECK(hipMemsetAsync(tc1.p + ntiles, 0, 4, s_));
-    hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> it(tc1.p, CastU64());
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, it, toffs.p, (int64_t)(ntiles + 1), s_); });
-    const uint64_t n = read1(toffs.p + ntiles);
+    // filtered: rows per block segment → total (and dense compaction when required)
+    DBuf<uint64_t> soffs(&pool_, o.nseg + 1);
+    hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> sit(o.seg_count.p, CastU64());
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, sit, soffs.p + 1, (int64_t)o.nseg, s_); });
+    HIP_CHECK(hipMemsetAsync(soffs.p, 0, 8, s_));
+    const uint64_t n = read1(soffs.p + o.nseg);
     o.n = n;
     if (write) kb += 4ull * (carry.size() + 1) * n;
     tm_.end(kb);
     alg_bytes_ += kb;
     if (!write || n == 0) return o;
+    if (allow_segmented) {
+      o.segmented = true;
+      o.dst = std::move(odst);
+      o.carry = std::move(outc);
+      return o;
+    }
     o.dst = DBuf<uint32_t>(&pool_, n);
-    std::vector<uint32_t *> ins{gdst.p}, outs{o.dst.p};
+    std::vector<uint32_t *> ins{odst.p}, outs{o.dst.p};
     for (size_t c = 0; c < carry.size(); ++c) {
       o.carry.emplace_back(&pool_, n);
-      ins.push_back(gap[c].p);
+      ins.push_back(outc[c].p);
       outs.push_back(o.carry.back().p);
     }
-    tm_.begin("k_compact_tiles");
-    launch_compact_tiles((int)ins.size(), ins.data(), outs.data(), part.p, tcount.p, toffs.p, ntiles, s_);
+    tm_.begin("k_compact_segments");
+    launch_compact_segments((int)ins.size(), ins.data(), outs.data(), o.seg_start.p, o.seg_count.p, soffs.p, o.nseg, s_);
     tm_.end(8ull * ins.size() * n);
     return o;
   }
 
-  void expand_step(const Step &st, bool write) {
+  void expand_step(const Step &st, bool write, bool allow_segmented) {
     std::vector<int> cols = bound_cols();
     std::vector<const uint32_t *> carry;
     for (int c : cols) carry.push_back(col_[c].p);
-    ExpandOut o = expand_core(col_[st.src].p, R_, st.adj, bitmap(st.filter_bm), carry, write);
+    ExpandOut o = expand_core(col_[st.src].p, R_, st.adj, bitmap(st.filter_bm), carry, write, allow_segmented);
     edges_ += o.E;
     R_ = o.n;
     if (!write || R_ == 0) return;
+    segmented_ = o.segmented;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
     col_[st.dst] = std::move(o.dst);
   }
@@ -644,11 +733,18 @@ class Executor {
       return;
     }
     const int k = (int)p_.out_aliases.size();
+    std::vector<int> taken(col_.size(), -1);
     for (int a : p_.out_aliases) {
-      out.emplace_back(&pool_, R_);
-      HIP_CHECK(hipMemcpyAsync(out.back().p, col_[a].p, R_ * 4, hipMemcpyDeviceToDevice, s_));
+      if (taken[a] < 0) {  // move the binding column (no copy); an alias returned twice is copied
+        taken[a] = (int)out.size();
+        out.push_back(std::move(col_[a]));
+      } else {
+        out.emplace_back(&pool_, R_);
+        HIP_CHECK(hipMemcpyAsync(out.back().p, out[taken[a]].p, R_ * 4, hipMemcpyDeviceToDevice, s_));
+      }
     }
     if (p_.unique_by_construction) return;
+    if (segmented_) fail(OMX_E_INVALID, "internal: segmented table reached dedup");
     dedup_ran_ = 1;
     tm_.begin("dedup");
     const int vbits = bits_for(g_.V);

@@ -13,18 +13,45 @@ constexpr int kExpandBlock = 256;  // 4 waves
 constexpr int kExpandIPT = 8;      // merge-path items per thread
 constexpr int kExpandTile = kExpandBlock * kExpandIPT;
 
+// Rows with at least kHeavyDeg neighbours are cut into chunks: one edge-set part of one row, inside
+// one kChunk-aligned window of the col[] array (so every lane's dwordx4 load is 16-B aligned).
+constexpr uint64_t kHeavyDeg = 1024;
+constexpr int kChunk = 1024;                       // edges per chunk = one wave × 16 dword loads per lane
+constexpr int kHeavyBlock = 256;                   // 4 independent waves
+constexpr int kHeavySlots = kChunk / 64;           // lane l takes edge l of each 64-edge slot
+
+struct ChunkDesc {
+  uint64_t lo, hi;  // absolute col[] range of the chunk inside part `part` (one kChunk-aligned window)
+  uint64_t dense;   // output index of edge lo in the dense (unfiltered) layout
+  uint32_t row;
+  uint32_t part;
+};
+
 struct ExpandArgs {
   const uint32_t *src;      // [R] source vertex of every binding row
-  const uint64_t *offs;     // [R+1] exclusive prefix sum of the rows' adjacency lengths
+  const uint64_t *offs;     // [R+1] exclusive prefix sum of the rows' LIGHT adjacency lengths
   const uint64_t *part;     // [ntiles+1] merge-path split: rows consumed before tile t
-  uint64_t R, E;            // rows, Σ adjacency length (= edges traversed)
+  uint64_t R, E;            // rows, Σ light adjacency length
+  uint64_t ntiles;
   DAdj adj;
   const uint64_t *filter;   // target bitmap (V bits) or nullptr
   int32_t ncarry;
   const uint32_t *carry_in[kMaxCols];
   uint32_t *carry_out[kMaxCols];
   uint32_t *out_dst;        // new column (neighbour)
-  uint32_t *tile_count;     // [ntiles] rows emitted per tile
+  // output placement. Dense (no filter): index = dense_base + edge index (light) or
+  // ChunkDesc::dense + position in the chunk (heavy). Arena (filter): each worker w of the launch
+  // (a block for the light kernel, a wave for the heavy one) appends to [arena_base + w·arena_cap, …)
+  // and reports its row count in seg_count[seg_base + w].
+  uint64_t dense_base;
+  uint64_t arena_base, arena_cap;
+  uint32_t *seg_count;
+  uint64_t *seg_start;
+  uint32_t seg_base;
+  // heavy chunks
+  const ChunkDesc *chunks;
+  uint64_t nchunks;
+  const uint64_t *hoffs;    // [R+1] exclusive prefix of the heavy rows' full degree (dense mode)
 };
 
 // predicate VM → V-bit bitmap (u64 words); depth = value of $depth
@@ -37,11 +64,19 @@ void launch_word_scatter(const uint64_t *words, uint64_t nwords, uint32_t V, int
                          const uint32_t *offsets, uint32_t *out, hipStream_t s);
 
 void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t *deg, hipStream_t s);
+// per row: light degree (0 for heavy rows), heavy degree (0 for light rows), number of heavy chunks
+void launch_row_split(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint64_t *light,
+                      uint64_t *heavy, uint32_t *nchunks, hipStream_t s);
+void launch_fill_chunks(const uint32_t *src, uint64_t R, const DAdj &adj, const uint64_t *choffs,
+                        const uint64_t *hoffs, ChunkDesc *out, hipStream_t s);
 void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part,
                          hipStream_t s);
-void launch_expand(const ExpandArgs &a, uint64_t ntiles, bool write, hipStream_t s);
-void launch_compact_tiles(int ncols, uint32_t *const *in, uint32_t *const *out, const uint64_t *part,
-                          const uint32_t *tile_count, const uint64_t *tile_offs, uint64_t ntiles, hipStream_t s);
+// persistent launches: `grid` blocks loop over the tiles / chunks
+void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);
+void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);
+int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write);
+void launch_compact_segments(int ncols, uint32_t *const *in, uint32_t *const *out, const uint64_t *seg_start,
+                             const uint32_t *seg_count, const uint64_t *seg_offs, uint32_t nseg, hipStream_t s);
 
 void launch_check(const uint32_t *src, const uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
                   uint8_t *flags, hipStream_t s);

@@ -1,17 +1,19 @@
 // kernels.hip — gfx950 (MI355X / CDNA4) kernels of the MATCH executor.
 //
 // None of this is a dense contraction: every kernel is HBM/L2-bound integer work (no MFMA). The
-// hot one is k_expand, the frontier expansion of one pattern edge over the binding table
+// hot path is the frontier expansion of one pattern edge over the binding table
 // (OMatchStatement.processContext P/OMatchStatement.java:412-568 → OMatchPathItem.executeTraversal
-// P/OMatchPathItem.java:49-78 → OrientVertex.getVertices B/OrientVertex.java:401-460):
-//   * merge-path load balance over (rows + edges), so RMAT hubs (deg ~1e4-1e5) and degree-1 rows
-//     cost the same per item; tile = 256 threads × 8 items;
-//   * per tile, row ownership of every edge is resolved in LDS (scatter of row starts + block
-//     max-scan), so the col[] loads are coalesced (lane l reads edge j0 + k·256 + l);
-//   * the target filter is a V-bit bitmap probe (L2-resident: 512 KiB at RMAT-22);
-//   * compaction by wave64 ballot + mbcnt, wave totals scanned in LDS; a tile writes its rows
-//     contiguously at its own edge offset ("gapped" output, no global atomics) and its count, which a
-//     scan + k_compact_tiles turns into a dense table. Without a filter the output is already dense.
+// P/OMatchPathItem.java:49-78 → OrientVertex.getVertices B/OrientVertex.java:401-460), split by degree:
+//   * heavy rows (≥ kHeavyDeg neighbours, the RMAT hubs that carry most edges) → k_expand_heavy:
+//     chunks of ≤ 4096 edges of one row in one aligned col window; per lane 4 × dwordx4 loads, 16
+//     independent bitmap probes, block scan, LDS-staged coalesced stores; row columns are constants;
+//   * light rows → k_expand: merge-path tiles over (rows + edges) of 256 threads × 8 items; row
+//     ownership of every edge resolved in LDS (scatter of row starts + block max-scan) so col[] loads
+//     stay coalesced; compaction by wave64 ballot + mbcnt with wave totals scanned in LDS;
+//   * both are persistent (grid = resident blocks) and append to a private per-block arena, so the
+//     filtered output needs no global atomics and no compaction pass; the table is block-segmented
+//     (k_compact_segments makes it dense only when a consumer needs it). Without a filter both write
+//     straight to the dense position of each edge.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -234,6 +236,65 @@ void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_
   KCHECK("k_row_degree");
 }
 
+// degree binning: light rows go to the merge-path kernel, heavy rows (≥ kHeavyDeg) to chunks
+__global__ void k_row_split(const uint32_t *src, uint64_t R, DAdj adj, uint64_t heavy_deg, uint64_t *light,
+                            uint64_t *heavy, uint32_t *nch) {
+  uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > R) return;
+  if (r == R) {
+    light[R] = 0;
+    heavy[R] = 0;
+    nch[R] = 0;
+    return;
+  }
+  const uint32_t v = src[r];
+  const uint64_t d = adj_degree(adj, v);
+  if (d >= heavy_deg) {
+    uint32_t c = 0;
+    for (int p = 0; p < adj.n; ++p) {
+      const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
+      if (e > b) c += (uint32_t)((e - 1) / kChunk - b / kChunk + 1);
+    }
+    light[r] = 0;
+    heavy[r] = d;
+    nch[r] = c;
+  } else {
+    light[r] = d;
+    heavy[r] = 0;
+    nch[r] = 0;
+  }
+}
+void launch_row_split(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint64_t *light,
+                      uint64_t *heavy, uint32_t *nch, hipStream_t s) {
+  hipLaunchKernelGGL(k_row_split, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, R, adj, heavy_deg, light, heavy,
+                     nch);
+  KCHECK("k_row_split");
+}
+
+__global__ void k_fill_chunks(const uint32_t *src, uint64_t R, DAdj adj, const uint64_t *choffs, const uint64_t *hoffs,
+                              ChunkDesc *out) {
+  uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  uint64_t o = choffs[r];
+  if (choffs[r + 1] == o) return;
+  const uint32_t v = src[r];
+  uint64_t pos = hoffs[r];  // dense output index of the row's first edge (parts in order)
+  for (int p = 0; p < adj.n; ++p) {
+    const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
+    for (uint64_t w = b / kChunk * kChunk; w < e; w += kChunk) {
+      const uint64_t lo = w > b ? w : b, hi = w + kChunk < e ? w + kChunk : e;
+      out[o++] = ChunkDesc{lo, hi, pos + (lo - b), (uint32_t)r, (uint32_t)p};
+    }
+    pos += e - b;
+  }
+}
+void launch_fill_chunks(const uint32_t *src, uint64_t R, const DAdj &adj, const uint64_t *choffs,
+                        const uint64_t *hoffs, ChunkDesc *out, hipStream_t s) {
+  if (!R) return;
+  hipLaunchKernelGGL(k_fill_chunks, dim3(nblocks(R, 256)), dim3(256), 0, s, src, R, adj, choffs, hoffs, out);
+  KCHECK("k_fill_chunks");
+}
+
 // merge path over A = row ends (offs[r+1]) and B = edge indices 0..E-1; a row end is consumed
 // before edge j when offs[r+1] <= j.
 __global__ void k_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part) {
@@ -255,6 +316,30 @@ void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t 
   KCHECK("k_mp_partition");
 }
 
+// block-wide exclusive scan of one u32 per thread (4 waves); returns the block total in *total
+template <int B>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *s_w, uint32_t *total) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= (uint32_t)off) incl += y;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint32_t woff = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < B / 64; ++w) {
+    uint32_t t = s_w[w];
+    woff += (w < (int)wave) ? t : 0;
+    tot += t;
+  }
+  *total = tot;
+  return woff + incl - x;
+}
+
+// Light rows: merge-path tiles of kExpandTile (rows + edges) items, persistent blocks.
 template <bool SINGLE, bool FILTER, bool WRITE>
 __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
   constexpr int B = kExpandBlock, IPT = kExpandIPT, T = kExpandTile, W = B / 64;
@@ -264,158 +349,262 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
   __shared__ uint16_t s_seg[T];       // local row owning each tile edge
   __shared__ uint32_t s_wave[IPT * W];
   __shared__ uint32_t s_wmax[W];
+  __shared__ uint32_t s_total;
 
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t t = blockIdx.x;
-  const uint64_t d0 = t * (uint64_t)T;
-  const uint64_t d1 = min(d0 + (uint64_t)T, a.R + a.E);
-  const uint64_t i0 = a.part[t], i1 = a.part[t + 1];
-  const uint64_t j0 = d0 - i0, j1 = d1 - i1;
-  const uint32_t ne = (uint32_t)(j1 - j0);
-  if (ne == 0) {
-    if (tid == 0) a.tile_count[t] = 0;
-    return;
-  }
-  const uint64_t rlast = min(i1, a.R - 1);
-  const uint32_t nr = (uint32_t)(rlast - i0 + 1);
+  const uint64_t arena = a.arena_base + (uint64_t)blockIdx.x * a.arena_cap;
+  uint64_t acc = 0;
+  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    const uint64_t d0 = t * (uint64_t)T;
+    const uint64_t d1 = min(d0 + (uint64_t)T, a.R + a.E);
+    const uint64_t i0 = a.part[t], i1 = a.part[t + 1];
+    const uint64_t j0 = d0 - i0, j1 = d1 - i1;
+    const uint32_t ne = (uint32_t)(j1 - j0);
+    if (ne == 0) continue;  // uniform
+    const uint64_t rlast = min(i1, a.R - 1);
+    const uint32_t nr = (uint32_t)(rlast - i0 + 1);
 
-  for (uint32_t x = tid; x < ne; x += B) s_seg[x] = 0;
-  __syncthreads();
-  for (uint32_t lr = tid; lr < nr; lr += B) {
-    const uint64_t r = i0 + lr;
-    const uint64_t rs = a.offs[r], re = a.offs[r + 1];
-    const uint64_t s = rs > j0 ? rs - j0 : 0;
-    const uint64_t e = re < j1 ? (re > j0 ? re - j0 : 0) : ne;
-    s_ls[lr] = (uint16_t)(s < ne ? s : ne);
-    if (e > s && s < ne) s_seg[s] = (uint16_t)lr;
-    const uint32_t v = a.src[r];
-    const uint64_t skip = rs < j0 ? j0 - rs : 0;
-    if (SINGLE) {
-      s_base[lr] = a.adj.p[0].rp[v] + skip;
-    } else {
-      s_vtx[lr] = v;
-      if (lr == 0) s_base[0] = skip;
-    }
-  }
-  __syncthreads();
-  // inclusive max-scan of s_seg (row index of the latest row starting at or before each edge)
-  {
-    uint32_t vals[IPT];
-    uint32_t m = 0;
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      uint32_t idx = tid * IPT + i;
-      uint32_t x = idx < ne ? s_seg[idx] : 0;
-      m = m > x ? m : x;
-      vals[i] = m;
-    }
-    uint32_t incl = m;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      uint32_t y = __shfl_up(incl, off, 64);
-      if (lane >= (uint32_t)off) incl = incl > y ? incl : y;
-    }
-    if (lane == 63) s_wmax[wave] = incl;
-    uint32_t excl = __shfl_up(incl, 1, 64);
-    if (lane == 0) excl = 0;
+    for (uint32_t x = tid; x < ne; x += B) s_seg[x] = 0;
     __syncthreads();
-    uint32_t wp = 0;
-    for (uint32_t w = 0; w < wave; ++w) wp = wp > s_wmax[w] ? wp : s_wmax[w];
-    uint32_t pre = excl > wp ? excl : wp;
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      uint32_t idx = tid * IPT + i;
-      if (idx < ne) s_seg[idx] = (uint16_t)(pre > vals[i] ? pre : vals[i]);
-    }
-  }
-  __syncthreads();
-
-  uint32_t nb[IPT];
-  uint16_t lrs[IPT];
-  uint32_t passmask = 0;
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const uint32_t jl = k * B + tid;
-    nb[k] = 0;
-    lrs[k] = 0;
-    if (jl < ne) {
-      const uint32_t lr = s_seg[jl];
-      uint64_t kk = jl - s_ls[lr];
-      uint32_t n;
+    for (uint32_t lr = tid; lr < nr; lr += B) {
+      const uint64_t r = i0 + lr;
+      const uint64_t rs = a.offs[r], re = a.offs[r + 1];
+      const uint64_t s = rs > j0 ? rs - j0 : 0;
+      const uint64_t e = re < j1 ? (re > j0 ? re - j0 : 0) : ne;
+      s_ls[lr] = (uint16_t)(s < ne ? s : ne);
+      if (e > s && s < ne) s_seg[s] = (uint16_t)lr;
+      const uint32_t v = a.src[r];
+      const uint64_t skip = rs < j0 ? j0 - rs : 0;
       if (SINGLE) {
-        n = a.adj.p[0].col[s_base[lr] + kk];
+        s_base[lr] = a.adj.p[0].rp[v] + skip;
       } else {
-        const uint32_t v = s_vtx[lr];
-        if (lr == 0) kk += s_base[0];
-        n = 0;
-        for (int p = 0; p < a.adj.n; ++p) {
-          const uint64_t b0 = a.adj.p[p].rp[v], dp = a.adj.p[p].rp[v + 1] - b0;
-          if (kk < dp) {
-            n = a.adj.p[p].col[b0 + kk];
-            break;
+        s_vtx[lr] = v;
+        if (lr == 0) s_base[0] = skip;
+      }
+    }
+    __syncthreads();
+    // inclusive max-scan of s_seg (row index of the latest row starting at or before each edge)
+    {
+      uint32_t vals[IPT];
+      uint32_t m = 0;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        uint32_t idx = tid * IPT + i;
+        uint32_t x = idx < ne ? s_seg[idx] : 0;
+        m = m > x ? m : x;
+        vals[i] = m;
+      }
+      uint32_t incl = m;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl = incl > y ? incl : y;
+      }
+      if (lane == 63) s_wmax[wave] = incl;
+      uint32_t excl = __shfl_up(incl, 1, 64);
+      if (lane == 0) excl = 0;
+      __syncthreads();
+      uint32_t wp = 0;
+      for (uint32_t w = 0; w < wave; ++w) wp = wp > s_wmax[w] ? wp : s_wmax[w];
+      uint32_t pre = excl > wp ? excl : wp;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        uint32_t idx = tid * IPT + i;
+        if (idx < ne) s_seg[idx] = (uint16_t)(pre > vals[i] ? pre : vals[i]);
+      }
+    }
+    __syncthreads();
+
+    uint32_t nb[IPT];
+    uint16_t lrs[IPT];
+    uint32_t passmask = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const uint32_t jl = k * B + tid;
+      nb[k] = 0;
+      lrs[k] = 0;
+      if (jl < ne) {
+        const uint32_t lr = s_seg[jl];
+        uint64_t kk = jl - s_ls[lr];
+        uint32_t n;
+        if (SINGLE) {
+          n = a.adj.p[0].col[s_base[lr] + kk];
+        } else {
+          const uint32_t v = s_vtx[lr];
+          if (lr == 0) kk += s_base[0];
+          n = 0;
+          for (int p = 0; p < a.adj.n; ++p) {
+            const uint64_t b0 = a.adj.p[p].rp[v], dp = a.adj.p[p].rp[v + 1] - b0;
+            if (kk < dp) {
+              n = a.adj.p[p].col[b0 + kk];
+              break;
+            }
+            kk -= dp;
           }
-          kk -= dp;
+        }
+        nb[k] = n;
+        lrs[k] = (uint16_t)lr;
+        bool pass = FILTER ? bm_test(a.filter, n) : true;
+        passmask |= (uint32_t)pass << k;
+      }
+    }
+
+    if (!FILTER) {
+      if (WRITE) {
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+          const uint32_t jl = k * B + tid;
+          if (jl < ne) {
+            const uint64_t o = a.dense_base + j0 + jl;
+            const uint64_t r = i0 + lrs[k];
+            a.out_dst[o] = nb[k];
+            for (int c = 0; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
+          }
         }
       }
-      nb[k] = n;
-      lrs[k] = (uint16_t)lr;
-      bool pass = FILTER ? bm_test(a.filter, n) : true;
-      passmask |= (uint32_t)pass << k;
+      __syncthreads();  // LDS reuse by the next tile
+      continue;
     }
-  }
 
-  if (!FILTER) {
+    // compaction: wave ballots per item row k, wave totals scanned in LDS (edge order preserved)
+    uint64_t masks[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      masks[k] = __ballot((passmask >> k) & 1u);
+      if (lane == 0) s_wave[k * W + wave] = (uint32_t)__popcll(masks[k]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t run = 0;
+      for (int x = 0; x < IPT * W; ++x) {
+        uint32_t c = s_wave[x];
+        s_wave[x] = run;
+        run += c;
+      }
+      s_total = run;
+    }
+    __syncthreads();
     if (WRITE) {
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
-        const uint32_t jl = k * B + tid;
-        if (jl < ne) {
-          const uint64_t o = j0 + jl;
+        if ((passmask >> k) & 1u) {
+          const uint64_t o = arena + acc + s_wave[k * W + wave] + lane_prefix(masks[k]);
           const uint64_t r = i0 + lrs[k];
           a.out_dst[o] = nb[k];
           for (int c = 0; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
         }
       }
     }
-    if (tid == 0) a.tile_count[t] = ne;
-    return;
+    acc += s_total;
+    __syncthreads();  // LDS reuse by the next tile
   }
-
-  // compaction: wave ballots per item row k, wave totals scanned in LDS (edge order preserved)
-  uint64_t masks[IPT];
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    masks[k] = __ballot((passmask >> k) & 1u);
-    if (lane == 0) s_wave[k * W + wave] = (uint32_t)__popcll(masks[k]);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t run = 0;
-    for (int x = 0; x < IPT * W; ++x) {
-      uint32_t c = s_wave[x];
-      s_wave[x] = run;
-      run += c;
-    }
-    a.tile_count[t] = run;
-  }
-  __syncthreads();
-  if (WRITE) {
-#pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      if ((passmask >> k) & 1u) {
-        const uint64_t o = j0 + s_wave[k * W + wave] + lane_prefix(masks[k]);
-        const uint64_t r = i0 + lrs[k];
-        a.out_dst[o] = nb[k];
-        for (int c = 0; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
-      }
-    }
+  if (FILTER && tid == 0) {
+    a.seg_count[a.seg_base + blockIdx.x] = (uint32_t)acc;
+    a.seg_start[a.seg_base + blockIdx.x] = arena;
   }
 }
 
-void launch_expand(const ExpandArgs &a, uint64_t ntiles, bool write, hipStream_t s) {
-  if (!ntiles) return;
+// Heavy rows: one chunk = ≤ kChunk edges of one row inside one kChunk-aligned col window, owned by
+// ONE wave (the 4 waves of a block are independent: no LDS, no barriers). Lane l takes edge l of
+// each of the 16 64-edge slots: col[] loads are fully coalesced dwords, and since a row's adjacency
+// is sorted, the 64 bitmap probes of one slot cover 64 consecutive neighbours — for hub rows a
+// handful of cache lines instead of one line per lane. Compaction by one ballot + mbcnt per slot, so
+// each slot's survivors land contiguously (coalesced stores) in the wave's private arena; the row's
+// carried columns are chunk constants. The next chunk's descriptor and col[] words are loaded before
+// the current chunk is filtered (software pipeline).
+__device__ __forceinline__ bool bm_test32(const uint32_t *bm, uint32_t v) { return (bm[v >> 5] >> (v & 31)) & 1u; }
+
+template <bool FILTER, bool WRITE>
+__global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
+  constexpr int NS = kHeavySlots, WPB = kHeavyBlock / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wid = (uint64_t)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * WPB;
+  const uint64_t arena = a.arena_base + wid * a.arena_cap;
+  const uint32_t *bm32 = reinterpret_cast<const uint32_t *>(a.filter);
+  uint64_t acc = 0;
+  auto load = [&](const ChunkDesc &d, uint32_t (&q)[NS]) {
+    const uint64_t win = d.lo / kChunk * kChunk;
+    const uint32_t *col = a.adj.p[d.part].col + win;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const uint64_t idx = win + i * 64 + lane;
+      q[i] = (idx >= d.lo && idx < d.hi) ? col[i * 64 + lane] : 0u;
+    }
+  };
+  uint64_t c = wid;
+  ChunkDesc d{};
+  uint32_t q[NS];
+  if (c < a.nchunks) {
+    d = a.chunks[c];
+    load(d, q);
+  }
+  while (c < a.nchunks) {
+    const uint64_t cn = c + nw;
+    const uint64_t win = d.lo / kChunk * kChunk;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const uint64_t idx = win + i * 64 + lane;
+      bool ok = idx >= d.lo && idx < d.hi;
+      if (FILTER && ok) ok = bm_test32(bm32, q[i]);
+      mask |= (uint32_t)ok << i;
+    }
+    // prefetch the next chunk
+    ChunkDesc dn = d;
+    uint32_t qn[NS];
+    if (cn < a.nchunks) {
+      dn = a.chunks[cn];
+      load(dn, qn);
+    }
+    const uint32_t r = d.row;
+    if (WRITE) {
+      uint32_t cv[4];
+      const int nc = a.ncarry;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cv[k] = k < nc ? a.carry_in[k][r] : 0;
+      uint64_t base = FILTER ? arena + acc : 0;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        const bool bit = (mask >> i) & 1u;
+        uint64_t o;
+        if (FILTER) {
+          const uint64_t m = __ballot(bit);
+          o = base + lane_prefix(m);
+          base += __popcll(m);
+        } else {
+          o = d.dense + (win + i * 64 + lane - d.lo);
+        }
+        if (bit) {
+          a.out_dst[o] = q[i];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k < nc) a.carry_out[k][o] = cv[k];
+          for (int k = 4; k < nc; ++k) a.carry_out[k][o] = a.carry_in[k][r];
+        }
+      }
+      if (FILTER) acc = base - arena;
+    } else if (FILTER) {
+      uint32_t cnt = __popc(mask);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+      acc += cnt;
+    }
+    c = cn;
+    d = dn;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) q[i] = qn[i];
+  }
+  if (FILTER && lane == 0) {
+    a.seg_count[a.seg_base + wid] = (uint32_t)acc;
+    a.seg_start[a.seg_base + wid] = arena;
+  }
+}
+
+void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s) {
+  if (!grid) return;
   const bool single = a.adj.n == 1, filter = a.filter != nullptr;
-  dim3 g((unsigned)ntiles), b(kExpandBlock);
+  dim3 g(grid), b(kExpandBlock);
 #define OMX_EXP(S, F, Wr) hipLaunchKernelGGL((k_expand<S, F, Wr>), g, b, 0, s, a)
   if (single) {
     if (filter) { if (write) OMX_EXP(true, true, true); else OMX_EXP(true, true, false); }
@@ -428,31 +617,62 @@ void launch_expand(const ExpandArgs &a, uint64_t ntiles, bool write, hipStream_t
   KCHECK("k_expand");
 }
 
+void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s) {
+  if (!grid) return;
+  const bool filter = a.filter != nullptr;
+  dim3 g(grid), b(kHeavyBlock);
+  if (filter) {
+    if (write) hipLaunchKernelGGL((k_expand_heavy<true, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_expand_heavy<true, false>), g, b, 0, s, a);
+  } else {
+    if (write) hipLaunchKernelGGL((k_expand_heavy<false, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_expand_heavy<false, false>), g, b, 0, s, a);
+  }
+  KCHECK("k_expand_heavy");
+}
+
+int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write) {
+  int n = 0;
+  hipError_t e;
+  if (heavy) {
+    if (filter) e = write ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand_heavy<true, true>, kHeavyBlock, 0)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand_heavy<true, false>, kHeavyBlock, 0);
+    else e = write ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand_heavy<false, true>, kHeavyBlock, 0)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand_heavy<false, false>, kHeavyBlock, 0);
+  } else if (single) {
+    e = filter ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand<true, true, true>, kExpandBlock, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand<true, false, true>, kExpandBlock, 0);
+  } else {
+    e = filter ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand<false, true, true>, kExpandBlock, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand<false, false, true>, kExpandBlock, 0);
+  }
+  if (e != hipSuccess || n < 1) n = 2;
+  return n;
+}
+
 struct ColPtrs {
   const uint32_t *in[kMaxCols];
   uint32_t *out[kMaxCols];
 };
 
-__global__ void k_compact_tiles(int ncols, ColPtrs cp, const uint64_t *part, const uint32_t *tile_count,
-                                const uint64_t *tile_offs) {
-  const uint64_t t = blockIdx.x;
-  const uint32_t cnt = tile_count[t];
-  if (!cnt) return;
-  const uint64_t j0 = t * (uint64_t)kExpandTile - part[t];
-  const uint64_t dst = tile_offs[t];
-  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
-    for (int c = 0; c < ncols; ++c) cp.out[c][dst + i] = cp.in[c][j0 + i];
+__global__ void k_compact_segments(int ncols, ColPtrs cp, const uint64_t *seg_start, const uint32_t *seg_count,
+                                   const uint64_t *seg_offs) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t cnt = seg_count[b];
+  const uint64_t src = seg_start[b], dst = seg_offs[b];
+  for (int c = 0; c < ncols; ++c)
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) cp.out[c][dst + i] = cp.in[c][src + i];
 }
-void launch_compact_tiles(int ncols, uint32_t *const *in, uint32_t *const *out, const uint64_t *part,
-                          const uint32_t *tile_count, const uint64_t *tile_offs, uint64_t ntiles, hipStream_t s) {
-  if (!ntiles) return;
+void launch_compact_segments(int ncols, uint32_t *const *in, uint32_t *const *out, const uint64_t *seg_start,
+                             const uint32_t *seg_count, const uint64_t *seg_offs, uint32_t nseg, hipStream_t s) {
+  if (!nseg) return;
   ColPtrs cp;
   for (int c = 0; c < ncols; ++c) {
     cp.in[c] = in[c];
     cp.out[c] = out[c];
   }
-  hipLaunchKernelGGL(k_compact_tiles, dim3((unsigned)ntiles), dim3(256), 0, s, ncols, cp, part, tile_count, tile_offs);
-  KCHECK("k_compact_tiles");
+  hipLaunchKernelGGL(k_compact_segments, dim3(nseg), dim3(256), 0, s, ncols, cp, seg_start, seg_count, seg_offs);
+  KCHECK("k_compact_segments");
 }
 
 // ---- bound-target check (existence of dst[r] in N(src[r]); P/OMatchStatement.java:468-477) ----------
