@@ -59,6 +59,14 @@ struct DPred {
   DAdj deg[kMaxDegAdj];
   const DColumn *cols;
   const uint16_t *vclass;
+  // fast path (no interpreter): n_atoms comparisons "column OP constant", all AND (conj=1) or all OR
+  int32_t n_atoms;
+  int32_t conj;
+  int32_t atom_col[4];
+  int32_t atom_op[4];
+  int64_t atom_i[4];
+  double atom_d[4];
+  int32_t atom_dbl[4];  // compare as double (double column or double constant)
 };
 
 }  // namespace omx

@@ -34,19 +34,20 @@ class Timer {
       (void)hipEventDestroy(r.b);
     }
   }
-  void begin(const char *name) {
+  void begin(const char *name, hipStream_t st = nullptr) {
     if (!on_) return;
     Rec r;
     r.name = name;
+    r.s = st ? st : s_;
     HIP_CHECK(hipEventCreate(&r.a));
     HIP_CHECK(hipEventCreate(&r.b));
-    HIP_CHECK(hipEventRecord(r.a, s_));
+    HIP_CHECK(hipEventRecord(r.a, r.s));
     recs_.push_back(r);
   }
   void end(uint64_t bytes = 0) {
     if (!on_) return;
     recs_.back().bytes = bytes;
-    HIP_CHECK(hipEventRecord(recs_.back().b, s_));
+    HIP_CHECK(hipEventRecord(recs_.back().b, recs_.back().s));
   }
   void collect(std::vector<omx_result::KStat> &out) {
     if (!on_) return;
@@ -69,6 +70,7 @@ class Timer {
   struct Rec {
     std::string name;
     hipEvent_t a, b;
+    hipStream_t s;
     uint64_t bytes = 0;
   };
   bool on_;
@@ -89,7 +91,7 @@ __global__ void k_unpack_tuple(const uint64_t *keys, uint64_t n, int k, int vbit
 class Executor {
  public:
   Executor(Graph &g, const Plan &p, const omx_exec_options &o)
-      : g_(g), p_(p), o_(o), s_(g.stream), pool_(g.pool), tm_((o.flags & OMX_FLAG_KERNEL_TIMING) != 0, g.stream) {
+      : g_(g), p_(p), o_(o), s_(g.stream), s2_(g.stream2), pool_(g.pool), tm_((o.flags & OMX_FLAG_KERNEL_TIMING) != 0, g.stream) {
     nwords_ = ((uint64_t)g.V + 63) / 64;
     // rows with at least this many neighbours take the chunked kernel (tests lower it to force the path)
     if (const char *h = std::getenv("OMX_HEAVY_DEG")) heavy_deg_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
@@ -175,7 +177,7 @@ class Executor {
   Graph &g_;
   const Plan &p_;
   omx_exec_options o_;
-  hipStream_t s_;
+  hipStream_t s_, s2_;
   DevicePool &pool_;
   Timer tm_;
   uint64_t nwords_;
@@ -229,8 +231,42 @@ class Executor {
       d.n = (int32_t)pp.code.size();
       for (size_t i = 0; i < pp.code.size(); ++i) d.code[i] = pp.code[i];
       for (size_t i = 0; i < pp.deg.size(); ++i) d.deg[i] = make_adj(pp.deg[i]);
+      match_atoms(pp, d);
     }
     return d;
+  }
+
+  // [COL c, INT/DBL k, CMP] (AND|OR [COL, INT/DBL, CMP])* → DPred atoms (evaluated without the VM)
+  void match_atoms(const PredProgram &pp, DPred &d) const {
+    const auto &c = pp.code;
+    if (c.size() < 3 || c.size() > 4 * 3 + 3) return;
+    int n = 0, conj = -1;
+    size_t i = 0;
+    while (i < c.size()) {
+      if (i + 2 >= c.size() || c[i].op != P_PUSH_COL || (c[i + 1].op != P_PUSH_INT && c[i + 1].op != P_PUSH_DBL) ||
+          c[i + 2].op < P_EQ || c[i + 2].op > P_GE || n >= 4)
+        return;
+      const int col = c[i].arg;
+      const bool dcol = g_.props[col].type == OMX_PROP_DOUBLE, dk = c[i + 1].op == P_PUSH_DBL;
+      d.atom_col[n] = col;
+      d.atom_op[n] = c[i + 2].op;
+      d.atom_dbl[n] = dcol || dk;
+      d.atom_i[n] = c[i + 1].i;
+      d.atom_d[n] = dk ? c[i + 1].d : (double)c[i + 1].i;
+      ++n;
+      i += 3;
+      if (n > 1) {
+        if (i >= c.size() || (c[i].op != P_AND && c[i].op != P_OR)) return;
+        int cj = c[i].op == P_AND;
+        if (conj >= 0 && cj != conj) return;
+        conj = cj;
+        ++i;
+      } else if (i < c.size()) {
+        // the second atom follows; its connective comes after it
+      }
+    }
+    d.n_atoms = n;
+    d.conj = conj < 0 ? 1 : conj;
   }
 
   void eval_bitmap(int prog, int class_id, int64_t depth, uint64_t *words) {
@@ -369,8 +405,12 @@ class Executor {
     // heavy kernel: a worker is a wave (4 per block); light kernel: a worker is a block
     constexpr unsigned WPB = kHeavyBlock / 64;
     const uint64_t hblocks = (nchunks + WPB - 1) / WPB;
-    const unsigned gh = nchunks ? (unsigned)std::min<uint64_t>(hblocks, (uint64_t)cus() * expand_blocks_per_cu(true, single, filt, write)) : 0;
-    const unsigned gl = ntiles ? (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus() * expand_blocks_per_cu(false, single, filt, write)) : 0;
+    // persistent grids: every resident slot. (Running the two kernels side by side on split grids
+    // was measured slower: the light kernel is latency-bound per tile and needs the whole chip.)
+    const uint64_t sh = (uint64_t)cus() * expand_blocks_per_cu(true, single, filt, write);
+    const uint64_t sl = (uint64_t)cus() * expand_blocks_per_cu(false, single, filt, write);
+    const unsigned gh = nchunks ? (unsigned)std::min<uint64_t>(hblocks, sh) : 0;
+    const unsigned gl = ntiles ? (unsigned)std::min<uint64_t>(ntiles, sl) : 0;
     const uint64_t wh = (uint64_t)gh * WPB;
     const uint64_t caph = gh ? (nchunks + wh - 1) / wh * (uint64_t)kChunk : 0;
     const uint64_t capl = gl ? (ntiles + gl - 1) / gl * (uint64_t)kExpandTile : 0;

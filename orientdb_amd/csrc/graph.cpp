@@ -79,6 +79,7 @@ Graph::~Graph() {
     for (auto &e : esets) { f(e.d_out_rp); f(e.d_in_rp); f(e.d_out_col); f(e.d_in_col); }
     for (auto &p : props) { f(p.d_values); f(p.d_present); }
     if (stream) (void)hipStreamDestroy(stream);
+    if (stream2) (void)hipStreamDestroy(stream2);
   }
 }
 
@@ -308,6 +309,7 @@ Graph *graph_create(const omx_graph_desc *d) {
   if (g->device >= 0) {
     HIP_CHECK(hipSetDevice(g->device));
     HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking));
     uint64_t &acc = g->device_bytes;
     g->d_vclass = upload(d->vertex_class, V, acc);
     g->d_rids = upload(d->rids, V, acc);

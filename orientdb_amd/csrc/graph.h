@@ -119,6 +119,7 @@ struct Graph {
   DColumn *d_cols = nullptr;
   uint64_t device_bytes = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // side stream: light-row expansion runs beside the heavy-row one
   DevicePool pool;
 
   ~Graph();

@@ -70,12 +70,36 @@ __device__ __forceinline__ int vm_cmp(const VmVal &a, const VmVal &b) {
 
 __device__ __forceinline__ bool vm_truthy(const VmVal &a) { return a.t == 3 && a.i != 0; }
 
+__device__ __forceinline__ bool atom_cmp(int op, int c) {
+  return op == P_EQ ? c == 0 : op == P_NE ? c != 0 : op == P_LT ? c < 0 : op == P_LE ? c <= 0 : op == P_GT ? c > 0 : c >= 0;
+}
+
 __device__ bool eval_pred(const DPred &P, uint32_t v, int64_t depth) {
   if (P.use_class) {
     uint32_t c = P.vclass[v];
     if (!((P.class_mask[c >> 6] >> (c & 63)) & 1ull)) return false;
   }
   if (P.n == 0) return true;
+  if (P.n_atoms) {  // column OP constant atoms: no interpreter stack (no scratch)
+    bool acc = P.conj != 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= P.n_atoms) break;
+      const VmVal x = vm_col(P.cols[P.atom_col[k]], v);
+      bool r;
+      if (x.t == 0) {
+        r = P.atom_op[k] == P_NE;  // null: = < <= > >= false, != true
+      } else if (P.atom_dbl[k]) {
+        const double a = x.t == 2 ? x.d : (double)x.i, b = P.atom_d[k];
+        r = atom_cmp(P.atom_op[k], a < b ? -1 : (a > b ? 1 : 0));
+      } else {
+        const int64_t b = P.atom_i[k];
+        r = atom_cmp(P.atom_op[k], x.i < b ? -1 : (x.i > b ? 1 : 0));
+      }
+      acc = P.conj ? (acc && r) : (acc || r);
+    }
+    return acc;
+  }
   VmVal st[16];
   int sp = 0;
   for (int pc = 0; pc < P.n; ++pc) {
