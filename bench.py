@@ -63,6 +63,20 @@ def cpu_baseline(g, query, target_s=12.0):
             "bindings_per_s": bindings / secs}
 
 
+def reduce_over_ranks(dist, dt, edges, bindings, rows):
+    """Whole-job totals from per-rank step statistics: time = MAX over ranks (the slowest rank ends the
+    job), edges/bindings/rows = SUM (roots are sharded v % N == rank, so every root's rows live on
+    exactly one rank and the per-rank results are disjoint). dist=None → single process."""
+    if dist is None:
+        return float(dt), float(edges), float(bindings), float(rows)
+    import torch
+    t = torch.tensor([float(dt)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    s = torch.tensor([float(edges), float(bindings), float(rows)], dtype=torch.float64)
+    dist.all_reduce(s, op=dist.ReduceOp.SUM)
+    return t.item(), s[0].item(), s[1].item(), s[2].item()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,14 +103,6 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    def allreduce(x, op):
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        dist.all_reduce(t, op=op)
-        return t.item()
-
     workload, query = QUERIES[args.query]
     t_build = time.perf_counter()
     g = o.GraphSnapshot.rmat(args.scale, device=local, keep_csr=(rank == 0 and world == 1 and not args.no_cpu_baseline))
@@ -122,13 +128,10 @@ def main():
     hip_sync()
     barrier()
     dt = time.perf_counter() - t0
-    dt_max = allreduce(dt, dist.ReduceOp.MAX if dist else None)
     edges = sum(i["edges_traversed"] for i in infos)
     bindings = sum(i["bindings"] for i in infos)
     rows = infos[-1]["n_rows"]
-    edges_all = allreduce(edges, dist.ReduceOp.SUM if dist else None)
-    bindings_all = allreduce(bindings, dist.ReduceOp.SUM if dist else None)
-    rows_all = allreduce(rows, dist.ReduceOp.SUM if dist else None)
+    dt_max, edges_all, bindings_all, rows_all = reduce_over_ranks(dist, dt, edges, bindings, rows)
     if rank != 0:
         if dist:
             dist.destroy_process_group()

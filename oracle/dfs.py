@@ -120,7 +120,7 @@ def _bm_from_mask(mask):
     return words
 
 
-def run(g, query, params=None, nthreads=1, emit=True, root_sample=None):
+def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=None):
     """Returns dict(rows=np.uint32[n, k] (distinct, sorted; None when emit=False), aliases, bindings,
     edges, seconds, nroots)."""
     mo = MatchOracle(g.schema, query)
@@ -188,6 +188,8 @@ def run(g, query, params=None, nthreads=1, emit=True, root_sample=None):
     if len(bound) != len(aliases):
         raise NotImplementedError("oracle C path: cartesian product")
     roots = np.nonzero(cand_mask(root))[0].astype(np.uint32)
+    if shard is not None:  # the multi-GPU partition: root vertex v belongs to rank v % world
+        roots = roots[roots % shard[1] == shard[0]]
     if root_sample is not None:
         roots = roots[:root_sample]
     out = C.POINTER(C.c_uint32)()
