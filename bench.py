@@ -21,12 +21,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "MATCH edges traversed/sec (GTEPS) + bindings/sec, RMAT-24 2-hop, 1-8 GPUs"
+# name → (workload, query, default RMAT scale)
 QUERIES = {
     "c2": ("C2: RMAT 2-hop MATCH with WHERE property filter on both ends",
-           "MATCH {class:Person,as:a,where:(age < 1)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a,b,c"),
-    "c1": ("C1: RMAT 2-hop MATCH friends-of-friends", "MATCH {class:Person}-Knows->{}-Knows->{as:fof} RETURN fof"),
-    "c4": ("C4: cyclic triangle MATCH", "MATCH {class:Person,as:a}-Knows->{as:b}-Knows->{as:c}-Knows->{as:a} RETURN a,b,c"),
+           "MATCH {class:Person,as:a,where:(age < 1)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a,b,c", 22),
+    "c1": ("C1: RMAT 2-hop MATCH friends-of-friends", "MATCH {class:Person}-Knows->{}-Knows->{as:fof} RETURN fof", 16),
+    "c3": ("C3: variable-length MATCH out('Knows'){while:($depth<4)} from 64 roots (multi-source BFS)",
+           "MATCH {class:Person,as:s,where:(uid < 64)}-Knows->{as:v, while:($depth < 4)} RETURN s, v", 24),
+    "c4": ("C4: cyclic triangle MATCH (a->b->c->a) via sorted-adjacency intersection, LDBC-SNB-like SF10 Knows",
+           "MATCH {class:Person,as:a}-Knows->{as:b}-Knows->{as:c}-Knows->{as:a} RETURN a,b,c", "ldbc"),
 }
+LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # ≈7e4 Person, ≈2e6 Knows
+# kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)
+HOT_KERNELS = ("k_expand_heavy", "k_expand_light", "k_check", "k_bfs_pull", "k_bfs_push", "k_bfs_prep", "k_bfs_emit",
+               "k_gather_cols", "k_compact_segments")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md §Chip-level parameters)
 
 
@@ -35,12 +43,35 @@ def hip_sync():
     ctypes.CDLL("libamdhip64.so.7").hipDeviceSynchronize()
 
 
+def cpu_baseline_varlen(g, nroots, depth, target_s, threads):
+    """configs[2]: the oracle's C BFS restatement (oracle/bfs_ref.c), one root per thread."""
+    import numpy as np
+    from oracle import dfs
+    rp, col = g.csr
+    roots = np.arange(nroots, dtype=np.uint32)
+    edges = pairs = 0
+    secs = 0.0
+    reps = 0
+    while secs < target_s and reps < 1000:
+        r = dfs.bfs_varlen(rp, col, roots, max_depth=depth, nthreads=threads, emit=False)
+        edges += r["edges"]
+        pairs += r["n"]
+        secs += r["seconds"]
+        reps += 1
+    return {"value": edges / secs / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
+            "sample": "all %d roots x %d repetitions (%.1f s, %d edges, %d result rows; oracle/bfs_ref.c BFS, %d threads)" % (
+                nroots, reps, secs, edges, pairs, threads),
+            "bindings_per_s": pairs / secs}
+
+
 def cpu_baseline(g, query, target_s=12.0):
     """The oracle's C DFS restatement (oracle/dfs_ref.c) on the host cores, on a bounded sample of
     the same workload's roots; GTEPS over the sampled roots."""
     import numpy as np
     from oracle import dfs
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    if "while:($depth < 4)" in query:
+        return cpu_baseline_varlen(g, 64, 4, target_s, threads)
     rp, col = g.csr
     cg = dfs.CsrGraph(rp, col, {"uid": np.arange(g.V, dtype=np.int64), "age": g.age})
     probe = dfs.run(cg, query, nthreads=threads, emit=False, root_sample=64)
@@ -82,7 +113,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--scale", type=int, default=22)
+    ap.add_argument("--scale", default=None, help="RMAT scale or 'ldbc' (default: the query's config)")
     ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -103,9 +134,18 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    workload, query = QUERIES[args.query]
+    workload, query, default_scale = QUERIES[args.query]
+    if args.scale is None:
+        args.scale = default_scale
     t_build = time.perf_counter()
-    g = o.GraphSnapshot.rmat(args.scale, device=local, keep_csr=(rank == 0 and world == 1 and not args.no_cpu_baseline))
+    keep = rank == 0 and world == 1 and not args.no_cpu_baseline
+    if args.scale == "ldbc":
+        g = o.GraphSnapshot.ldbc_like(device=local, keep_csr=keep, **LDBC_SF10)
+        graph_desc = {"graph": "LDBC-SNB-like Knows (gen.cpp omx_ldbc_knows_generate)", **LDBC_SF10}
+    else:
+        args.scale = int(args.scale)
+        g = o.GraphSnapshot.rmat(args.scale, device=local, keep_csr=keep)
+        graph_desc = {"graph": "RMAT", "scale": args.scale, "edge_factor": 16}
     t_build = time.perf_counter() - t_build
     st = o.OMatchStatement(query)
     flags = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_KERNEL_TIMING
@@ -136,8 +176,8 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    # the dominant kernel: the expansion kernel (heavy-row chunks or light-row merge path) with the most time
-    cands = {k: v for k, v in kst.items() if k in ("k_expand_heavy", "k_expand_light")}
+    # the dominant kernel: the hot-path kernel with the most device time
+    cands = {k: v for k, v in kst.items() if k in HOT_KERNELS}
     dom = max(cands, key=lambda k: cands[k]["ms"]) if cands else "k_expand_heavy"
     exp = cands.get(dom, {"launches": 1, "ms": 0.0, "alg_bytes": 0})
     achieved = exp["alg_bytes"] / (exp["ms"] / 1e3) / 1e9 if exp["ms"] > 0 else 0.0
@@ -153,8 +193,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic (Graph500 RMAT, deterministic splitmix64 generator in libomx)",
-        "config": {"workload": workload, "query": query, "scale": args.scale, "edge_factor": 16,
+        "data": "synthetic (%s, deterministic splitmix64 generator in libomx)" % graph_desc["graph"],
+        "config": {"workload": workload, "query": query, **graph_desc,
                    "V": g.V, "E": g.n_edges, "rows_per_step": int(rows_all),
                    "edges_per_step": int(edges_all / args.steps), "bindings_per_step": int(bindings_all / args.steps),
                    "parallelism": "roots sharded v%%N across %d GPU(s), graph replicated" % world,

@@ -190,6 +190,11 @@ const char *omx_version(void);
  * and parallel edges. Outputs are host arrays owned by the library (omx_host_free). */
 int omx_rmat_generate(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t simple, uint64_t **out_row_ptr,
                       uint32_t **out_col, uint64_t *n_edges);
+/* LDBC-SNB-like Knows graph (configs[3]): n_persons vertices, ≈ target_edges directed
+ * edges (unique pairs, one direction each), skewed degrees and high clustering from correlated
+ * windows; rows sorted. Deterministic in (n_persons, target_edges, seed). */
+int omx_ldbc_knows_generate(uint32_t n_persons, uint64_t target_edges, uint64_t seed, uint64_t **out_row_ptr,
+                            uint32_t **out_col, uint64_t *n_edges);
 /* CSR transpose (host, multi-threaded); rows of the output are sorted. */
 int omx_csr_transpose(uint32_t n_vertices, const uint64_t *row_ptr, const uint32_t *col, uint64_t **t_row_ptr,
                       uint32_t **t_col);

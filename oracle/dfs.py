@@ -43,6 +43,10 @@ def lib():
         L.dfs_run.argtypes = [C.POINTER(dfs_plan), C.c_int32, C.POINTER(C.c_uint32), C.c_int64, C.c_int32, C.c_int32,
                               C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.dfs_free.argtypes = [C.c_void_p]
+        L.bfs_varlen.restype = C.c_int64
+        L.bfs_varlen.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
+                                 C.c_int64, C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
+                                 C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         _lib = L
     return _lib
 
@@ -206,3 +210,28 @@ def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=No
         lib().dfs_free(C.cast(out, C.c_void_p))
         rows = np.unique(arr.reshape(n, len(aliases)), axis=0) if n else arr.reshape(0, len(aliases))
     return {"rows": rows, "aliases": aliases, "bindings": b, "edges": edges.value, "seconds": dt, "nroots": len(roots)}
+
+
+def bfs_varlen(rp, col, roots, max_depth=-1, where_mask=None, nthreads=1, emit=True):
+    """oracle/bfs_ref.c: variable-length item with depth-free WHERE and a depth-only while (the result
+    is the BFS ball of radius max_depth; -1 = unbounded). Returns dict(pairs=np.uint32[n, 2] of
+    (root index, v) or None, n, edges, seconds)."""
+    rp = np.ascontiguousarray(rp, np.uint64)
+    col = np.ascontiguousarray(col, np.uint32)
+    roots = np.ascontiguousarray(roots, np.uint32)
+    V = len(rp) - 1
+    wb = _bm_from_mask(np.asarray(where_mask, bool)) if where_mask is not None else None
+    out = C.POINTER(C.c_uint32)()
+    npairs = C.c_uint64()
+    edges = C.c_uint64()
+    t0 = time.perf_counter()
+    n = lib().bfs_varlen(rp.ctypes.data_as(C.POINTER(C.c_uint64)), col.ctypes.data_as(C.POINTER(C.c_uint32)), V,
+                         roots.ctypes.data_as(C.POINTER(C.c_uint32)), len(roots), int(max_depth),
+                         wb.ctypes.data_as(C.POINTER(C.c_uint64)) if wb is not None else None, int(nthreads),
+                         int(emit), C.byref(out), C.byref(npairs), C.byref(edges))
+    dt = time.perf_counter() - t0
+    pairs = None
+    if emit:
+        pairs = np.ctypeslib.as_array(out, shape=(max(1, npairs.value) * 2,))[:npairs.value * 2].reshape(-1, 2).copy()
+        lib().dfs_free(C.cast(out, C.c_void_p))
+    return {"pairs": pairs, "n": int(n), "edges": int(edges.value), "seconds": dt}

@@ -83,6 +83,8 @@ SIGNATURES = {
     "omx_rmat_generate": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int32,
                                     C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)),
                                     C.POINTER(C.c_uint64)]),
+    "omx_ldbc_knows_generate": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(C.POINTER(C.c_uint64)),
+                                          C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64)]),
     "omx_csr_transpose": (C.c_int, [C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
                                     C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32))]),
     "omx_synthetic_int_column": (C.c_int, [C.c_uint32, C.c_uint64, C.c_int32, C.POINTER(C.POINTER(C.c_int32))]),

@@ -1,0 +1,344 @@
+// bfs.hip — multi-source level-synchronous BFS for variable-length MATCH items.
+//
+// OMatchPathItem.executeTraversal with while/maxDepth (P/OMatchPathItem.java:79-105) enumerates
+// walks depth-first without a visited set. When WHERE does not read $depth and `while` is either
+// depth-free or reads nothing but $depth, the reference's result set for one start vertex is exactly
+// {v : BFS distance(start, v) ≤ D in the graph restricted to expandable nodes, WHERE(v)} — so it is
+// computed here by BFS, 64 binding rows at a time: every vertex holds a u64 lane mask (bit i = row i
+// of the batch), and one level is
+//     next[w] = OR_{v→w} (frontier[v] ∧ while(v)) ∧ ¬visited[w]
+// evaluated top-down (push: atomicOr over the frontier's edges, for small frontiers) or bottom-up
+// (pull: merge-path tiles over the reversed adjacency of the vertices that still miss a lane — the
+// RMAT levels that cover most of the graph). The result is emitted once per batch from the visited
+// masks.
+#include <hip/hip_runtime.h>
+
+#include "devutil.h"
+#include "kernels.h"
+
+namespace omx {
+
+namespace {
+constexpr int kB = 256;
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+}  // namespace
+
+// seeds: lane i of the batch starts at src[row0 + i]
+__global__ void k_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier) {
+  int i = threadIdx.x;
+  if (i < nl) atomicOr((unsigned long long *)&frontier[src[row0 + i]], 1ull << i);
+}
+void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, hipStream_t s) {
+  hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(64), 0, s, src, row0, nl, frontier);
+  KCHECK("k_bfs_seed");
+}
+
+// Level prologue over every vertex (grid-stride): m = frontier ∧ ¬visited (the level's new vertices) is
+// merged into visited; if the level expands, m is cut to the `while` bitmap and the frontier's
+// statistics are accumulated (one atomic per block and counter): stats[0] = Σ popc(m)·deg (the edges
+// the reference traverses, SURVEY §8(d) E_t), stats[1] = Σ deg over active vertices (push work),
+// stats[2] = active vertices.
+__global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V,
+                                                 const uint64_t *while_bm, int expand, DAdj adj,
+                                                 unsigned long long *stats) {
+  __shared__ uint64_t s_r[3][kB / 64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t te = 0, td = 0, tn = 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x; v < V; v += (uint64_t)gridDim.x * kB) {
+    const uint64_t f = frontier[v];
+    if (!f) continue;
+    const uint64_t vis = visited[v];
+    uint64_t m = f & ~vis;
+    if (m) visited[v] = vis | m;
+    if (expand && while_bm && !bm_test(while_bm, (uint32_t)v)) m = 0;
+    if (m != f) frontier[v] = m;
+    if (m && expand) {
+      const uint64_t d = adj_degree(adj, (uint32_t)v);
+      te += (uint64_t)__popcll(m) * d;
+      td += d;
+      tn += 1;
+    }
+  }
+  if (!expand) return;
+  te = wave_sum_u64(te);
+  td = wave_sum_u64(td);
+  tn = wave_sum_u64(tn);
+  if (lane == 0) {
+    s_r[0][wave] = te;
+    s_r[1][wave] = td;
+    s_r[2][wave] = tn;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    uint64_t x = 0;
+    for (int w = 0; w < kB / 64; ++w) x += s_r[threadIdx.x][w];
+    if (x) atomicAdd(&stats[threadIdx.x], (unsigned long long)x);
+  }
+}
+void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
+                     const DAdj &adj, unsigned long long *stats, int cus, hipStream_t s) {
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 8);
+  hipLaunchKernelGGL(k_bfs_prep, dim3(g), dim3(kB), 0, s, frontier, visited, V, while_bm, (int)expand, adj, stats);
+  KCHECK("k_bfs_prep");
+}
+
+// active vertices (non-zero frontier mask) → list, one atomic per block and iteration (push levels only)
+__global__ __launch_bounds__(kB) void k_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list,
+                                                 unsigned long long *count) {
+  __shared__ uint32_t s_w[kB / 64];
+  __shared__ uint32_t s_base;
+  for (uint64_t v0 = (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
+    const uint64_t v = v0 + threadIdx.x;
+    const bool act = v < V && frontier[v] != 0;
+    uint32_t tot;
+    const uint32_t off = block_excl_scan<kB>(act ? 1u : 0u, s_w, &tot);
+    if (threadIdx.x == 0 && tot) s_base = (uint32_t)atomicAdd(count, (unsigned long long)tot);
+    __syncthreads();
+    if (act) list[s_base + off] = (uint32_t)v;
+    __syncthreads();
+  }
+}
+void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsigned long long *count, int cus,
+                     hipStream_t s) {
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 8);
+  hipLaunchKernelGGL(k_bfs_list, dim3(g), dim3(kB), 0, s, frontier, V, list, count);
+  KCHECK("k_bfs_list");
+}
+
+// degree of every listed vertex in one adjacency part (+ a trailing 0 for the exclusive scan)
+__global__ void k_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nl) deg[i] = rp[list[i] + 1] - rp[list[i]];
+  else if (i == nl) deg[nl] = 0;
+}
+void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg, hipStream_t s) {
+  hipLaunchKernelGGL(k_bfs_list_deg, dim3(nblocks(nl + 1, kB)), dim3(kB), 0, s, list, nl, rp, deg);
+  KCHECK("k_bfs_list_deg");
+}
+
+// Top-down: one thread per frontier edge (consecutive threads → consecutive col[] entries); the
+// owning list entry is found by binary search in the degree prefix.
+__global__ __launch_bounds__(kB) void k_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl,
+                                                 uint64_t etot, const uint64_t *rp, const uint32_t *col,
+                                                 const uint64_t *frontier, const uint64_t *visited, uint64_t *next) {
+  const uint64_t stride = (uint64_t)gridDim.x * kB;
+  for (uint64_t e = (uint64_t)blockIdx.x * kB + threadIdx.x; e < etot; e += stride) {
+    uint64_t lo = 0, hi = nl;  // largest i with loffs[i] <= e
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (loffs[mid] <= e) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t v = list[lo];
+    const uint32_t w = col[rp[v] + (e - loffs[lo])];
+    const uint64_t m = frontier[v] & ~visited[w];
+    if (m && (next[w] & m) != m) atomicOr((unsigned long long *)&next[w], (unsigned long long)m);
+  }
+}
+void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, uint64_t etot, const uint64_t *rp,
+                     const uint32_t *col, const uint64_t *frontier, const uint64_t *visited, uint64_t *next,
+                     int cus, hipStream_t s) {
+  if (!etot) return;
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(etot, kB), (uint64_t)cus * 16);
+  hipLaunchKernelGGL(k_bfs_push, dim3(g), dim3(kB), 0, s, list, loffs, nl, etot, rp, col, frontier, visited, next);
+  KCHECK("k_bfs_push");
+}
+
+__global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part);
+
+// Bottom-up over one reversed adjacency part: merge-path tiles of kPullTile items over (vertices +
+// in-edges), partitioned once per traversal from the part's row_ptr (k_pull_partition with offs = rp). Consecutive lanes take consecutive in-edges (coalesced col[] loads); the in-edges of a
+// vertex whose lanes are all visited are skipped; each edge gathers its source's frontier mask.
+// Masks are OR-reduced per vertex by a segmented wave scan, merged in LDS (ds_or_b64) and written
+// with one atomicOr per vertex and tile (next[] is zeroed first; k_bfs_prep masks out visited lanes).
+constexpr int kPullB = 256, kPullIPT = 4, kPullTile = kPullB * kPullIPT;
+
+__global__ __launch_bounds__(kPullB) void k_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col,
+                                                     const uint64_t *part, uint64_t E, uint64_t ntiles,
+                                                     uint64_t lanes, const uint64_t *frontier,
+                                                     const uint64_t *visited, uint64_t *next) {
+  constexpr int B = kPullB, IPT = kPullIPT, T = kPullTile, W = B / 64;
+  __shared__ uint64_t s_base[T + 1];
+  __shared__ uint64_t s_need[T + 1];
+  __shared__ unsigned long long s_acc[T + 1];
+  __shared__ uint16_t s_ls[T + 1];
+  __shared__ uint16_t s_seg[T];
+  __shared__ uint32_t s_wmax[W];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint64_t d0 = t * (uint64_t)T;
+    const uint64_t d1 = min(d0 + (uint64_t)T, (uint64_t)V + E);
+    const uint64_t i0 = part[t], i1 = part[t + 1];
+    const uint64_t j0 = d0 - i0, j1 = d1 - i1;
+    const uint32_t ne = (uint32_t)(j1 - j0);
+    if (ne == 0) continue;  // uniform: only edge-less vertices in this tile
+    const uint64_t rlast = min(i1, (uint64_t)V - 1);
+    const uint32_t nr = (uint32_t)(rlast - i0 + 1);
+    for (uint32_t x = tid; x < ne; x += B) s_seg[x] = 0;
+    __syncthreads();
+    for (uint32_t lr = tid; lr < nr; lr += B) {
+      const uint64_t r = i0 + lr;
+      const uint64_t rs = rp[r], re = rp[r + 1];
+      const uint64_t s = rs > j0 ? rs - j0 : 0;
+      const uint64_t e = re < j1 ? (re > j0 ? re - j0 : 0) : ne;
+      s_ls[lr] = (uint16_t)(s < ne ? s : ne);
+      if (e > s && s < ne) s_seg[s] = (uint16_t)lr;
+      s_base[lr] = rs + (rs < j0 ? j0 - rs : 0);
+      s_need[lr] = (e > s) ? (lanes & ~visited[r]) : 0;
+      s_acc[lr] = 0;
+    }
+    __syncthreads();
+    {  // inclusive max-scan of s_seg → owning vertex of every tile edge
+      uint32_t vals[IPT];
+      uint32_t m = 0;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const uint32_t idx = tid * IPT + i;
+        const uint32_t x = idx < ne ? s_seg[idx] : 0;
+        m = m > x ? m : x;
+        vals[i] = m;
+      }
+      uint32_t incl = m;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl = incl > y ? incl : y;
+      }
+      if (lane == 63) s_wmax[wave] = incl;
+      uint32_t excl = __shfl_up(incl, 1, 64);
+      if (lane == 0) excl = 0;
+      __syncthreads();
+      uint32_t wp = 0;
+      for (uint32_t w = 0; w < wave; ++w) wp = wp > s_wmax[w] ? wp : s_wmax[w];
+      const uint32_t pre = excl > wp ? excl : wp;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const uint32_t idx = tid * IPT + i;
+        if (idx < ne) s_seg[idx] = (uint16_t)(pre > vals[i] ? pre : vals[i]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const uint32_t jl = k * B + tid;
+      const bool valid = jl < ne;
+      const uint32_t lr = valid ? s_seg[jl] : 0xFFFFu;
+      uint64_t f = 0;
+      if (valid) {
+        const uint64_t need = s_need[lr];
+        if (need) f = frontier[col[s_base[lr] + (jl - s_ls[lr])]] & need;
+      }
+      // segmented inclusive OR over the wave (a vertex's edges are consecutive lanes)
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t yf = __shfl_up(f, off, 64);
+        const uint32_t ylr = __shfl_up(lr, off, 64);
+        if (lane >= (uint32_t)off && ylr == lr) f |= yf;
+      }
+      const uint32_t nlr = __shfl_down(lr, 1, 64);
+      const bool tail = valid && (lane == 63 || nlr != lr);
+      if (tail && f) atomicOr(&s_acc[lr], (unsigned long long)f);
+    }
+    __syncthreads();
+    for (uint32_t lr = tid; lr < nr; lr += B) {
+      const unsigned long long a = s_acc[lr];
+      if (a) atomicOr((unsigned long long *)&next[i0 + lr], a);
+    }
+    __syncthreads();
+  }
+}
+uint64_t bfs_pull_tiles(uint32_t V, uint64_t E) { return ((uint64_t)V + E + kPullTile - 1) / kPullTile; }
+void launch_bfs_pull_partition(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t *part, hipStream_t s) {
+  // merge path over A = row ends and B = edges with tiles of kPullTile (same split as k_mp_partition)
+  const uint64_t ntiles = bfs_pull_tiles(V, E);
+  hipLaunchKernelGGL(k_pull_partition, dim3(nblocks(ntiles + 1, kB)), dim3(kB), 0, s, rp, (uint64_t)V, E, ntiles, part);
+  KCHECK("k_pull_partition");
+}
+void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const uint64_t *part, uint64_t E,
+                     uint64_t lanes, const uint64_t *frontier, const uint64_t *visited, uint64_t *next, int cus,
+                     hipStream_t s) {
+  const uint64_t ntiles = bfs_pull_tiles(V, E);
+  if (!ntiles) return;
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bfs_pull, kPullB, 0) != hipSuccess || per < 1) per = 2;
+  const unsigned g = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * per);
+  hipLaunchKernelGGL(k_bfs_pull, dim3(g), dim3(kPullB), 0, s, V, rp, col, part, E, ntiles, lanes, frontier, visited,
+                     next);
+  KCHECK("k_bfs_pull");
+}
+
+__global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  uint64_t d = t * (uint64_t)kPullTile;
+  if (d > R + E) d = R + E;
+  uint64_t lo = d > E ? d - E : 0, hi = d < R ? d : R;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (offs[mid + 1] <= d - 1 - mid) lo = mid + 1;
+    else hi = mid;
+  }
+  part[t] = lo;
+}
+
+// Result emission from the visited masks: (row0 + lane, v) for every set lane of v with emit(v).
+__global__ __launch_bounds__(kB) void k_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V,
+                                                       uint32_t *blk) {
+  __shared__ uint32_t s_w[kB / 64];
+  const uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  uint32_t c = 0;
+  if (v < V && (!emit_bm || bm_test(emit_bm, (uint32_t)v))) c = (uint32_t)__popcll(visited[v]);
+  uint32_t tot;
+  block_excl_scan<kB>(c, s_w, &tot);
+  if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(kB) void k_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V,
+                                                       const uint64_t *blk_offs, uint32_t row0, uint32_t *out_row,
+                                                       uint32_t *out_v) {
+  __shared__ uint32_t s_w[kB / 64];
+  const uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  uint64_t m = 0;
+  if (v < V && (!emit_bm || bm_test(emit_bm, (uint32_t)v))) m = visited[v];
+  uint32_t tot;
+  const uint32_t off = block_excl_scan<kB>((uint32_t)__popcll(m), s_w, &tot);
+  uint64_t o = blk_offs[blockIdx.x] + off;
+  while (m) {
+    const int l = __builtin_ctzll(m);
+    out_row[o] = row0 + (uint32_t)l;
+    out_v[o] = (uint32_t)v;
+    ++o;
+    m &= m - 1;
+  }
+}
+void launch_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, uint32_t *blk, hipStream_t s) {
+  hipLaunchKernelGGL(k_bfs_emit_count, dim3(nblocks(V, kB)), dim3(kB), 0, s, visited, emit_bm, V, blk);
+  KCHECK("k_bfs_emit_count");
+}
+void launch_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, const uint64_t *blk_offs,
+                           uint32_t row0, uint32_t *out_row, uint32_t *out_v, hipStream_t s) {
+  hipLaunchKernelGGL(k_bfs_emit_write, dim3(nblocks(V, kB)), dim3(kB), 0, s, visited, emit_bm, V, blk_offs, row0,
+                     out_row, out_v);
+  KCHECK("k_bfs_emit_write");
+}
+unsigned bfs_blocks(uint32_t V) { return nblocks(V, kB); }
+
+// T_BOUND: row r (lane r - row0) keeps its binding iff its bound target was reached and passes emit
+__global__ void k_bfs_bound(const uint32_t *dst, uint64_t row0, int nl, const uint64_t *visited,
+                            const uint64_t *emit_bm, uint8_t *flags) {
+  const int i = threadIdx.x;
+  if (i >= nl) return;
+  const uint32_t t = dst[row0 + i];
+  flags[row0 + i] = ((visited[t] >> i) & 1ull) && (!emit_bm || bm_test(emit_bm, t));
+}
+void launch_bfs_bound(const uint32_t *dst, uint64_t row0, int nl, const uint64_t *visited, const uint64_t *emit_bm,
+                      uint8_t *flags, hipStream_t s) {
+  hipLaunchKernelGGL(k_bfs_bound, dim3(1), dim3(64), 0, s, dst, row0, nl, visited, emit_bm, flags);
+  KCHECK("k_bfs_bound");
+}
+
+}  // namespace omx

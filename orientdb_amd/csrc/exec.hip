@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdint>
 #include <cstdlib>
 
 #include "kernels.h"
@@ -48,6 +49,14 @@ class Timer {
     if (!on_) return;
     recs_.back().bytes = bytes;
     HIP_CHECK(hipEventRecord(recs_.back().b, recs_.back().s));
+  }
+  // algorithmic bytes of a record when they are only known after the launch
+  void amend(uint64_t bytes) {
+    if (on_ && !recs_.empty()) recs_.back().bytes = bytes;
+  }
+  size_t last() const { return recs_.empty() ? 0 : recs_.size() - 1; }
+  void amend_at(size_t i, uint64_t bytes) {
+    if (on_ && i < recs_.size()) recs_[i].bytes = bytes;
   }
   void collect(std::vector<omx_result::KStat> &out) {
     if (!on_) return;
@@ -91,10 +100,14 @@ __global__ void k_unpack_tuple(const uint64_t *keys, uint64_t n, int k, int vbit
 class Executor {
  public:
   Executor(Graph &g, const Plan &p, const omx_exec_options &o)
-      : g_(g), p_(p), o_(o), s_(g.stream), s2_(g.stream2), pool_(g.pool), tm_((o.flags & OMX_FLAG_KERNEL_TIMING) != 0, g.stream) {
+      : g_(g), p_(p), o_(o), s_(g.stream), pool_(g.pool), tm_((o.flags & OMX_FLAG_KERNEL_TIMING) != 0, g.stream) {
     nwords_ = ((uint64_t)g.V + 63) / 64;
     // rows with at least this many neighbours take the chunked kernel (tests lower it to force the path)
     if (const char *h = std::getenv("OMX_HEAVY_DEG")) heavy_deg_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
+    // variable-length strategy: "bfs" (multi-source BFS whenever exact), "pairs" ((row, v) levels), auto
+    if (const char *v = std::getenv("OMX_VARLEN")) varlen_mode_ = v;
+    if (const char *f = std::getenv("OMX_FUSE_CHECK")) fuse_mode_ = f;  // "0" disables the intersection
+    if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max<uint64_t>(1, std::strtoull(d, nullptr, 10));
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
   }
@@ -117,6 +130,18 @@ class Executor {
         // segmented in HBM when the rows are not copied to the host
         bool seg_ok = last && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES &&
                       (o_.flags & OMX_FLAG_KEEP_DEVICE);
+        // expansion + closing check fused into one intersection pass
+        const Step *fuse = nullptr;
+        if (st.kind == S_EXPAND && i + 1 < p_.steps.size() && fuse_ok(st, p_.steps[i + 1])) {
+          fuse = &p_.steps[i + 1];
+          const bool last2 = i + 2 == p_.steps.size();
+          count_only = last2 && o_.mode == OMX_MODE_COUNT && p_.unique_by_construction;
+          seg_ok = last2 && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES && (o_.flags & OMX_FLAG_KEEP_DEVICE);
+          expand_step(st, !count_only, seg_ok, fuse);
+          counted_only = count_only;
+          ++i;
+          continue;
+        }
         switch (st.kind) {
           case S_ROOT: root(st); break;
           case S_EXPAND: expand_step(st, !count_only, seg_ok); counted_only = count_only; break;
@@ -177,7 +202,7 @@ class Executor {
   Graph &g_;
   const Plan &p_;
   omx_exec_options o_;
-  hipStream_t s_, s2_;
+  hipStream_t s_;
   DevicePool &pool_;
   Timer tm_;
   uint64_t nwords_;
@@ -188,6 +213,9 @@ class Executor {
   int dedup_ran_ = 0;
   int cus_ = 0;
   uint64_t heavy_deg_ = kHeavyDeg;
+  std::string varlen_mode_ = "auto";
+  std::string fuse_mode_ = "1";
+  uint64_t pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
 
   // ---- helpers -----------------------------------------------------------------------------------
@@ -339,6 +367,7 @@ class Executor {
     std::vector<DBuf<uint32_t>> carry;
     uint64_t n = 0;
     uint64_t E = 0;
+    uint64_t E_member = 0;  // edges of a fused closing check
     // block-segmented result (filtered expansion left un-compacted)
     bool segmented = false;
     DBuf<uint64_t> seg_start;
@@ -358,11 +387,21 @@ class Executor {
   // One pattern-edge expansion of R rows (src column) with an optional target bitmap, carrying the
   // listed columns. write=false only counts. allow_segmented leaves a filtered result as per-block
   // segments (the final step of a plan whose rows are distinct by construction).
+  // member_src/member_adj: fused closing check (ExpandArgs::member_src); the edges it stands for are
+  // returned in ExpandOut::E_member.
   ExpandOut expand_core(const uint32_t *src, uint64_t R, const AdjSpec &adjs, const uint64_t *filter,
-                        const std::vector<const uint32_t *> &carry, bool write, bool allow_segmented = false) {
+                        const std::vector<const uint32_t *> &carry, bool write, bool allow_segmented = false,
+                        const uint32_t *member_src = nullptr, const AdjSpec *member_adj = nullptr,
+                        const uint64_t *member_filter = nullptr) {
     ExpandOut o;
     DAdj adj = make_adj(adjs);
     if (adj.n == 0 || R == 0) return o;
+    const bool member = member_src != nullptr;
+    DBuf<unsigned long long> medges;
+    if (member) {
+      medges = DBuf<unsigned long long>(&pool_, 1);
+      HIP_CHECK(hipMemsetAsync(medges.p, 0, sizeof(unsigned long long), s_));
+    }
     // 1. degree binning + scans (light edges: merge path; heavy rows: chunks)
     DBuf<uint64_t> light(&pool_, R + 1), heavy(&pool_, R + 1), loffs(&pool_, R + 1), hoffs(&pool_, R + 1);
     DBuf<uint32_t> nch(&pool_, R + 1);
@@ -401,14 +440,14 @@ class Executor {
       tm_.end((ntiles + 1) * 8 * 20);
     }
     // 2. persistent grids and output placement
-    const bool single = adj.n == 1, filt = filter != nullptr;
+    const bool single = adj.n == 1, filt = filter != nullptr || member;
     // heavy kernel: a worker is a wave (4 per block); light kernel: a worker is a block
     constexpr unsigned WPB = kHeavyBlock / 64;
     const uint64_t hblocks = (nchunks + WPB - 1) / WPB;
     // persistent grids: every resident slot. (Running the two kernels side by side on split grids
     // was measured slower: the light kernel is latency-bound per tile and needs the whole chip.)
-    const uint64_t sh = (uint64_t)cus() * expand_blocks_per_cu(true, single, filt, write);
-    const uint64_t sl = (uint64_t)cus() * expand_blocks_per_cu(false, single, filt, write);
+    const uint64_t sh = (uint64_t)cus() * expand_blocks_per_cu(true, single, filt, write, member);
+    const uint64_t sl = (uint64_t)cus() * expand_blocks_per_cu(false, single, filt, write, member);
     const unsigned gh = nchunks ? (unsigned)std::min<uint64_t>(hblocks, sh) : 0;
     const unsigned gl = ntiles ? (unsigned)std::min<uint64_t>(ntiles, sl) : 0;
     const uint64_t wh = (uint64_t)gh * WPB;
@@ -429,6 +468,12 @@ class Executor {
     a.nchunks = nchunks;
     a.hoffs = hoffs.p;
     a.dense_base = EH;
+    if (member) {
+      a.member_src = member_src;
+      a.member_adj = make_adj(*member_adj);
+      a.member_filter = member_filter;
+      a.member_edges = medges.p;
+    }
     std::vector<DBuf<uint32_t>> outc;
     DBuf<uint32_t> odst;
     if (write) {
@@ -451,13 +496,18 @@ class Executor {
     // per emitted row, added below)
     uint64_t kb = 8 * R + 4 * E;
     // per-kernel algorithmic bytes: heavy rows carry EH edges, light rows EL (+ 8 B per row each)
+    // per-kernel algorithmic bytes (amended below once the emitted rows are known): heavy = 4·EH + out,
+    // light = 8·R + 4·EL + out, out = 4 B × written columns × rows the kernel emitted
+    const uint64_t outw = write ? 4ull * (carry.size() + 1) : 0;
+    size_t rec_h = SIZE_MAX, rec_l = SIZE_MAX;
     if (gh) {
       a.arena_base = 0;
       a.arena_cap = caph;
       a.seg_base = 0;
       tm_.begin("k_expand_heavy");
       launch_expand_heavy(a, gh, write, s_);
-      tm_.end(4 * EH + 24 * nchunks);
+      tm_.end(4 * EH + outw * (filt ? 0 : EH));
+      rec_h = tm_.last();
     }
     if (gl) {
       a.arena_base = wh * caph;
@@ -465,7 +515,8 @@ class Executor {
       a.seg_base = (uint32_t)wh;
       tm_.begin("k_expand_light");
       launch_expand(a, gl, write, s_);
-      tm_.end(8 * R + 4 * EL);
+      tm_.end(8 * R + 4 * EL + outw * (filt ? 0 : EL));
+      rec_l = tm_.last();
     }
     tm_.begin("expand_total");
     if (!filt) {
@@ -484,7 +535,15 @@ class Executor {
     hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> sit(o.seg_count.p, CastU64());
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, sit, soffs.p + 1, (int64_t)o.nseg, s_); });
     HIP_CHECK(hipMemsetAsync(soffs.p, 0, 8, s_));
-    const uint64_t n = read1(soffs.p + o.nseg);
+    uint64_t nh_n[3] = {0, 0, 0};  // rows emitted by the heavy kernel's segments, all rows, member edges
+    HIP_CHECK(hipMemcpyAsync(&nh_n[0], soffs.p + wh, 8, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipMemcpyAsync(&nh_n[1], soffs.p + o.nseg, 8, hipMemcpyDeviceToHost, s_));
+    if (member) HIP_CHECK(hipMemcpyAsync(&nh_n[2], medges.p, 8, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    o.E_member = nh_n[2];
+    const uint64_t n = nh_n[1];
+    if (rec_h != SIZE_MAX) tm_.amend_at(rec_h, 4 * EH + outw * nh_n[0]);
+    if (rec_l != SIZE_MAX) tm_.amend_at(rec_l, 8 * R + 4 * EL + outw * (n - nh_n[0]));
     o.n = n;
     if (write) kb += 4ull * (carry.size() + 1) * n;
     tm_.end(kb);
@@ -509,12 +568,16 @@ class Executor {
     return o;
   }
 
-  void expand_step(const Step &st, bool write, bool allow_segmented) {
+  // fused: the following S_CHECK closes a cycle on this step's new column (sorted-
+  // adjacency intersection instead of materialising the wedges and probing each)
+  void expand_step(const Step &st, bool write, bool allow_segmented, const Step *check = nullptr) {
     std::vector<int> cols = bound_cols();
     std::vector<const uint32_t *> carry;
     for (int c : cols) carry.push_back(col_[c].p);
-    ExpandOut o = expand_core(col_[st.src].p, R_, st.adj, bitmap(st.filter_bm), carry, write, allow_segmented);
-    edges_ += o.E;
+    ExpandOut o = expand_core(col_[st.src].p, R_, st.adj, bitmap(st.filter_bm), carry, write, allow_segmented,
+                              check ? col_[check->src].p : nullptr, check ? &check->adj : nullptr,
+                              check ? bitmap(check->filter_bm) : nullptr);
+    edges_ += o.E + o.E_member;
     R_ = o.n;
     if (!write || R_ == 0) return;
     segmented_ = o.segmented;
@@ -547,6 +610,15 @@ class Executor {
     tm_.end(n * (4 + 8ull * cols.size()));
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(nc[i]);
     R_ = n;
+  }
+
+  // S_EXPAND (x → t) followed by S_CHECK (y → t, t bound by the expansion): the check keeps a row iff
+  // t ∈ N(y), which a sorted adjacency answers by binary search inside the expansion kernels
+  bool fuse_ok(const Step &ex, const Step &ck) const {
+    if (fuse_mode_ == "0") return false;
+    if (ck.kind != S_CHECK || ck.dst != ex.dst || ck.src == ex.dst || !col_[ck.src].p) return false;
+    if (!ck.adj.sorted || ck.adj.parts.empty()) return false;
+    return true;
   }
 
   uint64_t degree_sum(const uint32_t *src, uint64_t R, const AdjSpec &adjs) {
@@ -619,6 +691,172 @@ class Executor {
   // while d < maxDepth. Without $depth in where/while a visited set per row is exact and
   // terminates on cycles.
   void varlen_step(const Step &st) {
+    bool depth_only_while = false;
+    if (varlen_mode_ != "pairs" && bfs_exact(st, depth_only_while)) {
+      const uint64_t nb = (R_ + 63) / 64;
+      if (varlen_mode_ == "bfs" || nb <= 64 || nb * (uint64_t)g_.V <= (1ull << 30)) {
+        varlen_msbfs(st, depth_only_while);
+        return;
+      }
+    }
+    varlen_pairs(st);
+  }
+
+  // The walk semantics of P/OMatchPathItem.java:79-105 equal BFS distance (bfs.hip) when WHERE does not
+  // read $depth and `while` either does not read $depth or reads nothing else (then it is a constant
+  // per level: the first depth where it is false ends the expansion).
+  bool bfs_exact(const Step &st, bool &depth_only_while) const {
+    if (st.where_prog >= 0 && p_.progs[st.where_prog].uses_depth) return false;
+    depth_only_while = false;
+    if (st.while_prog < 0 || !p_.progs[st.while_prog].uses_depth) return true;
+    const PredProgram &w = p_.progs[st.while_prog];
+    for (const auto &in : w.code)
+      if (in.op == P_PUSH_COL || in.op == P_PUSH_DEG) return false;
+    depth_only_while = true;
+    return true;
+  }
+
+  // Multi-source BFS over 64-row batches (bfs.hip). Rows (row, v) come out distinct per row.
+  void varlen_msbfs(const Step &st, bool depth_only_while) {
+    const uint64_t R = R_;
+    const uint32_t V = g_.V;
+    const DAdj adj = make_adj(st.adj);
+    AdjSpec rspec = st.adj;
+    for (auto &p : rspec.parts) p.second ^= 1;
+    const DAdj radj = make_adj(rspec);
+    uint64_t eadj = 0;
+    for (const auto &p : st.adj.parts) eadj += g_.esets[p.first].n_edges;
+    // emission bitmap = WHERE (depth-free) ∧ candidates (prefetched target)
+    DBuf<uint64_t> emit;
+    const uint64_t *emit_bm = nullptr;
+    if (st.where_prog >= 0) {
+      emit = DBuf<uint64_t>(&pool_, nwords_);
+      eval_bitmap(st.where_prog, -1, 0, emit.p);
+      emit_bm = emit.p;
+    }
+    if (st.mode == T_CAND) {
+      const uint64_t *c = bitmap(st.cand_bm);
+      if (emit_bm) launch_bitmap_and(c, emit.p, nwords_, s_);
+      else emit_bm = c;
+    }
+    DBuf<uint64_t> wbm;
+    const uint64_t *while_bm = nullptr;
+    DPred wconst{};
+    if (st.while_prog >= 0 && !depth_only_while) {
+      wbm = DBuf<uint64_t>(&pool_, nwords_);
+      eval_bitmap(st.while_prog, -1, 0, wbm.p);
+      while_bm = wbm.p;
+    }
+    const bool while_never = depth_only_while && p_.progs[st.while_prog].const_false;
+    if (depth_only_while) wconst = make_pred(st.while_prog, -1);
+    DBuf<uint64_t> fr(&pool_, V), nx(&pool_, V), vis(&pool_, V);
+    DBuf<uint32_t> list;
+    DBuf<unsigned long long> stats(&pool_, 4);
+    // bottom-up partitions of every reversed part (once per traversal; built on the first pull level)
+    std::vector<DBuf<uint64_t>> pull_part(radj.n);
+    std::vector<uint64_t> pull_E(radj.n);
+    for (int p = 0; p < radj.n; ++p) pull_E[p] = g_.esets[rspec.parts[p].first].n_edges;
+    DBuf<uint8_t> bflags;
+    if (st.mode == T_BOUND) bflags = DBuf<uint8_t>(&pool_, R);
+    const unsigned nb = bfs_blocks(V);
+    DBuf<uint32_t> blk(&pool_, nb);
+    DBuf<uint64_t> blk_offs(&pool_, nb + 1);
+    std::vector<DBuf<uint32_t>> orow, ov;
+    std::vector<uint64_t> on;
+    uint64_t ntotal = 0;
+    for (uint64_t row0 = 0; row0 < R; row0 += 64) {
+      const int nl = (int)std::min<uint64_t>(64, R - row0);
+      const uint64_t lanes = nl == 64 ? ~0ull : ((1ull << nl) - 1);
+      HIP_CHECK(hipMemsetAsync(fr.p, 0, (size_t)V * 8, s_));
+      HIP_CHECK(hipMemsetAsync(vis.p, 0, (size_t)V * 8, s_));
+      launch_bfs_seed(col_[st.src].p, row0, nl, fr.p, s_);
+      for (int64_t d = 0;; ++d) {
+        if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate");
+        bool expand = !(st.has_max_depth && d >= st.max_depth);
+        if (expand && depth_only_while) expand = !while_never && eval_pred_const(wconst, d);
+        HIP_CHECK(hipMemsetAsync(stats.p, 0, 4 * sizeof(unsigned long long), s_));
+        tm_.begin("k_bfs_prep");
+        launch_bfs_prep(fr.p, vis.p, V, while_bm, expand, adj, stats.p, cus(), s_);
+        tm_.end(8ull * V);
+        if (!expand) break;
+        unsigned long long h[3];
+        HIP_CHECK(hipMemcpyAsync(h, stats.p, sizeof(h), hipMemcpyDeviceToHost, s_));
+        HIP_CHECK(hipStreamSynchronize(s_));
+        tm_.amend(8ull * V + 24ull * h[2]);  // frontier scan + visited and row_ptr pair of the active vertices
+        if (h[2] == 0) break;
+        edges_ += h[0];
+        HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
+        if (h[1] * pull_div_ > eadj) {
+          for (int p = 0; p < radj.n; ++p) {
+            const uint64_t nt = bfs_pull_tiles(V, pull_E[p]);
+            if (!pull_part[p].p) {
+              pull_part[p] = DBuf<uint64_t>(&pool_, nt + 1);
+              launch_bfs_pull_partition(radj.p[p].rp, V, pull_E[p], pull_part[p].p, s_);
+            }
+            tm_.begin("k_bfs_pull");
+            launch_bfs_pull(V, radj.p[p].rp, radj.p[p].col, pull_part[p].p, pull_E[p], lanes, fr.p, vis.p, nx.p, cus(), s_);
+            // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask
+            tm_.end(16ull * V + 12ull * pull_E[p]);
+          }
+        } else {
+          if (!list.p) list = DBuf<uint32_t>(&pool_, V);
+          tm_.begin("k_bfs_list");
+          launch_bfs_list(fr.p, V, list.p, stats.p + 3, cus(), s_);
+          tm_.end(8ull * V + 4ull * h[2]);
+          const uint64_t nl_act = h[2];
+          DBuf<uint64_t> deg(&pool_, nl_act + 1), loffs(&pool_, nl_act + 1);
+          for (int p = 0; p < adj.n; ++p) {
+            launch_bfs_list_deg(list.p, nl_act, adj.p[p].rp, deg.p, s_);
+            cub([&](void *t, size_t &b) {
+              return hipcub::DeviceScan::ExclusiveSum(t, b, deg.p, loffs.p, (int64_t)(nl_act + 1), s_);
+            });
+            const uint64_t etot = read1(loffs.p + nl_act);
+            tm_.begin("k_bfs_push");
+            launch_bfs_push(list.p, loffs.p, nl_act, etot, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, cus(), s_);
+            // per frontier edge: col + visited + next (+ row_ptr and frontier mask per listed vertex)
+            tm_.end(20ull * etot + 24ull * nl_act);
+          }
+        }
+        std::swap(fr, nx);
+      }
+      if (st.mode == T_BOUND) {
+        launch_bfs_bound(col_[st.dst].p, row0, nl, vis.p, emit_bm, bflags.p, s_);
+        continue;
+      }
+      tm_.begin("k_bfs_emit");
+      launch_bfs_emit_count(vis.p, emit_bm, V, blk.p, s_);
+      HIP_CHECK(hipMemsetAsync(blk_offs.p, 0, 8, s_));
+      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> bit(blk.p, CastU64());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, bit, blk_offs.p + 1, (int64_t)nb, s_); });
+      const uint64_t n = read1(blk_offs.p + nb);
+      if (n) {
+        orow.emplace_back(&pool_, n);
+        ov.emplace_back(&pool_, n);
+        on.push_back(n);
+        launch_bfs_emit_write(vis.p, emit_bm, V, blk_offs.p, (uint32_t)row0, orow.back().p, ov.back().p, s_);
+        ntotal += n;
+      }
+      tm_.end(16ull * V + 8ull * n);
+    }
+    if (st.mode == T_BOUND) {
+      select_rows(bflags.p, R);
+      return;
+    }
+    DBuf<uint32_t> rrow(&pool_, std::max<uint64_t>(ntotal, 1)), rv(&pool_, std::max<uint64_t>(ntotal, 1));
+    uint64_t off = 0;
+    for (size_t i = 0; i < on.size(); ++i) {
+      HIP_CHECK(hipMemcpyAsync(rrow.p + off, orow[i].p, on[i] * 4, hipMemcpyDeviceToDevice, s_));
+      HIP_CHECK(hipMemcpyAsync(rv.p + off, ov[i].p, on[i] * 4, hipMemcpyDeviceToDevice, s_));
+      off += on[i];
+    }
+    orow.clear();
+    ov.clear();
+    gather_rows(rrow.p, ntotal);
+    col_[st.dst] = std::move(rv);
+  }
+
+  // (row, vertex) pairs level by level: the general form (any $depth use)
+  void varlen_pairs(const Step &st) {
     const uint64_t R = R_;
     const bool dep_where = st.where_prog >= 0 && p_.progs[st.where_prog].uses_depth;
     const bool dep_while = st.while_prog >= 0 && p_.progs[st.while_prog].uses_depth;

@@ -6,9 +6,12 @@
 // so hubs are spread over the id space (and over GPUs under a modulo partition).
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <numeric>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "common.h"
@@ -151,6 +154,96 @@ int omx_rmat_generate(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t
     if (shrunk) col = shrunk;
   }
   *out_rp = orp;
+  *out_col = col;
+  *n_edges = E;
+  return OMX_OK;
+}
+
+// LDBC-SNB-like Knows graph (configs[3]). LDBC Datagen creates knows edges between persons that are
+// close in a correlation dimension (university, interests, random), so the graph has a skewed degree
+// distribution and many triangles. Restated here: target degrees from a log-normal scaled to
+// 2·target_edges endpoint slots; three passes (45 % / 45 % / 10 % of every person's slots) each sort
+// the persons by a key — community id with a skewed size distribution + random, twice, then random —
+// and connect each person to the following ones in that order with a probability decaying with the
+// distance, while both have slots left. Pairs are unique (no self loops); each undirected pair gets
+// one directed Knows edge, oriented by a hash of the pair. Deterministic in (n_persons, edges, seed).
+int omx_ldbc_knows_generate(uint32_t n_persons, uint64_t target_edges, uint64_t seed, uint64_t **out_rp,
+                            uint32_t **out_col, uint64_t *n_edges) {
+  if (n_persons < 2 || !out_rp || !out_col || !n_edges) return OMX_E_INVALID;
+  const uint32_t N = n_persons;
+  auto u01 = [](uint64_t h) { return (double)(h >> 11) * (1.0 / 9007199254740992.0); };
+  std::vector<double> t(N);
+  double tsum = 0;
+  for (uint32_t i = 0; i < N; ++i) {
+    double z = 0;  // ≈ N(0,1): Irwin–Hall of 12 uniforms
+    for (int k = 0; k < 12; ++k) z += u01(omx::splitmix64(seed ^ (0xD6E8FEB86659FD93ull * (i * 12ull + k + 1))));
+    z -= 6.0;
+    t[i] = std::exp(1.1 * z);
+    tsum += t[i];
+  }
+  const double scale = 2.0 * (double)target_edges / tsum;
+  std::vector<uint32_t> slots(N);
+  for (uint32_t i = 0; i < N; ++i) slots[i] = (uint32_t)std::min<double>(std::max(1.0, std::round(t[i] * scale)), N / 4.0);
+  std::unordered_set<uint64_t> pairs;
+  pairs.reserve(target_edges * 2);
+  const double share[3] = {0.45, 0.45, 0.10};
+  const uint32_t ncomm[2] = {std::max<uint32_t>(1, N / 120), std::max<uint32_t>(1, N / 400)};
+  std::vector<uint32_t> order(N), cap(N);
+  std::vector<uint64_t> key(N);
+  for (int pass = 0; pass < 3; ++pass) {
+    for (uint32_t i = 0; i < N; ++i) {
+      const uint64_t h = omx::splitmix64(seed * 31 + (uint64_t)pass * 0x100000001ull + i);
+      if (pass < 2) {
+        const double u = u01(omx::splitmix64(h ^ 0xC0FFEE));
+        const uint64_t c = (uint64_t)(ncomm[pass] * u * u);  // low ids = large communities
+        key[i] = (c << 32) | (h & 0xffffffffull);
+      } else {
+        key[i] = h;
+      }
+      cap[i] = (uint32_t)std::round(slots[i] * share[pass]);
+    }
+    std::iota(order.begin(), order.end(), 0u);
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b] || (key[a] == key[b] && a < b); });
+    for (uint32_t k = 0; k < N; ++k) {
+      const uint32_t i = order[k];
+      const double lambda = 4.0 * (cap[i] + 1);
+      for (uint32_t d = 1; cap[i] > 0 && d <= 4000 && k + d < N; ++d) {
+        const uint32_t j = order[k + d];
+        if (!cap[j]) continue;
+        const uint64_t a = std::min(i, j), b = std::max(i, j), pk = (a << 32) | b;
+        const double p = 0.9 * std::exp(-(double)d / lambda);
+        if (u01(omx::splitmix64(pk ^ (seed + 0x51ED27u * (pass + 1)))) >= p) continue;
+        if (pairs.insert(pk).second) {
+          --cap[i];
+          --cap[j];
+        }
+      }
+    }
+  }
+  std::vector<uint64_t> deg(N + 1, 0);
+  std::vector<std::pair<uint32_t, uint32_t>> edges;
+  edges.reserve(pairs.size());
+  for (uint64_t pk : pairs) {
+    const uint32_t a = (uint32_t)(pk >> 32), b = (uint32_t)pk;
+    if (omx::splitmix64(pk ^ seed ^ 0xABCDEFull) & 1) edges.emplace_back(a, b);
+    else edges.emplace_back(b, a);
+  }
+  std::sort(edges.begin(), edges.end());
+  const uint64_t E = edges.size();
+  uint64_t *rp = (uint64_t *)std::malloc(sizeof(uint64_t) * ((size_t)N + 1));
+  uint32_t *col = (uint32_t *)std::malloc(sizeof(uint32_t) * std::max<uint64_t>(E, 1));
+  if (!rp || !col) {
+    std::free(rp);
+    std::free(col);
+    return OMX_E_OOM;
+  }
+  std::memset(rp, 0, sizeof(uint64_t) * ((size_t)N + 1));
+  for (uint64_t e = 0; e < E; ++e) {
+    rp[edges[e].first + 1]++;
+    col[e] = edges[e].second;
+  }
+  for (uint32_t v = 0; v < N; ++v) rp[v + 1] += rp[v];
+  *out_rp = rp;
   *out_col = col;
   *n_edges = E;
   return OMX_OK;

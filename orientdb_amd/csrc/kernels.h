@@ -52,6 +52,14 @@ struct ExpandArgs {
   const ChunkDesc *chunks;
   uint64_t nchunks;
   const uint64_t *hoffs;    // [R+1] exclusive prefix of the heavy rows' full degree (dense mode)
+  // fused closing check of a cyclic pattern (sorted-adjacency intersection): neighbour n of row r is
+  // kept only if n ∈ N_member(member_src[r]); member_edges accumulates Σ |N_member(member_src[r])| over
+  // the (row, n) pairs that reach the check, i.e. the edges the unfused check step traverses.
+  // member_filter: the check's own target bitmap, applied after the edges are counted (k_check order).
+  const uint32_t *member_src;
+  DAdj member_adj;
+  const uint64_t *member_filter;
+  unsigned long long *member_edges;
 };
 
 // predicate VM → V-bit bitmap (u64 words); depth = value of $depth
@@ -74,7 +82,7 @@ void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t 
 // persistent launches: `grid` blocks loop over the tiles / chunks
 void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);
 void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);
-int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write);
+int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool member = false);
 void launch_compact_segments(int ncols, uint32_t *const *in, uint32_t *const *out, const uint64_t *seg_start,
                              const uint32_t *seg_count, const uint64_t *seg_offs, uint32_t nseg, hipStream_t s);
 
@@ -95,5 +103,29 @@ void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uin
 void launch_flag_row_change(int ncols, const uint32_t *const *cols, uint64_t n, uint8_t *flags, hipStream_t s);
 void launch_map_rids(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, uint64_t *out,
                      hipStream_t s);
+// host evaluation of a predicate program that reads no vertex data (constants and $depth only)
+bool eval_pred_const(const DPred &pred, int64_t depth);
+
+// multi-source BFS (bfs.hip): u64 lane mask per vertex, 64 binding rows per batch
+void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, hipStream_t s);
+void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
+                     const DAdj &adj, unsigned long long *stats, int cus, hipStream_t s);
+void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsigned long long *count, int cus,
+                     hipStream_t s);
+void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg, hipStream_t s);
+void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, uint64_t etot, const uint64_t *rp,
+                     const uint32_t *col, const uint64_t *frontier, const uint64_t *visited, uint64_t *next,
+                     int cus, hipStream_t s);
+uint64_t bfs_pull_tiles(uint32_t V, uint64_t E);
+void launch_bfs_pull_partition(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t *part, hipStream_t s);
+void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const uint64_t *part, uint64_t E,
+                     uint64_t lanes, const uint64_t *frontier, const uint64_t *visited, uint64_t *next, int cus,
+                     hipStream_t s);
+unsigned bfs_blocks(uint32_t V);
+void launch_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, uint32_t *blk, hipStream_t s);
+void launch_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, const uint64_t *blk_offs,
+                           uint32_t row0, uint32_t *out_row, uint32_t *out_v, hipStream_t s);
+void launch_bfs_bound(const uint32_t *dst, uint64_t row0, int nl, const uint64_t *visited, const uint64_t *emit_bm,
+                      uint8_t *flags, hipStream_t s);
 
 }  // namespace omx

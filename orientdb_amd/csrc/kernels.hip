@@ -17,23 +17,11 @@
 #include <hip/hip_runtime.h>
 
 #include "common.h"
+#include "devutil.h"
 #include "kernels.h"
 
 namespace omx {
 
-#define KCHECK(name)                                                                                    \
-  do {                                                                                                  \
-    hipError_t e_ = hipGetLastError();                                                                  \
-    if (e_ != hipSuccess) fail(OMX_E_DEVICE, std::string("launch of ") + name + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
-static inline unsigned nblocks(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
-
-__device__ __forceinline__ bool bm_test(const uint64_t *bm, uint32_t v) { return (bm[v >> 6] >> (v & 63)) & 1ull; }
-
-__device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
 
 // ---- predicate VM (compiled WHERE / while; P/OWhereClause.java:36-41, operators P/O*Operator.java) ----
 
@@ -43,7 +31,7 @@ struct VmVal {
   int32_t t;  // 0 null, 1 int, 2 double, 3 bool
 };
 
-__device__ __forceinline__ VmVal vm_col(const DColumn &c, uint32_t v) {
+__host__ __device__ __forceinline__ VmVal vm_col(const DColumn &c, uint32_t v) {
   VmVal x{0, 0.0, 0};
   if (c.present && !c.present[v]) return x;
   switch (c.type) {
@@ -62,19 +50,19 @@ __device__ __forceinline__ VmVal vm_col(const DColumn &c, uint32_t v) {
   return x;
 }
 
-__device__ __forceinline__ int vm_cmp(const VmVal &a, const VmVal &b) {
+__host__ __device__ __forceinline__ int vm_cmp(const VmVal &a, const VmVal &b) {
   if (a.t != 2 && b.t != 2) return a.i < b.i ? -1 : (a.i > b.i ? 1 : 0);
   double x = a.t == 2 ? a.d : (double)a.i, y = b.t == 2 ? b.d : (double)b.i;
   return x < y ? -1 : (x > y ? 1 : 0);
 }
 
-__device__ __forceinline__ bool vm_truthy(const VmVal &a) { return a.t == 3 && a.i != 0; }
+__host__ __device__ __forceinline__ bool vm_truthy(const VmVal &a) { return a.t == 3 && a.i != 0; }
 
-__device__ __forceinline__ bool atom_cmp(int op, int c) {
+__host__ __device__ __forceinline__ bool atom_cmp(int op, int c) {
   return op == P_EQ ? c == 0 : op == P_NE ? c != 0 : op == P_LT ? c < 0 : op == P_LE ? c <= 0 : op == P_GT ? c > 0 : c >= 0;
 }
 
-__device__ bool eval_pred(const DPred &P, uint32_t v, int64_t depth) {
+__host__ __device__ bool eval_pred(const DPred &P, uint32_t v, int64_t depth) {
   if (P.use_class) {
     uint32_t c = P.vclass[v];
     if (!((P.class_mask[c >> 6] >> (c & 63)) & 1ull)) return false;
@@ -176,6 +164,9 @@ __device__ bool eval_pred(const DPred &P, uint32_t v, int64_t depth) {
   return vm_truthy(st[0]);
 }
 
+// host evaluation of a program that reads no vertex data (only constants and $depth)
+bool eval_pred_const(const DPred &pred, int64_t depth) { return eval_pred(pred, 0, depth); }
+
 // one lane per vertex, 64 vertices per wave → one u64 bitmap word per wave via ballot
 __global__ __launch_bounds__(256) void k_eval_bitmap(DPred P, uint32_t V, int64_t depth, uint64_t *words) {
   uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -244,11 +235,6 @@ void launch_word_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank
 
 // ---- expansion ------------------------------------------------------------------------------------
 
-__device__ __forceinline__ uint64_t adj_degree(const DAdj &a, uint32_t v) {
-  uint64_t d = 0;
-  for (int p = 0; p < a.n; ++p) d += a.p[p].rp[v + 1] - a.p[p].rp[v];
-  return d;
-}
 
 __global__ void k_row_degree(const uint32_t *src, uint64_t R, DAdj adj, uint64_t *deg) {
   uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -340,31 +326,32 @@ void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t 
   KCHECK("k_mp_partition");
 }
 
-// block-wide exclusive scan of one u32 per thread (4 waves); returns the block total in *total
-template <int B>
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *s_w, uint32_t *total) {
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t incl = x;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    uint32_t y = __shfl_up(incl, off, 64);
-    if (lane >= (uint32_t)off) incl += y;
+
+// t ∈ N(v) for a sorted adjacency (lower_bound per part)
+__device__ __forceinline__ bool adj_contains(const DAdj &a, uint32_t v, uint32_t t) {
+  for (int p = 0; p < a.n; ++p) {
+    uint64_t lo = a.p[p].rp[v], hi = a.p[p].rp[v + 1];
+    const uint64_t end = hi;
+    const uint32_t *col = a.p[p].col;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (col[mid] < t) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < end && col[lo] == t) return true;
   }
-  if (lane == 63) s_w[wave] = incl;
-  __syncthreads();
-  uint32_t woff = 0, tot = 0;
+  return false;
+}
+
+__device__ __forceinline__ void wave_add_u64(unsigned long long *dst, uint64_t x) {
 #pragma unroll
-  for (int w = 0; w < B / 64; ++w) {
-    uint32_t t = s_w[w];
-    woff += (w < (int)wave) ? t : 0;
-    tot += t;
-  }
-  *total = tot;
-  return woff + incl - x;
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  if ((threadIdx.x & 63) == 0 && x) atomicAdd(dst, (unsigned long long)x);
 }
 
 // Light rows: merge-path tiles of kExpandTile (rows + edges) items, persistent blocks.
-template <bool SINGLE, bool FILTER, bool WRITE>
+// MEMBER (implies FILTER): fused closing check, see ExpandArgs::member_src.
+template <bool SINGLE, bool FILTER, bool WRITE, bool MEMBER>
 __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
   constexpr int B = kExpandBlock, IPT = kExpandIPT, T = kExpandTile, W = B / 64;
   __shared__ uint64_t s_base[T + 1];  // SINGLE: first col index of the row's remaining edges; else [0] = skip of row 0
@@ -374,10 +361,13 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
   __shared__ uint32_t s_wave[IPT * W];
   __shared__ uint32_t s_wmax[W];
   __shared__ uint32_t s_total;
+  __shared__ uint32_t s_y[MEMBER ? T + 1 : 1];     // member source vertex of each tile row
+  __shared__ uint32_t s_ydeg[MEMBER ? T + 1 : 1];  // its member-adjacency length
 
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t arena = a.arena_base + (uint64_t)blockIdx.x * a.arena_cap;
   uint64_t acc = 0;
+  uint64_t medges = 0;
   for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
     const uint64_t d0 = t * (uint64_t)T;
     const uint64_t d1 = min(d0 + (uint64_t)T, a.R + a.E);
@@ -399,6 +389,11 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
       if (e > s && s < ne) s_seg[s] = (uint16_t)lr;
       const uint32_t v = a.src[r];
       const uint64_t skip = rs < j0 ? j0 - rs : 0;
+      if (MEMBER) {
+        const uint32_t y = a.member_src[r];
+        s_y[lr] = y;
+        s_ydeg[lr] = (uint32_t)adj_degree(a.member_adj, y);
+      }
       if (SINGLE) {
         s_base[lr] = a.adj.p[0].rp[v] + skip;
       } else {
@@ -468,7 +463,11 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
         }
         nb[k] = n;
         lrs[k] = (uint16_t)lr;
-        bool pass = FILTER ? bm_test(a.filter, n) : true;
+        bool pass = FILTER ? (!a.filter || bm_test(a.filter, n)) : true;
+        if (MEMBER && pass) {
+          medges += s_ydeg[lr];
+          pass = (!a.member_filter || bm_test(a.member_filter, n)) && adj_contains(a.member_adj, s_y[lr], n);
+        }
         passmask |= (uint32_t)pass << k;
       }
     }
@@ -522,6 +521,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
     acc += s_total;
     __syncthreads();  // LDS reuse by the next tile
   }
+  if (MEMBER) wave_add_u64(a.member_edges, medges);
   if (FILTER && tid == 0) {
     a.seg_count[a.seg_base + blockIdx.x] = (uint32_t)acc;
     a.seg_start[a.seg_base + blockIdx.x] = arena;
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
 // the current chunk is filtered (software pipeline).
 __device__ __forceinline__ bool bm_test32(const uint32_t *bm, uint32_t v) { return (bm[v >> 5] >> (v & 31)) & 1u; }
 
-template <bool FILTER, bool WRITE>
+template <bool FILTER, bool WRITE, bool MEMBER>
 __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
   constexpr int NS = kHeavySlots, WPB = kHeavyBlock / 64;
   const uint32_t lane = threadIdx.x & 63;
@@ -547,6 +547,7 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
   const uint64_t arena = a.arena_base + wid * a.arena_cap;
   const uint32_t *bm32 = reinterpret_cast<const uint32_t *>(a.filter);
   uint64_t acc = 0;
+  uint64_t medges = 0;
   auto load = [&](const ChunkDesc &d, uint32_t (&q)[NS]) {
     const uint64_t win = d.lo / kChunk * kChunk;
     const uint32_t *col = a.adj.p[d.part].col + win;
@@ -571,8 +572,18 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
     for (int i = 0; i < NS; ++i) {
       const uint64_t idx = win + i * 64 + lane;
       bool ok = idx >= d.lo && idx < d.hi;
-      if (FILTER && ok) ok = bm_test32(bm32, q[i]);
+      if (FILTER && ok && bm32) ok = bm_test32(bm32, q[i]);
       mask |= (uint32_t)ok << i;
+    }
+    if (MEMBER) {  // the chunk's row has one member source: every lane searches the same sorted list
+      const uint32_t y = a.member_src[d.row];
+      medges += (uint64_t)__popc(mask) * adj_degree(a.member_adj, y);
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        if ((mask >> i) & 1u) {
+          const bool keep = (!a.member_filter || bm_test(a.member_filter, q[i])) && adj_contains(a.member_adj, y, q[i]);
+          mask &= ~((uint32_t)!keep << i);
+        }
     }
     // prefetch the next chunk
     ChunkDesc dn = d;
@@ -619,6 +630,7 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
 #pragma unroll
     for (int i = 0; i < NS; ++i) q[i] = qn[i];
   }
+  if (MEMBER) wave_add_u64(a.member_edges, medges);
   if (FILTER && lane == 0) {
     a.seg_count[a.seg_base + wid] = (uint32_t)acc;
     a.seg_start[a.seg_base + wid] = arena;
@@ -627,49 +639,53 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
 
 void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s) {
   if (!grid) return;
-  const bool single = a.adj.n == 1, filter = a.filter != nullptr;
+  const bool single = a.adj.n == 1, member = a.member_src != nullptr, filter = a.filter != nullptr || member;
   dim3 g(grid), b(kExpandBlock);
-#define OMX_EXP(S, F, Wr) hipLaunchKernelGGL((k_expand<S, F, Wr>), g, b, 0, s, a)
+#define OMX_EXP(S, F, Wr, M) hipLaunchKernelGGL((k_expand<S, F, Wr, M>), g, b, 0, s, a)
+#define OMX_EXP_W(S, F, M) { if (write) OMX_EXP(S, F, true, M); else OMX_EXP(S, F, false, M); }
   if (single) {
-    if (filter) { if (write) OMX_EXP(true, true, true); else OMX_EXP(true, true, false); }
-    else { if (write) OMX_EXP(true, false, true); else OMX_EXP(true, false, false); }
+    if (member) OMX_EXP_W(true, true, true)
+    else if (filter) OMX_EXP_W(true, true, false)
+    else OMX_EXP_W(true, false, false)
   } else {
-    if (filter) { if (write) OMX_EXP(false, true, true); else OMX_EXP(false, true, false); }
-    else { if (write) OMX_EXP(false, false, true); else OMX_EXP(false, false, false); }
+    if (member) OMX_EXP_W(false, true, true)
+    else if (filter) OMX_EXP_W(false, true, false)
+    else OMX_EXP_W(false, false, false)
   }
+#undef OMX_EXP_W
 #undef OMX_EXP
   KCHECK("k_expand");
 }
 
 void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s) {
   if (!grid) return;
-  const bool filter = a.filter != nullptr;
+  const bool member = a.member_src != nullptr, filter = a.filter != nullptr || member;
   dim3 g(grid), b(kHeavyBlock);
-  if (filter) {
-    if (write) hipLaunchKernelGGL((k_expand_heavy<true, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_expand_heavy<true, false>), g, b, 0, s, a);
-  } else {
-    if (write) hipLaunchKernelGGL((k_expand_heavy<false, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_expand_heavy<false, false>), g, b, 0, s, a);
-  }
+#define OMX_EXH(F, Wr, M) hipLaunchKernelGGL((k_expand_heavy<F, Wr, M>), g, b, 0, s, a)
+  if (member) { if (write) OMX_EXH(true, true, true); else OMX_EXH(true, false, true); }
+  else if (filter) { if (write) OMX_EXH(true, true, false); else OMX_EXH(true, false, false); }
+  else { if (write) OMX_EXH(false, true, false); else OMX_EXH(false, false, false); }
+#undef OMX_EXH
   KCHECK("k_expand_heavy");
 }
 
-int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write) {
+int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool member) {
   int n = 0;
   hipError_t e;
+  filter = filter || member;
+#define OCC(K, BS) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, K, BS, 0)
   if (heavy) {
-    if (filter) e = write ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand_heavy<true, true>, kHeavyBlock, 0)
-                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand_heavy<true, false>, kHeavyBlock, 0);
-    else e = write ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand_heavy<false, true>, kHeavyBlock, 0)
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand_heavy<false, false>, kHeavyBlock, 0);
+    if (member) e = write ? OCC((k_expand_heavy<true, true, true>), kHeavyBlock) : OCC((k_expand_heavy<true, false, true>), kHeavyBlock);
+    else if (filter) e = write ? OCC((k_expand_heavy<true, true, false>), kHeavyBlock) : OCC((k_expand_heavy<true, false, false>), kHeavyBlock);
+    else e = write ? OCC((k_expand_heavy<false, true, false>), kHeavyBlock) : OCC((k_expand_heavy<false, false, false>), kHeavyBlock);
   } else if (single) {
-    e = filter ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand<true, true, true>, kExpandBlock, 0)
-               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand<true, false, true>, kExpandBlock, 0);
+    e = member ? OCC((k_expand<true, true, true, true>), kExpandBlock)
+               : filter ? OCC((k_expand<true, true, true, false>), kExpandBlock) : OCC((k_expand<true, false, true, false>), kExpandBlock);
   } else {
-    e = filter ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand<false, true, true>, kExpandBlock, 0)
-               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_expand<false, false, true>, kExpandBlock, 0);
+    e = member ? OCC((k_expand<false, true, true, true>), kExpandBlock)
+               : filter ? OCC((k_expand<false, true, true, false>), kExpandBlock) : OCC((k_expand<false, false, true, false>), kExpandBlock);
   }
+#undef OCC
   if (e != hipSuccess || n < 1) n = 2;
   return n;
 }

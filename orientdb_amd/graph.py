@@ -179,6 +179,30 @@ class GraphSnapshot:
         return g
 
     @classmethod
+    def person_knows(cls, rp, col, seed, device=0, keep_csr=False):
+        """Person/Knows snapshot over a given out-CSR (SURVEY.md §8(d) schema): vertices of class Person
+        (one cluster → RID #11:v), edge class Knows, properties uid (int64 = v) and age (int32 uniform
+        [0,100) from a seeded splitmix64)."""
+        V = len(rp) - 1
+        classes = [("V", -1, False, 9), ("E", -1, True, 10), ("Person", 0, False, 11), ("Knows", 1, True, 12)]
+        vclass = np.full(V, 2, np.uint16)
+        rids = (np.uint64(11) << np.uint64(RID_POS_BITS)) | np.arange(V, dtype=np.uint64)
+        props = [{"name": "uid", "type": N.OMX_PROP_INT64, "values": np.arange(V, dtype=np.int64)},
+                 {"name": "age", "type": N.OMX_PROP_INT32, "values": synthetic_int_column(V, seed ^ 0xA9E, 100)}]
+        g = cls(V, classes, vclass, rids, [{"cls": 3, "out_rp": rp, "out_col": col}], props, [], device)
+        g.n_edges = int(rp[-1])
+        if keep_csr:
+            g.csr = (rp, col)
+        g.age = props[1]["values"]
+        return g
+
+    @classmethod
+    def ldbc_like(cls, n_persons=70000, target_edges=2_000_000, seed=10, device=0, keep_csr=False):
+        """LDBC-SNB-like SF10 Knows graph (configs[3]; generator in gen.cpp) with the Person/Knows schema."""
+        rp, col = ldbc_csr(n_persons, target_edges, seed)
+        return cls.person_knows(rp, col, seed, device, keep_csr)
+
+    @classmethod
     def rmat(cls, scale, edge_factor=16, seed=None, simple=True, device=0, keep_csr=False):
         """Synthetic Person/Knows graph: Graph500 RMAT, vertices of class Person
         (one cluster → RID #11:v), edge class Knows, properties uid (int64 = v) and age (int32 uniform
@@ -198,6 +222,20 @@ class GraphSnapshot:
             g.csr = (rp, col)
         g.age = props[1]["values"]
         return g
+
+
+def ldbc_csr(n_persons=70000, target_edges=2_000_000, seed=10):
+    """(row_ptr u64[V+1], col u32[E]) of the LDBC-SNB-like Knows generator in libomx (configs[3])."""
+    L = N.lib()
+    prp = C.POINTER(C.c_uint64)()
+    pcol = C.POINTER(C.c_uint32)()
+    ne = C.c_uint64()
+    N.check(L.omx_ldbc_knows_generate(n_persons, target_edges, seed, C.byref(prp), C.byref(pcol), C.byref(ne)))
+    rp = np.ctypeslib.as_array(prp, shape=(n_persons + 1,)).copy()
+    col = np.ctypeslib.as_array(pcol, shape=(max(1, ne.value),))[:ne.value].copy()
+    L.omx_host_free(C.cast(prp, C.c_void_p))
+    L.omx_host_free(C.cast(pcol, C.c_void_p))
+    return rp, col
 
 
 def rmat_csr(scale, edge_factor=16, seed=None, simple=True):

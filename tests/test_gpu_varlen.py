@@ -1,0 +1,107 @@
+"""Variable-length MATCH items (while / maxDepth; P/OMatchPathItem.java:79-105, SURVEY §8 a9, configs[2]).
+
+Every case runs through both device strategies — the multi-source BFS (bfs.hip, 64 rows per lane mask,
+push/pull levels) and the (row, vertex) level expansion — and must equal the oracle's walk enumeration
+(oracle/match_ref.py _traverse_edge, the reference's recursion restated) bit for bit.
+"""
+import pytest
+
+from tests.test_gpu_parity import _parity, rmat10, rmat10_raw  # noqa: F401  (fixtures)
+
+pytestmark = pytest.mark.gpu
+
+VARLEN = [
+    ("depth_only", "MATCH {class:Person,as:s,where:(uid = 14)}-Knows->{as:v, while:($depth < 3)} RETURN s, v"),
+    ("two_batches", "MATCH {class:Person,as:s,where:(uid < 70)}-Knows->{as:v, while:($depth < 2)} RETURN s, v"),
+    ("shared_sources", "MATCH {class:Person,as:a,where:(uid < 10)}-Knows->{as:b}-Knows->{as:c, while:($depth < 2)} RETURN a, b, c"),
+    ("where_target", "MATCH {class:Person,as:s,where:(uid < 6)}-Knows->{as:v, while:($depth < 3), where:(age < 30)} RETURN s, v"),
+    ("maxdepth", "MATCH {class:Person,as:s,where:(uid = 16)}-Knows->{as:v, maxDepth: 2, where:(age < 50)} RETURN s, v"),
+    ("maxdepth0", "MATCH {class:Person,as:s,where:(uid < 4)}-Knows->{as:v, maxDepth: 0} RETURN s, v"),
+    ("while_prop", "MATCH {class:Person,as:s,where:(uid < 18)}-Knows->{as:v, maxDepth: 3, while:(age < 60)} RETURN s, v"),
+    ("while_false_at_1", "MATCH {class:Person,as:s,where:(uid < 8)}-Knows->{as:v, while:($depth != 1)} RETURN s, v"),
+    ("in_dir", "MATCH {class:Person,as:s,where:(uid < 5)}<-Knows-{as:v, while:($depth < 3), where:(age > 40)} RETURN s, v"),
+    ("both_dir", "MATCH {class:Person,as:s,where:(uid = 3)}-Knows-{as:v, maxDepth: 2} RETURN s, v"),
+    ("method_form", "MATCH {class:Person,as:s,where:(uid = 17)}.out('Knows'){as:v, while:($depth < 3)} RETURN v"),
+    ("depth_and_prop", "MATCH {class:Person,as:s,where:(uid < 18)}-Knows->{as:v, while:($depth < 3 and age < 70)} RETURN s, v"),
+    ("where_depth", "MATCH {class:Person,as:s,where:(uid < 4)}-Knows->{as:v, while:($depth < 3), where:($depth = 2)} RETURN s, v"),
+    ("bound_target", "MATCH {class:Person,as:a,where:(uid < 8)}-Knows->{as:b}, {as:a}-Knows->{as:b, while:($depth < 2)} RETURN a, b"),
+]
+
+
+def _cols(q):
+    ret = q.split("RETURN")[1]
+    return [c.strip() for c in ret.split(",")]
+
+
+# (strategy, OMX_BFS_PULL_DIV): auto push/pull, every level top-down, every level bottom-up
+MODES = [("bfs", None), ("bfs", "1"), ("bfs", "1000000000000"), ("pairs", None)]
+
+
+@pytest.mark.parametrize("mode", MODES, ids=["bfs_auto", "bfs_push", "bfs_pull", "pairs"])
+@pytest.mark.parametrize("q", VARLEN, ids=[q[0] for q in VARLEN])
+def test_varlen_parity(rmat10, q, mode, monkeypatch):
+    monkeypatch.setenv("OMX_VARLEN", mode[0])
+    if mode[1]:
+        monkeypatch.setenv("OMX_BFS_PULL_DIV", mode[1])
+    g, ref = rmat10
+    _parity(g, ref, q[1], _cols(q[1]))
+
+
+@pytest.mark.parametrize("q", [q for q in VARLEN if q[0] in ("two_batches", "both_dir", "while_prop")], ids=lambda q: q[0])
+def test_varlen_parity_multigraph(rmat10_raw, q, monkeypatch):
+    monkeypatch.setenv("OMX_VARLEN", "bfs")
+    g, ref = rmat10_raw
+    _parity(g, ref, q[1], _cols(q[1]))
+
+
+@pytest.mark.parametrize("q", [q for q in VARLEN if q[0] in ("two_batches", "where_target", "while_prop", "both_dir")],
+                         ids=lambda q: q[0])
+def test_bfs_edge_count_matches_visited_levels(rmat10, q, monkeypatch):
+    """With a depth-free while the (row, vertex) path also keeps a visited set, so both strategies
+    traverse exactly the same frontier edges (SURVEY §8(d) E_t: Σ over levels of the frontier degree sum)."""
+    import orientdb_amd as o
+    g, _ = rmat10
+    if "$depth" in q[1]:
+        # depth-only while: the pair path walks without a visited set; only the row sets must agree
+        pytest.skip("depth-reading while: pair path has no visited set")
+    out = {}
+    for mode in ("bfs", "pairs"):
+        monkeypatch.setenv("OMX_VARLEN", mode)
+        out[mode] = o.OMatchStatement(q[1]).execute(g).info
+    assert out["bfs"]["edges_traversed"] == out["pairs"]["edges_traversed"]
+    assert out["bfs"]["n_rows"] == out["pairs"]["n_rows"]
+
+
+def test_bfs_kernels_reported(rmat10, monkeypatch):
+    import orientdb_amd as o
+    g, _ = rmat10
+    monkeypatch.setenv("OMX_VARLEN", "bfs")
+    rs = o.OMatchStatement(VARLEN[1][1]).execute(g, flags=o.OMX_FLAG_KERNEL_TIMING)
+    names = {k["name"] for k in rs.kernel_stats}
+    assert "k_bfs_prep" in names and "k_bfs_emit" in names
+    assert names & {"k_bfs_push", "k_bfs_pull"}
+
+
+@pytest.fixture(scope="module")
+def rmat16():
+    import orientdb_amd as o
+    return o.GraphSnapshot.rmat(16, device=0, keep_csr=True)
+
+
+@pytest.mark.parametrize("depth,nroots", [(4, 64), (3, 200)])
+def test_c3_shape_rmat16_vs_c_bfs(rmat16, depth, nroots):
+    """configs[2] query shape at RMAT-16 against oracle/bfs_ref.c: identical (s, v) rows and the same
+    traversed-edge count (Σ over levels of the frontier degree sum)."""
+    import numpy as np
+    import orientdb_amd as o
+    from oracle import dfs
+    g = rmat16
+    q = "MATCH {class:Person,as:s,where:(uid < %d)}-Knows->{as:v, while:($depth < %d)} RETURN s, v" % (nroots, depth)
+    rs = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_NO_RID_MAP)
+    ref = dfs.bfs_varlen(g.csr[0], g.csr[1], np.arange(nroots, dtype=np.uint32), max_depth=depth, nthreads=8)
+    assert rs.info["n_rows"] == ref["n"]
+    assert rs.info["edges_traversed"] == ref["edges"]
+    si, vi = rs.columns.index("s"), rs.columns.index("v")
+    got = np.sort(rs.rows[:, si].astype(np.uint64) << np.uint64(32) | rs.rows[:, vi].astype(np.uint64))
+    want = np.sort(ref["pairs"][:, 0].astype(np.uint64) << np.uint64(32) | ref["pairs"][:, 1].astype(np.uint64))
+    assert np.array_equal(got, want)
