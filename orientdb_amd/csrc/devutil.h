@@ -9,9 +9,12 @@
 
 namespace omx {
 
+// OMX_SYNC_LAUNCH=1: synchronise after every launch so an asynchronous fault names its kernel
+bool sync_launches();
 #define KCHECK(name)                                                                                    \
   do {                                                                                                  \
     hipError_t e_ = hipGetLastError();                                                                  \
+    if (e_ == hipSuccess && sync_launches()) e_ = hipStreamSynchronize(s);                              \
     if (e_ != hipSuccess) fail(OMX_E_DEVICE, std::string("launch of ") + name + ": " + hipGetErrorString(e_)); \
   } while (0)
 
@@ -21,6 +24,12 @@ __device__ __forceinline__ bool bm_test(const uint64_t *bm, uint32_t v) { return
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// wave-uniform copy of a 64-bit value (lane 0's); the compiler can then keep it in SGPRs
+__device__ __forceinline__ uint64_t wave_bcast64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x), hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint64_t adj_degree(const DAdj &a, uint32_t v) {

@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 
 #include "kernels.h"
 
@@ -106,6 +107,9 @@ class Executor {
     if (const char *h = std::getenv("OMX_HEAVY_DEG")) heavy_deg_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
     // variable-length strategy: "bfs" (multi-source BFS whenever exact), "pairs" ((row, v) levels), auto
     if (const char *v = std::getenv("OMX_VARLEN")) varlen_mode_ = v;
+    if (const char *sl = std::getenv("OMX_SLICED")) sliced_ = std::strcmp(sl, "0") != 0;
+    if (const char *sh = std::getenv("OMX_SLICE_SHIFT"))
+      slice_shift_ = (uint32_t)std::min<long>(20, std::max<long>(6, std::strtol(sh, nullptr, 10)));
     if (const char *f = std::getenv("OMX_FUSE_CHECK")) fuse_mode_ = f;  // "0" disables the intersection
     if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max<uint64_t>(1, std::strtoull(d, nullptr, 10));
     bms_.resize(p.bitmaps.size());
@@ -213,6 +217,8 @@ class Executor {
   int dedup_ran_ = 0;
   int cus_ = 0;
   uint64_t heavy_deg_ = kHeavyDeg;
+  bool sliced_ = true;  // LDS-sliced heavy kernel for filtered hops (OMX_SLICED=0 disables)
+  uint32_t slice_shift_ = 20;  // log2 vertices per slice (OMX_SLICE_SHIFT, 6..20: tests cut small graphs)
   std::string varlen_mode_ = "auto";
   std::string fuse_mode_ = "1";
   uint64_t pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
@@ -402,34 +408,51 @@ class Executor {
       medges = DBuf<unsigned long long>(&pool_, 1);
       HIP_CHECK(hipMemsetAsync(medges.p, 0, sizeof(unsigned long long), s_));
     }
-    // 1. degree binning + scans (light edges: merge path; heavy rows: chunks)
+    // 1. degree binning + scans (light edges: merge path; heavy rows: chunks). A filtered hop over a
+    // sorted adjacency cuts the heavy rows' chunks at bitmap-slice boundaries (LDS-sliced kernel).
+    const bool sliced = filter != nullptr && !member && adj.sorted && sliced_ &&
+                        (uint64_t)g_.V <= ((uint64_t)kMaxSlices << slice_shift_);
+    const uint32_t P = sliced ? (uint32_t)(((uint64_t)g_.V + (1ull << slice_shift_) - 1) >> slice_shift_) : 1;
+    const uint64_t nchn = sliced ? (uint64_t)P * (R + 1) + 1 : R + 1;
     DBuf<uint64_t> light(&pool_, R + 1), heavy(&pool_, R + 1), loffs(&pool_, R + 1), hoffs(&pool_, R + 1);
-    DBuf<uint32_t> nch(&pool_, R + 1);
-    DBuf<uint64_t> choffs(&pool_, R + 1);
+    DBuf<uint32_t> nch(&pool_, nchn);
+    DBuf<uint64_t> choffs(&pool_, nchn);
     tm_.begin("k_row_split");
-    launch_row_split(src, R, adj, heavy_deg_, light.p, heavy.p, nch.p, s_);
+    if (sliced) launch_row_split_sliced(src, R, adj, heavy_deg_, P, slice_shift_, light.p, heavy.p, nch.p, s_);
+    else launch_row_split(src, R, adj, heavy_deg_, light.p, heavy.p, nch.p, s_);
     tm_.end(R * (4 + 16ull * adj.n) + (R + 1) * 20);
     tm_.begin("scan_degrees");
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, light.p, loffs.p, (int64_t)(R + 1), s_); });
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, heavy.p, hoffs.p, (int64_t)(R + 1), s_); });
     hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> nit(nch.p, CastU64());
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, nit, choffs.p, (int64_t)(R + 1), s_); });
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, nit, choffs.p, (int64_t)nchn, s_); });
     tm_.end((R + 1) * 40);
     uint64_t tot[3];
     HIP_CHECK(hipMemcpyAsync(&tot[0], loffs.p + R, 8, hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipMemcpyAsync(&tot[1], hoffs.p + R, 8, hipMemcpyDeviceToHost, s_));
-    HIP_CHECK(hipMemcpyAsync(&tot[2], choffs.p + R, 8, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipMemcpyAsync(&tot[2], choffs.p + (nchn - 1), 8, hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipStreamSynchronize(s_));
     const uint64_t EL = tot[0], EH = tot[1], nchunks = tot[2];
     const uint64_t E = EL + EH;
     o.E = E;
     if (E == 0) return o;
     DBuf<ChunkDesc> chunks;
+    DBuf<uint64_t> qb;
+    std::vector<uint64_t> hqb;
     if (nchunks) {
       chunks = DBuf<ChunkDesc>(&pool_, nchunks);
       tm_.begin("k_fill_chunks");
-      launch_fill_chunks(src, R, adj, choffs.p, hoffs.p, chunks.p, s_);
+      if (sliced) {
+        launch_fill_chunks_sliced(src, R, adj, P, slice_shift_, choffs.p, hoffs.p, chunks.p, s_);
+        qb = DBuf<uint64_t>(&pool_, P + 1);
+        launch_slice_bounds(choffs.p, R, P, qb.p, s_);
+        hqb.resize(P + 1);
+        HIP_CHECK(hipMemcpyAsync(hqb.data(), qb.p, (P + 1) * 8, hipMemcpyDeviceToHost, s_));
+      } else {
+        launch_fill_chunks(src, R, adj, choffs.p, hoffs.p, chunks.p, s_);
+      }
       tm_.end(nchunks * sizeof(ChunkDesc));
+      if (sliced) HIP_CHECK(hipStreamSynchronize(s_));
     }
     const uint64_t ntiles = EL ? (R + EL + kExpandTile - 1) / kExpandTile : 0;
     DBuf<uint64_t> part;
@@ -448,12 +471,36 @@ class Executor {
     // was measured slower: the light kernel is latency-bound per tile and needs the whole chip.)
     const uint64_t sh = (uint64_t)cus() * expand_blocks_per_cu(true, single, filt, write, member);
     const uint64_t sl = (uint64_t)cus() * expand_blocks_per_cu(false, single, filt, write, member);
-    const unsigned gh = nchunks ? (unsigned)std::min<uint64_t>(hblocks, sh) : 0;
+    constexpr unsigned SWPB = kSliceBlock / 64;
+    // sliced: one workgroup per CU, split over the slices in proportion to their chunk counts
+    SliceArgs sa{};
+    uint64_t caph_sliced = 0;
+    if (sliced && nchunks) {
+      const uint64_t G = std::min<uint64_t>((uint64_t)cus(), (nchunks + SWPB - 1) / SWPB);
+      sa.qb = qb.p;
+      sa.V = g_.V;
+      sa.nslices = P;
+      sa.shift = slice_shift_;
+      uint32_t w = 0;
+      for (uint32_t q = 0; q < P; ++q) {
+        const uint64_t nq = hqb[q + 1] - hqb[q];
+        uint64_t k = nq ? std::max<uint64_t>(1, (G * nq + nchunks / 2) / nchunks) : 0;
+        k = std::min<uint64_t>(k, (nq + SWPB - 1) / SWPB);
+        sa.wg0[q] = w;
+        w += (uint32_t)k;
+        if (k) caph_sliced = std::max<uint64_t>(caph_sliced, (nq + k * SWPB - 1) / (k * SWPB) * (uint64_t)kChunk);
+      }
+      sa.wg0[P] = w;
+    }
+    const unsigned gh = !nchunks ? 0 : sliced ? sa.wg0[P] : (unsigned)std::min<uint64_t>(hblocks, sh);
     const unsigned gl = ntiles ? (unsigned)std::min<uint64_t>(ntiles, sl) : 0;
-    const uint64_t wh = (uint64_t)gh * WPB;
-    const uint64_t caph = gh ? (nchunks + wh - 1) / wh * (uint64_t)kChunk : 0;
+    // heavy output: one arena per wave, sized for the most chunks a wave of the launch owns
+    const uint64_t wh = (uint64_t)gh * (sliced ? SWPB : WPB);
+    const uint64_t caph = !gh ? 0 : sliced ? caph_sliced : (nchunks + wh - 1) / wh * (uint64_t)kChunk;
+    const uint64_t nseg_h = wh;
+    const uint64_t heavy_rows_cap = wh * caph;
     const uint64_t capl = gl ? (ntiles + gl - 1) / gl * (uint64_t)kExpandTile : 0;
-    const uint64_t cap = filt ? wh * caph + gl * capl : E;
+    const uint64_t cap = filt ? heavy_rows_cap + gl * capl : E;
     ExpandArgs a{};
     a.src = src;
     a.offs = loffs.p;
@@ -486,7 +533,7 @@ class Executor {
       }
     }
     if (filt) {
-      o.nseg = (uint32_t)(wh + gl);
+      o.nseg = (uint32_t)(nseg_h + gl);
       o.seg_start = DBuf<uint64_t>(&pool_, o.nseg);
       o.seg_count = DBuf<uint32_t>(&pool_, o.nseg);
       a.seg_start = o.seg_start.p;
@@ -504,15 +551,20 @@ class Executor {
       a.arena_base = 0;
       a.arena_cap = caph;
       a.seg_base = 0;
-      tm_.begin("k_expand_heavy");
-      launch_expand_heavy(a, gh, write, s_);
+      if (sliced) {
+        tm_.begin("k_expand_heavy");
+        launch_expand_heavy_sliced(a, sa, gh, write, s_);
+      } else {
+        tm_.begin("k_expand_heavy");
+        launch_expand_heavy(a, gh, write, s_);
+      }
       tm_.end(4 * EH + outw * (filt ? 0 : EH));
       rec_h = tm_.last();
     }
     if (gl) {
-      a.arena_base = wh * caph;
+      a.arena_base = heavy_rows_cap;
       a.arena_cap = capl;
-      a.seg_base = (uint32_t)wh;
+      a.seg_base = (uint32_t)nseg_h;
       tm_.begin("k_expand_light");
       launch_expand(a, gl, write, s_);
       tm_.end(8 * R + 4 * EL + outw * (filt ? 0 : EL));
@@ -536,7 +588,7 @@ class Executor {
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, sit, soffs.p + 1, (int64_t)o.nseg, s_); });
     HIP_CHECK(hipMemsetAsync(soffs.p, 0, 8, s_));
     uint64_t nh_n[3] = {0, 0, 0};  // rows emitted by the heavy kernel's segments, all rows, member edges
-    HIP_CHECK(hipMemcpyAsync(&nh_n[0], soffs.p + wh, 8, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipMemcpyAsync(&nh_n[0], soffs.p + nseg_h, 8, hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipMemcpyAsync(&nh_n[1], soffs.p + o.nseg, 8, hipMemcpyDeviceToHost, s_));
     if (member) HIP_CHECK(hipMemcpyAsync(&nh_n[2], medges.p, 8, hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipStreamSynchronize(s_));

@@ -20,6 +20,23 @@ constexpr int kChunk = 1024;                       // edges per chunk = one wave
 constexpr int kHeavyBlock = 256;                   // 4 independent waves
 constexpr int kHeavySlots = kChunk / 64;           // lane l takes edge l of each 64-edge slot
 
+// LDS-sliced heavy expansion (filtered hops): the target bitmap is cut into slices of kSliceBits
+// vertices (128 KiB each) and each heavy row's sorted adjacency is cut at the slice boundaries, so a
+// chunk's neighbours all probe one slice; one workgroup per CU holds a slice in LDS and pulls that
+// slice's chunks in a static round-robin. Bitmap probes become LDS reads instead of L2 requests.
+constexpr uint32_t kSliceBits = 1u << 20;
+constexpr uint32_t kSliceWords = kSliceBits / 32;  // u32 words per slice
+constexpr int kMaxSlices = 16;                     // V ≤ 16·2^20; beyond that the L2-probe kernel is used
+constexpr int kSliceBlock = 1024;                  // 16 waves: one workgroup per CU (LDS-limited)
+
+struct SliceArgs {
+  const uint64_t *qb;            // [P+1] chunk index bounds of each slice
+  uint32_t wg0[kMaxSlices + 1];  // workgroups [wg0[q], wg0[q+1]) own slice q
+  uint32_t V;
+  uint32_t nslices;
+  uint32_t shift;  // slice = 2^shift vertices (6 ≤ shift ≤ 20; tests shrink it to cut small graphs)
+};
+
 struct ChunkDesc {
   uint64_t lo, hi;  // absolute col[] range of the chunk inside part `part` (one kChunk-aligned window)
   uint64_t dense;   // output index of edge lo in the dense (unfiltered) layout
@@ -79,6 +96,17 @@ void launch_fill_chunks(const uint32_t *src, uint64_t R, const DAdj &adj, const 
                         const uint64_t *hoffs, ChunkDesc *out, hipStream_t s);
 void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part,
                          hipStream_t s);
+// sliced chunks: nchq[q·(R+1) + r] = chunks of heavy row r inside slice q (layout slice-major so one
+// scan gives each slice a contiguous chunk range); light/heavy degrees as launch_row_split
+void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint32_t nslices,
+                             uint32_t shift, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s);
+void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint32_t nslices, uint32_t shift,
+                               const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out, hipStream_t s);
+// qb[q] = choffs[q·(R+1)] for q ≤ P
+void launch_slice_bounds(const uint64_t *choffs, uint64_t R, uint32_t nslices, uint64_t *qb, hipStream_t s);
+// grid = sa.wg0[P] workgroups (one per CU); wave w appends to arena_base + w·arena_cap and reports
+// seg_count/seg_start[seg_base + w]
+void launch_expand_heavy_sliced(const ExpandArgs &a, const SliceArgs &sa, unsigned grid, bool write, hipStream_t s);
 // persistent launches: `grid` blocks loop over the tiles / chunks
 void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);
 void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);

@@ -16,12 +16,21 @@
 //     straight to the dense position of each edge.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "devutil.h"
 #include "kernels.h"
 
 namespace omx {
 
+bool sync_launches() {
+  static const bool on = [] {
+    const char *e = std::getenv("OMX_SYNC_LAUNCH");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
 
 // ---- predicate VM (compiled WHERE / while; P/OWhereClause.java:36-41, operators P/O*Operator.java) ----
 
@@ -291,7 +300,7 @@ __global__ void k_fill_chunks(const uint32_t *src, uint64_t R, DAdj adj, const u
   uint64_t pos = hoffs[r];  // dense output index of the row's first edge (parts in order)
   for (int p = 0; p < adj.n; ++p) {
     const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
-    for (uint64_t w = b / kChunk * kChunk; w < e; w += kChunk) {
+    for (uint64_t w = b / kChunk * kChunk; e > b && w < e; w += kChunk) {  // an empty part has no chunk
       const uint64_t lo = w > b ? w : b, hi = w + kChunk < e ? w + kChunk : e;
       out[o++] = ChunkDesc{lo, hi, pos + (lo - b), (uint32_t)r, (uint32_t)p};
     }
@@ -635,6 +644,275 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
     a.seg_count[a.seg_base + wid] = (uint32_t)acc;
     a.seg_start[a.seg_base + wid] = arena;
   }
+}
+
+// ---- LDS-sliced heavy expansion ---------------------------------------------------------------------
+// The L2-probe kernel above issues one L1→L2 request per filtered edge whenever a 64-neighbour slot
+// spans more than a few cache lines (rows of degree ~1K–100K on a V = 4M graph), and that request rate,
+// not HBM, bounds it. Here the V-bit target bitmap is cut into 128 KiB slices (2^20 vertices) that a
+// workgroup stages in LDS, and every heavy row's sorted adjacency is cut at the slice boundaries, so a
+// chunk's probes all land in the slice its workgroup holds. HBM then only streams col[] (coalesced
+// dwords, next chunk prefetched) and the surviving rows.
+
+__device__ __forceinline__ uint64_t col_lower_bound(const uint32_t *col, uint64_t lo, uint64_t hi, uint64_t x) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if ((uint64_t)col[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// sliced chunks need no window alignment (buffer loads with a per-chunk base): ⌈len / kChunk⌉ pieces
+__device__ __forceinline__ uint32_t chunk_pieces(uint64_t lo, uint64_t hi) {
+  return hi > lo ? (uint32_t)((hi - lo + kChunk - 1) / kChunk) : 0u;
+}
+
+__global__ void k_row_split_sliced(const uint32_t *src, uint64_t R, DAdj adj, uint64_t heavy_deg, uint32_t P,
+                                   uint32_t shift, uint64_t *light, uint64_t *heavy, uint32_t *nchq) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > R) return;
+  const uint64_t stride = R + 1;
+  if (r == R) {
+    light[R] = 0;
+    heavy[R] = 0;
+    for (uint32_t q = 0; q < P; ++q) nchq[q * stride + R] = 0;
+    nchq[P * stride] = 0;
+    return;
+  }
+  const uint32_t v = src[r];
+  const uint64_t d = adj_degree(adj, v);
+  if (d < heavy_deg) {
+    light[r] = d;
+    heavy[r] = 0;
+    for (uint32_t q = 0; q < P; ++q) nchq[q * stride + r] = 0;
+    return;
+  }
+  light[r] = 0;
+  heavy[r] = d;
+  uint32_t cnt[kMaxSlices];
+  for (uint32_t q = 0; q < P; ++q) cnt[q] = 0;
+  for (int p = 0; p < adj.n; ++p) {
+    const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
+    uint64_t lo = b;
+    for (uint32_t q = 0; q < P; ++q) {
+      const uint64_t hi = q + 1 == P ? e : col_lower_bound(adj.p[p].col, lo, e, (uint64_t)(q + 1) << shift);
+      cnt[q] += chunk_pieces(lo, hi);
+      lo = hi;
+    }
+  }
+  for (uint32_t q = 0; q < P; ++q) nchq[q * stride + r] = cnt[q];
+}
+void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint32_t nslices,
+                             uint32_t shift, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s) {
+  hipLaunchKernelGGL(k_row_split_sliced, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, R, adj, heavy_deg, nslices,
+                     shift, light, heavy, nchq);
+  KCHECK("k_row_split_sliced");
+}
+
+__global__ void k_fill_chunks_sliced(const uint32_t *src, uint64_t R, DAdj adj, uint32_t P, uint32_t shift,
+                                     const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R || hoffs[r + 1] == hoffs[r]) return;  // light row
+  const uint64_t stride = R + 1;
+  const uint32_t v = src[r];
+  uint64_t o[kMaxSlices];
+  for (uint32_t q = 0; q < P; ++q) o[q] = choffs[q * stride + r];
+  uint64_t pos = hoffs[r];  // dense index of the row's first edge (parts in order)
+  for (int p = 0; p < adj.n; ++p) {
+    const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
+    uint64_t lo = b;
+    for (uint32_t q = 0; q < P; ++q) {
+      const uint64_t hi = q + 1 == P ? e : col_lower_bound(adj.p[p].col, lo, e, (uint64_t)(q + 1) << shift);
+      for (uint64_t clo = lo; clo < hi; clo += kChunk) {  // as chunk_pieces
+        const uint64_t chi = clo + kChunk < hi ? clo + kChunk : hi;
+        out[o[q]++] = ChunkDesc{clo, chi, pos + (clo - b), (uint32_t)r, (uint32_t)p};
+      }
+      lo = hi;
+    }
+    pos += e - b;
+  }
+}
+void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint32_t nslices, uint32_t shift,
+                               const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out, hipStream_t s) {
+  if (!R) return;
+  hipLaunchKernelGGL(k_fill_chunks_sliced, dim3(nblocks(R, 256)), dim3(256), 0, s, src, R, adj, nslices, shift, choffs,
+                     hoffs, out);
+  KCHECK("k_fill_chunks_sliced");
+}
+
+__global__ void k_slice_bounds(const uint64_t *choffs, uint64_t R, uint32_t P, uint64_t *qb) {
+  const uint32_t q = threadIdx.x;
+  if (q <= P) qb[q] = choffs[(uint64_t)q * (R + 1)];
+}
+void launch_slice_bounds(const uint64_t *choffs, uint64_t R, uint32_t nslices, uint64_t *qb, hipStream_t s) {
+  hipLaunchKernelGGL(k_slice_bounds, dim3(1), dim3(64), 0, s, choffs, R, nslices, qb);
+  KCHECK("k_slice_bounds");
+}
+
+// Workgroups [wg0[q], wg0[q+1]) own slice q (the host sizes each range by the slice's chunk count);
+// wave j of those takes the slice's chunks j, j + NW_q, … (static: a device-wide work counter would
+// be one hot address that every XCD's atomics serialise on). Each wave appends its survivors to a
+// private arena, like k_expand_heavy.
+// load through the constant address space: a wave-uniform address becomes an s_load (the data must
+// not change during the kernel)
+template <typename T>
+__device__ __forceinline__ T sload(const T *p) {
+  return *(const __attribute__((address_space(4))) T *)(p);
+}
+
+// chunk descriptor through scalar loads (wave-uniform address; chunks are read-only in the kernel).
+// The compiler turns a plain load here into a vector load whose wait would also drain the
+// in-flight col[] prefetch (vmcnt is in order), so the two s_loads are explicit.
+__device__ __forceinline__ ChunkDesc sload_chunk(const ChunkDesc *p) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  const ChunkDesc *pu = (const ChunkDesc *)wave_bcast64((uint64_t)p);
+  u32x4 a;
+  u32x2 b;
+  u32x2 dn;
+  asm volatile(
+      "s_load_dwordx4 %0, %3, 0x0\n\t"
+      "s_load_dwordx2 %1, %3, 0x10\n\t"
+      "s_load_dwordx2 %2, %3, 0x18\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(a), "=&s"(dn), "=&s"(b)  // early-clobber: the loads land after the base is read
+      : "s"(pu)
+      : "memory");
+  ChunkDesc d;
+  d.lo = ((uint64_t)a.y << 32) | a.x;
+  d.hi = ((uint64_t)a.w << 32) | a.z;
+  d.dense = ((uint64_t)dn.y << 32) | dn.x;
+  d.row = b.x;
+  d.part = b.y;
+  return d;
+}
+
+// NC = carried columns stored through per-wave buffer descriptors (0…4); NC = -1: any count, plain
+// global stores (more than 4 bound aliases). Per chunk: the next chunk's descriptor, carried values
+// and 16 col dwords are issued first, then the current chunk's 16 LDS probes, then one ballot and the
+// stores per 64-edge slot.
+template <bool WRITE, int NC>
+__global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs a, SliceArgs sa) {
+  constexpr int NS = kHeavySlots, WPB = kSliceBlock / 64, NCV = NC < 0 ? 4 : (NC > 0 ? NC : 1);
+  __shared__ uint32_t s_bm[kSliceBits / 32];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t gw = blockIdx.x * WPB + wave;
+  uint32_t qs = 0;
+  while (qs + 1 < sa.nslices && blockIdx.x >= sa.wg0[qs + 1]) ++qs;
+  {  // stage the slice
+    const uint64_t nw = ((uint64_t)sa.V + 63) / 64 * 2;  // u32 words of the bitmap
+    const uint32_t sw = (1u << sa.shift) / 32;
+    const uint64_t w0 = (uint64_t)qs * sw;
+    const uint32_t *bm = reinterpret_cast<const uint32_t *>(a.filter);
+    for (uint32_t i = threadIdx.x; i < sw; i += kSliceBlock) s_bm[i] = w0 + i < nw ? bm[w0 + i] : 0u;
+  }
+  __syncthreads();
+  const uint32_t vbase = qs << sa.shift, smask = (1u << sa.shift) - 1;
+  const uint64_t qend = sa.qb[qs + 1];
+  const uint32_t nwq = (sa.wg0[qs + 1] - sa.wg0[qs]) * WPB;
+  const uint64_t arena = a.arena_base + (uint64_t)gw * a.arena_cap;
+  const int nc = NC < 0 ? a.ncarry : NC;
+  // per-wave output descriptors (arena-relative byte offsets fit 32 bits: arena_cap·4 < 2 GiB)
+  const int32_t arena_bytes = WRITE ? (int32_t)(a.arena_cap * 4 < 0x7fffffffull ? a.arena_cap * 4 : 0x7fffffffull) : 0;
+  auto out_rsrc = [&](int k) {
+    uint32_t *p = k < 0 ? a.out_dst : (k < nc ? a.carry_out[k] : a.out_dst);
+    return __builtin_amdgcn_make_buffer_rsrc(p + arena, 0, arena_bytes, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t od = out_rsrc(-1), oc0 = out_rsrc(0), oc1 = out_rsrc(1), oc2 = out_rsrc(2),
+                               oc3 = out_rsrc(3);
+  uint32_t acc = 0;
+  // chunk descriptors and carried values are read through the constant address space (scalar loads:
+  // they stay in SGPRs, so the col[] buffer descriptor needs no waterfall loop, and they wait on
+  // lgkmcnt instead of queueing behind the in-flight col[] loads on vmcnt)
+  struct Cur {
+    uint64_t lo;
+    uint32_t n, row, part;
+    uint32_t cv[NCV];
+    uint32_t q[NS];
+  };
+  // unconditional (a past-the-end chunk becomes an empty copy of the last one): a skipped load
+  // would make the waitcnt pass assume the worst at the join and drain the prefetch
+  auto load = [&](uint64_t c, Cur &x) {
+    const bool live = c < qend;
+    const ChunkDesc d = sload_chunk(a.chunks + (live ? c : qend - 1));
+    x.lo = d.lo;
+    x.n = live ? (uint32_t)(d.hi - d.lo) : 0u;
+    x.row = d.row;
+    x.part = d.part;
+    if (WRITE) {
+#pragma unroll
+      for (int k = 0; k < NCV; ++k) x.cv[k] = k < nc ? sload(a.carry_in[k] + x.row) : 0u;
+    }
+    // lanes past the chunk end read 0 through the descriptor's range check
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t *>(a.adj.p[x.part].col + x.lo), 0, (int32_t)(x.n * 4), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) x.q[i] = __builtin_amdgcn_raw_buffer_load_b32(cr, (i * 64 + lane) * 4, 0, 0);
+  };
+  auto process = [&](const Cur &x) {
+    uint32_t w[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) w[i] = s_bm[((x.q[i] - vbase) & smask) >> 5];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const uint32_t v = x.q[i];
+      const bool bit = (((w[i] >> (v & 31)) & 1u) != 0) & ((uint32_t)(i * 64) + lane < x.n);
+      const uint64_t m = __ballot(bit);
+      if (WRITE && bit) {
+        const uint32_t pre = lane_prefix(m);
+        const uint32_t off = pre * 4;
+        const int32_t so = (int32_t)(acc * 4);
+        __builtin_amdgcn_raw_buffer_store_b32(v, od, off, so, 0);
+        if (nc > 0) __builtin_amdgcn_raw_buffer_store_b32(x.cv[0], oc0, off, so, 0);
+        if (nc > 1) __builtin_amdgcn_raw_buffer_store_b32(x.cv[1], oc1, off, so, 0);
+        if (nc > 2) __builtin_amdgcn_raw_buffer_store_b32(x.cv[2], oc2, off, so, 0);
+        if (nc > 3) __builtin_amdgcn_raw_buffer_store_b32(x.cv[3], oc3, off, so, 0);
+        if (NC < 0)
+          for (int kk = 4; kk < nc; ++kk) a.carry_out[kk][arena + acc + pre] = a.carry_in[kk][x.row];
+      }
+      acc += (uint32_t)__popcll(m);
+    }
+  };
+  // ping-pong over two register sets (no copy of in-flight load destinations)
+  uint64_t c = sa.qb[qs] + (uint64_t)(blockIdx.x - sa.wg0[qs]) * WPB + wave;
+  Cur A, B;
+  if (c < qend) {
+    load(c, A);
+    while (true) {
+      c += nwq;
+      load(c, B);
+      process(A);
+      if (c >= qend) break;
+      c += nwq;
+      load(c, A);
+      process(B);
+      if (c >= qend) break;
+    }
+  }
+  if (lane == 0) {
+    a.seg_count[a.seg_base + gw] = acc;
+    a.seg_start[a.seg_base + gw] = arena;
+  }
+}
+
+void launch_expand_heavy_sliced(const ExpandArgs &a, const SliceArgs &sa, unsigned grid, bool write, hipStream_t s) {
+  if (!grid) return;
+  const dim3 g(grid), b(kSliceBlock);
+  if (!write) {
+    hipLaunchKernelGGL((k_expand_heavy_sliced<false, 0>), g, b, 0, s, a, sa);
+  } else {
+    switch (a.ncarry) {
+      case 0: hipLaunchKernelGGL((k_expand_heavy_sliced<true, 0>), g, b, 0, s, a, sa); break;
+      case 1: hipLaunchKernelGGL((k_expand_heavy_sliced<true, 1>), g, b, 0, s, a, sa); break;
+      case 2: hipLaunchKernelGGL((k_expand_heavy_sliced<true, 2>), g, b, 0, s, a, sa); break;
+      case 3: hipLaunchKernelGGL((k_expand_heavy_sliced<true, 3>), g, b, 0, s, a, sa); break;
+      case 4: hipLaunchKernelGGL((k_expand_heavy_sliced<true, 4>), g, b, 0, s, a, sa); break;
+      default: hipLaunchKernelGGL((k_expand_heavy_sliced<true, -1>), g, b, 0, s, a, sa); break;
+    }
+  }
+  KCHECK("k_expand_heavy_sliced");
 }
 
 void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s) {

@@ -169,6 +169,46 @@ def test_rmat_parity_all_rows_chunked(rmat10, q, monkeypatch):
     _parity(g, ref, q[1], q[2])
 
 
+SLICED_IDS = ("c2_both_ends", "in_dir", "both_dir", "three_hop", "triangle_filtered", "matches", "varlen_maxdepth",
+              "two_cols_dedup")
+
+
+@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in SLICED_IDS], ids=lambda q: q[0])
+def test_rmat_parity_sliced(rmat10, q, monkeypatch):
+    """Filtered hops through the LDS-sliced heavy kernel with 64-vertex bitmap slices (V = 1024 →
+    16 slices), so every heavy row's adjacency is cut at many slice boundaries."""
+    monkeypatch.setenv("OMX_HEAVY_DEG", "2")
+    monkeypatch.setenv("OMX_SLICE_SHIFT", "6")
+    g, ref = rmat10
+    _parity(g, ref, q[1], q[2])
+    c = __import__("orientdb_amd").OMatchStatement(q[1]).execute(g, mode=__import__("orientdb_amd").OMX_MODE_COUNT)
+    assert c.info["edges_traversed"] >= 0
+
+
+@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in SLICED_IDS], ids=lambda q: q[0])
+def test_rmat_parity_l2_probe_heavy(rmat10, q, monkeypatch):
+    """The same cases through the L2-probe heavy kernel (slicing disabled)."""
+    monkeypatch.setenv("OMX_HEAVY_DEG", "2")
+    monkeypatch.setenv("OMX_SLICED", "0")
+    g, ref = rmat10
+    _parity(g, ref, q[1], q[2])
+
+
+def test_sliced_count_mode_and_segments(rmat10, monkeypatch):
+    """Count mode and the KEEP_DEVICE block-segmented result of the sliced kernel agree with the
+    materialized rows."""
+    import orientdb_amd as o
+    monkeypatch.setenv("OMX_HEAVY_DEG", "2")
+    monkeypatch.setenv("OMX_SLICE_SHIFT", "7")
+    g, _ = rmat10
+    q = RMAT_QUERIES[0][1]
+    m = o.OMatchStatement(q).execute(g)
+    c = o.OMatchStatement(q).execute(g, mode=o.OMX_MODE_COUNT)
+    k = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_KEEP_DEVICE)
+    assert c.info["n_rows"] == m.info["n_rows"] == k.info["n_rows"] == c.info["bindings"] > 0
+    assert c.info["edges_traversed"] == m.info["edges_traversed"] == k.info["edges_traversed"]
+
+
 def test_keep_device_segmented_result(rmat10):
     """KEEP_DEVICE leaves the last filtered expansion block-segmented in HBM; row and edge counts
     equal the materialized (compacted) run."""
@@ -203,6 +243,16 @@ RMAT16 = [
 @pytest.mark.parametrize("q", RMAT16, ids=[q[0] for q in RMAT16])
 def test_rmat16_parity(rmat16, q):
     """configs[0] scale (RMAT-16, the reference's CPU-runnable case) against the C oracle."""
+    g, ref = rmat16
+    _parity(g, ref, q[1], q[2])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("q", RMAT16[1:], ids=[q[0] for q in RMAT16[1:]])
+def test_rmat16_parity_sliced(rmat16, q, monkeypatch):
+    """RMAT-16 through the sliced kernel cut into 16 slices of 4096 vertices, rows of degree ≥ 64."""
+    monkeypatch.setenv("OMX_HEAVY_DEG", "64")
+    monkeypatch.setenv("OMX_SLICE_SHIFT", "12")
     g, ref = rmat16
     _parity(g, ref, q[1], q[2])
 
