@@ -148,7 +148,7 @@ def main():
         graph_desc = {"graph": "RMAT", "scale": args.scale, "edge_factor": 16}
     t_build = time.perf_counter() - t_build
     st = o.OMatchStatement(query)
-    flags = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_KERNEL_TIMING
+    flags = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_KERNEL_TIMING | o.OMX_FLAG_TIME_HOT
     shard = (rank, world)
     for _ in range(args.warmup):
         st.execute(g, flags=flags, shard=shard, documents=False)

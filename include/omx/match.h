@@ -145,6 +145,8 @@ int omx_statement_explain(omx_statement *s, const omx_graph *g, const omx_value 
 #define OMX_FLAG_KERNEL_TIMING 1 /* time every kernel with HIP events (omx_result_kernel_stat)     */
 #define OMX_FLAG_NO_RID_MAP    2 /* return dense vertex ids instead of RIDs                         */
 #define OMX_FLAG_KEEP_DEVICE   4 /* do not copy rows to the host (benchmarking; rows stay in HBM)   */
+#define OMX_FLAG_TIME_HOT      8 /* with KERNEL_TIMING: time only the traversal kernels (expansion,  */
+                                 /* check, BFS levels), so the events do not stretch a timed step     */
 
 typedef struct omx_exec_options {
   int32_t mode;          /* OMX_MODE_*                                                            */

@@ -13,7 +13,7 @@ OMX_OK, OMX_E_UNSUPPORTED, OMX_E_INVALID, OMX_E_OOM, OMX_E_DEVICE, OMX_E_PARSE, 
 OMX_PROP_INT32, OMX_PROP_INT64, OMX_PROP_DOUBLE, OMX_PROP_STRING, OMX_PROP_BOOL = 1, 2, 3, 4, 5
 OMX_VAL_NULL, OMX_VAL_INT, OMX_VAL_DOUBLE, OMX_VAL_STRING, OMX_VAL_BOOL = 0, 1, 2, 3, 4
 OMX_MODE_MATERIALIZE, OMX_MODE_COUNT = 0, 1
-OMX_FLAG_KERNEL_TIMING, OMX_FLAG_NO_RID_MAP, OMX_FLAG_KEEP_DEVICE = 1, 2, 4
+OMX_FLAG_KERNEL_TIMING, OMX_FLAG_NO_RID_MAP, OMX_FLAG_KEEP_DEVICE, OMX_FLAG_TIME_HOT = 1, 2, 4, 8
 
 
 class omx_class_desc(C.Structure):

@@ -29,33 +29,44 @@ struct CastU64 {
 
 class Timer {
  public:
-  Timer(bool on, hipStream_t s) : on_(on), s_(s) {}
+  Timer(bool on, bool hot_only, hipStream_t s, std::vector<hipEvent_t> *pool)
+      : on_(on), hot_only_(hot_only), s_(s), pool_(pool) {}
   ~Timer() {
     for (auto &r : recs_) {
-      (void)hipEventDestroy(r.a);
-      (void)hipEventDestroy(r.b);
+      pool_->push_back(r.a);
+      pool_->push_back(r.b);
     }
   }
+  // the traversal kernels (what OMX_FLAG_TIME_HOT keeps)
+  static bool hot(const char *name) {
+    static const char *const kHot[] = {"k_expand_heavy", "k_expand_light", "k_check", "k_bfs_pull", "k_bfs_push",
+                                       "k_bfs_emit"};
+    for (const char *h : kHot)
+      if (std::strcmp(name, h) == 0) return true;
+    return false;
+  }
   void begin(const char *name, hipStream_t st = nullptr) {
-    if (!on_) return;
+    skip_ = !on_ || (hot_only_ && !hot(name));
+    if (skip_) return;
     Rec r;
     r.name = name;
     r.s = st ? st : s_;
-    HIP_CHECK(hipEventCreate(&r.a));
-    HIP_CHECK(hipEventCreate(&r.b));
+    r.a = event();
+    r.b = event();
     HIP_CHECK(hipEventRecord(r.a, r.s));
     recs_.push_back(r);
   }
   void end(uint64_t bytes = 0) {
-    if (!on_) return;
+    if (skip_) return;
     recs_.back().bytes = bytes;
     HIP_CHECK(hipEventRecord(recs_.back().b, recs_.back().s));
   }
   // algorithmic bytes of a record when they are only known after the launch
   void amend(uint64_t bytes) {
-    if (on_ && !recs_.empty()) recs_.back().bytes = bytes;
+    if (!skip_ && !recs_.empty()) recs_.back().bytes = bytes;
   }
-  size_t last() const { return recs_.empty() ? 0 : recs_.size() - 1; }
+  // index of the record just closed (SIZE_MAX when it was not recorded)
+  size_t last() const { return skip_ || recs_.empty() ? SIZE_MAX : recs_.size() - 1; }
   void amend_at(size_t i, uint64_t bytes) {
     if (on_ && i < recs_.size()) recs_[i].bytes = bytes;
   }
@@ -77,14 +88,26 @@ class Timer {
   }
 
  private:
+  hipEvent_t event() {
+    hipEvent_t e;
+    if (!pool_->empty()) {
+      e = pool_->back();
+      pool_->pop_back();
+    } else {
+      HIP_CHECK(hipEventCreate(&e));
+    }
+    return e;
+  }
   struct Rec {
     std::string name;
     hipEvent_t a, b;
     hipStream_t s;
     uint64_t bytes = 0;
   };
-  bool on_;
+  bool on_, hot_only_;
+  bool skip_ = true;
   hipStream_t s_;
+  std::vector<hipEvent_t> *pool_;
   std::vector<Rec> recs_;
 };
 
@@ -101,10 +124,13 @@ __global__ void k_unpack_tuple(const uint64_t *keys, uint64_t n, int k, int vbit
 class Executor {
  public:
   Executor(Graph &g, const Plan &p, const omx_exec_options &o)
-      : g_(g), p_(p), o_(o), s_(g.stream), pool_(g.pool), tm_((o.flags & OMX_FLAG_KERNEL_TIMING) != 0, g.stream) {
+      : g_(g), p_(p), o_(o), s_(g.stream), pool_(g.pool), tm_((o.flags & OMX_FLAG_KERNEL_TIMING) != 0, (o.flags & OMX_FLAG_TIME_HOT) != 0, g.stream, &g.event_pool) {
     nwords_ = ((uint64_t)g.V + 63) / 64;
     // rows with at least this many neighbours take the chunked kernel (tests lower it to force the path)
-    if (const char *h = std::getenv("OMX_HEAVY_DEG")) heavy_deg_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
+    if (const char *h = std::getenv("OMX_HEAVY_DEG")) {
+      heavy_deg_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
+      heavy_deg_sliced_ = heavy_deg_;
+    }
     // variable-length strategy: "bfs" (multi-source BFS whenever exact), "pairs" ((row, v) levels), auto
     if (const char *v = std::getenv("OMX_VARLEN")) varlen_mode_ = v;
     if (const char *sl = std::getenv("OMX_SLICED")) sliced_ = std::strcmp(sl, "0") != 0;
@@ -217,6 +243,7 @@ class Executor {
   int dedup_ran_ = 0;
   int cus_ = 0;
   uint64_t heavy_deg_ = kHeavyDeg;
+  uint64_t heavy_deg_sliced_ = kHeavyDegSliced;
   bool sliced_ = true;  // LDS-sliced heavy kernel for filtered hops (OMX_SLICED=0 disables)
   uint32_t slice_shift_ = 20;  // log2 vertices per slice (OMX_SLICE_SHIFT, 6..20: tests cut small graphs)
   std::string varlen_mode_ = "auto";
@@ -234,9 +261,11 @@ class Executor {
   }
   template <class T>
   T read1(const T *dptr) {
-    T v;
-    HIP_CHECK(hipMemcpyAsync(&v, dptr, sizeof(T), hipMemcpyDeviceToHost, s_));
+    static_assert(sizeof(T) <= sizeof(uint64_t), "read1 reads one word");
+    HIP_CHECK(hipMemcpyAsync(g_.h_stage, dptr, sizeof(T), hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipStreamSynchronize(s_));
+    T v;
+    std::memcpy(&v, g_.h_stage, sizeof(T));
     return v;
   }
 
@@ -418,7 +447,7 @@ class Executor {
     DBuf<uint32_t> nch(&pool_, nchn);
     DBuf<uint64_t> choffs(&pool_, nchn);
     tm_.begin("k_row_split");
-    if (sliced) launch_row_split_sliced(src, R, adj, heavy_deg_, P, slice_shift_, light.p, heavy.p, nch.p, s_);
+    if (sliced) launch_row_split_sliced(src, R, adj, heavy_deg_sliced_, P, slice_shift_, light.p, heavy.p, nch.p, s_);
     else launch_row_split(src, R, adj, heavy_deg_, light.p, heavy.p, nch.p, s_);
     tm_.end(R * (4 + 16ull * adj.n) + (R + 1) * 20);
     tm_.begin("scan_degrees");
@@ -427,32 +456,24 @@ class Executor {
     hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> nit(nch.p, CastU64());
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, nit, choffs.p, (int64_t)nchn, s_); });
     tm_.end((R + 1) * 40);
-    uint64_t tot[3];
-    HIP_CHECK(hipMemcpyAsync(&tot[0], loffs.p + R, 8, hipMemcpyDeviceToHost, s_));
-    HIP_CHECK(hipMemcpyAsync(&tot[1], hoffs.p + R, 8, hipMemcpyDeviceToHost, s_));
-    HIP_CHECK(hipMemcpyAsync(&tot[2], choffs.p + (nchn - 1), 8, hipMemcpyDeviceToHost, s_));
+    // one host read for the totals (and the slices' chunk bounds)
+    DBuf<uint64_t> meta(&pool_, 4 + P), qb;
+    if (sliced) qb = DBuf<uint64_t>(&pool_, P + 1);
+    launch_expand_meta(loffs.p, hoffs.p, choffs.p, R, nchn, sliced ? P : 0, qb.p, meta.p, s_);
+    HIP_CHECK(hipMemcpyAsync(g_.h_stage, meta.p, (4 + P) * 8, hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipStreamSynchronize(s_));
-    const uint64_t EL = tot[0], EH = tot[1], nchunks = tot[2];
+    const uint64_t EL = g_.h_stage[0], EH = g_.h_stage[1], nchunks = g_.h_stage[2];
+    std::vector<uint64_t> hqb(g_.h_stage + 3, g_.h_stage + 3 + (sliced ? P + 1 : 0));
     const uint64_t E = EL + EH;
     o.E = E;
     if (E == 0) return o;
     DBuf<ChunkDesc> chunks;
-    DBuf<uint64_t> qb;
-    std::vector<uint64_t> hqb;
     if (nchunks) {
       chunks = DBuf<ChunkDesc>(&pool_, nchunks);
       tm_.begin("k_fill_chunks");
-      if (sliced) {
-        launch_fill_chunks_sliced(src, R, adj, P, slice_shift_, choffs.p, hoffs.p, chunks.p, s_);
-        qb = DBuf<uint64_t>(&pool_, P + 1);
-        launch_slice_bounds(choffs.p, R, P, qb.p, s_);
-        hqb.resize(P + 1);
-        HIP_CHECK(hipMemcpyAsync(hqb.data(), qb.p, (P + 1) * 8, hipMemcpyDeviceToHost, s_));
-      } else {
-        launch_fill_chunks(src, R, adj, choffs.p, hoffs.p, chunks.p, s_);
-      }
+      if (sliced) launch_fill_chunks_sliced(src, R, adj, P, slice_shift_, choffs.p, hoffs.p, chunks.p, s_);
+      else launch_fill_chunks(src, R, adj, choffs.p, hoffs.p, chunks.p, s_);
       tm_.end(nchunks * sizeof(ChunkDesc));
-      if (sliced) HIP_CHECK(hipStreamSynchronize(s_));
     }
     const uint64_t ntiles = EL ? (R + EL + kExpandTile - 1) / kExpandTile : 0;
     DBuf<uint64_t> part;
@@ -587,11 +608,13 @@ class Executor {
     hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> sit(o.seg_count.p, CastU64());
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, sit, soffs.p + 1, (int64_t)o.nseg, s_); });
     HIP_CHECK(hipMemsetAsync(soffs.p, 0, 8, s_));
-    uint64_t nh_n[3] = {0, 0, 0};  // rows emitted by the heavy kernel's segments, all rows, member edges
-    HIP_CHECK(hipMemcpyAsync(&nh_n[0], soffs.p + nseg_h, 8, hipMemcpyDeviceToHost, s_));
-    HIP_CHECK(hipMemcpyAsync(&nh_n[1], soffs.p + o.nseg, 8, hipMemcpyDeviceToHost, s_));
-    if (member) HIP_CHECK(hipMemcpyAsync(&nh_n[2], medges.p, 8, hipMemcpyDeviceToHost, s_));
+    // rows emitted by the heavy kernel's segments, all rows, member edges: one host read
+    const uint64_t *words[3] = {soffs.p + nseg_h, soffs.p + o.nseg, member ? (const uint64_t *)medges.p : nullptr};
+    DBuf<uint64_t> wbuf(&pool_, 3);
+    launch_gather_words(words, 3, wbuf.p, s_);
+    HIP_CHECK(hipMemcpyAsync(g_.h_stage, wbuf.p, 3 * 8, hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipStreamSynchronize(s_));
+    const uint64_t nh_n[3] = {g_.h_stage[0], g_.h_stage[1], g_.h_stage[2]};
     o.E_member = nh_n[2];
     const uint64_t n = nh_n[1];
     if (rec_h != SIZE_MAX) tm_.amend_at(rec_h, 4 * EH + outw * nh_n[0]);

@@ -80,6 +80,8 @@ Graph::~Graph() {
     for (auto &p : props) { f(p.d_values); f(p.d_present); }
     if (stream) (void)hipStreamDestroy(stream);
     if (stream2) (void)hipStreamDestroy(stream2);
+    if (h_stage) (void)hipHostFree(h_stage);
+    for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
   }
 }
 
@@ -310,6 +312,7 @@ Graph *graph_create(const omx_graph_desc *d) {
     HIP_CHECK(hipSetDevice(g->device));
     HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking));
+    HIP_CHECK(hipHostMalloc((void **)&g->h_stage, Graph::kStageWords * sizeof(uint64_t), hipHostMallocDefault));
     uint64_t &acc = g->device_bytes;
     g->d_vclass = upload(d->vertex_class, V, acc);
     g->d_rids = upload(d->rids, V, acc);

@@ -121,6 +121,9 @@ struct Graph {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // side stream: light-row expansion runs beside the heavy-row one
   DevicePool pool;
+  uint64_t *h_stage = nullptr;             // pinned host words for small device→host reads
+  static constexpr int kStageWords = 512;
+  std::vector<hipEvent_t> event_pool;      // reusable timing events (OMX_FLAG_KERNEL_TIMING)
 
   ~Graph();
   bool on_device() const { return device >= 0; }

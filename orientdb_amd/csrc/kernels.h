@@ -27,6 +27,7 @@ constexpr int kHeavySlots = kChunk / 64;           // lane l takes edge l of eac
 constexpr uint32_t kSliceBits = 1u << 20;
 constexpr uint32_t kSliceWords = kSliceBits / 32;  // u32 words per slice
 constexpr int kMaxSlices = 16;                     // V ≤ 16·2^20; beyond that the L2-probe kernel is used
+constexpr uint64_t kHeavyDegSliced = 256;         // LDS probes make short chunks cheap: a lower cut
 constexpr int kSliceBlock = 1024;                  // 16 waves: one workgroup per CU (LDS-limited)
 
 struct SliceArgs {
@@ -102,8 +103,9 @@ void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, u
                              uint32_t shift, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s);
 void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint32_t nslices, uint32_t shift,
                                const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out, hipStream_t s);
-// qb[q] = choffs[q·(R+1)] for q ≤ P
-void launch_slice_bounds(const uint64_t *choffs, uint64_t R, uint32_t nslices, uint64_t *qb, hipStream_t s);
+// meta = {loffs[R], hoffs[R], choffs[nchn-1], qb[0..P]}; qb[q] = choffs[q·(R+1)] (nslices = 0: unsliced)
+void launch_expand_meta(const uint64_t *loffs, const uint64_t *hoffs, const uint64_t *choffs, uint64_t R,
+                        uint64_t nchn, uint32_t nslices, uint64_t *qb, uint64_t *meta, hipStream_t s);
 // grid = sa.wg0[P] workgroups (one per CU); wave w appends to arena_base + w·arena_cap and reports
 // seg_count/seg_start[seg_base + w]
 void launch_expand_heavy_sliced(const ExpandArgs &a, const SliceArgs &sa, unsigned grid, bool write, hipStream_t s);
@@ -113,6 +115,9 @@ void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStre
 int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool member = false);
 void launch_compact_segments(int ncols, uint32_t *const *in, uint32_t *const *out, const uint64_t *seg_start,
                              const uint32_t *seg_count, const uint64_t *seg_offs, uint32_t nseg, hipStream_t s);
+
+// out[i] = *ptrs[i] (nullptr → 0), i < n ≤ 8: several device words for one host read
+void launch_gather_words(const uint64_t *const *ptrs, int n, uint64_t *out, hipStream_t s);
 
 void launch_check(const uint32_t *src, const uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
                   uint8_t *flags, hipStream_t s);

@@ -654,22 +654,52 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
 // chunk's probes all land in the slice its workgroup holds. HBM then only streams col[] (coalesced
 // dwords, next chunk prefetched) and the surviving rows.
 
-__device__ __forceinline__ uint64_t col_lower_bound(const uint32_t *col, uint64_t lo, uint64_t hi, uint64_t x) {
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if ((uint64_t)col[mid] < x) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
 // sliced chunks need no window alignment (buffer loads with a per-chunk base): ⌈len / kChunk⌉ pieces
 __device__ __forceinline__ uint32_t chunk_pieces(uint64_t lo, uint64_t hi) {
   return hi > lo ? (uint32_t)((hi - lo + kChunk - 1) / kChunk) : 0u;
 }
 
-__global__ void k_row_split_sliced(const uint32_t *src, uint64_t R, DAdj adj, uint64_t heavy_deg, uint32_t P,
-                                   uint32_t shift, uint64_t *light, uint64_t *heavy, uint32_t *nchq) {
+// cut[q] = first index in col[b, e) whose neighbour is ≥ q·2^shift (cut[0] = b, cut[P] = e); the P−1
+// binary searches run side by side so their loads overlap. MAXP ≥ P is a compile-time bound so the
+// per-slice arrays stay in registers; positions are kept relative to b (a row has < 2^32 edges).
+template <int MAXP>
+__device__ __forceinline__ void slice_cuts(const uint32_t *col, uint64_t b, uint64_t e, uint32_t P, uint32_t shift,
+                                           uint32_t (&cut)[MAXP + 1]) {
+  const uint32_t n = (uint32_t)(e - b);
+  const uint32_t *c = col + b;
+  uint32_t hi[MAXP];
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q) {
+    cut[q] = 0;
+    hi[q] = q > 0 && (uint32_t)q < P ? n : 0;
+  }
+  bool any = n > 0;
+  while (any) {
+    any = false;
+    uint32_t x[MAXP], mid[MAXP];
+#pragma unroll
+    for (int q = 1; q < MAXP; ++q) {
+      mid[q] = (cut[q] + hi[q]) >> 1;
+      x[q] = cut[q] < hi[q] ? c[mid[q]] : 0u;
+    }
+#pragma unroll
+    for (int q = 1; q < MAXP; ++q) {
+      if (cut[q] < hi[q]) {
+        if ((uint64_t)x[q] < ((uint64_t)q << shift)) cut[q] = mid[q] + 1;
+        else hi[q] = mid[q];
+        any |= cut[q] < hi[q];
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 1; q <= MAXP; ++q)
+    if ((uint32_t)q >= P) cut[q] = n;
+}
+
+template <int MAXP>
+__global__ __launch_bounds__(256) void k_row_split_sliced(const uint32_t *src, uint64_t R, DAdj adj, uint64_t heavy_deg,
+                                                          uint32_t P, uint32_t shift, uint64_t *light, uint64_t *heavy,
+                                                          uint32_t *nchq) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r > R) return;
   const uint64_t stride = R + 1;
@@ -690,64 +720,95 @@ __global__ void k_row_split_sliced(const uint32_t *src, uint64_t R, DAdj adj, ui
   }
   light[r] = 0;
   heavy[r] = d;
-  uint32_t cnt[kMaxSlices];
-  for (uint32_t q = 0; q < P; ++q) cnt[q] = 0;
+  uint32_t cnt[MAXP];
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q) cnt[q] = 0;
   for (int p = 0; p < adj.n; ++p) {
-    const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
-    uint64_t lo = b;
-    for (uint32_t q = 0; q < P; ++q) {
-      const uint64_t hi = q + 1 == P ? e : col_lower_bound(adj.p[p].col, lo, e, (uint64_t)(q + 1) << shift);
-      cnt[q] += chunk_pieces(lo, hi);
-      lo = hi;
-    }
+    uint32_t cut[MAXP + 1];
+    slice_cuts<MAXP>(adj.p[p].col, adj.p[p].rp[v], adj.p[p].rp[v + 1], P, shift, cut);
+#pragma unroll
+    for (int q = 0; q < MAXP; ++q) cnt[q] += chunk_pieces(cut[q], cut[q + 1]);
   }
-  for (uint32_t q = 0; q < P; ++q) nchq[q * stride + r] = cnt[q];
-}
-void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint32_t nslices,
-                             uint32_t shift, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s) {
-  hipLaunchKernelGGL(k_row_split_sliced, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, R, adj, heavy_deg, nslices,
-                     shift, light, heavy, nchq);
-  KCHECK("k_row_split_sliced");
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q)
+    if ((uint32_t)q < P) nchq[q * stride + r] = cnt[q];
 }
 
-__global__ void k_fill_chunks_sliced(const uint32_t *src, uint64_t R, DAdj adj, uint32_t P, uint32_t shift,
-                                     const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out) {
+template <int MAXP>
+__global__ __launch_bounds__(256) void k_fill_chunks_sliced(const uint32_t *src, uint64_t R, DAdj adj, uint32_t P,
+                                                            uint32_t shift, const uint64_t *choffs,
+                                                            const uint64_t *hoffs, ChunkDesc *out) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || hoffs[r + 1] == hoffs[r]) return;  // light row
   const uint64_t stride = R + 1;
   const uint32_t v = src[r];
-  uint64_t o[kMaxSlices];
-  for (uint32_t q = 0; q < P; ++q) o[q] = choffs[q * stride + r];
   uint64_t pos = hoffs[r];  // dense index of the row's first edge (parts in order)
+  uint64_t o[MAXP];
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q) o[q] = (uint32_t)q < P ? choffs[q * stride + r] : 0;
   for (int p = 0; p < adj.n; ++p) {
     const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
-    uint64_t lo = b;
-    for (uint32_t q = 0; q < P; ++q) {
-      const uint64_t hi = q + 1 == P ? e : col_lower_bound(adj.p[p].col, lo, e, (uint64_t)(q + 1) << shift);
-      for (uint64_t clo = lo; clo < hi; clo += kChunk) {  // as chunk_pieces
-        const uint64_t chi = clo + kChunk < hi ? clo + kChunk : hi;
-        out[o[q]++] = ChunkDesc{clo, chi, pos + (clo - b), (uint32_t)r, (uint32_t)p};
+    uint32_t cut[MAXP + 1];
+    slice_cuts<MAXP>(adj.p[p].col, b, e, P, shift, cut);
+#pragma unroll
+    for (int q = 0; q < MAXP; ++q) {
+      for (uint32_t clo = cut[q]; clo < cut[q + 1]; clo += kChunk) {  // as chunk_pieces
+        const uint32_t chi = clo + kChunk < cut[q + 1] ? clo + kChunk : cut[q + 1];
+        out[o[q]++] = ChunkDesc{b + clo, b + chi, pos + clo, (uint32_t)r, (uint32_t)p};
       }
-      lo = hi;
     }
     pos += e - b;
   }
 }
+
+#define OMX_BY_MAXP(P, CALL) \
+  do {                       \
+    if ((P) <= 1) CALL(1);   \
+    else if ((P) <= 2) CALL(2); \
+    else if ((P) <= 4) CALL(4); \
+    else if ((P) <= 8) CALL(8); \
+    else CALL(16);           \
+  } while (0)
+
+void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint32_t nslices,
+                             uint32_t shift, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s) {
+#define OMX_RS(M) hipLaunchKernelGGL(k_row_split_sliced<M>, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, R, adj, \
+                                     heavy_deg, nslices, shift, light, heavy, nchq)
+  OMX_BY_MAXP(nslices, OMX_RS);
+#undef OMX_RS
+  KCHECK("k_row_split_sliced");
+}
+
 void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint32_t nslices, uint32_t shift,
                                const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out, hipStream_t s) {
   if (!R) return;
-  hipLaunchKernelGGL(k_fill_chunks_sliced, dim3(nblocks(R, 256)), dim3(256), 0, s, src, R, adj, nslices, shift, choffs,
-                     hoffs, out);
+#define OMX_FC(M) hipLaunchKernelGGL(k_fill_chunks_sliced<M>, dim3(nblocks(R, 256)), dim3(256), 0, s, src, R, adj, \
+                                     nslices, shift, choffs, hoffs, out)
+  OMX_BY_MAXP(nslices, OMX_FC);
+#undef OMX_FC
   KCHECK("k_fill_chunks_sliced");
 }
 
-__global__ void k_slice_bounds(const uint64_t *choffs, uint64_t R, uint32_t P, uint64_t *qb) {
-  const uint32_t q = threadIdx.x;
-  if (q <= P) qb[q] = choffs[(uint64_t)q * (R + 1)];
+// the totals one host read needs after the binning scans: meta = {Σ light, Σ heavy, chunks,
+// qb[0..P]} and qb[q] = first chunk of slice q (P = 0: unsliced)
+__global__ void k_expand_meta(const uint64_t *loffs, const uint64_t *hoffs, const uint64_t *choffs, uint64_t R,
+                              uint64_t nchn, uint32_t P, uint64_t *qb, uint64_t *meta) {
+  const uint32_t t = threadIdx.x;
+  if (t == 0) {
+    meta[0] = loffs[R];
+    meta[1] = hoffs[R];
+    meta[2] = choffs[nchn - 1];
+  }
+  if (P && t <= P) {
+    const uint64_t x = choffs[(uint64_t)t * (R + 1)];
+    qb[t] = x;
+    meta[3 + t] = x;
+  }
 }
-void launch_slice_bounds(const uint64_t *choffs, uint64_t R, uint32_t nslices, uint64_t *qb, hipStream_t s) {
-  hipLaunchKernelGGL(k_slice_bounds, dim3(1), dim3(64), 0, s, choffs, R, nslices, qb);
-  KCHECK("k_slice_bounds");
+void launch_expand_meta(const uint64_t *loffs, const uint64_t *hoffs, const uint64_t *choffs, uint64_t R,
+                        uint64_t nchn, uint32_t nslices, uint64_t *qb, uint64_t *meta, hipStream_t s) {
+  hipLaunchKernelGGL(k_expand_meta, dim3(1), dim3(64), 0, s, loffs, hoffs, choffs, R, nchn, nslices, qb, meta);
+  KCHECK("k_expand_meta");
 }
 
 // Workgroups [wg0[q], wg0[q+1]) own slice q (the host sizes each range by the slice's chunk count);
@@ -1025,6 +1086,21 @@ void launch_check(const uint32_t *src, const uint32_t *dst, uint64_t R, const DA
   if (!R) return;
   hipLaunchKernelGGL(k_check, dim3(nblocks(R, 256)), dim3(256), 0, s, src, dst, R, adj, filter, flags);
   KCHECK("k_check");
+}
+
+// ---- small host reads ------------------------------------------------------------------------------
+struct WordPtrs {
+  const unsigned long long *p[8];
+};
+__global__ void k_gather_words(WordPtrs w, int n, unsigned long long *out) {
+  const int i = threadIdx.x;
+  if (i < n) out[i] = w.p[i] ? *w.p[i] : 0ull;
+}
+void launch_gather_words(const uint64_t *const *ptrs, int n, uint64_t *out, hipStream_t s) {
+  WordPtrs w{};
+  for (int i = 0; i < n && i < 8; ++i) w.p[i] = reinterpret_cast<const unsigned long long *>(ptrs[i]);
+  hipLaunchKernelGGL(k_gather_words, dim3(1), dim3(64), 0, s, w, n, reinterpret_cast<unsigned long long *>(out));
+  KCHECK("k_gather_words");
 }
 
 // ---- helpers ----------------------------------------------------------------------------------------
