@@ -419,6 +419,26 @@ class Executor {
     return cus_;
   }
 
+  // the slice-cut index of every part of an adjacency (built once per CSR and slice size)
+  DCuts slice_cuts_of(const AdjSpec &adjs, uint32_t P) {
+    DCuts c{};
+    if (P < 2) return c;
+    for (size_t i = 0; i < adjs.parts.size(); ++i) {
+      EdgeSet &es = g_.esets[adjs.parts[i].first];
+      const int dir = adjs.parts[i].second;
+      uint32_t *&d = es.d_cuts[dir][slice_shift_];
+      if (!d) {
+        const size_t bytes = (size_t)g_.V * (P - 1) * sizeof(uint32_t);
+        HIP_CHECK(hipMalloc((void **)&d, std::max<size_t>(bytes, 4)));
+        g_.device_bytes += bytes;
+        launch_build_cuts(dir == 0 ? es.d_out_rp : es.d_in_rp, dir == 0 ? es.d_out_col : es.d_in_col, g_.V, P,
+                          slice_shift_, d, s_);
+      }
+      c.c[i] = d;
+    }
+    return c;
+  }
+
   // One pattern-edge expansion of R rows (src column) with an optional target bitmap, carrying the
   // listed columns. write=false only counts. allow_segmented leaves a filtered result as per-block
   // segments (the final step of a plan whose rows are distinct by construction).
@@ -443,11 +463,12 @@ class Executor {
                         (uint64_t)g_.V <= ((uint64_t)kMaxSlices << slice_shift_);
     const uint32_t P = sliced ? (uint32_t)(((uint64_t)g_.V + (1ull << slice_shift_) - 1) >> slice_shift_) : 1;
     const uint64_t nchn = sliced ? (uint64_t)P * (R + 1) + 1 : R + 1;
+    const DCuts cuts = sliced ? slice_cuts_of(adjs, P) : DCuts{};
     DBuf<uint64_t> light(&pool_, R + 1), heavy(&pool_, R + 1), loffs(&pool_, R + 1), hoffs(&pool_, R + 1);
     DBuf<uint32_t> nch(&pool_, nchn);
     DBuf<uint64_t> choffs(&pool_, nchn);
     tm_.begin("k_row_split");
-    if (sliced) launch_row_split_sliced(src, R, adj, heavy_deg_sliced_, P, slice_shift_, light.p, heavy.p, nch.p, s_);
+    if (sliced) launch_row_split_sliced(src, R, adj, cuts, heavy_deg_sliced_, P, light.p, heavy.p, nch.p, s_);
     else launch_row_split(src, R, adj, heavy_deg_, light.p, heavy.p, nch.p, s_);
     tm_.end(R * (4 + 16ull * adj.n) + (R + 1) * 20);
     tm_.begin("scan_degrees");
@@ -471,7 +492,7 @@ class Executor {
     if (nchunks) {
       chunks = DBuf<ChunkDesc>(&pool_, nchunks);
       tm_.begin("k_fill_chunks");
-      if (sliced) launch_fill_chunks_sliced(src, R, adj, P, slice_shift_, choffs.p, hoffs.p, chunks.p, s_);
+      if (sliced) launch_fill_chunks_sliced(src, R, adj, cuts, P, choffs.p, hoffs.p, chunks.p, s_);
       else launch_fill_chunks(src, R, adj, choffs.p, hoffs.p, chunks.p, s_);
       tm_.end(nchunks * sizeof(ChunkDesc));
     }

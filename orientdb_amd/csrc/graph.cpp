@@ -76,7 +76,11 @@ Graph::~Graph() {
     f(d_vclass);
     f(d_rids);
     f(d_cols);
-    for (auto &e : esets) { f(e.d_out_rp); f(e.d_in_rp); f(e.d_out_col); f(e.d_in_col); }
+    for (auto &e : esets) {
+      f(e.d_out_rp); f(e.d_in_rp); f(e.d_out_col); f(e.d_in_col);
+      for (auto &m : e.d_cuts)
+        for (auto &kv : m) f(kv.second);
+    }
     for (auto &p : props) { f(p.d_values); f(p.d_present); }
     if (stream) (void)hipStreamDestroy(stream);
     if (stream2) (void)hipStreamDestroy(stream2);

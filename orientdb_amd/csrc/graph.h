@@ -85,6 +85,10 @@ struct EdgeSet {
   bool out_simple = true, in_simple = true;  // rows strictly ascending (no parallel edges)
   uint64_t *d_out_rp = nullptr, *d_in_rp = nullptr;
   uint32_t *d_out_col = nullptr, *d_in_col = nullptr;
+  // slice-cut index of a CSR (0 = out, 1 = in), per slice shift: for every vertex, the offsets inside
+  // its sorted row where neighbours reach q·2^shift (q = 1…P−1); built on the first filtered hop
+  // that uses the CSR (a property of the immutable snapshot, like the sort order)
+  std::map<uint32_t, uint32_t *> d_cuts[2];
 };
 
 struct Property {

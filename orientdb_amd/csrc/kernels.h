@@ -30,6 +30,11 @@ constexpr int kMaxSlices = 16;                     // V ≤ 16·2^20; beyond tha
 constexpr uint64_t kHeavyDegSliced = 256;         // LDS probes make short chunks cheap: a lower cut
 constexpr int kSliceBlock = 1024;                  // 16 waves: one workgroup per CU (LDS-limited)
 
+// per adjacency part: the CSR's slice-cut index (EdgeSet::d_cuts), P−1 offsets per vertex
+struct DCuts {
+  const uint32_t *c[kMaxAdjParts];
+};
+
 struct SliceArgs {
   const uint64_t *qb;            // [P+1] chunk index bounds of each slice
   uint32_t wg0[kMaxSlices + 1];  // workgroups [wg0[q], wg0[q+1]) own slice q
@@ -99,9 +104,11 @@ void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t 
                          hipStream_t s);
 // sliced chunks: nchq[q·(R+1) + r] = chunks of heavy row r inside slice q (layout slice-major so one
 // scan gives each slice a contiguous chunk range); light/heavy degrees as launch_row_split
-void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint32_t nslices,
-                             uint32_t shift, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s);
-void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint32_t nslices, uint32_t shift,
+void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t V, uint32_t nslices, uint32_t shift,
+                       uint32_t *cuts, hipStream_t s);
+void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint64_t heavy_deg,
+                             uint32_t nslices, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s);
+void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint32_t nslices,
                                const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out, hipStream_t s);
 // meta = {loffs[R], hoffs[R], choffs[nchn-1], qb[0..P]}; qb[q] = choffs[q·(R+1)] (nslices = 0: unsliced)
 void launch_expand_meta(const uint64_t *loffs, const uint64_t *hoffs, const uint64_t *choffs, uint64_t R,

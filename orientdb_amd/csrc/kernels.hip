@@ -696,10 +696,32 @@ __device__ __forceinline__ void slice_cuts(const uint32_t *col, uint64_t b, uint
     if ((uint32_t)q >= P) cut[q] = n;
 }
 
+// slice-cut index of one CSR: cuts[v·(P−1) + q−1] = cut[q] of row v (relative to the row start)
 template <int MAXP>
-__global__ __launch_bounds__(256) void k_row_split_sliced(const uint32_t *src, uint64_t R, DAdj adj, uint64_t heavy_deg,
-                                                          uint32_t P, uint32_t shift, uint64_t *light, uint64_t *heavy,
-                                                          uint32_t *nchq) {
+__global__ __launch_bounds__(256) void k_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t V, uint32_t P,
+                                                    uint32_t shift, uint32_t *cuts) {
+  const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= V) return;
+  uint32_t cut[MAXP + 1];
+  slice_cuts<MAXP>(col, rp[v], rp[v + 1], P, shift, cut);
+#pragma unroll
+  for (int q = 1; q < MAXP; ++q)
+    if ((uint32_t)q < P) cuts[v * (P - 1) + q - 1] = cut[q];
+}
+
+// the slice bounds of row v in part p (cut[0] = 0, cut[P] = degree)
+template <int MAXP>
+__device__ __forceinline__ void load_cuts(const uint32_t *c, uint32_t v, uint32_t n, uint32_t P,
+                                          uint32_t (&cut)[MAXP + 1]) {
+  cut[0] = 0;
+#pragma unroll
+  for (int q = 1; q <= MAXP; ++q) cut[q] = (uint32_t)q < P ? c[(uint64_t)v * (P - 1) + q - 1] : n;
+}
+
+template <int MAXP>
+__global__ __launch_bounds__(256) void k_row_split_sliced(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
+                                                          uint64_t heavy_deg, uint32_t P, uint64_t *light,
+                                                          uint64_t *heavy, uint32_t *nchq) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r > R) return;
   const uint64_t stride = R + 1;
@@ -725,7 +747,7 @@ __global__ __launch_bounds__(256) void k_row_split_sliced(const uint32_t *src, u
   for (int q = 0; q < MAXP; ++q) cnt[q] = 0;
   for (int p = 0; p < adj.n; ++p) {
     uint32_t cut[MAXP + 1];
-    slice_cuts<MAXP>(adj.p[p].col, adj.p[p].rp[v], adj.p[p].rp[v + 1], P, shift, cut);
+    load_cuts<MAXP>(cuts.c[p], v, (uint32_t)(adj.p[p].rp[v + 1] - adj.p[p].rp[v]), P, cut);
 #pragma unroll
     for (int q = 0; q < MAXP; ++q) cnt[q] += chunk_pieces(cut[q], cut[q + 1]);
   }
@@ -735,9 +757,9 @@ __global__ __launch_bounds__(256) void k_row_split_sliced(const uint32_t *src, u
 }
 
 template <int MAXP>
-__global__ __launch_bounds__(256) void k_fill_chunks_sliced(const uint32_t *src, uint64_t R, DAdj adj, uint32_t P,
-                                                            uint32_t shift, const uint64_t *choffs,
-                                                            const uint64_t *hoffs, ChunkDesc *out) {
+__global__ __launch_bounds__(256) void k_fill_chunks_sliced(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
+                                                            uint32_t P, const uint64_t *choffs, const uint64_t *hoffs,
+                                                            ChunkDesc *out) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || hoffs[r + 1] == hoffs[r]) return;  // light row
   const uint64_t stride = R + 1;
@@ -749,7 +771,7 @@ __global__ __launch_bounds__(256) void k_fill_chunks_sliced(const uint32_t *src,
   for (int p = 0; p < adj.n; ++p) {
     const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
     uint32_t cut[MAXP + 1];
-    slice_cuts<MAXP>(adj.p[p].col, b, e, P, shift, cut);
+    load_cuts<MAXP>(cuts.c[p], v, (uint32_t)(e - b), P, cut);
 #pragma unroll
     for (int q = 0; q < MAXP; ++q) {
       for (uint32_t clo = cut[q]; clo < cut[q + 1]; clo += kChunk) {  // as chunk_pieces
@@ -770,20 +792,30 @@ __global__ __launch_bounds__(256) void k_fill_chunks_sliced(const uint32_t *src,
     else CALL(16);           \
   } while (0)
 
-void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint32_t nslices,
-                             uint32_t shift, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s) {
+void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t V, uint32_t nslices, uint32_t shift,
+                       uint32_t *cuts, hipStream_t s) {
+  if (!V || nslices < 2) return;
+#define OMX_BC(M) hipLaunchKernelGGL(k_build_cuts<M>, dim3(nblocks(V, 256)), dim3(256), 0, s, rp, col, V, nslices, \
+                                     shift, cuts)
+  OMX_BY_MAXP(nslices, OMX_BC);
+#undef OMX_BC
+  KCHECK("k_build_cuts");
+}
+
+void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint64_t heavy_deg,
+                             uint32_t nslices, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s) {
 #define OMX_RS(M) hipLaunchKernelGGL(k_row_split_sliced<M>, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, R, adj, \
-                                     heavy_deg, nslices, shift, light, heavy, nchq)
+                                     cuts, heavy_deg, nslices, light, heavy, nchq)
   OMX_BY_MAXP(nslices, OMX_RS);
 #undef OMX_RS
   KCHECK("k_row_split_sliced");
 }
 
-void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, uint32_t nslices, uint32_t shift,
+void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint32_t nslices,
                                const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out, hipStream_t s) {
   if (!R) return;
 #define OMX_FC(M) hipLaunchKernelGGL(k_fill_chunks_sliced<M>, dim3(nblocks(R, 256)), dim3(256), 0, s, src, R, adj, \
-                                     nslices, shift, choffs, hoffs, out)
+                                     cuts, nslices, choffs, hoffs, out)
   OMX_BY_MAXP(nslices, OMX_FC);
 #undef OMX_FC
   KCHECK("k_fill_chunks_sliced");
@@ -936,20 +968,24 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
       acc += (uint32_t)__popcll(m);
     }
   };
-  // ping-pong over two register sets (no copy of in-flight load destinations)
-  uint64_t c = sa.qb[qs] + (uint64_t)(blockIdx.x - sa.wg0[qs]) * WPB + wave;
-  Cur A, B;
-  if (c < qend) {
-    load(c, A);
-    while (true) {
-      c += nwq;
-      load(c, B);
+  // three register sets in rotation, two chunks in flight while one is filtered (no copy of in-flight
+  // load destinations: the waitcnt pass then only waits for the chunk it processes)
+  const uint64_t c0 = sa.qb[qs] + (uint64_t)(blockIdx.x - sa.wg0[qs]) * WPB + wave;
+  if (c0 < qend) {
+    const uint64_t K = (qend - c0 + nwq - 1) / nwq;  // chunks of this wave
+    Cur A, B, C;
+    load(c0, A);
+    load(c0 + nwq, B);
+    for (uint64_t k = 0;; k += 3) {
+      load(c0 + (k + 2) * nwq, C);
       process(A);
-      if (c >= qend) break;
-      c += nwq;
-      load(c, A);
+      if (k + 1 >= K) break;
+      load(c0 + (k + 3) * nwq, A);
       process(B);
-      if (c >= qend) break;
+      if (k + 2 >= K) break;
+      load(c0 + (k + 4) * nwq, B);
+      process(C);
+      if (k + 3 >= K) break;
     }
   }
   if (lane == 0) {
