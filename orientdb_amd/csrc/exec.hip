@@ -530,7 +530,8 @@ class Executor {
         k = std::min<uint64_t>(k, (nq + SWPB - 1) / SWPB);
         sa.wg0[q] = w;
         w += (uint32_t)k;
-        if (k) caph_sliced = std::max<uint64_t>(caph_sliced, (nq + k * SWPB - 1) / (k * SWPB) * (uint64_t)kChunk);
+        // + a 64-row tail pad (k_expand_heavy_sliced may write one dropped row past a wave's count)
+        if (k) caph_sliced = std::max<uint64_t>(caph_sliced, (nq + k * SWPB - 1) / (k * SWPB) * (uint64_t)kChunk + 64);
       }
       sa.wg0[P] = w;
     }

@@ -902,13 +902,13 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
     for (uint32_t i = threadIdx.x; i < sw; i += kSliceBlock) s_bm[i] = w0 + i < nw ? bm[w0 + i] : 0u;
   }
   __syncthreads();
-  const uint32_t vbase = qs << sa.shift, smask = (1u << sa.shift) - 1;
   const uint64_t qend = sa.qb[qs + 1];
   const uint32_t nwq = (sa.wg0[qs + 1] - sa.wg0[qs]) * WPB;
   const uint64_t arena = a.arena_base + (uint64_t)gw * a.arena_cap;
   const int nc = NC < 0 ? a.ncarry : NC;
   // per-wave output descriptors (arena-relative byte offsets fit 32 bits: arena_cap·4 < 2 GiB)
   const int32_t arena_bytes = WRITE ? (int32_t)(a.arena_cap * 4 < 0x7fffffffull ? a.arena_cap * 4 : 0x7fffffffull) : 0;
+  static_assert(kChunk * 4 <= 0x7fffffff, "in-range store offsets stay below the 0x80000000 drop marker");
   auto out_rsrc = [&](int k) {
     uint32_t *p = k < 0 ? a.out_dst : (k < nc ? a.carry_out[k] : a.out_dst);
     return __builtin_amdgcn_make_buffer_rsrc(p + arena, 0, arena_bytes, 0x00020000);
@@ -944,26 +944,41 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
 #pragma unroll
     for (int i = 0; i < NS; ++i) x.q[i] = __builtin_amdgcn_raw_buffer_load_b32(cr, (i * 64 + lane) * 4, 0, 0);
   };
+  // per 64-edge slot: 2 VALU for the LDS word (a neighbour of the slice, so its low bits are the
+  // offset), one bit-field extract, the ballot, a lane prefix, and exec-masked compacted stores
+  const uint32_t wbits = sa.shift - 5;  // bitmap words per slice = 2^wbits
   auto process = [&](const Cur &x) {
     uint32_t w[NS];
 #pragma unroll
-    for (int i = 0; i < NS; ++i) w[i] = s_bm[((x.q[i] - vbase) & smask) >> 5];
+    for (int i = 0; i < NS; ++i) w[i] = s_bm[__builtin_amdgcn_ubfe(x.q[i], 5, wbits)];
+    // all 16 probes are in flight before the first is used (one LDS wait, not one per slot)
+#pragma unroll
+    for (int i = 0; i < NS; ++i) asm volatile("" : "+v"(w[i]));
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
+      if ((uint32_t)(i * 64) >= x.n) break;  // uniform: slice cuts leave chunks short (≈600 of 1024 edges)
       const uint32_t v = x.q[i];
-      const bool bit = (((w[i] >> (v & 31)) & 1u) != 0) & ((uint32_t)(i * 64) + lane < x.n);
-      const uint64_t m = __ballot(bit);
-      if (WRITE && bit) {
-        const uint32_t pre = lane_prefix(m);
-        const uint32_t off = pre * 4;
-        const int32_t so = (int32_t)(acc * 4);
-        __builtin_amdgcn_raw_buffer_store_b32(v, od, off, so, 0);
-        if (nc > 0) __builtin_amdgcn_raw_buffer_store_b32(x.cv[0], oc0, off, so, 0);
-        if (nc > 1) __builtin_amdgcn_raw_buffer_store_b32(x.cv[1], oc1, off, so, 0);
-        if (nc > 2) __builtin_amdgcn_raw_buffer_store_b32(x.cv[2], oc2, off, so, 0);
-        if (nc > 3) __builtin_amdgcn_raw_buffer_store_b32(x.cv[3], oc3, off, so, 0);
-        if (NC < 0)
-          for (int kk = 4; kk < nc; ++kk) a.carry_out[kk][arena + acc + pre] = a.carry_in[kk][x.row];
+      // v_bfe_u32 reads the low 5 bits of its offset operand. Lanes past the chunk end (last slot
+      // only) are cut from the ballot on the scalar side; if their (zero-filled) probe is set they
+      // store one garbage row at acc + popc(m), past this slot's survivors — overwritten by the next
+      // slot or left in the arena's 64-row tail pad, never counted.
+      const bool bit = __builtin_amdgcn_ubfe(w[i], v, 1) != 0;
+      uint64_t m = __builtin_amdgcn_ballot_w64(bit);
+      const uint32_t rem = x.n - (uint32_t)(i * 64);
+      if (rem < 64) m &= (1ull << rem) - 1;
+      if (WRITE) {
+        if (bit) {  // exec-masked: stores with every lane live but range-dropped were measured slower
+          const uint32_t pre = lane_prefix(m);
+          const uint32_t off = pre * 4;
+          const int32_t so = (int32_t)(acc * 4);
+          __builtin_amdgcn_raw_buffer_store_b32(v, od, off, so, 0);
+          if (nc > 0) __builtin_amdgcn_raw_buffer_store_b32(x.cv[0], oc0, off, so, 0);
+          if (nc > 1) __builtin_amdgcn_raw_buffer_store_b32(x.cv[1], oc1, off, so, 0);
+          if (nc > 2) __builtin_amdgcn_raw_buffer_store_b32(x.cv[2], oc2, off, so, 0);
+          if (nc > 3) __builtin_amdgcn_raw_buffer_store_b32(x.cv[3], oc3, off, so, 0);
+          if (NC < 0)
+            for (int kk = 4; kk < nc; ++kk) a.carry_out[kk][arena + acc + pre] = a.carry_in[kk][x.row];
+        }
       }
       acc += (uint32_t)__popcll(m);
     }
