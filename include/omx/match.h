@@ -63,11 +63,13 @@ typedef struct omx_class_desc {
  * is free; omx sorts rows it finds unsorted. */
 typedef struct omx_edge_set_desc {
   int32_t edge_class;           /* index into classes[]                                            */
-  uint64_t n_edges;             /* E                                                               */
-  const uint64_t *out_row_ptr;  /* [V+1]                                                           */
+  uint64_t n_edges;             /* E (of the owned rows, for a partition)                          */
+  const uint64_t *out_row_ptr;  /* [V+1] ([part_hi − part_lo + 1] for a partition)                 */
   const uint32_t *out_col;      /* [E] dense vertex ids                                            */
-  const uint64_t *in_row_ptr;   /* [V+1] (the transpose); may be NULL → built by omx              */
-  const uint32_t *in_col;       /* [E]                                                             */
+  const uint64_t *in_row_ptr;   /* [V+1] (the transpose); may be NULL → built by omx (required for */
+                                /* a partition: the in-rows of the owned vertices)                 */
+  const uint32_t *in_col;       /* [n_in_edges]                                                    */
+  uint64_t n_in_edges;          /* edges of the in CSR; 0 = n_edges (always equal when unpartitioned) */
 } omx_edge_set_desc;
 
 typedef struct omx_property_desc {
@@ -100,11 +102,16 @@ typedef struct omx_graph_desc {
   int32_t n_indexes;
   const omx_index_desc *indexes;
   int32_t device;                      /* HIP device ordinal; -1 = host-only (plan/explain only)   */
+  /* 1-D partition: this snapshot holds the out/in CSR rows of the vertices
+   * [part_lo, part_hi) only; classes, RIDs and properties stay replicated for all V vertices. Rank r of
+   * a world of N owns [r·B, min(V, (r+1)·B)) with B = ⌈V/N⌉. part_lo = part_hi = 0: every row. */
+  uint32_t part_lo, part_hi;
 } omx_graph_desc;
 
 typedef struct omx_graph omx_graph;
 typedef struct omx_statement omx_statement;
 typedef struct omx_result omx_result;
+typedef struct omx_comm omx_comm;
 
 /* ---- graph snapshot --------------------------------------------------------------------------- */
 int omx_graph_create(const omx_graph_desc *desc, omx_graph **out);
@@ -156,6 +163,7 @@ typedef struct omx_exec_options {
   int32_t shard_world;   /* 1 = no sharding                                                       */
   const omx_value *params;
   int32_t n_params;
+  omx_comm *comm;        /* partitioned snapshot: the ranks' communicator (NULL otherwise)        */
 } omx_exec_options;
 
 void omx_exec_options_init(omx_exec_options *o);
@@ -186,6 +194,25 @@ void omx_result_free(omx_result *r);
 const char *omx_last_error(void);
 const char *omx_version(void);
 
+/* ---- multi-GPU: communicator of a 1-D partitioned MATCH ------------------------ */
+/* With a partitioned snapshot, omx_execute routes binding rows to the rank owning the vertex whose
+ * adjacency the next step reads (an all-to-all of counts, then of every bound column), and before a
+ * de-duplicating projection routes rows by a hash of the projected tuple. Every rank returns its share
+ * of the distinct rows; their union is the result. All ranks must execute the same statements in the
+ * same order. The reference has no counterpart (OMatchStatement.isLocalExecution, :1009-1011). */
+#define OMX_COMM_ID_BYTES 128
+/* RCCL unique id (ncclGetUniqueId) created on one rank and shared with the others by the caller. */
+int omx_comm_unique_id(uint8_t id[OMX_COMM_ID_BYTES]);
+/* One process per GPU: RCCL over xGMI (ncclCommInitRank on `device`). */
+int omx_comm_create_rccl(int32_t rank, int32_t world, int32_t device, const uint8_t id[OMX_COMM_ID_BYTES],
+                         omx_comm **out);
+/* Ranks that are threads of this process (any devices, one GPU included): out[0..world-1]. The exchange
+ * is device-to-device copies behind a barrier; each rank's omx_execute runs on its own thread. */
+int omx_comm_create_threads(int32_t world, omx_comm **out);
+int32_t omx_comm_rank(const omx_comm *c);
+int32_t omx_comm_world(const omx_comm *c);
+void omx_comm_destroy(omx_comm *c);
+
 /* ---- synthetic graphs (benchmark / test inputs) -------------------------------- */
 /* Graph500 RMAT (a=.57,b=.19,c=.19), V = 2^scale, edge_factor·V raw directed edges, deterministic
  * counter-based RNG (splitmix64), vertex ids scrambled by a bijection. simple != 0 removes self loops
@@ -197,6 +224,12 @@ int omx_rmat_generate(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t
  * windows; rows sorted. Deterministic in (n_persons, target_edges, seed). */
 int omx_ldbc_knows_generate(uint32_t n_persons, uint64_t target_edges, uint64_t seed, uint64_t **out_row_ptr,
                             uint32_t **out_col, uint64_t *n_edges);
+/* The partition [lo, hi) of the same RMAT graph: out rows and in rows (the transpose's rows) of the
+ * owned vertices, local row pointers of hi − lo + 1 entries, rows sorted; identical to the rows of
+ * omx_rmat_generate (+ omx_csr_transpose) for those vertices. */
+int omx_rmat_generate_part(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t simple, uint32_t lo, uint32_t hi,
+                           uint64_t **out_row_ptr, uint32_t **out_col, uint64_t *n_out, uint64_t **in_row_ptr,
+                           uint32_t **in_col, uint64_t *n_in);
 /* CSR transpose (host, multi-threaded); rows of the output are sorted. */
 int omx_csr_transpose(uint32_t n_vertices, const uint64_t *row_ptr, const uint32_t *col, uint64_t **t_row_ptr,
                       uint32_t **t_col);

@@ -24,7 +24,7 @@ class omx_class_desc(C.Structure):
 class omx_edge_set_desc(C.Structure):
     _fields_ = [("edge_class", C.c_int32), ("n_edges", C.c_uint64),
                 ("out_row_ptr", C.POINTER(C.c_uint64)), ("out_col", C.POINTER(C.c_uint32)),
-                ("in_row_ptr", C.POINTER(C.c_uint64)), ("in_col", C.POINTER(C.c_uint32))]
+                ("in_row_ptr", C.POINTER(C.c_uint64)), ("in_col", C.POINTER(C.c_uint32)), ("n_in_edges", C.c_uint64)]
 
 
 class omx_property_desc(C.Structure):
@@ -41,7 +41,8 @@ class omx_graph_desc(C.Structure):
                 ("vertex_class", C.POINTER(C.c_uint16)), ("rids", C.POINTER(C.c_uint64)),
                 ("n_edge_sets", C.c_int32), ("edge_sets", C.POINTER(omx_edge_set_desc)),
                 ("n_properties", C.c_int32), ("properties", C.POINTER(omx_property_desc)),
-                ("n_indexes", C.c_int32), ("indexes", C.POINTER(omx_index_desc)), ("device", C.c_int32)]
+                ("n_indexes", C.c_int32), ("indexes", C.POINTER(omx_index_desc)), ("device", C.c_int32),
+                ("part_lo", C.c_uint32), ("part_hi", C.c_uint32)]
 
 
 class omx_value(C.Structure):
@@ -51,7 +52,8 @@ class omx_value(C.Structure):
 
 class omx_exec_options(C.Structure):
     _fields_ = [("mode", C.c_int32), ("flags", C.c_int32), ("limit", C.c_int64), ("shard_rank", C.c_int32),
-                ("shard_world", C.c_int32), ("params", C.POINTER(omx_value)), ("n_params", C.c_int32)]
+                ("shard_world", C.c_int32), ("params", C.POINTER(omx_value)), ("n_params", C.c_int32),
+                ("comm", C.c_void_p)]
 
 
 class omx_result_info(C.Structure):
@@ -89,7 +91,18 @@ SIGNATURES = {
                                     C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32))]),
     "omx_synthetic_int_column": (C.c_int, [C.c_uint32, C.c_uint64, C.c_int32, C.POINTER(C.POINTER(C.c_int32))]),
     "omx_host_free": (None, [C.c_void_p]),
+    "omx_rmat_generate_part": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int32, C.c_uint32, C.c_uint32,
+                                         C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)),
+                                         C.POINTER(C.c_uint64), C.POINTER(C.POINTER(C.c_uint64)),
+                                         C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64)]),
+    "omx_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "omx_comm_create_rccl": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]),
+    "omx_comm_create_threads": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "omx_comm_rank": (C.c_int32, [C.c_void_p]),
+    "omx_comm_world": (C.c_int32, [C.c_void_p]),
+    "omx_comm_destroy": (None, [C.c_void_p]),
 }
+OMX_COMM_ID_BYTES = 128
 
 _lib = None
 

@@ -3,6 +3,7 @@
 #include <memory>
 #include <string>
 
+#include "dist.h"
 #include "exec.h"
 #include "graph.h"
 #include "plan.h"
@@ -14,6 +15,9 @@ struct omx_graph {
 struct omx_statement {
   std::unique_ptr<omx::Statement> st;
   std::string text;
+};
+struct omx_comm {
+  std::unique_ptr<omx::Transport> t;
 };
 
 namespace {
@@ -117,6 +121,7 @@ void omx_exec_options_init(omx_exec_options *o) {
   o->mode = OMX_MODE_MATERIALIZE;
   o->limit = -1;
   o->shard_world = 1;
+  o->comm = nullptr;
 }
 
 int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, omx_result **out) {
@@ -128,9 +133,42 @@ int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, om
     if (o.shard_world < 1 || o.shard_rank < 0 || o.shard_rank >= o.shard_world) omx::fail(OMX_E_INVALID, "bad shard");
     omx::Params p = make_params(o.params, o.n_params);
     auto plan = omx::build_plan(*s->st, *g->g, p, false);
-    *out = omx::execute_plan(*g->g, *plan, o);
+    *out = omx::execute_plan(*g->g, *plan, o, o.comm ? o.comm->t.get() : nullptr);
   });
 }
+
+int omx_comm_unique_id(uint8_t *id) {
+  return guard([&] {
+    if (!id) omx::fail(OMX_E_INVALID, "null argument");
+    omx::rccl_unique_id(id);
+  });
+}
+
+int omx_comm_create_rccl(int32_t rank, int32_t world, int32_t device, const uint8_t *id, omx_comm **out) {
+  return guard([&] {
+    if (!id || !out) omx::fail(OMX_E_INVALID, "null argument");
+    auto c = std::make_unique<omx_comm>();
+    c->t = omx::make_rccl_transport(rank, world, device, id);
+    *out = c.release();
+  });
+}
+
+int omx_comm_create_threads(int32_t world, omx_comm **out) {
+  return guard([&] {
+    if (!out || world < 1) omx::fail(OMX_E_INVALID, "bad argument");
+    auto hub = std::make_shared<omx::ThreadHub>(world);
+    std::vector<std::unique_ptr<omx_comm>> cs;
+    for (int r = 0; r < world; ++r) {
+      cs.push_back(std::make_unique<omx_comm>());
+      cs.back()->t = omx::make_thread_transport(hub, r);
+    }
+    for (int r = 0; r < world; ++r) out[r] = cs[r].release();
+  });
+}
+
+int32_t omx_comm_rank(const omx_comm *c) { return c ? c->t->rank() : -1; }
+int32_t omx_comm_world(const omx_comm *c) { return c ? c->t->world() : 0; }
+void omx_comm_destroy(omx_comm *c) { delete c; }
 
 int omx_result_info_get(const omx_result *r, omx_result_info *info) {
   return guard([&] {

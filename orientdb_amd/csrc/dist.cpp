@@ -1,0 +1,159 @@
+// dist.cpp — transports of the partitioned MATCH exchange (dist.h).
+#include "dist.h"
+
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+
+#include "common.h"
+
+#define HIP_OK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) omx::fail(OMX_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+#define NCCL_OK(x)                                                                                  \
+  do {                                                                                              \
+    ncclResult_t r_ = (x);                                                                          \
+    if (r_ != ncclSuccess) omx::fail(OMX_E_DEVICE, std::string(#x ": ") + ncclGetErrorString(r_)); \
+  } while (0)
+
+namespace omx {
+
+// ---- threads ----------------------------------------------------------------------------------------
+
+ThreadHub::ThreadHub(int w) : world(w), counts(w, std::vector<uint64_t>(w, 0)), sbuf(w), sdispl(w) {}
+
+void ThreadHub::barrier() {
+  std::unique_lock<std::mutex> lk(m);
+  const uint64_t gen = generation;
+  if (++arrived == world) {
+    arrived = 0;
+    ++generation;
+    cv.notify_all();
+  } else {
+    cv.wait(lk, [&] { return generation != gen; });
+  }
+}
+
+namespace {
+
+class ThreadTransport : public Transport {
+ public:
+  ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int world() const override { return hub_->world; }
+
+  void counts(const uint64_t *d_send, std::vector<uint64_t> &send, std::vector<uint64_t> &recv,
+              hipStream_t s) override {
+    const int W = world();
+    send.assign(W, 0);
+    HIP_OK(hipMemcpyAsync(send.data(), d_send, W * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    {
+      std::lock_guard<std::mutex> lk(hub_->m);
+      hub_->counts[rank_] = send;
+    }
+    hub_->barrier();
+    recv.assign(W, 0);
+    {
+      std::lock_guard<std::mutex> lk(hub_->m);
+      for (int p = 0; p < W; ++p) recv[p] = hub_->counts[p][rank_];
+    }
+    hub_->barrier();  // the count slots may be reused
+  }
+
+  void alltoallv(const std::vector<const uint32_t *> &sbuf, const std::vector<uint64_t> &send,
+                 const std::vector<uint64_t> &sdispl, const std::vector<uint32_t *> &rbuf,
+                 const std::vector<uint64_t> &recv, const std::vector<uint64_t> &rdispl, hipStream_t s) override {
+    (void)send;
+    const int W = world();
+    HIP_OK(hipStreamSynchronize(s));  // this rank's send buffers are complete before peers read them
+    {
+      std::lock_guard<std::mutex> lk(hub_->m);
+      hub_->sbuf[rank_] = sbuf;
+      hub_->sdispl[rank_] = sdispl;
+    }
+    hub_->barrier();
+    for (int p = 0; p < W; ++p) {
+      if (!recv[p]) continue;
+      const std::vector<const uint32_t *> &src = hub_->sbuf[p];
+      const uint64_t off = hub_->sdispl[p][rank_];
+      for (size_t c = 0; c < rbuf.size(); ++c)
+        HIP_OK(hipMemcpyAsync(rbuf[c] + rdispl[p], src[c] + off, recv[p] * sizeof(uint32_t), hipMemcpyDefault, s));
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    hub_->barrier();  // peers are done reading this rank's send buffers
+  }
+
+ private:
+  std::shared_ptr<ThreadHub> hub_;
+  int rank_;
+};
+
+// ---- RCCL -------------------------------------------------------------------------------------------
+
+class RcclTransport : public Transport {
+ public:
+  RcclTransport(int rank, int world, int device, const uint8_t *id) : rank_(rank), world_(world), device_(device) {
+    ncclUniqueId uid;
+    static_assert(sizeof(uid.internal) == 128, "RCCL unique id size");
+    std::memcpy(uid.internal, id, sizeof(uid.internal));
+    HIP_OK(hipSetDevice(device));
+    NCCL_OK(ncclCommInitRank(&comm_, world, uid, rank));
+    HIP_OK(hipMalloc((void **)&d_recv_, std::max(1, world) * sizeof(uint64_t)));
+  }
+  ~RcclTransport() override {
+    (void)hipSetDevice(device_);
+    if (d_recv_) (void)hipFree(d_recv_);
+    if (comm_) (void)ncclCommDestroy(comm_);
+  }
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+
+  void counts(const uint64_t *d_send, std::vector<uint64_t> &send, std::vector<uint64_t> &recv,
+              hipStream_t s) override {
+    NCCL_OK(ncclAllToAll(d_send, d_recv_, 1, ncclUint64, comm_, s));
+    send.assign(world_, 0);
+    recv.assign(world_, 0);
+    HIP_OK(hipMemcpyAsync(send.data(), d_send, world_ * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(recv.data(), d_recv_, world_ * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+  }
+
+  void alltoallv(const std::vector<const uint32_t *> &sbuf, const std::vector<uint64_t> &send,
+                 const std::vector<uint64_t> &sdispl, const std::vector<uint32_t *> &rbuf,
+                 const std::vector<uint64_t> &recv, const std::vector<uint64_t> &rdispl, hipStream_t s) override {
+    std::vector<size_t> sc(send.begin(), send.end()), sd(sdispl.begin(), sdispl.end()), rc(recv.begin(), recv.end()),
+        rd(rdispl.begin(), rdispl.end());
+    NCCL_OK(ncclGroupStart());
+    for (size_t c = 0; c < sbuf.size(); ++c)
+      NCCL_OK(ncclAllToAllv(sbuf[c], sc.data(), sd.data(), rbuf[c], rc.data(), rd.data(), ncclUint32, comm_, s));
+    NCCL_OK(ncclGroupEnd());
+  }
+
+ private:
+  int rank_, world_, device_;
+  ncclComm_t comm_ = nullptr;
+  uint64_t *d_recv_ = nullptr;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> make_thread_transport(std::shared_ptr<ThreadHub> hub, int rank) {
+  return std::make_unique<ThreadTransport>(std::move(hub), rank);
+}
+
+std::unique_ptr<Transport> make_rccl_transport(int rank, int world, int device, const uint8_t *unique_id) {
+  if (world < 1 || rank < 0 || rank >= world) fail(OMX_E_INVALID, "bad communicator rank/world");
+  return std::make_unique<RcclTransport>(rank, world, device, unique_id);
+}
+
+void rccl_unique_id(uint8_t *out) {
+  ncclUniqueId uid;
+  NCCL_OK(ncclGetUniqueId(&uid));
+  std::memcpy(out, uid.internal, sizeof(uid.internal));
+}
+
+}  // namespace omx

@@ -20,5 +20,7 @@ struct omx_result {
 };
 
 namespace omx {
-omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts);
+class Transport;
+// tr: the ranks' communicator for a partitioned snapshot (nullptr otherwise)
+omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts, Transport *tr = nullptr);
 }

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "dist.h"
 #include "kernels.h"
 
 namespace omx {
@@ -123,8 +124,8 @@ __global__ void k_unpack_tuple(const uint64_t *keys, uint64_t n, int k, int vbit
 
 class Executor {
  public:
-  Executor(Graph &g, const Plan &p, const omx_exec_options &o)
-      : g_(g), p_(p), o_(o), s_(g.stream), pool_(g.pool), tm_((o.flags & OMX_FLAG_KERNEL_TIMING) != 0, (o.flags & OMX_FLAG_TIME_HOT) != 0, g.stream, &g.event_pool) {
+  Executor(Graph &g, const Plan &p, const omx_exec_options &o, Transport *tr)
+      : g_(g), p_(p), o_(o), tr_(tr), s_(g.stream), pool_(g.pool), tm_((o.flags & OMX_FLAG_KERNEL_TIMING) != 0, (o.flags & OMX_FLAG_TIME_HOT) != 0, g.stream, &g.event_pool) {
     nwords_ = ((uint64_t)g.V + 63) / 64;
     // rows with at least this many neighbours take the chunked kernel (tests lower it to force the path)
     if (const char *h = std::getenv("OMX_HEAVY_DEG")) {
@@ -140,6 +141,9 @@ class Executor {
     if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max<uint64_t>(1, std::strtoull(d, nullptr, 10));
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
+    bound_.assign(p.aliases.size(), 0);
+    if (const char *r = std::getenv("OMX_ROUTE_SELF")) route_self_ = std::strcmp(r, "0") != 0;
+    dist_setup();
   }
 
   omx_result *run() {
@@ -152,7 +156,8 @@ class Executor {
     bool empty = p_.empty || !check_candidates();
     bool counted_only = false;
     if (!empty) {
-      for (size_t i = 0; i < p_.steps.size() && R_ > 0; ++i) {
+      // a partitioned run keeps stepping with no local rows: every rank takes part in every exchange
+      for (size_t i = 0; i < p_.steps.size() && (R_ > 0 || dist_); ++i) {
         const Step &st = p_.steps[i];
         bool last = i + 1 == p_.steps.size();
         bool count_only = last && o_.mode == OMX_MODE_COUNT && p_.unique_by_construction && st.kind == S_EXPAND;
@@ -190,6 +195,8 @@ class Executor {
     uint64_t n = 0;
     int ncols = 0;
     std::vector<DBuf<uint32_t>> out;
+    // partitioned + distinct projection: equal tuples meet on one rank first
+    if (dist_ && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
     if (R_ > 0 && !counted_only) {
       project_dedup(out, n);
       ncols = (int)out.size();
@@ -232,6 +239,12 @@ class Executor {
   Graph &g_;
   const Plan &p_;
   omx_exec_options o_;
+  Transport *tr_ = nullptr;
+  bool dist_ = false;        // partitioned execution: rows routed between ranks (dist.h)
+  bool route_self_ = false;  // OMX_ROUTE_SELF=1: route through the transport even with one rank (tests)
+  int owner_col_ = -1;       // rows currently sit on the owner of this column's vertex
+  uint32_t block_ = 0;       // vertices per rank (block partition)
+  std::vector<char> bound_;  // aliases bound so far (the same on every rank, whatever its row count)
   hipStream_t s_;
   DevicePool &pool_;
   Timer tm_;
@@ -275,8 +288,8 @@ class Executor {
     d.sorted = a.sorted;
     for (size_t i = 0; i < a.parts.size(); ++i) {
       const EdgeSet &es = g_.esets[a.parts[i].first];
-      d.p[i].rp = a.parts[i].second == 0 ? es.d_out_rp : es.d_in_rp;
-      d.p[i].col = a.parts[i].second == 0 ? es.d_out_col : es.d_in_col;
+      d.p[i].rp = g_.rp(es, a.parts[i].second);
+      d.p[i].col = g_.col(es, a.parts[i].second);
     }
     return d;
   }
@@ -354,23 +367,26 @@ class Executor {
 
   uint64_t bitmap_count(const uint64_t *words, int rank, int world) {
     DBuf<uint32_t> cnt(&pool_, nwords_);
-    launch_word_popc(words, nwords_, g_.V, rank, world, cnt.p, s_);
+    launch_word_popc(words, nwords_, g_.V, rank, world, 0, g_.V, cnt.p, s_);
     DBuf<uint64_t> sum(&pool_, 1);
     hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> it(cnt.p, CastU64());
     cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, it, sum.p, (int)nwords_, s_); });
     return read1(sum.p);
   }
 
-  DBuf<uint32_t> bitmap_list(const uint64_t *words, int rank, int world, uint64_t &n) {
+  // vertices of a bitmap as a list, restricted to [lo, hi) (and to v % world == rank)
+  DBuf<uint32_t> bitmap_list(const uint64_t *words, int rank, int world, uint64_t &n, uint32_t lo = 0,
+                             uint32_t hi = UINT32_MAX) {
+    hi = std::min(hi, g_.V);
     DBuf<uint32_t> cnt(&pool_, nwords_ + 1);
     DBuf<uint32_t> offs(&pool_, nwords_ + 1);
     tm_.begin("k_bitmap_to_list");
-    launch_word_popc(words, nwords_, g_.V, rank, world, cnt.p, s_);
+    launch_word_popc(words, nwords_, g_.V, rank, world, lo, hi, cnt.p, s_);
     HIP_CHECK(hipMemsetAsync(cnt.p + nwords_, 0, 4, s_));
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, offs.p, (int)(nwords_ + 1), s_); });
     n = read1(offs.p + nwords_);
     DBuf<uint32_t> out(&pool_, std::max<uint64_t>(n, 1));
-    launch_word_scatter(words, nwords_, g_.V, rank, world, offs.p, out.p, s_);
+    launch_word_scatter(words, nwords_, g_.V, rank, world, lo, hi, offs.p, out.p, s_);
     tm_.end(nwords_ * 8 + n * 4);
     return out;
   }
@@ -385,16 +401,121 @@ class Executor {
   std::vector<int> bound_cols() const {
     std::vector<int> c;
     for (size_t a = 0; a < col_.size(); ++a)
-      if (col_[a].p) c.push_back((int)a);
+      if (dist_ ? bound_[a] != 0 : col_[a].p != nullptr) c.push_back((int)a);
     return c;
+  }
+
+  // ---- 1-D partitioned execution (dist.h) ----------------------------------------------------------
+  void dist_setup() {
+    if (!tr_) {
+      if (g_.partitioned())
+        fail(OMX_E_INVALID, "partitioned snapshot executed without a communicator (omx_exec_options.comm)");
+      return;
+    }
+    const int W = tr_->world(), r = tr_->rank();
+    if (W < 1 || W > kMaxRanks) fail(OMX_E_INVALID, "communicator world must be in [1, 64]");
+    if (o_.shard_world > 1) fail(OMX_E_INVALID, "root shards and a partitioned communicator are exclusive");
+    block_ = (uint32_t)(((uint64_t)g_.V + W - 1) / W);
+    const uint32_t lo = (uint32_t)std::min<uint64_t>(g_.V, (uint64_t)r * block_);
+    const uint32_t hi = (uint32_t)std::min<uint64_t>(g_.V, (uint64_t)(r + 1) * block_);
+    if (g_.part_lo != lo || g_.part_hi != hi)
+      fail(OMX_E_INVALID, "snapshot rows [" + std::to_string(g_.part_lo) + ", " + std::to_string(g_.part_hi) +
+                              ") are not rank " + std::to_string(r) + "'s block of " + std::to_string(W));
+    for (const Step &st : p_.steps)
+      if (st.kind == S_VARLEN || st.kind == S_NEWROOT || st.kind == S_CARTESIAN)
+        unsupported("variable-length items and disconnected patterns are not supported on a partitioned snapshot");
+    for (const PredProgram &pp : p_.progs)
+      for (const DPredInstr &in : pp.code)
+        if (in.op == P_PUSH_DEG) unsupported("out()/in()/both().size() in WHERE is not supported on a partitioned snapshot");
+    if (p_.proj == Plan::PROJ_ELEMENTS) unsupported("$elements / $pathElements are not supported on a partitioned snapshot");
+    if (p_.limit >= 0 || o_.limit >= 0) unsupported("LIMIT is not supported on a partitioned snapshot");
+    dist_ = true;
+  }
+
+  // rows travel to dest[r]; hist[p] = rows for rank p (both on the device)
+  void route_rows(DBuf<uint32_t> &dest, DBuf<uint64_t> &hist) {
+    const int W = tr_->world();
+    const uint64_t R = R_;
+    const std::vector<int> cols = bound_cols();
+    DBuf<uint32_t> perm;
+    if (R) {
+      DBuf<uint32_t> iota(&pool_, R), sdest(&pool_, R);
+      perm = DBuf<uint32_t>(&pool_, R);
+      launch_iota(iota.p, R, s_);
+      const int bits = std::max(1, bits_for((uint64_t)W - 1));
+      cub([&](void *t, size_t &b) {
+        return hipcub::DeviceRadixSort::SortPairs(t, b, dest.p, sdest.p, iota.p, perm.p, (int64_t)R, 0, bits, s_);
+      });
+    }
+    std::vector<uint64_t> send, recv;
+    tr_->counts(hist.p, send, recv, s_);
+    std::vector<uint64_t> sdispl(W, 0), rdispl(W, 0);
+    uint64_t Rn = 0;
+    for (int p = 0; p < W; ++p) {
+      if (p) sdispl[p] = sdispl[p - 1] + send[p - 1];
+      rdispl[p] = Rn;
+      Rn += recv[p];
+    }
+    std::vector<DBuf<uint32_t>> sb, rb;
+    std::vector<const uint32_t *> sp;
+    std::vector<uint32_t *> rp;
+    tm_.begin("k_route_gather");
+    for (int c : cols) {
+      sb.emplace_back(&pool_, std::max<uint64_t>(R, 1));
+      if (R) launch_gather_u32(col_[c].p, perm.p, R, sb.back().p, s_);
+      rb.emplace_back(&pool_, std::max<uint64_t>(Rn, 1));
+      sp.push_back(sb.back().p);
+      rp.push_back(rb.back().p);
+    }
+    tm_.end(R * 12ull * cols.size());
+    tm_.begin("exchange");
+    tr_->alltoallv(sp, send, sdispl, rp, recv, rdispl, s_);
+    tm_.end((R + Rn) * 4ull * cols.size());
+    for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(rb[i]);
+    R_ = Rn;
+    segmented_ = false;
+  }
+
+  // before a step that reads column c's adjacency: rows go to the rank that owns row[c]
+  void route_owner(int c) {
+    if (!dist_ || owner_col_ == c) return;
+    owner_col_ = c;
+    if (tr_->world() == 1 && !route_self_) return;
+    const int W = tr_->world();
+    DBuf<uint32_t> dest(&pool_, std::max<uint64_t>(R_, 1));
+    DBuf<uint64_t> hist(&pool_, W);
+    HIP_CHECK(hipMemsetAsync(hist.p, 0, W * sizeof(uint64_t), s_));
+    tm_.begin("k_route_owner");
+    launch_route_owner(col_[c].p, R_, block_, (uint32_t)W, dest.p, hist.p, s_);
+    tm_.end(R_ * 8);
+    route_rows(dest, hist);
+  }
+
+  // before a distinct projection: rows go to the rank given by a hash of the projected tuple
+  void route_hash(const std::vector<int> &aliases) {
+    owner_col_ = -1;
+    if (tr_->world() == 1 && !route_self_) return;
+    const int W = tr_->world();
+    std::vector<const uint32_t *> cs;
+    for (int a : aliases) cs.push_back(col_[a].p);
+    DBuf<uint32_t> dest(&pool_, std::max<uint64_t>(R_, 1));
+    DBuf<uint64_t> hist(&pool_, W);
+    HIP_CHECK(hipMemsetAsync(hist.p, 0, W * sizeof(uint64_t), s_));
+    tm_.begin("k_route_hash");
+    launch_route_hash((int)cs.size(), cs.data(), R_, (uint32_t)W, dest.p, hist.p, s_);
+    tm_.end(R_ * (4ull * cs.size() + 4));
+    route_rows(dest, hist);
   }
 
   // ---- steps -------------------------------------------------------------------------------------
   void root(const Step &st) {
     uint64_t n = 0;
     int world = std::max(1, o_.shard_world);
-    col_[st.dst] = bitmap_list(bitmap(st.cand_bm), world > 1 ? o_.shard_rank : 0, world, n);
+    // a partition starts the rows of the roots it owns (their adjacency is local)
+    col_[st.dst] = bitmap_list(bitmap(st.cand_bm), world > 1 ? o_.shard_rank : 0, world, n, g_.part_lo, g_.part_hi);
     R_ = n;
+    bound_[st.dst] = 1;
+    owner_col_ = st.dst;
   }
 
   struct ExpandOut {
@@ -431,8 +552,7 @@ class Executor {
         const size_t bytes = (size_t)g_.V * (P - 1) * sizeof(uint32_t);
         HIP_CHECK(hipMalloc((void **)&d, std::max<size_t>(bytes, 4)));
         g_.device_bytes += bytes;
-        launch_build_cuts(dir == 0 ? es.d_out_rp : es.d_in_rp, dir == 0 ? es.d_out_col : es.d_in_col, g_.V, P,
-                          slice_shift_, d, s_);
+        launch_build_cuts(g_.rp(es, dir), g_.col(es, dir), g_.part_lo, g_.part_hi, P, slice_shift_, d, s_);
       }
       c.c[i] = d;
     }
@@ -668,7 +788,9 @@ class Executor {
   // fused: the following S_CHECK closes a cycle on this step's new column (sorted-
   // adjacency intersection instead of materialising the wedges and probing each)
   void expand_step(const Step &st, bool write, bool allow_segmented, const Step *check = nullptr) {
-    std::vector<int> cols = bound_cols();
+    route_owner(st.src);
+    std::vector<int> cols = bound_cols();  // the carried columns (st.dst is not bound yet)
+    bound_[st.dst] = 1;
     std::vector<const uint32_t *> carry;
     for (int c : cols) carry.push_back(col_[c].p);
     ExpandOut o = expand_core(col_[st.src].p, R_, st.adj, bitmap(st.filter_bm), carry, write, allow_segmented,
@@ -712,7 +834,7 @@ class Executor {
   // S_EXPAND (x → t) followed by S_CHECK (y → t, t bound by the expansion): the check keeps a row iff
   // t ∈ N(y), which a sorted adjacency answers by binary search inside the expansion kernels
   bool fuse_ok(const Step &ex, const Step &ck) const {
-    if (fuse_mode_ == "0") return false;
+    if (fuse_mode_ == "0" || dist_) return false;  // partitioned: N(y) of the check may live on another rank
     if (ck.kind != S_CHECK || ck.dst != ex.dst || ck.src == ex.dst || !col_[ck.src].p) return false;
     if (!ck.adj.sorted || ck.adj.parts.empty()) return false;
     return true;
@@ -728,6 +850,8 @@ class Executor {
   }
 
   void check_step(const Step &st) {
+    route_owner(st.src);
+    if (R_ == 0) return;  // (a partitioned rank with no local rows after the exchange)
     const uint64_t R = R_;
     const uint64_t E = degree_sum(col_[st.src].p, R, st.adj);
     edges_ += E;
@@ -1196,10 +1320,10 @@ void Executor::unpack_tuple(const uint64_t *keys, uint64_t n, std::vector<DBuf<u
 
 }  // namespace
 
-omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts) {
+omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts, Transport *tr) {
   if (!g.on_device()) fail(OMX_E_DEVICE, "graph snapshot is host-only (device = -1)");
   HIP_CHECK(hipSetDevice(g.device));
-  Executor ex(g, p, opts);
+  Executor ex(g, p, opts, tr);
   return ex.run();
 }
 

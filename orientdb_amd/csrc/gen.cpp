@@ -159,6 +159,86 @@ int omx_rmat_generate(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t
   return OMX_OK;
 }
 
+// One 1-D partition of the same RMAT graph: every rank replays all M edge draws (they are pure
+// functions of the edge index) and keeps the out-edges of its sources and the in-edges of its
+// destinations; each row is then sorted (and, for the simple graph, deduplicated and stripped of the
+// self loop) exactly like the full generator's rows and the rows of their transpose.
+static int rmat_rows(uint64_t M, const Rmat &g, uint32_t lo, uint32_t hi, bool by_dst, int32_t simple,
+                     uint64_t **out_rp, uint32_t **out_col, uint64_t *n_edges) {
+  const uint64_t VL = (uint64_t)hi - lo;
+  std::vector<std::atomic<uint64_t>> deg(VL);
+  for (auto &d : deg) d.store(0, std::memory_order_relaxed);
+  auto key = [&](uint32_t u, uint32_t v) { return by_dst ? v : u; };
+  par(M, [&](uint64_t a, uint64_t b) {
+    for (uint64_t i = a; i < b; ++i) {
+      uint32_t u, v;
+      g.edge(i, u, v);
+      const uint32_t k = key(u, v);
+      if (k >= lo && k < hi) deg[k - lo].fetch_add(1, std::memory_order_relaxed);
+    }
+  });
+  std::vector<uint64_t> rp(VL + 1, 0);
+  for (uint64_t x = 0; x < VL; ++x) rp[x + 1] = rp[x] + deg[x].load(std::memory_order_relaxed);
+  for (uint64_t x = 0; x < VL; ++x) deg[x].store(rp[x], std::memory_order_relaxed);
+  uint32_t *col = (uint32_t *)std::malloc(sizeof(uint32_t) * std::max<uint64_t>(rp[VL], 1));
+  if (!col) return OMX_E_OOM;
+  par(M, [&](uint64_t a, uint64_t b) {
+    for (uint64_t i = a; i < b; ++i) {
+      uint32_t u, v;
+      g.edge(i, u, v);
+      const uint32_t k = key(u, v);
+      if (k >= lo && k < hi) col[deg[k - lo].fetch_add(1, std::memory_order_relaxed)] = by_dst ? u : v;
+    }
+  });
+  std::vector<uint64_t> keep(VL, 0);
+  par(VL, [&](uint64_t a, uint64_t b) {
+    for (uint64_t x = a; x < b; ++x) {
+      uint32_t *s = col + rp[x], *e = col + rp[x + 1];
+      std::sort(s, e);
+      if (simple) {
+        uint32_t *w = s;
+        for (uint32_t *y = s; y < e; ++y)
+          if (*y != (uint32_t)(lo + x) && (w == s || *(w - 1) != *y)) *w++ = *y;
+        keep[x] = (uint64_t)(w - s);
+      } else {
+        keep[x] = (uint64_t)(e - s);
+      }
+    }
+  });
+  uint64_t *orp = (uint64_t *)std::malloc(sizeof(uint64_t) * (VL + 1));
+  if (!orp) {
+    std::free(col);
+    return OMX_E_OOM;
+  }
+  orp[0] = 0;
+  for (uint64_t x = 0; x < VL; ++x) orp[x + 1] = orp[x] + keep[x];
+  if (simple)
+    for (uint64_t x = 0; x < VL; ++x)
+      if (orp[x] != rp[x]) std::memmove(col + orp[x], col + rp[x], keep[x] * sizeof(uint32_t));
+  *out_rp = orp;
+  *out_col = col;
+  *n_edges = orp[VL];
+  return OMX_OK;
+}
+
+int omx_rmat_generate_part(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t simple, uint32_t lo, uint32_t hi,
+                           uint64_t **out_rp, uint32_t **out_col, uint64_t *n_out, uint64_t **in_rp, uint32_t **in_col,
+                           uint64_t *n_in) {
+  if (scale < 1 || scale > 31 || edge_factor < 1 || lo > hi || hi > (1ull << scale) || !out_rp || !out_col ||
+      !n_out || !in_rp || !in_col || !n_in)
+    return OMX_E_INVALID;
+  const uint64_t M = (uint64_t)edge_factor << scale;
+  Rmat g(scale, seed);
+  int rc = rmat_rows(M, g, lo, hi, false, simple, out_rp, out_col, n_out);
+  if (rc != OMX_OK) return rc;
+  rc = rmat_rows(M, g, lo, hi, true, simple, in_rp, in_col, n_in);
+  if (rc != OMX_OK) {
+    std::free(*out_rp);
+    std::free(*out_col);
+  }
+  return rc;
+}
+
 // LDBC-SNB-like Knows graph (configs[3]). LDBC Datagen creates knows edges between persons that are
 // close in a correlation dimension (university, interests, random), so the graph has a skewed degree
 // distribution and many triangles. Restated here: target degrees from a log-normal scaled to

@@ -205,6 +205,14 @@ Graph *graph_create(const omx_graph_desc *d) {
   g->V = d->n_vertices;
   g->device = d->device;
   uint32_t V = g->V;
+  if (d->part_lo == 0 && d->part_hi == 0) {
+    g->part_hi = V;
+  } else {
+    if (d->part_lo > d->part_hi || d->part_hi > V) fail(OMX_E_INVALID, "bad partition range");
+    g->part_lo = d->part_lo;
+    g->part_hi = d->part_hi;
+  }
+  const uint32_t VL = g->part_hi - g->part_lo;  // rows held
 
   for (int i = 0; i < d->n_classes; ++i) {
     ClassInfo c;
@@ -271,37 +279,41 @@ Graph *graph_create(const omx_graph_desc *d) {
     EdgeSet es;
     es.cls = ed.edge_class;
     es.n_edges = ed.n_edges;
+    es.n_in_edges = ed.n_in_edges ? ed.n_in_edges : ed.n_edges;
     if (es.cls < 0 || es.cls >= d->n_classes) fail(OMX_E_INVALID, "bad edge class index");
     if (!ed.out_row_ptr || (ed.n_edges && !ed.out_col)) fail(OMX_E_INVALID, "edge set without out CSR");
-    if (ed.out_row_ptr[0] != 0 || ed.out_row_ptr[V] != ed.n_edges) fail(OMX_E_INVALID, "out_row_ptr inconsistent");
+    if (ed.out_row_ptr[0] != 0 || ed.out_row_ptr[VL] != ed.n_edges) fail(OMX_E_INVALID, "out_row_ptr inconsistent");
+    if (g->partitioned() && !(ed.in_row_ptr && ed.in_col))
+      fail(OMX_E_INVALID, "a partition needs the in CSR of its rows (in_row_ptr / in_col)");
     Tmp &t = tmp[i];
     t.orp = ed.out_row_ptr;
     t.ocol = ed.out_col;
     for (uint64_t e = 0; e < ed.n_edges; e += std::max<uint64_t>(1, ed.n_edges / 4096))
       if (ed.out_col[e] >= V) fail(OMX_E_INVALID, "out_col out of range");
-    auto so = scan_rows(V, t.orp, t.ocol);
+    auto so = scan_rows(VL, t.orp, t.ocol);
     if (!so.first) {
       sorted_copies.emplace_back(t.ocol, t.ocol + ed.n_edges);
-      sort_rows(V, t.orp, sorted_copies.back().data());
+      sort_rows(VL, t.orp, sorted_copies.back().data());
       t.ocol = sorted_copies.back().data();
-      so = scan_rows(V, t.orp, t.ocol);
+      so = scan_rows(VL, t.orp, t.ocol);
     }
     es.out_sorted = so.first;
     es.out_simple = so.second;
     if (ed.in_row_ptr && ed.in_col) {
-      if (ed.in_row_ptr[V] != ed.n_edges) fail(OMX_E_INVALID, "in_row_ptr inconsistent");
+      if (ed.in_row_ptr[0] != 0 || ed.in_row_ptr[VL] != es.n_in_edges) fail(OMX_E_INVALID, "in_row_ptr inconsistent");
       t.irp = ed.in_row_ptr;
       t.icol = ed.in_col;
-      auto si = scan_rows(V, t.irp, t.icol);
+      auto si = scan_rows(VL, t.irp, t.icol);
       if (!si.first) {
-        sorted_copies.emplace_back(t.icol, t.icol + ed.n_edges);
-        sort_rows(V, t.irp, sorted_copies.back().data());
+        sorted_copies.emplace_back(t.icol, t.icol + es.n_in_edges);
+        sort_rows(VL, t.irp, sorted_copies.back().data());
         t.icol = sorted_copies.back().data();
-        si = scan_rows(V, t.irp, t.icol);
+        si = scan_rows(VL, t.irp, t.icol);
       }
       es.in_sorted = si.first;
       es.in_simple = si.second;
     } else {
+      if (es.n_in_edges != es.n_edges) fail(OMX_E_INVALID, "n_in_edges without an in CSR");
       omx_csr_transpose(V, t.orp, t.ocol, &t.own_rp, &t.own_col);
       t.irp = t.own_rp;
       t.icol = t.own_col;
@@ -322,10 +334,10 @@ Graph *graph_create(const omx_graph_desc *d) {
     g->d_rids = upload(d->rids, V, acc);
     for (int i = 0; i < d->n_edge_sets; ++i) {
       EdgeSet &es = g->esets[i];
-      es.d_out_rp = upload(tmp[i].orp, (size_t)V + 1, acc);
+      es.d_out_rp = upload(tmp[i].orp, (size_t)VL + 1, acc);
       es.d_out_col = upload(tmp[i].ocol, es.n_edges, acc);
-      es.d_in_rp = upload(tmp[i].irp, (size_t)V + 1, acc);
-      es.d_in_col = upload(tmp[i].icol, es.n_edges, acc);
+      es.d_in_rp = upload(tmp[i].irp, (size_t)VL + 1, acc);
+      es.d_in_col = upload(tmp[i].icol, es.n_in_edges, acc);
     }
     std::vector<DColumn> cols;
     for (int i = 0; i < d->n_properties; ++i) {

@@ -80,7 +80,8 @@ struct ClassInfo {
 
 struct EdgeSet {
   int cls = -1;
-  uint64_t n_edges = 0;
+  uint64_t n_edges = 0;     // out CSR edges (of the owned rows)
+  uint64_t n_in_edges = 0;  // in CSR edges (of the owned rows)
   bool out_sorted = true, in_sorted = true;  // rows ascending
   bool out_simple = true, in_simple = true;  // rows strictly ascending (no parallel edges)
   uint64_t *d_out_rp = nullptr, *d_in_rp = nullptr;
@@ -113,6 +114,10 @@ struct IndexInfo {
 struct Graph {
   uint32_t V = 0;
   int device = -1;
+  // 1-D partition: the CSR rows held are those of [part_lo, part_hi) (local row pointers); the
+  // device row-pointer arrays are addressed with a global vertex id through rp(): base − part_lo
+  uint32_t part_lo = 0, part_hi = 0;
+  bool partitioned() const { return part_lo != 0 || part_hi != V; }
   std::vector<ClassInfo> classes;
   std::vector<EdgeSet> esets;
   std::vector<Property> props;
@@ -128,6 +133,10 @@ struct Graph {
   uint64_t *h_stage = nullptr;             // pinned host words for small device→host reads
   static constexpr int kStageWords = 512;
   std::vector<hipEvent_t> event_pool;      // reusable timing events (OMX_FLAG_KERNEL_TIMING)
+
+  // row pointers indexed by a global (owned) vertex id; dir 0 = out, 1 = in
+  const uint64_t *rp(const EdgeSet &e, int dir) const { return (dir == 0 ? e.d_out_rp : e.d_in_rp) - part_lo; }
+  const uint32_t *col(const EdgeSet &e, int dir) const { return dir == 0 ? e.d_out_col : e.d_in_col; }
 
   ~Graph();
   bool on_device() const { return device >= 0; }

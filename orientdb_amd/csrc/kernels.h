@@ -88,11 +88,17 @@ struct ExpandArgs {
 // predicate VM → V-bit bitmap (u64 words); depth = value of $depth
 void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s);
 void launch_bitmap_and(const uint64_t *a, uint64_t *b, uint64_t nwords, hipStream_t s);
-// per-word popcount (optionally restricted to v % world == rank)
-void launch_word_popc(const uint64_t *words, uint64_t nwords, uint32_t V, int rank, int world, uint32_t *counts,
-                      hipStream_t s);
-void launch_word_scatter(const uint64_t *words, uint64_t nwords, uint32_t V, int rank, int world,
-                         const uint32_t *offsets, uint32_t *out, hipStream_t s);
+// per-word popcount of the bits v with lo <= v < hi (optionally also v % world == rank)
+void launch_word_popc(const uint64_t *words, uint64_t nwords, uint32_t V, int rank, int world, uint32_t lo,
+                      uint32_t hi, uint32_t *counts, hipStream_t s);
+void launch_word_scatter(const uint64_t *words, uint64_t nwords, uint32_t V, int rank, int world, uint32_t lo,
+                         uint32_t hi, const uint32_t *offsets, uint32_t *out, hipStream_t s);
+// partitioned execution (dist.h): dest[r] = destination rank of row r, hist[p] += rows to rank p
+constexpr int kMaxRanks = 64;
+void launch_route_owner(const uint32_t *v, uint64_t R, uint32_t block, uint32_t W, uint32_t *dest, uint64_t *hist,
+                        hipStream_t s);
+void launch_route_hash(int ncols, const uint32_t *const *cols, uint64_t R, uint32_t W, uint32_t *dest, uint64_t *hist,
+                       hipStream_t s);
 
 void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t *deg, hipStream_t s);
 // per row: light degree (0 for heavy rows), heavy degree (0 for light rows), number of heavy chunks
@@ -104,8 +110,9 @@ void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t 
                          hipStream_t s);
 // sliced chunks: nchq[q·(R+1) + r] = chunks of heavy row r inside slice q (layout slice-major so one
 // scan gives each slice a contiguous chunk range); light/heavy degrees as launch_row_split
-void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t V, uint32_t nslices, uint32_t shift,
-                       uint32_t *cuts, hipStream_t s);
+// rows [vlo, vhi) (the owned rows of a partition; rp indexed by global vertex id)
+void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t vlo, uint32_t vhi, uint32_t nslices,
+                       uint32_t shift, uint32_t *cuts, hipStream_t s);
 void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint64_t heavy_deg,
                              uint32_t nslices, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s);
 void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint32_t nslices,

@@ -200,9 +200,19 @@ void launch_bitmap_and(const uint64_t *a, uint64_t *b, uint64_t n, hipStream_t s
   KCHECK("k_bitmap_and");
 }
 
-__device__ __forceinline__ uint64_t shard_word(uint64_t w, uint64_t word, uint32_t V, int rank, int world) {
+__device__ __forceinline__ uint64_t range_mask(uint64_t base, uint32_t lo, uint32_t hi) {
+  // bits b of the word with lo <= base + b < hi
+  if (base + 64 <= lo || base >= hi) return 0;
+  uint64_t m = ~0ull;
+  if (base < lo) m &= ~0ull << (lo - base);
+  if (base + 64 > hi) m &= (hi - base >= 64) ? ~0ull : ((1ull << (hi - base)) - 1);
+  return m;
+}
+
+__device__ __forceinline__ uint64_t shard_word(uint64_t w, uint64_t word, uint32_t V, int rank, int world,
+                                               uint32_t lo, uint32_t hi) {
   uint64_t base = word * 64;
-  if (base + 64 > V) w &= (V - base >= 64) ? ~0ull : ((1ull << (V - base)) - 1);
+  w &= range_mask(base, lo, hi < V ? hi : V);
   if (world > 1) {
     uint64_t m = 0;
     for (int b = 0; b < 64; ++b)
@@ -212,22 +222,23 @@ __device__ __forceinline__ uint64_t shard_word(uint64_t w, uint64_t word, uint32
   return w;
 }
 
-__global__ void k_word_popc(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t *counts) {
+__global__ void k_word_popc(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t lo,
+                            uint32_t hi, uint32_t *counts) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) counts[i] = __popcll(shard_word(words[i], i, V, rank, world));
+  if (i < n) counts[i] = __popcll(shard_word(words[i], i, V, rank, world, lo, hi));
 }
-void launch_word_popc(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t *counts,
-                      hipStream_t s) {
+void launch_word_popc(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t lo, uint32_t hi,
+                      uint32_t *counts, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_word_popc, dim3(nblocks(n, 256)), dim3(256), 0, s, words, n, V, rank, world, counts);
+  hipLaunchKernelGGL(k_word_popc, dim3(nblocks(n, 256)), dim3(256), 0, s, words, n, V, rank, world, lo, hi, counts);
   KCHECK("k_word_popc");
 }
 
-__global__ void k_word_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world,
-                               const uint32_t *offsets, uint32_t *out) {
+__global__ void k_word_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t lo,
+                               uint32_t hi, const uint32_t *offsets, uint32_t *out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t w = shard_word(words[i], i, V, rank, world);
+  uint64_t w = shard_word(words[i], i, V, rank, world, lo, hi);
   uint32_t o = offsets[i];
   while (w) {
     int b = __builtin_ctzll(w);
@@ -235,10 +246,11 @@ __global__ void k_word_scatter(const uint64_t *words, uint64_t n, uint32_t V, in
     w &= w - 1;
   }
 }
-void launch_word_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world,
+void launch_word_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t lo, uint32_t hi,
                          const uint32_t *offsets, uint32_t *out, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_word_scatter, dim3(nblocks(n, 256)), dim3(256), 0, s, words, n, V, rank, world, offsets, out);
+  hipLaunchKernelGGL(k_word_scatter, dim3(nblocks(n, 256)), dim3(256), 0, s, words, n, V, rank, world, lo, hi, offsets,
+                     out);
   KCHECK("k_word_scatter");
 }
 
@@ -698,10 +710,10 @@ __device__ __forceinline__ void slice_cuts(const uint32_t *col, uint64_t b, uint
 
 // slice-cut index of one CSR: cuts[v·(P−1) + q−1] = cut[q] of row v (relative to the row start)
 template <int MAXP>
-__global__ __launch_bounds__(256) void k_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t V, uint32_t P,
-                                                    uint32_t shift, uint32_t *cuts) {
-  const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= V) return;
+__global__ __launch_bounds__(256) void k_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t vlo, uint32_t vhi,
+                                                    uint32_t P, uint32_t shift, uint32_t *cuts) {
+  const uint64_t v = vlo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= vhi) return;
   uint32_t cut[MAXP + 1];
   slice_cuts<MAXP>(col, rp[v], rp[v + 1], P, shift, cut);
 #pragma unroll
@@ -792,11 +804,11 @@ __global__ __launch_bounds__(256) void k_fill_chunks_sliced(const uint32_t *src,
     else CALL(16);           \
   } while (0)
 
-void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t V, uint32_t nslices, uint32_t shift,
-                       uint32_t *cuts, hipStream_t s) {
-  if (!V || nslices < 2) return;
-#define OMX_BC(M) hipLaunchKernelGGL(k_build_cuts<M>, dim3(nblocks(V, 256)), dim3(256), 0, s, rp, col, V, nslices, \
-                                     shift, cuts)
+void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t vlo, uint32_t vhi, uint32_t nslices,
+                       uint32_t shift, uint32_t *cuts, hipStream_t s) {
+  if (vhi <= vlo || nslices < 2) return;
+#define OMX_BC(M) hipLaunchKernelGGL(k_build_cuts<M>, dim3(nblocks(vhi - vlo, 256)), dim3(256), 0, s, rp, col, vlo, vhi, \
+                                     nslices, shift, cuts)
   OMX_BY_MAXP(nslices, OMX_BC);
 #undef OMX_BC
   KCHECK("k_build_cuts");
@@ -1137,6 +1149,65 @@ void launch_check(const uint32_t *src, const uint32_t *dst, uint64_t R, const DA
   if (!R) return;
   hipLaunchKernelGGL(k_check, dim3(nblocks(R, 256)), dim3(256), 0, s, src, dst, R, adj, filter, flags);
   KCHECK("k_check");
+}
+
+// ---- partitioned execution: destination rank of every binding row (dist.h) -----------------------
+__device__ __forceinline__ void route_count(uint32_t d, bool live, uint32_t W, unsigned long long *s_h,
+                                            unsigned long long *hist) {
+  if (live) atomicAdd(&s_h[d], 1ull);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x)
+    if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
+
+// owner of the row's vertex under the block partition: min(v / block, W − 1)
+__global__ void k_route_owner(const uint32_t *v, uint64_t R, uint32_t block, uint32_t W, uint32_t *dest,
+                              unsigned long long *hist) {
+  __shared__ unsigned long long s_h[kMaxRanks];
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) s_h[i] = 0;
+  __syncthreads();
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t d = 0;
+  if (r < R) {
+    d = min(v[r] / block, W - 1);
+    dest[r] = d;
+  }
+  route_count(d, r < R, W, s_h, hist);
+}
+void launch_route_owner(const uint32_t *v, uint64_t R, uint32_t block, uint32_t W, uint32_t *dest, uint64_t *hist,
+                        hipStream_t s) {
+  if (!R) return;
+  hipLaunchKernelGGL(k_route_owner, dim3(nblocks(R, 256)), dim3(256), 0, s, v, R, block, W, dest,
+                     reinterpret_cast<unsigned long long *>(hist));
+  KCHECK("k_route_owner");
+}
+
+// a hash of the projected tuple: equal rows meet on one rank for the distinct pass
+__global__ void k_route_hash(int ncols, ColPtrs cp, uint64_t R, uint32_t W, uint32_t *dest, unsigned long long *hist) {
+  __shared__ unsigned long long s_h[kMaxRanks];
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) s_h[i] = 0;
+  __syncthreads();
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t d = 0;
+  if (r < R) {
+    uint64_t h = 0x243F6A8885A308D3ull;
+    for (int c = 0; c < ncols; ++c) {
+      h = (h ^ cp.in[c][r]) * 0x9E3779B97F4A7C15ull;
+      h ^= h >> 29;
+    }
+    d = (uint32_t)((h >> 32) % W);
+    dest[r] = d;
+  }
+  route_count(d, r < R, W, s_h, hist);
+}
+void launch_route_hash(int ncols, const uint32_t *const *cols, uint64_t R, uint32_t W, uint32_t *dest, uint64_t *hist,
+                       hipStream_t s) {
+  if (!R) return;
+  ColPtrs cp;
+  for (int c = 0; c < ncols; ++c) cp.in[c] = cols[c];
+  hipLaunchKernelGGL(k_route_hash, dim3(nblocks(R, 256)), dim3(256), 0, s, ncols, cp, R, W, dest,
+                     reinterpret_cast<unsigned long long *>(hist));
+  KCHECK("k_route_hash");
 }
 
 // ---- small host reads ------------------------------------------------------------------------------

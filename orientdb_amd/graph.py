@@ -33,7 +33,10 @@ class GraphSnapshot:
     `properties` = list of dicts {name, type, values[, present][, dict]};
     `indexes` = list of (class index, property name, unique)."""
 
-    def __init__(self, n_vertices, classes, vertex_class, rids, edge_sets, properties=(), indexes=(), device=0):
+    def __init__(self, n_vertices, classes, vertex_class, rids, edge_sets, properties=(), indexes=(), device=0,
+                 part=None):
+        """part = (lo, hi): a 1-D partition holding the CSR rows of vertices [lo, hi) only (local row
+        pointers of hi − lo + 1 entries; the in CSR is required); see include/omx/match.h."""
         L = N.lib()
         self.V = int(n_vertices)
         self.classes = list(classes)
@@ -57,7 +60,8 @@ class GraphSnapshot:
             icol = None if icol is None else np.ascontiguousarray(icol, dtype=np.uint32)
             keep += [orp, ocol, irp, icol]
             es_arr[i] = N.omx_edge_set_desc(es["cls"], int(orp[-1]), _ptr(orp, C.c_uint64), _ptr(ocol, C.c_uint32),
-                                            _ptr(irp, C.c_uint64), _ptr(icol, C.c_uint32))
+                                            _ptr(irp, C.c_uint64), _ptr(icol, C.c_uint32),
+                                            int(irp[-1]) if irp is not None else 0)
         pr_arr = (N.omx_property_desc * max(1, len(properties)))()
         for i, p in enumerate(properties):
             t = p["type"]
@@ -77,9 +81,10 @@ class GraphSnapshot:
             b = prop.encode()
             keep.append(b)
             ix_arr[i] = N.omx_index_desc(ci, b, int(unique))
+        self.part = (0, self.V) if part is None else (int(part[0]), int(part[1]))
         desc = N.omx_graph_desc(self.V, len(self.classes), cls_arr, _ptr(self.vertex_class, C.c_uint16),
                                 _ptr(self.rids, C.c_uint64), len(edge_sets), es_arr, len(properties), pr_arr,
-                                len(indexes), ix_arr, device)
+                                len(indexes), ix_arr, device, *((0, 0) if part is None else self.part))
         h = C.c_void_p()
         N.check(L.omx_graph_create(C.byref(desc), C.byref(h)))
         self._h = h
@@ -203,19 +208,27 @@ class GraphSnapshot:
         return cls.person_knows(rp, col, seed, device, keep_csr)
 
     @classmethod
-    def rmat(cls, scale, edge_factor=16, seed=None, simple=True, device=0, keep_csr=False):
+    def rmat(cls, scale, edge_factor=16, seed=None, simple=True, device=0, keep_csr=False, partition=None):
         """Synthetic Person/Knows graph: Graph500 RMAT, vertices of class Person
         (one cluster → RID #11:v), edge class Knows, properties uid (int64 = v) and age (int32 uniform
-        [0,100) from a seeded splitmix64)."""
+        [0,100) from a seeded splitmix64). partition = (rank, world): the 1-D partition of that rank
+        (rows of the vertices [rank·B, (rank+1)·B), B = ⌈V/world⌉; generated without the other rows)."""
         seed = scale if seed is None else seed
-        rp, col = rmat_csr(scale, edge_factor, seed, simple)
         V = 1 << scale
+        part = None
+        if partition is None:
+            rp, col = rmat_csr(scale, edge_factor, seed, simple)
+            es = {"cls": 3, "out_rp": rp, "out_col": col}
+        else:
+            part = partition_range(V, *partition)
+            rp, col, irp, icol = rmat_partition(scale, part[0], part[1], edge_factor, seed, simple)
+            es = {"cls": 3, "out_rp": rp, "out_col": col, "in_rp": irp, "in_col": icol}
         classes = [("V", -1, False, 9), ("E", -1, True, 10), ("Person", 0, False, 11), ("Knows", 1, True, 12)]
         vclass = np.full(V, 2, np.uint16)
         rids = (np.uint64(11) << np.uint64(RID_POS_BITS)) | np.arange(V, dtype=np.uint64)
         props = [{"name": "uid", "type": N.OMX_PROP_INT64, "values": np.arange(V, dtype=np.int64)},
                  {"name": "age", "type": N.OMX_PROP_INT32, "values": synthetic_int_column(V, seed ^ 0xA9E, 100)}]
-        g = cls(V, classes, vclass, rids, [{"cls": 3, "out_rp": rp, "out_col": col}], props, [], device)
+        g = cls(V, classes, vclass, rids, [es], props, [], device, part)
         g.scale = scale
         g.n_edges = int(rp[-1])
         if keep_csr:
@@ -252,6 +265,30 @@ def rmat_csr(scale, edge_factor=16, seed=None, simple=True):
     L.omx_host_free(C.cast(prp, C.c_void_p))
     L.omx_host_free(C.cast(pcol, C.c_void_p))
     return rp, col
+
+
+def partition_range(V, rank, world):
+    """Rows [lo, hi) of rank `rank` under the block partition of include/omx/match.h (B = ⌈V/world⌉)."""
+    b = -(-int(V) // int(world))
+    return min(V, rank * b), min(V, (rank + 1) * b)
+
+
+def rmat_partition(scale, lo, hi, edge_factor=16, seed=None, simple=True):
+    """(out_rp, out_col, in_rp, in_col) of the RMAT rows [lo, hi) (local row pointers)."""
+    L = N.lib()
+    seed = scale if seed is None else seed
+    orp, ocol, irp, icol = C.POINTER(C.c_uint64)(), C.POINTER(C.c_uint32)(), C.POINTER(C.c_uint64)(), C.POINTER(C.c_uint32)()
+    no, ni = C.c_uint64(), C.c_uint64()
+    N.check(L.omx_rmat_generate_part(scale, edge_factor, seed, int(simple), lo, hi, C.byref(orp), C.byref(ocol),
+                                     C.byref(no), C.byref(irp), C.byref(icol), C.byref(ni)))
+    n = hi - lo
+    out = (np.ctypeslib.as_array(orp, shape=(n + 1,)).copy(),
+           np.ctypeslib.as_array(ocol, shape=(max(1, no.value),))[:no.value].copy(),
+           np.ctypeslib.as_array(irp, shape=(n + 1,)).copy(),
+           np.ctypeslib.as_array(icol, shape=(max(1, ni.value),))[:ni.value].copy())
+    for p in (orp, ocol, irp, icol):
+        L.omx_host_free(C.cast(p, C.c_void_p))
+    return out
 
 
 def csr_transpose(V, rp, col):

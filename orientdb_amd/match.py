@@ -122,7 +122,10 @@ class OMatchStatement:
         N.check(N.lib().omx_statement_explain(self._h, graph.handle, arr, n, buf, len(buf)))
         return json.loads(buf.value.decode())
 
-    def execute(self, graph, *args, mode=N.OMX_MODE_MATERIALIZE, flags=0, shard=(0, 1), documents=True, **named):
+    def execute(self, graph, *args, mode=N.OMX_MODE_MATERIALIZE, flags=0, shard=(0, 1), documents=True, comm=None,
+                **named):
+        """comm: the ranks' Comm (orientdb_amd.dist) when `graph` is a partition; every rank then
+        returns its share of the distinct rows (their union is the result)."""
         arr, n = _values(args, named)
         o = N.omx_exec_options()
         N.lib().omx_exec_options_init(C.byref(o))
@@ -132,6 +135,7 @@ class OMatchStatement:
         o.shard_rank, o.shard_world = shard
         o.params = arr
         o.n_params = n
+        o.comm = comm.handle if comm is not None else None
         r = C.c_void_p()
         N.check(N.lib().omx_execute(graph.handle, self._h, C.byref(o), C.byref(r)))
         try:

@@ -1,0 +1,129 @@
+"""The 1-D partitioned MATCH on one MI355X: `world` partitions of one RMAT graph, each
+rank a thread of this process with its own snapshot and stream on cuda:0, rows exchanged by the
+thread transport (device-to-device copies) — the same routing code the RCCL transport drives across
+GPUs. The union of the ranks' rows is compared bit-exactly with the oracle; RCCL itself is exercised
+with a one-rank communicator routing through itself (OMX_ROUTE_SELF=1).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import RMAT_QUERIES, _Ref, gpu_set
+
+pytestmark = pytest.mark.gpu
+
+DIST_IDS = ("c2_both_ends", "c1_fof", "c1_abc", "two_cols_dedup", "in_dir", "both_dir", "three_hop", "triangle",
+            "triangle_filtered", "matches", "paths", "bound_candidate")
+DIST_QUERIES = [q for q in RMAT_QUERIES if q[0] in DIST_IDS]
+
+
+@pytest.fixture(scope="module")
+def rmat10_full():
+    import orientdb_amd as o
+    g = o.GraphSnapshot.rmat(10, device=0, keep_csr=True)
+    return g, _Ref(g, True)
+
+
+_parts_cache = {}
+
+
+def _parts(world):
+    import orientdb_amd as o
+    if world not in _parts_cache:
+        _parts_cache[world] = [o.GraphSnapshot.rmat(10, device=0, partition=(r, world)) for r in range(world)]
+    return _parts_cache[world]
+
+
+def run_ranks(parts, query, **kw):
+    """One thread per rank (ctypes releases the GIL inside omx_execute); returns the ranks' results."""
+    import orientdb_amd as o
+    comms = o.Comm.threads(len(parts))
+    out, err = [None] * len(parts), []
+
+    def work(r):
+        try:
+            out[r] = o.OMatchStatement(query).execute(parts[r], comm=comms[r], **kw)
+        except BaseException as e:  # noqa: BLE001 — reported to the test thread
+            err.append(e)
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(len(parts))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a rank did not finish (exchange deadlock)"
+    for c in comms:
+        c.close()
+    if err:
+        raise err[0]
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("q", DIST_QUERIES, ids=[q[0] for q in DIST_QUERIES])
+def test_partitioned_parity(rmat10_full, world, q):
+    _, ref = rmat10_full
+    name, query, cols = q
+    want = ref.expected(query, cols)
+    res = run_ranks(_parts(world), query)
+    got = [gpu_set(r, cols) for r in res]
+    union = set().union(*got)
+    assert union == want
+    if name in ("c1_fof", "two_cols_dedup", "matches", "paths"):
+        # distinct projections: the hash exchange puts each tuple on exactly one rank
+        assert sum(len(g) for g in got) == len(want)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_counts_match_replicated(rmat10_full, world):
+    """COUNT mode: the ranks' edges/bindings add up to the single-snapshot run."""
+    import orientdb_amd as o
+    g, _ = rmat10_full
+    for qn in ("c2_both_ends", "three_hop"):
+        query = dict((x[0], x[1]) for x in RMAT_QUERIES)[qn]
+        full = o.OMatchStatement(query).execute(g, mode=o.OMX_MODE_COUNT)
+        res = run_ranks(_parts(world), query, mode=o.OMX_MODE_COUNT)
+        assert sum(r.info["edges_traversed"] for r in res) == full.info["edges_traversed"]
+        assert sum(r.info["bindings"] for r in res) == full.info["bindings"]
+        assert sum(r.info["n_rows"] for r in res) == full.info["n_rows"]
+
+
+def test_partitioned_sliced_kernel(rmat10_full, monkeypatch):
+    """Filtered hops through the LDS-sliced heavy kernel on partitions (slice-cut index of owned rows)."""
+    monkeypatch.setenv("OMX_HEAVY_DEG", "2")
+    monkeypatch.setenv("OMX_SLICE_SHIFT", "7")
+    _, ref = rmat10_full
+    name, query, cols = [q for q in RMAT_QUERIES if q[0] == "c2_both_ends"][0]
+    res = run_ranks(_parts(2), query)
+    assert set().union(*[gpu_set(r, cols) for r in res]) == ref.expected(query, cols)
+
+
+def test_rccl_one_rank_routes_through_itself(rmat10_full, monkeypatch):
+    import orientdb_amd as o
+    monkeypatch.setenv("OMX_ROUTE_SELF", "1")
+    _, ref = rmat10_full
+    part = o.GraphSnapshot.rmat(10, device=0, partition=(0, 1))
+    comm = o.Comm.rccl(0, 1, 0, o.Comm.unique_id())
+    try:
+        for qn in ("c2_both_ends", "two_cols_dedup", "three_hop"):
+            name, query, cols = [q for q in RMAT_QUERIES if q[0] == qn][0]
+            rs = o.OMatchStatement(query).execute(part, comm=comm)
+            assert gpu_set(rs, cols) == ref.expected(query, cols)
+    finally:
+        comm.close()
+
+
+def test_partition_errors(rmat10_full):
+    import orientdb_amd as o
+    parts = _parts(2)
+    with pytest.raises(o.OmxError):  # a partition needs its communicator
+        o.OMatchStatement(RMAT_QUERIES[0][1]).execute(parts[0])
+    comms = o.Comm.threads(2)
+    with pytest.raises(o.OmxError):  # rank 1's communicator with rank 0's rows
+        o.OMatchStatement(RMAT_QUERIES[0][1]).execute(parts[0], comm=comms[1])
+    with pytest.raises(o.OmxUnsupported):  # variable-length items stay on replicated snapshots
+        q = [x for x in RMAT_QUERIES if x[0] == "varlen_depth"][0][1]
+        o.OMatchStatement(q).execute(parts[0], comm=comms[0])
+    for c in comms:
+        c.close()
