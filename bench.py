@@ -30,7 +30,11 @@ QUERIES = {
            "MATCH {class:Person,as:s,where:(uid < 64)}-Knows->{as:v, while:($depth < 4)} RETURN s, v", 24),
     "c4": ("C4: cyclic triangle MATCH (a->b->c->a) via sorted-adjacency intersection, LDBC-SNB-like SF10 Knows",
            "MATCH {class:Person,as:a}-Knows->{as:b}-Knows->{as:c}-Knows->{as:a} RETURN a,b,c", "ldbc"),
+    "c5": ("C5: RMAT 3-hop MATCH (COUNT), 1-D partitioned graph, per-hop all-to-all row exchange (RCCL)",
+           "MATCH {class:Person,as:a,where:(uid < 64)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d", 26),
 }
+PARTITIONED = {"c5"}  # queries whose graph is 1-D partitioned across the ranks
+COUNT_MODE = {"c5"}   # the last hop counts its rows (count mode)
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # ≈7e4 Person, ≈2e6 Knows
 # kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)
 HOT_KERNELS = ("k_expand_heavy", "k_expand_light", "k_check", "k_bfs_pull", "k_bfs_push", "k_bfs_prep", "k_bfs_emit",
@@ -75,7 +79,9 @@ def cpu_baseline(g, query, target_s=12.0):
     rp, col = g.csr
     cg = dfs.CsrGraph(rp, col, {"uid": np.arange(g.V, dtype=np.int64), "age": g.age})
     probe = dfs.run(cg, query, nthreads=threads, emit=False, root_sample=64)
-    nroots_total = len(np.nonzero(cg.columns["age"] < 1)[0]) if "age < 1" in query else g.V
+    import re
+    m = re.search(r"\((age|uid) < (\d+)\)", query.split("-")[0])
+    nroots_total = int(np.count_nonzero(cg.columns[m.group(1)] < int(m.group(2)))) if m else g.V
     per_root = max(probe["seconds"] / max(probe["nroots"], 1), 1e-7)
     sample = int(min(nroots_total, max(64, target_s / per_root)))
     # repeat the bounded sample until ≈ target_s of CPU work has been timed
@@ -108,6 +114,20 @@ def reduce_over_ranks(dist, dt, edges, bindings, rows):
     return t.item(), s[0].item(), s[1].item(), s[2].item()
 
 
+def with_heartbeat(label, fn, every=20.0):
+    """Run fn() while a child process prints a progress line to stderr every `every` s (a long
+    RMAT-26 build would otherwise look hung to a silence watchdog; a child is immune to the GIL)."""
+    import subprocess
+    code = ("import sys, time\nt0 = time.time()\nwhile True:\n    time.sleep(%f)\n"
+            "    print('[bench] %s: %%.0f s' %% (time.time() - t0), file=sys.stderr, flush=True)\n" % (every, label))
+    hb = subprocess.Popen([sys.executable, "-c", code])
+    try:
+        return fn()
+    finally:
+        hb.kill()
+        hb.wait()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,6 +137,8 @@ def main():
     ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--partitioned", action="store_true",
+                    help="1-D partition the graph across the ranks and exchange rows per hop (default for c5)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -137,28 +159,43 @@ def main():
     workload, query, default_scale = QUERIES[args.query]
     if args.scale is None:
         args.scale = default_scale
+    partitioned = (args.partitioned or args.query in PARTITIONED) and args.scale != "ldbc"
     t_build = time.perf_counter()
     keep = rank == 0 and world == 1 and not args.no_cpu_baseline
+    comm = None
     if args.scale == "ldbc":
         g = o.GraphSnapshot.ldbc_like(device=local, keep_csr=keep, **LDBC_SF10)
         graph_desc = {"graph": "LDBC-SNB-like Knows (gen.cpp omx_ldbc_knows_generate)", **LDBC_SF10}
+    elif partitioned and world > 1:
+        # every rank generates and uploads only the rows it owns; the RCCL unique id travels over gloo
+        args.scale = int(args.scale)
+        g = with_heartbeat("graph build", lambda: o.GraphSnapshot.rmat(args.scale, device=local,
+                                                                        partition=(rank, world)))
+        uid = [o.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = o.Comm.rccl(rank, world, local, uid[0])
+        graph_desc = {"graph": "RMAT, 1-D partitioned (block of ceil(V/N) vertices per GPU)", "scale": args.scale,
+                      "edge_factor": 16, "rows_owned": list(g.part)}
     else:
         args.scale = int(args.scale)
-        g = o.GraphSnapshot.rmat(args.scale, device=local, keep_csr=keep)
+        g = with_heartbeat("graph build", lambda: o.GraphSnapshot.rmat(args.scale, device=local, keep_csr=keep))
         graph_desc = {"graph": "RMAT", "scale": args.scale, "edge_factor": 16}
     t_build = time.perf_counter() - t_build
     st = o.OMatchStatement(query)
     flags = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_KERNEL_TIMING | o.OMX_FLAG_TIME_HOT
-    shard = (rank, world)
+    mode = o.OMX_MODE_COUNT if args.query in COUNT_MODE else o.OMX_MODE_MATERIALIZE
+    # replicated graph: roots sharded v % N == rank; partitioned: each rank starts from the roots it owns
+    shard = (0, 1) if comm is not None else (rank, world)
+    run_kw = dict(flags=flags, shard=shard, documents=False, mode=mode, comm=comm)
     for _ in range(args.warmup):
-        st.execute(g, flags=flags, shard=shard, documents=False)
+        st.execute(g, **run_kw)
     barrier()
     hip_sync()
     t0 = time.perf_counter()
     infos = []
     kst = {}
     for _ in range(args.steps):
-        rs = st.execute(g, flags=flags, shard=shard, documents=False)
+        rs = st.execute(g, **run_kw)
         infos.append(rs.info)
         for k in rs.kernel_stats:
             a = kst.setdefault(k["name"], {"launches": 0, "ms": 0.0, "alg_bytes": 0})
@@ -169,9 +206,13 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     edges = sum(i["edges_traversed"] for i in infos)
+    edges_read = sum(i["edges_read"] for i in infos)
     bindings = sum(i["bindings"] for i in infos)
     rows = infos[-1]["n_rows"]
     dt_max, edges_all, bindings_all, rows_all = reduce_over_ranks(dist, dt, edges, bindings, rows)
+    edges_read_all = reduce_over_ranks(dist, dt, edges_read, 0, 0)[1]
+    if comm is not None:
+        comm.close()
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -197,7 +238,13 @@ def main():
         "config": {"workload": workload, "query": query, **graph_desc,
                    "V": g.V, "E": g.n_edges, "rows_per_step": int(rows_all),
                    "edges_per_step": int(edges_all / args.steps), "bindings_per_step": int(bindings_all / args.steps),
-                   "parallelism": "roots sharded v%%N across %d GPU(s), graph replicated" % world,
+                   # edges whose neighbour ids a kernel read; a COUNT run sums an unfiltered last hop
+                   # from degrees (E_t per SURVEY §8(d) still counts those edges)
+                   "edges_read_per_step": int(edges_read_all / args.steps),
+                   "parallelism": ("1-D partitioned graph over %d GPU(s), rows exchanged per hop (RCCL all-to-all)"
+                                   % world) if comm is not None else
+                                  ("roots sharded v%%N across %d GPU(s), graph replicated" % world),
+                   "mode": "count" if mode == o.OMX_MODE_COUNT else "materialize (rows kept in HBM)",
                    "graph_build_s": round(t_build, 2)},
         "bindings_per_s": bindings_all / dt_max,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -178,6 +178,8 @@ typedef struct omx_result_info {
   uint64_t alg_bytes;        /* algorithmic HBM bytes, SURVEY §8(d)                                */
   double device_ms;          /* wall time of the device part (root scan → last kernel)             */
   double total_ms;           /* wall time of omx_execute                                           */
+  uint64_t edges_read;       /* edges whose neighbour ids were read: edges_traversed minus the hops */
+                             /* a COUNT run sums from degrees (an unfiltered last hop)              */
 } omx_result_info;
 
 int omx_result_info_get(const omx_result *r, omx_result_info *info);

@@ -59,7 +59,7 @@ class omx_exec_options(C.Structure):
 class omx_result_info(C.Structure):
     _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_int32), ("deduplicated", C.c_int32),
                 ("edges_traversed", C.c_uint64), ("bindings", C.c_uint64), ("alg_bytes", C.c_uint64),
-                ("device_ms", C.c_double), ("total_ms", C.c_double)]
+                ("device_ms", C.c_double), ("total_ms", C.c_double), ("edges_read", C.c_uint64)]
 
 
 # every exported symbol of include/omx/match.h: name -> (restype, argtypes)

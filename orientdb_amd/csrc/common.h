@@ -26,6 +26,10 @@ inline std::string lower(std::string s) {
 }
 inline bool ieq(const std::string &a, const std::string &b) { return lower(a) == lower(b); }
 
+// host worker threads: the machine's CPUs, capped by OMP_NUM_THREADS (the CPU share a job gets on a
+// shared box can be far below what hardware_concurrency reports) and by 64
+unsigned host_threads();
+
 inline uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -227,6 +227,7 @@ class Executor {
     res->info.n_cols = n ? ncols : 0;
     res->info.deduplicated = dedup_ran_;
     res->info.edges_traversed = edges_;
+    res->info.edges_read = edges_ - degree_counted_;
     res->info.bindings = bindings_;
     res->info.alg_bytes = alg_bytes_;
     res->info.device_ms = dms;
@@ -253,6 +254,7 @@ class Executor {
   std::vector<DBuf<uint32_t>> col_;
   uint64_t R_ = 1;
   uint64_t edges_ = 0, alg_bytes_ = 0, bindings_ = 0;
+  uint64_t degree_counted_ = 0;  // edges of count-only unfiltered hops (summed from degrees, not read)
   int dedup_ran_ = 0;
   int cus_ = 0;
   uint64_t heavy_deg_ = kHeavyDeg;
@@ -524,6 +526,7 @@ class Executor {
     uint64_t n = 0;
     uint64_t E = 0;
     uint64_t E_member = 0;  // edges of a fused closing check
+    bool counted_from_degrees = false;  // count-only unfiltered hop: no col[] read
     // block-segmented result (filtered expansion left un-compacted)
     bool segmented = false;
     DBuf<uint64_t> seg_start;
@@ -608,6 +611,14 @@ class Executor {
     const uint64_t E = EL + EH;
     o.E = E;
     if (E == 0) return o;
+    if (!write && filter == nullptr && !member) {
+      // counting an unfiltered hop: its bindings are Σ degree, known from the scan — no col[] reads
+      // (reported apart: omx_result_info.edges_read excludes these edges)
+      o.n = E;
+      o.counted_from_degrees = true;
+      alg_bytes_ += 8 * R;
+      return o;
+    }
     DBuf<ChunkDesc> chunks;
     if (nchunks) {
       chunks = DBuf<ChunkDesc>(&pool_, nchunks);
@@ -797,6 +808,7 @@ class Executor {
                               check ? col_[check->src].p : nullptr, check ? &check->adj : nullptr,
                               check ? bitmap(check->filter_bm) : nullptr);
     edges_ += o.E + o.E_member;
+    if (o.counted_from_degrees) degree_counted_ += o.E;
     R_ = o.n;
     if (!write || R_ == 0) return;
     segmented_ = o.segmented;

@@ -20,7 +20,7 @@ namespace {
 
 template <class F>
 void par(uint64_t n, F f) {
-  unsigned nt = std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+  unsigned nt = omx::host_threads();
   if (n < (1u << 16)) nt = 1;
   std::vector<std::thread> th;
   for (unsigned t = 0; t < nt; ++t) th.emplace_back([=] { f(n * t / nt, n * (t + 1) / nt); });
@@ -66,6 +66,17 @@ struct Rmat {
 };
 
 }  // namespace
+
+namespace omx {
+unsigned host_threads() {
+  unsigned n = std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+  if (const char *e = std::getenv("OMP_NUM_THREADS")) {
+    const long k = std::strtol(e, nullptr, 10);
+    if (k > 0) n = std::min<unsigned>(n, (unsigned)k);
+  }
+  return n;
+}
+}  // namespace omx
 
 extern "C" {
 

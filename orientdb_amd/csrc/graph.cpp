@@ -151,7 +151,7 @@ int64_t Graph::index_hits(int cls, int prop, const Value &v) const {
 
 template <class F>
 static void parallel_for(uint64_t n, F f) {
-  unsigned nt = std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+  unsigned nt = host_threads();
   if (n < 65536) nt = 1;
   std::vector<std::thread> th;
   for (unsigned t = 0; t < nt; ++t)
