@@ -137,6 +137,7 @@ def main():
     ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--count", action="store_true", help="COUNT mode (the last hop counts its rows)")
     ap.add_argument("--partitioned", action="store_true",
                     help="1-D partition the graph across the ranks and exchange rows per hop (default for c5)")
     args = ap.parse_args()
@@ -183,7 +184,7 @@ def main():
     t_build = time.perf_counter() - t_build
     st = o.OMatchStatement(query)
     flags = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_KERNEL_TIMING | o.OMX_FLAG_TIME_HOT
-    mode = o.OMX_MODE_COUNT if args.query in COUNT_MODE else o.OMX_MODE_MATERIALIZE
+    mode = o.OMX_MODE_COUNT if (args.query in COUNT_MODE or args.count) else o.OMX_MODE_MATERIALIZE
     # replicated graph: roots sharded v % N == rank; partitioned: each rank starts from the roots it owns
     shard = (0, 1) if comm is not None else (rank, world)
     run_kw = dict(flags=flags, shard=shard, documents=False, mode=mode, comm=comm)

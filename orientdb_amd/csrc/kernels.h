@@ -28,6 +28,7 @@ constexpr uint32_t kSliceBits = 1u << 20;
 constexpr uint32_t kSliceWords = kSliceBits / 32;  // u32 words per slice
 constexpr int kMaxSlices = 16;                     // V ≤ 16·2^20; beyond that the L2-probe kernel is used
 constexpr uint64_t kHeavyDegSliced = 256;         // LDS probes make short chunks cheap: a lower cut
+constexpr int kStage = 448;                        // staged survivors per wave (16 waves × 1.75 KiB of LDS)
 constexpr int kSliceBlock = 1024;                  // 16 waves: one workgroup per CU (LDS-limited)
 
 // per adjacency part: the CSR's slice-cut index (EdgeSet::d_cuts), P−1 offsets per vertex

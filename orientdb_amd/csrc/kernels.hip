@@ -901,6 +901,9 @@ template <bool WRITE, int NC>
 __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs a, SliceArgs sa) {
   constexpr int NS = kHeavySlots, WPB = kSliceBlock / 64, NCV = NC < 0 ? 4 : (NC > 0 ? NC : 1);
   __shared__ uint32_t s_bm[kSliceBits / 32];
+  // per-wave staging of a chunk's surviving neighbours: flushed with full-wave coalesced stores (the
+  // chunk's carried columns are constants), instead of one partial store per column and 64-edge slot
+  __shared__ uint32_t s_stage[WPB * (kStage + 1)];  // +1: a masked-off lane's probe may stage one row past
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t gw = blockIdx.x * WPB + wave;
@@ -959,6 +962,23 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
   // per 64-edge slot: 2 VALU for the LDS word (a neighbour of the slice, so its low bits are the
   // offset), one bit-field extract, the ballot, a lane prefix, and exec-masked compacted stores
   const uint32_t wbits = sa.shift - 5;  // bitmap words per slice = 2^wbits
+  uint32_t *const stage = s_stage + wave * (kStage + 1);
+  // writes the `n` staged rows (neighbour from LDS, carried columns constant) at the arena's acc
+  auto flush = [&](const Cur &x, uint32_t n) {
+    const int32_t so = (int32_t)(acc * 4);
+    for (uint32_t k = 0; k < n; k += 64) {
+      const uint32_t idx = k + lane;
+      if (idx < n) {
+        const uint32_t off = idx * 4;
+        __builtin_amdgcn_raw_buffer_store_b32(stage[idx], od, off, so, 0);
+        if (nc > 0) __builtin_amdgcn_raw_buffer_store_b32(x.cv[0], oc0, off, so, 0);
+        if (nc > 1) __builtin_amdgcn_raw_buffer_store_b32(x.cv[1], oc1, off, so, 0);
+        if (nc > 2) __builtin_amdgcn_raw_buffer_store_b32(x.cv[2], oc2, off, so, 0);
+        if (nc > 3) __builtin_amdgcn_raw_buffer_store_b32(x.cv[3], oc3, off, so, 0);
+      }
+    }
+    acc += n;
+  };
   auto process = [&](const Cur &x) {
     uint32_t w[NS];
 #pragma unroll
@@ -966,34 +986,42 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
     // all 16 probes are in flight before the first is used (one LDS wait, not one per slot)
 #pragma unroll
     for (int i = 0; i < NS; ++i) asm volatile("" : "+v"(w[i]));
+    uint32_t st = 0;  // rows staged for this chunk
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       if ((uint32_t)(i * 64) >= x.n) break;  // uniform: slice cuts leave chunks short (≈600 of 1024 edges)
       const uint32_t v = x.q[i];
       // v_bfe_u32 reads the low 5 bits of its offset operand. Lanes past the chunk end (last slot
-      // only) are cut from the ballot on the scalar side; if their (zero-filled) probe is set they
-      // store one garbage row at acc + popc(m), past this slot's survivors — overwritten by the next
-      // slot or left in the arena's 64-row tail pad, never counted.
+      // only) are cut from the ballot on the scalar side (a set probe there stages one row past the
+      // counted ones, never flushed).
       const bool bit = __builtin_amdgcn_ubfe(w[i], v, 1) != 0;
       uint64_t m = __builtin_amdgcn_ballot_w64(bit);
       const uint32_t rem = x.n - (uint32_t)(i * 64);
       if (rem < 64) m &= (1ull << rem) - 1;
+      const uint32_t cnt = (uint32_t)__popcll(m);
       if (WRITE) {
-        if (bit) {  // exec-masked: stores with every lane live but range-dropped were measured slower
+        if (NC >= 0) {
+          if (bit) stage[st + lane_prefix(m)] = v;
+          st += cnt;
+          if (st > kStage - 64) {  // uniform: room for one more slot
+            flush(x, st);
+            st = 0;
+          }
+        } else if (bit) {  // more than 4 carried columns: direct stores
           const uint32_t pre = lane_prefix(m);
           const uint32_t off = pre * 4;
           const int32_t so = (int32_t)(acc * 4);
           __builtin_amdgcn_raw_buffer_store_b32(v, od, off, so, 0);
-          if (nc > 0) __builtin_amdgcn_raw_buffer_store_b32(x.cv[0], oc0, off, so, 0);
-          if (nc > 1) __builtin_amdgcn_raw_buffer_store_b32(x.cv[1], oc1, off, so, 0);
-          if (nc > 2) __builtin_amdgcn_raw_buffer_store_b32(x.cv[2], oc2, off, so, 0);
-          if (nc > 3) __builtin_amdgcn_raw_buffer_store_b32(x.cv[3], oc3, off, so, 0);
-          if (NC < 0)
-            for (int kk = 4; kk < nc; ++kk) a.carry_out[kk][arena + acc + pre] = a.carry_in[kk][x.row];
+          __builtin_amdgcn_raw_buffer_store_b32(x.cv[0], oc0, off, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(x.cv[1], oc1, off, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(x.cv[2], oc2, off, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(x.cv[3], oc3, off, so, 0);
+          for (int kk = 4; kk < nc; ++kk) a.carry_out[kk][arena + acc + pre] = a.carry_in[kk][x.row];
         }
       }
-      acc += (uint32_t)__popcll(m);
+      if (!WRITE || NC < 0) acc += cnt;
     }
+    if (WRITE && NC >= 0 && st) flush(x, st);
   };
   // three register sets in rotation, two chunks in flight while one is filtered (no copy of in-flight
   // load destinations: the waitcnt pass then only waits for the chunk it processes)
