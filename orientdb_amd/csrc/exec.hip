@@ -395,8 +395,10 @@ class Executor {
 
   // calculateMatch (:340-357): an empty candidate set of a prefetched alias → empty result
   bool check_candidates() {
+    // the root's own candidate set needs no separate count: an empty root list already yields no row
+    const int root_bm = !p_.steps.empty() && p_.steps[0].kind == S_ROOT ? p_.steps[0].cand_bm : -1;
     for (int bm : p_.must_be_nonempty)
-      if (bm >= 0 && bitmap_count(bitmap(bm), 0, 1) == 0) return false;
+      if (bm >= 0 && bm != root_bm && bitmap_count(bitmap(bm), 0, 1) == 0) return false;
     return true;
   }
 
@@ -620,12 +622,17 @@ class Executor {
       return o;
     }
     DBuf<ChunkDesc> chunks;
+    DBuf<SliceChunk> schunks;
     if (nchunks) {
-      chunks = DBuf<ChunkDesc>(&pool_, nchunks);
       tm_.begin("k_fill_chunks");
-      if (sliced) launch_fill_chunks_sliced(src, R, adj, cuts, P, choffs.p, hoffs.p, chunks.p, s_);
-      else launch_fill_chunks(src, R, adj, choffs.p, hoffs.p, chunks.p, s_);
-      tm_.end(nchunks * sizeof(ChunkDesc));
+      if (sliced) {
+        schunks = DBuf<SliceChunk>(&pool_, nchunks);
+        launch_fill_chunks_sliced(src, R, adj, cuts, P, choffs.p, hoffs.p, schunks.p, s_);
+      } else {
+        chunks = DBuf<ChunkDesc>(&pool_, nchunks);
+        launch_fill_chunks(src, R, adj, choffs.p, hoffs.p, chunks.p, s_);
+      }
+      tm_.end(nchunks * (sliced ? sizeof(SliceChunk) : sizeof(ChunkDesc)));
     }
     const uint64_t ntiles = EL ? (R + EL + kExpandTile - 1) / kExpandTile : 0;
     DBuf<uint64_t> part;
@@ -686,6 +693,7 @@ class Executor {
     a.filter = filter;
     a.ncarry = (int32_t)carry.size();
     a.chunks = chunks.p;
+    a.schunks = schunks.p;
     a.nchunks = nchunks;
     a.hoffs = hoffs.p;
     a.dense_base = EH;

@@ -44,6 +44,16 @@ struct SliceArgs {
   uint32_t shift;  // slice = 2^shift vertices (6 ≤ shift ≤ 20; tests shrink it to cut small graphs)
 };
 
+// a chunk of the sliced kernel: ≤ kChunk edges of one row part inside one bitmap slice (16 B: one
+// scalar dwordx4 load)
+struct SliceChunk {
+  uint64_t lo;    // first col[] index
+  uint32_t row;   // binding row
+  uint16_t n;     // edges (1…kChunk)
+  uint16_t part;  // adjacency part
+};
+static_assert(sizeof(SliceChunk) == 16, "SliceChunk is one dwordx4");
+
 struct ChunkDesc {
   uint64_t lo, hi;  // absolute col[] range of the chunk inside part `part` (one kChunk-aligned window)
   uint64_t dense;   // output index of edge lo in the dense (unfiltered) layout
@@ -74,6 +84,7 @@ struct ExpandArgs {
   uint32_t seg_base;
   // heavy chunks
   const ChunkDesc *chunks;
+  const SliceChunk *schunks;  // sliced kernel
   uint64_t nchunks;
   const uint64_t *hoffs;    // [R+1] exclusive prefix of the heavy rows' full degree (dense mode)
   // fused closing check of a cyclic pattern (sorted-adjacency intersection): neighbour n of row r is
@@ -117,7 +128,7 @@ void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t vlo, ui
 void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint64_t heavy_deg,
                              uint32_t nslices, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s);
 void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint32_t nslices,
-                               const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out, hipStream_t s);
+                               const uint64_t *choffs, const uint64_t *hoffs, SliceChunk *out, hipStream_t s);
 // meta = {loffs[R], hoffs[R], choffs[nchn-1], qb[0..P]}; qb[q] = choffs[q·(R+1)] (nslices = 0: unsliced)
 void launch_expand_meta(const uint64_t *loffs, const uint64_t *hoffs, const uint64_t *choffs, uint64_t R,
                         uint64_t nchn, uint32_t nslices, uint64_t *qb, uint64_t *meta, hipStream_t s);

@@ -771,12 +771,11 @@ __global__ __launch_bounds__(256) void k_row_split_sliced(const uint32_t *src, u
 template <int MAXP>
 __global__ __launch_bounds__(256) void k_fill_chunks_sliced(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
                                                             uint32_t P, const uint64_t *choffs, const uint64_t *hoffs,
-                                                            ChunkDesc *out) {
+                                                            SliceChunk *out) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || hoffs[r + 1] == hoffs[r]) return;  // light row
   const uint64_t stride = R + 1;
   const uint32_t v = src[r];
-  uint64_t pos = hoffs[r];  // dense index of the row's first edge (parts in order)
   uint64_t o[MAXP];
 #pragma unroll
   for (int q = 0; q < MAXP; ++q) o[q] = (uint32_t)q < P ? choffs[q * stride + r] : 0;
@@ -788,10 +787,9 @@ __global__ __launch_bounds__(256) void k_fill_chunks_sliced(const uint32_t *src,
     for (int q = 0; q < MAXP; ++q) {
       for (uint32_t clo = cut[q]; clo < cut[q + 1]; clo += kChunk) {  // as chunk_pieces
         const uint32_t chi = clo + kChunk < cut[q + 1] ? clo + kChunk : cut[q + 1];
-        out[o[q]++] = ChunkDesc{b + clo, b + chi, pos + clo, (uint32_t)r, (uint32_t)p};
+        out[o[q]++] = SliceChunk{b + clo, (uint32_t)r, (uint16_t)(chi - clo), (uint16_t)p};
       }
     }
-    pos += e - b;
   }
 }
 
@@ -824,7 +822,7 @@ void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, c
 }
 
 void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint32_t nslices,
-                               const uint64_t *choffs, const uint64_t *hoffs, ChunkDesc *out, hipStream_t s) {
+                               const uint64_t *choffs, const uint64_t *hoffs, SliceChunk *out, hipStream_t s) {
   if (!R) return;
 #define OMX_FC(M) hipLaunchKernelGGL(k_fill_chunks_sliced<M>, dim3(nblocks(R, 256)), dim3(256), 0, s, src, R, adj, \
                                      cuts, nslices, choffs, hoffs, out)
@@ -869,27 +867,21 @@ __device__ __forceinline__ T sload(const T *p) {
 // chunk descriptor through scalar loads (wave-uniform address; chunks are read-only in the kernel).
 // The compiler turns a plain load here into a vector load whose wait would also drain the
 // in-flight col[] prefetch (vmcnt is in order), so the two s_loads are explicit.
-__device__ __forceinline__ ChunkDesc sload_chunk(const ChunkDesc *p) {
+__device__ __forceinline__ SliceChunk sload_chunk(const SliceChunk *p) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  const ChunkDesc *pu = (const ChunkDesc *)wave_bcast64((uint64_t)p);
+  const SliceChunk *pu = (const SliceChunk *)wave_bcast64((uint64_t)p);
   u32x4 a;
-  u32x2 b;
-  u32x2 dn;
   asm volatile(
-      "s_load_dwordx4 %0, %3, 0x0\n\t"
-      "s_load_dwordx2 %1, %3, 0x10\n\t"
-      "s_load_dwordx2 %2, %3, 0x18\n\t"
+      "s_load_dwordx4 %0, %1, 0x0\n\t"
       "s_waitcnt lgkmcnt(0)"
-      : "=&s"(a), "=&s"(dn), "=&s"(b)  // early-clobber: the loads land after the base is read
+      : "=&s"(a)  // early-clobber: the load lands after the base is read
       : "s"(pu)
       : "memory");
-  ChunkDesc d;
+  SliceChunk d;
   d.lo = ((uint64_t)a.y << 32) | a.x;
-  d.hi = ((uint64_t)a.w << 32) | a.z;
-  d.dense = ((uint64_t)dn.y << 32) | dn.x;
-  d.row = b.x;
-  d.part = b.y;
+  d.row = a.z;
+  d.n = (uint16_t)(a.w & 0xffffu);
+  d.part = (uint16_t)(a.w >> 16);
   return d;
 }
 
@@ -944,9 +936,9 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
   // would make the waitcnt pass assume the worst at the join and drain the prefetch
   auto load = [&](uint64_t c, Cur &x) {
     const bool live = c < qend;
-    const ChunkDesc d = sload_chunk(a.chunks + (live ? c : qend - 1));
+    const SliceChunk d = sload_chunk(a.schunks + (live ? c : qend - 1));
     x.lo = d.lo;
-    x.n = live ? (uint32_t)(d.hi - d.lo) : 0u;
+    x.n = live ? (uint32_t)d.n : 0u;
     x.row = d.row;
     x.part = d.part;
     if (WRITE) {
@@ -963,6 +955,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
   // offset), one bit-field extract, the ballot, a lane prefix, and exec-masked compacted stores
   const uint32_t wbits = sa.shift - 5;  // bitmap words per slice = 2^wbits
   uint32_t *const stage = s_stage + wave * (kStage + 1);
+  auto cvk = [](const Cur &x, int k) { return k < NCV ? x.cv[k < NCV ? k : 0] : 0u; };
   // writes the `n` staged rows (neighbour from LDS, carried columns constant) at the arena's acc
   auto flush = [&](const Cur &x, uint32_t n) {
     const int32_t so = (int32_t)(acc * 4);
@@ -971,10 +964,10 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
       if (idx < n) {
         const uint32_t off = idx * 4;
         __builtin_amdgcn_raw_buffer_store_b32(stage[idx], od, off, so, 0);
-        if (nc > 0) __builtin_amdgcn_raw_buffer_store_b32(x.cv[0], oc0, off, so, 0);
-        if (nc > 1) __builtin_amdgcn_raw_buffer_store_b32(x.cv[1], oc1, off, so, 0);
-        if (nc > 2) __builtin_amdgcn_raw_buffer_store_b32(x.cv[2], oc2, off, so, 0);
-        if (nc > 3) __builtin_amdgcn_raw_buffer_store_b32(x.cv[3], oc3, off, so, 0);
+        if (nc > 0) __builtin_amdgcn_raw_buffer_store_b32(cvk(x, 0), oc0, off, so, 0);
+        if (nc > 1) __builtin_amdgcn_raw_buffer_store_b32(cvk(x, 1), oc1, off, so, 0);
+        if (nc > 2) __builtin_amdgcn_raw_buffer_store_b32(cvk(x, 2), oc2, off, so, 0);
+        if (nc > 3) __builtin_amdgcn_raw_buffer_store_b32(cvk(x, 3), oc3, off, so, 0);
       }
     }
     acc += n;
@@ -1012,10 +1005,10 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
           const uint32_t off = pre * 4;
           const int32_t so = (int32_t)(acc * 4);
           __builtin_amdgcn_raw_buffer_store_b32(v, od, off, so, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(x.cv[0], oc0, off, so, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(x.cv[1], oc1, off, so, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(x.cv[2], oc2, off, so, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(x.cv[3], oc3, off, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(cvk(x, 0), oc0, off, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(cvk(x, 1), oc1, off, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(cvk(x, 2), oc2, off, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(cvk(x, 3), oc3, off, so, 0);
           for (int kk = 4; kk < nc; ++kk) a.carry_out[kk][arena + acc + pre] = a.carry_in[kk][x.row];
         }
       }
