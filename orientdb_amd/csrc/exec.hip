@@ -579,8 +579,8 @@ class Executor {
     const bool member = member_src != nullptr;
     DBuf<unsigned long long> medges;
     if (member) {
-      medges = DBuf<unsigned long long>(&pool_, 1);
-      HIP_CHECK(hipMemsetAsync(medges.p, 0, sizeof(unsigned long long), s_));
+      medges = DBuf<unsigned long long>(&pool_, 2);
+      HIP_CHECK(hipMemsetAsync(medges.p, 0, 2 * sizeof(unsigned long long), s_));
     }
     // 1. degree binning + scans (light edges: merge path; heavy rows: chunks). A filtered hop over a
     // sorted adjacency cuts the heavy rows' chunks at bitmap-slice boundaries (LDS-sliced kernel).
@@ -770,16 +770,21 @@ class Executor {
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, sit, soffs.p + 1, (int64_t)o.nseg, s_); });
     HIP_CHECK(hipMemsetAsync(soffs.p, 0, 8, s_));
     // rows emitted by the heavy kernel's segments, all rows, member edges: one host read
-    const uint64_t *words[3] = {soffs.p + nseg_h, soffs.p + o.nseg, member ? (const uint64_t *)medges.p : nullptr};
-    DBuf<uint64_t> wbuf(&pool_, 3);
-    launch_gather_words(words, 3, wbuf.p, s_);
-    HIP_CHECK(hipMemcpyAsync(g_.h_stage, wbuf.p, 3 * 8, hipMemcpyDeviceToHost, s_));
+    const uint64_t *words[4] = {soffs.p + nseg_h, soffs.p + o.nseg, member ? (const uint64_t *)medges.p : nullptr,
+                                member ? (const uint64_t *)medges.p + 1 : nullptr};
+    DBuf<uint64_t> wbuf(&pool_, 4);
+    launch_gather_words(words, 4, wbuf.p, s_);
+    HIP_CHECK(hipMemcpyAsync(g_.h_stage, wbuf.p, 4 * 8, hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipStreamSynchronize(s_));
     const uint64_t nh_n[3] = {g_.h_stage[0], g_.h_stage[1], g_.h_stage[2]};
+    const uint64_t probes = g_.h_stage[3];  // col[] probes of a fused closing check (4 B each, §8(d))
     o.E_member = nh_n[2];
     const uint64_t n = nh_n[1];
-    if (rec_h != SIZE_MAX) tm_.amend_at(rec_h, 4 * EH + outw * nh_n[0]);
-    if (rec_l != SIZE_MAX) tm_.amend_at(rec_l, 8 * R + 4 * EL + outw * (n - nh_n[0]));
+    // the probes are split between the kernels in proportion to their edges (one counter for both)
+    const uint64_t ph = E ? (uint64_t)((double)probes * (double)EH / (double)E) : 0;
+    if (rec_h != SIZE_MAX) tm_.amend_at(rec_h, 4 * EH + outw * nh_n[0] + 4 * ph);
+    if (rec_l != SIZE_MAX) tm_.amend_at(rec_l, 8 * R + 4 * EL + outw * (n - nh_n[0]) + 4 * (probes - ph));
+    kb += 4 * probes;
     o.n = n;
     if (write) kb += 4ull * (carry.size() + 1) * n;
     tm_.end(kb);

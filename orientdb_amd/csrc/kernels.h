@@ -94,7 +94,7 @@ struct ExpandArgs {
   const uint32_t *member_src;
   DAdj member_adj;
   const uint64_t *member_filter;
-  unsigned long long *member_edges;
+  unsigned long long *member_edges;  // [0] Σ |N_member| of checked pairs, [1] col[] probes of the checks
 };
 
 // predicate VM → V-bit bitmap (u64 words); depth = value of $depth

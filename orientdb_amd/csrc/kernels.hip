@@ -388,7 +388,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t arena = a.arena_base + (uint64_t)blockIdx.x * a.arena_cap;
   uint64_t acc = 0;
-  uint64_t medges = 0;
+  uint64_t medges = 0, mprobes = 0;  // member-adjacency edges the check stands for, col[] probes made
   for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
     const uint64_t d0 = t * (uint64_t)T;
     const uint64_t d1 = min(d0 + (uint64_t)T, a.R + a.E);
@@ -487,10 +487,50 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
         bool pass = FILTER ? (!a.filter || bm_test(a.filter, n)) : true;
         if (MEMBER && pass) {
           medges += s_ydeg[lr];
-          pass = (!a.member_filter || bm_test(a.member_filter, n)) && adj_contains(a.member_adj, s_y[lr], n);
+          pass = !a.member_filter || bm_test(a.member_filter, n);
+          if (pass && a.member_adj.n != 1) pass = adj_contains(a.member_adj, s_y[lr], n);
         }
         passmask |= (uint32_t)pass << k;
       }
+    }
+    if (MEMBER && a.member_adj.n == 1) {
+      // closing check n ∈ N(y) for the thread's IPT items at once: the binary searches advance in
+      // lockstep, so each round issues up to IPT independent loads instead of one dependent chain
+      const uint64_t *mrp = a.member_adj.p[0].rp;
+      const uint32_t *mcol = a.member_adj.p[0].col;
+      uint64_t lo[IPT], hi[IPT], end[IPT];
+      uint32_t act = passmask;
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        lo[k] = hi[k] = end[k] = 0;
+        if ((act >> k) & 1u) {
+          const uint32_t y = s_y[lrs[k]];
+          lo[k] = mrp[y];
+          hi[k] = end[k] = mrp[y + 1];
+        }
+      }
+      uint32_t srch = act;
+      while (srch) {
+        mprobes += (uint64_t)__popc(srch);
+        uint32_t x[IPT];
+        uint64_t mid[IPT];
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+          mid[k] = (lo[k] + hi[k]) >> 1;
+          x[k] = ((srch >> k) & 1u) ? mcol[mid[k]] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+          if ((srch >> k) & 1u) {
+            if (x[k] < nb[k]) lo[k] = mid[k] + 1;
+            else hi[k] = mid[k];
+            if (lo[k] >= hi[k]) srch &= ~(1u << k);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < IPT; ++k)
+        if (((act >> k) & 1u) && !(lo[k] < end[k] && mcol[lo[k]] == nb[k])) passmask &= ~(1u << k);
     }
 
     if (!FILTER) {
@@ -542,7 +582,10 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
     acc += s_total;
     __syncthreads();  // LDS reuse by the next tile
   }
-  if (MEMBER) wave_add_u64(a.member_edges, medges);
+  if (MEMBER) {
+    wave_add_u64(a.member_edges, medges);
+    wave_add_u64(a.member_edges + 1, mprobes);
+  }
   if (FILTER && tid == 0) {
     a.seg_count[a.seg_base + blockIdx.x] = (uint32_t)acc;
     a.seg_start[a.seg_base + blockIdx.x] = arena;
@@ -568,7 +611,7 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
   const uint64_t arena = a.arena_base + wid * a.arena_cap;
   const uint32_t *bm32 = reinterpret_cast<const uint32_t *>(a.filter);
   uint64_t acc = 0;
-  uint64_t medges = 0;
+  uint64_t medges = 0, mprobes = 0;
   auto load = [&](const ChunkDesc &d, uint32_t (&q)[NS]) {
     const uint64_t win = d.lo / kChunk * kChunk;
     const uint32_t *col = a.adj.p[d.part].col + win;
@@ -598,7 +641,9 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
     }
     if (MEMBER) {  // the chunk's row has one member source: every lane searches the same sorted list
       const uint32_t y = a.member_src[d.row];
-      medges += (uint64_t)__popc(mask) * adj_degree(a.member_adj, y);
+      const uint64_t ydeg = adj_degree(a.member_adj, y);
+      medges += (uint64_t)__popc(mask) * ydeg;
+      mprobes += (uint64_t)__popc(mask) * (uint64_t)(64 - __builtin_clzll(ydeg | 1));  // ⌈log₂⌉-ish steps
 #pragma unroll
       for (int i = 0; i < NS; ++i)
         if ((mask >> i) & 1u) {
@@ -651,7 +696,10 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
 #pragma unroll
     for (int i = 0; i < NS; ++i) q[i] = qn[i];
   }
-  if (MEMBER) wave_add_u64(a.member_edges, medges);
+  if (MEMBER) {
+    wave_add_u64(a.member_edges, medges);
+    wave_add_u64(a.member_edges + 1, mprobes);
+  }
   if (FILTER && lane == 0) {
     a.seg_count[a.seg_base + wid] = (uint32_t)acc;
     a.seg_start[a.seg_base + wid] = arena;
