@@ -1,4 +1,5 @@
 // capi.cpp — the extern "C" boundary (include/omx/match.h).
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -15,6 +16,11 @@ struct omx_graph {
 struct omx_statement {
   std::unique_ptr<omx::Statement> st;
   std::string text;
+  // the last compiled plan, reused while the graph and the parameters are the same (the reference's
+  // statement cache keeps parsed statements; a plan here is the parse + planner output)
+  uint64_t plan_graph = 0;
+  std::string plan_key;
+  std::unique_ptr<omx::Plan> plan;
 };
 struct omx_comm {
   std::unique_ptr<omx::Transport> t;
@@ -63,6 +69,27 @@ omx::Params make_params(const omx_value *vals, int32_t n) {
     }
   }
   return p;
+}
+// identity of a parameter list (type, position/name, value) for the plan cache
+std::string params_key(const omx_value *vals, int32_t n) {
+  std::string k;
+  for (int32_t i = 0; i < n; ++i) {
+    const omx_value &v = vals[i];
+    k += std::to_string(v.type) + ":" + std::to_string(v.index) + ":" + (v.name ? v.name : "") + "=";
+    switch (v.type) {
+      case OMX_VAL_INT: case OMX_VAL_BOOL: k += std::to_string(v.i); break;
+      case OMX_VAL_DOUBLE: {
+        char b[32];
+        std::snprintf(b, sizeof(b), "%a", v.d);
+        k += b;
+        break;
+      }
+      case OMX_VAL_STRING: k += std::to_string(v.s ? std::strlen(v.s) : 0) + ":" + (v.s ? v.s : ""); break;
+      default: break;
+    }
+    k += ";";
+  }
+  return k;
 }
 }  // namespace
 
@@ -131,9 +158,15 @@ int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, om
     omx_exec_options_init(&o);
     if (opts) o = *opts;
     if (o.shard_world < 1 || o.shard_rank < 0 || o.shard_rank >= o.shard_world) omx::fail(OMX_E_INVALID, "bad shard");
-    omx::Params p = make_params(o.params, o.n_params);
-    auto plan = omx::build_plan(*s->st, *g->g, p, false);
-    *out = omx::execute_plan(*g->g, *plan, o, o.comm ? o.comm->t.get() : nullptr);
+    const std::string key = params_key(o.params, o.n_params);
+    if (!s->plan || s->plan_graph != g->g->uid || s->plan_key != key) {
+      omx::Params p = make_params(o.params, o.n_params);
+      s->plan.reset();
+      s->plan = omx::build_plan(*s->st, *g->g, p, false);
+      s->plan_graph = g->g->uid;
+      s->plan_key = key;
+    }
+    *out = omx::execute_plan(*g->g, *s->plan, o, o.comm ? o.comm->t.get() : nullptr);
   });
 }
 

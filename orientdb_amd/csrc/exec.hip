@@ -380,6 +380,16 @@ class Executor {
   DBuf<uint32_t> bitmap_list(const uint64_t *words, int rank, int world, uint64_t &n, uint32_t lo = 0,
                              uint32_t hi = UINT32_MAX) {
     hi = std::min(hi, g_.V);
+    if (bitmap_list_blocks(nwords_) <= 4096) {  // two launches (≤ 64 M vertices)
+      DBuf<uint32_t> out(&pool_, std::max<uint64_t>(hi > lo ? hi - lo : 0, 1));
+      DBuf<uint32_t> blk(&pool_, bitmap_list_blocks(nwords_));
+      DBuf<uint64_t> cnt1(&pool_, 1);
+      tm_.begin("k_bitmap_to_list");
+      launch_bitmap_list_2k(words, nwords_, g_.V, rank, world, lo, hi, blk.p, out.p, cnt1.p, s_);
+      n = read1(cnt1.p);
+      tm_.end(nwords_ * 8 + n * 4);
+      return out;
+    }
     DBuf<uint32_t> cnt(&pool_, nwords_ + 1);
     DBuf<uint32_t> offs(&pool_, nwords_ + 1);
     tm_.begin("k_bitmap_to_list");
@@ -766,14 +776,10 @@ class Executor {
     }
     // filtered: rows per block segment → total (and dense compaction when required)
     DBuf<uint64_t> soffs(&pool_, o.nseg + 1);
-    hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> sit(o.seg_count.p, CastU64());
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, sit, soffs.p + 1, (int64_t)o.nseg, s_); });
-    HIP_CHECK(hipMemsetAsync(soffs.p, 0, 8, s_));
-    // rows emitted by the heavy kernel's segments, all rows, member edges: one host read
-    const uint64_t *words[4] = {soffs.p + nseg_h, soffs.p + o.nseg, member ? (const uint64_t *)medges.p : nullptr,
-                                member ? (const uint64_t *)medges.p + 1 : nullptr};
+    // segment offsets + rows emitted by the heavy kernel's segments, all rows, member words: one
+    // workgroup, one host read
     DBuf<uint64_t> wbuf(&pool_, 4);
-    launch_gather_words(words, 4, wbuf.p, s_);
+    launch_seg_totals(o.seg_count.p, o.nseg, nseg_h, soffs.p, member ? medges.p : nullptr, wbuf.p, s_);
     HIP_CHECK(hipMemcpyAsync(g_.h_stage, wbuf.p, 4 * 8, hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipStreamSynchronize(s_));
     const uint64_t nh_n[3] = {g_.h_stage[0], g_.h_stage[1], g_.h_stage[2]};

@@ -202,6 +202,8 @@ Graph *graph_create(const omx_graph_desc *d) {
   if (d->n_classes <= 0 || d->n_classes > 256) fail(OMX_E_INVALID, "n_classes must be in [1, 256]");
   if (d->n_vertices > 0 && (!d->vertex_class || !d->rids)) fail(OMX_E_INVALID, "vertex_class and rids required");
   auto g = std::make_unique<Graph>();
+  static std::atomic<uint64_t> next_uid{1};
+  g->uid = next_uid.fetch_add(1);
   g->V = d->n_vertices;
   g->device = d->device;
   uint32_t V = g->V;

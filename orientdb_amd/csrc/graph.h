@@ -112,6 +112,7 @@ struct IndexInfo {
 };
 
 struct Graph {
+  uint64_t uid = 0;  // process-unique id (plan caches key on it, not on the address)
   uint32_t V = 0;
   int device = -1;
   // 1-D partition: the CSR rows held are those of [part_lo, part_hi) (local row pointers); the

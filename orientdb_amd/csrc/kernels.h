@@ -142,6 +142,15 @@ int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool 
 void launch_compact_segments(int ncols, uint32_t *const *in, uint32_t *const *out, const uint64_t *seg_start,
                              const uint32_t *seg_count, const uint64_t *seg_offs, uint32_t nseg, hipStream_t s);
 
+// two launches: the bitmap's vertices in [lo, hi) (and v % world == rank), in order, and their count;
+// blk holds bitmap_list_blocks(nwords) words of scratch
+unsigned bitmap_list_blocks(uint64_t nwords);
+void launch_bitmap_list_2k(const uint64_t *words, uint64_t nwords, uint32_t V, int rank, int world, uint32_t lo,
+                           uint32_t hi, uint32_t *blk, uint32_t *out, uint64_t *count, hipStream_t s);
+// one workgroup: soffs = inclusive prefix of cnt (soffs[0] = 0); out = {soffs[nseg_h], soffs[nseg],
+// member[0], member[1]} (member may be nullptr → 0)
+void launch_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h, uint64_t *soffs,
+                       const unsigned long long *member, uint64_t *out, hipStream_t s);
 // out[i] = *ptrs[i] (nullptr → 0), i < n ≤ 8: several device words for one host read
 void launch_gather_words(const uint64_t *const *ptrs, int n, uint64_t *out, hipStream_t s);
 

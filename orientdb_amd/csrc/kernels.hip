@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <mutex>
 
 #include "common.h"
 #include "devutil.h"
@@ -1141,9 +1142,17 @@ void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStre
 }
 
 int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool member) {
+  // the occupancy query costs a host round trip into the runtime: answer each variant once
+  static int cache[32];
+  static std::mutex cache_m;
+  filter = filter || member;
+  const int key = (int)heavy | (int)single << 1 | (int)filter << 2 | (int)write << 3 | (int)member << 4;
+  {
+    std::lock_guard<std::mutex> lk(cache_m);
+    if (cache[key]) return cache[key];
+  }
   int n = 0;
   hipError_t e;
-  filter = filter || member;
 #define OCC(K, BS) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, K, BS, 0)
   if (heavy) {
     if (member) e = write ? OCC((k_expand_heavy<true, true, true>), kHeavyBlock) : OCC((k_expand_heavy<true, false, true>), kHeavyBlock);
@@ -1158,6 +1167,8 @@ int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool 
   }
 #undef OCC
   if (e != hipSuccess || n < 1) n = 2;
+  std::lock_guard<std::mutex> lk(cache_m);
+  cache[key] = n;
   return n;
 }
 
@@ -1277,6 +1288,99 @@ void launch_route_hash(int ncols, const uint32_t *const *cols, uint64_t R, uint3
   hipLaunchKernelGGL(k_route_hash, dim3(nblocks(R, 256)), dim3(256), 0, s, ncols, cp, R, W, dest,
                      reinterpret_cast<unsigned long long *>(hist));
   KCHECK("k_route_hash");
+}
+
+// ---- one-workgroup scans (few elements; saves the launches of a device-wide scan) ----------------
+
+// the vertices of a bitmap (range/shard restricted) in order, and their count, in two launches:
+// per-block popcounts, then every block adds the counts of the blocks before it (≤ a few hundred
+// words, read in parallel) to its own scan and scatters; the last block writes the total
+constexpr int kListB = 256;
+__global__ __launch_bounds__(kListB) void k_list_counts(const uint64_t *words, uint64_t n, uint32_t V, int rank,
+                                                        int world, uint32_t lo, uint32_t hi, uint32_t *blk) {
+  __shared__ uint32_t s_w[kListB / 64];
+  const uint64_t i = (uint64_t)blockIdx.x * kListB + threadIdx.x;
+  const uint32_t c = i < n ? __popcll(shard_word(words[i], i, V, rank, world, lo, hi)) : 0;
+  uint32_t tot;
+  block_excl_scan<kListB>(c, s_w, &tot);
+  if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(kListB) void k_list_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank,
+                                                         int world, uint32_t lo, uint32_t hi, const uint32_t *blk,
+                                                         uint32_t *out, unsigned long long *count) {
+  __shared__ uint32_t s_w[kListB / 64];
+  __shared__ unsigned long long s_pre[kListB / 64];
+  // prefix of the blocks before this one
+  unsigned long long p = 0;
+  for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kListB) p += blk[b];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) p += __shfl_xor(p, off, 64);
+  if ((threadIdx.x & 63) == 0) s_pre[threadIdx.x >> 6] = p;
+  __syncthreads();
+  unsigned long long pre = 0;
+#pragma unroll
+  for (int w = 0; w < kListB / 64; ++w) pre += s_pre[w];
+  const uint64_t i = (uint64_t)blockIdx.x * kListB + threadIdx.x;
+  uint64_t w = i < n ? shard_word(words[i], i, V, rank, world, lo, hi) : 0;
+  uint32_t tot;
+  uint64_t o = pre + block_excl_scan<kListB>((uint32_t)__popcll(w), s_w, &tot);
+  while (w) {
+    out[o++] = (uint32_t)(i * 64 + __builtin_ctzll(w));
+    w &= w - 1;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *count = pre + tot;
+}
+void launch_bitmap_list_2k(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t lo,
+                           uint32_t hi, uint32_t *blk, uint32_t *out, uint64_t *count, hipStream_t s) {
+  const unsigned g = nblocks(n, kListB);
+  hipLaunchKernelGGL(k_list_counts, dim3(g), dim3(kListB), 0, s, words, n, V, rank, world, lo, hi, blk);
+  KCHECK("k_list_counts");
+  hipLaunchKernelGGL(k_list_scatter, dim3(g), dim3(kListB), 0, s, words, n, V, rank, world, lo, hi, blk, out,
+                     reinterpret_cast<unsigned long long *>(count));
+  KCHECK("k_list_scatter");
+}
+unsigned bitmap_list_blocks(uint64_t nwords) { return nblocks(nwords, kListB); }
+
+// inclusive prefix of the segments' row counts (soffs[0] = 0, soffs[i+1] = Σ_{j<=i}) and the four
+// words a filtered expansion reads back: rows of the first nseg_h segments, all rows, member words
+__global__ __launch_bounds__(1024) void k_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h,
+                                                     uint64_t *soffs, const unsigned long long *member,
+                                                     uint64_t *out) {
+  __shared__ unsigned long long s_w[16];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t per = (nseg + 1023) / 1024;
+  const uint64_t i0 = min(nseg, (uint64_t)threadIdx.x * per), i1 = min(nseg, i0 + per);
+  unsigned long long c = 0;
+  for (uint64_t i = i0; i < i1; ++i) c += cnt[i];
+  unsigned long long incl = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(incl, off, 64);
+    if (lane >= (uint32_t)off) incl += y;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  unsigned long long base = 0;
+  for (uint32_t w = 0; w < wave; ++w) base += s_w[w];
+  unsigned long long run = base + incl - c;
+  if (threadIdx.x == 0) soffs[0] = 0;
+  for (uint64_t i = i0; i < i1; ++i) {
+    run += cnt[i];
+    soffs[i + 1] = run;
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[0] = soffs[nseg_h];
+    out[1] = soffs[nseg];
+    out[2] = member ? member[0] : 0;
+    out[3] = member ? member[1] : 0;
+  }
+}
+void launch_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h, uint64_t *soffs,
+                       const unsigned long long *member, uint64_t *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_seg_totals, dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, out);
+  KCHECK("k_seg_totals");
 }
 
 // ---- small host reads ------------------------------------------------------------------------------
