@@ -6,6 +6,7 @@
 
 #include "common.h"
 #include "devtypes.h"
+#include "kernels.h"
 
 namespace omx {
 
@@ -36,6 +37,12 @@ __device__ __forceinline__ uint64_t adj_degree(const DAdj &a, uint32_t v) {
   uint64_t d = 0;
   for (int p = 0; p < a.n; ++p) d += a.p[p].rp[v + 1] - a.p[p].rp[v];
   return d;
+}
+
+// publish a host mailbox (kernels.h Mail): the payload stores become visible before the sequence word
+__device__ __forceinline__ void mail_post(const Mail &m) {
+  __threadfence_system();
+  __hip_atomic_store(m.p + kMailSeq, m.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // block-wide exclusive scan of one u32 per thread (4 waves); returns the block total in *total

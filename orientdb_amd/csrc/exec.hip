@@ -274,13 +274,34 @@ class Executor {
     DBuf<uint8_t> tmp(&pool_, std::max<size_t>(bytes, 16));
     HIP_CHECK(f((void *)tmp.p, bytes));
   }
+  // the next mailbox a kernel posts to (kernels.h Mail), and the host side of it: spin on the
+  // sequence word; every few thousand spins ask the stream whether it ended (or faulted) without
+  // posting, so a failed launch surfaces as an error rather than a hang
+  Mail mail() { return Mail{g_.h_mail, ++g_.mail_seq}; }
+  const uint64_t *wait_mail() {
+    volatile uint64_t *f = g_.h_mail + kMailSeq;
+    const uint64_t seq = g_.mail_seq;
+    for (uint32_t spins = 1; *f != seq; ++spins) {
+      if (spins % 4096 == 0) {
+        const hipError_t e = hipStreamQuery(s_);
+        if (e == hipErrorNotReady) continue;
+        if (e != hipSuccess) fail(OMX_E_DEVICE, std::string("stream failed: ") + hipGetErrorString(e));
+        if (*f == seq) break;
+        fail(OMX_E_DEVICE, "a device mailbox was not posted");
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return g_.h_mail;
+  }
   template <class T>
   T read1(const T *dptr) {
-    static_assert(sizeof(T) <= sizeof(uint64_t), "read1 reads one word");
-    HIP_CHECK(hipMemcpyAsync(g_.h_stage, dptr, sizeof(T), hipMemcpyDeviceToHost, s_));
-    HIP_CHECK(hipStreamSynchronize(s_));
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "read1 reads one 4- or 8-byte word");
+    launch_post_words(dptr, 1, mail(), s_, (int)sizeof(T));
+    const uint64_t w = wait_mail()[0];
     T v;
-    std::memcpy(&v, g_.h_stage, sizeof(T));
+    if (sizeof(T) == 8) std::memcpy(&v, &w, 8);
+    else { const uint32_t lo = (uint32_t)w; std::memcpy(&v, &lo, sizeof(T)); }
     return v;
   }
 
@@ -383,10 +404,9 @@ class Executor {
     if (bitmap_list_blocks(nwords_) <= 4096) {  // two launches (≤ 64 M vertices)
       DBuf<uint32_t> out(&pool_, std::max<uint64_t>(hi > lo ? hi - lo : 0, 1));
       DBuf<uint32_t> blk(&pool_, bitmap_list_blocks(nwords_));
-      DBuf<uint64_t> cnt1(&pool_, 1);
       tm_.begin("k_bitmap_to_list");
-      launch_bitmap_list_2k(words, nwords_, g_.V, rank, world, lo, hi, blk.p, out.p, cnt1.p, s_);
-      n = read1(cnt1.p);
+      launch_bitmap_list_2k(words, nwords_, g_.V, rank, world, lo, hi, blk.p, out.p, mail(), s_);
+      n = wait_mail()[0];
       tm_.end(nwords_ * 8 + n * 4);
       return out;
     }
@@ -597,29 +617,17 @@ class Executor {
     const bool sliced = filter != nullptr && !member && adj.sorted && sliced_ &&
                         (uint64_t)g_.V <= ((uint64_t)kMaxSlices << slice_shift_);
     const uint32_t P = sliced ? (uint32_t)(((uint64_t)g_.V + (1ull << slice_shift_) - 1) >> slice_shift_) : 1;
-    const uint64_t nchn = sliced ? (uint64_t)P * (R + 1) + 1 : R + 1;
     const DCuts cuts = sliced ? slice_cuts_of(adjs, P) : DCuts{};
-    DBuf<uint64_t> light(&pool_, R + 1), heavy(&pool_, R + 1), loffs(&pool_, R + 1), hoffs(&pool_, R + 1);
-    DBuf<uint32_t> nch(&pool_, nchn);
-    DBuf<uint64_t> choffs(&pool_, nchn);
-    tm_.begin("k_row_split");
-    if (sliced) launch_row_split_sliced(src, R, adj, cuts, heavy_deg_sliced_, P, light.p, heavy.p, nch.p, s_);
-    else launch_row_split(src, R, adj, heavy_deg_, light.p, heavy.p, nch.p, s_);
-    tm_.end(R * (4 + 16ull * adj.n) + (R + 1) * 20);
-    tm_.begin("scan_degrees");
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, light.p, loffs.p, (int64_t)(R + 1), s_); });
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, heavy.p, hoffs.p, (int64_t)(R + 1), s_); });
-    hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> nit(nch.p, CastU64());
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, nit, choffs.p, (int64_t)nchn, s_); });
-    tm_.end((R + 1) * 40);
-    // one host read for the totals (and the slices' chunk bounds)
-    DBuf<uint64_t> meta(&pool_, 4 + P), qb;
-    if (sliced) qb = DBuf<uint64_t>(&pool_, P + 1);
-    launch_expand_meta(loffs.p, hoffs.p, choffs.p, R, nchn, sliced ? P : 0, qb.p, meta.p, s_);
-    HIP_CHECK(hipMemcpyAsync(g_.h_stage, meta.p, (4 + P) * 8, hipMemcpyDeviceToHost, s_));
-    HIP_CHECK(hipStreamSynchronize(s_));
-    const uint64_t EL = g_.h_stage[0], EH = g_.h_stage[1], nchunks = g_.h_stage[2];
-    std::vector<uint64_t> hqb(g_.h_stage + 3, g_.h_stage + 3 + (sliced ? P + 1 : 0));
+    const uint64_t hd = sliced ? heavy_deg_sliced_ : heavy_deg_;
+    // per-tile sums → one-workgroup scan (posts the totals to the host) → per-tile offsets and chunks
+    DBuf<uint64_t> blk(&pool_, (uint64_t)(2 + P) * bin_tiles(R)), qb(&pool_, P + 1), loffs(&pool_, R + 1);
+    tm_.begin("k_bin_rows");
+    launch_bin_count(sliced, src, R, adj, cuts, hd, P, blk.p, s_);
+    launch_bin_scan(blk.p, R, P, qb.p, mail(), s_);
+    const uint64_t *m = wait_mail();
+    const uint64_t EL = m[0], EH = m[1], nchunks = m[2];
+    std::vector<uint64_t> hqb(m + 3, m + 4 + P);
+    tm_.end(R * (4 + 16ull * adj.n + (sliced ? 4ull * (P - 1) * adj.n : 0)));
     const uint64_t E = EL + EH;
     o.E = E;
     if (E == 0) return o;
@@ -633,17 +641,11 @@ class Executor {
     }
     DBuf<ChunkDesc> chunks;
     DBuf<SliceChunk> schunks;
-    if (nchunks) {
-      tm_.begin("k_fill_chunks");
-      if (sliced) {
-        schunks = DBuf<SliceChunk>(&pool_, nchunks);
-        launch_fill_chunks_sliced(src, R, adj, cuts, P, choffs.p, hoffs.p, schunks.p, s_);
-      } else {
-        chunks = DBuf<ChunkDesc>(&pool_, nchunks);
-        launch_fill_chunks(src, R, adj, choffs.p, hoffs.p, chunks.p, s_);
-      }
-      tm_.end(nchunks * (sliced ? sizeof(SliceChunk) : sizeof(ChunkDesc)));
-    }
+    if (sliced) schunks = DBuf<SliceChunk>(&pool_, std::max<uint64_t>(nchunks, 1));
+    else chunks = DBuf<ChunkDesc>(&pool_, std::max<uint64_t>(nchunks, 1));
+    tm_.begin("k_bin_fill");
+    launch_bin_fill(sliced, src, R, adj, cuts, hd, P, blk.p, qb.p, loffs.p, chunks.p, schunks.p, s_);
+    tm_.end(R * (4 + 16ull * adj.n + 8) + nchunks * (sliced ? sizeof(SliceChunk) : sizeof(ChunkDesc)));
     const uint64_t ntiles = EL ? (R + EL + kExpandTile - 1) / kExpandTile : 0;
     DBuf<uint64_t> part;
     if (ntiles) {
@@ -705,7 +707,6 @@ class Executor {
     a.chunks = chunks.p;
     a.schunks = schunks.p;
     a.nchunks = nchunks;
-    a.hoffs = hoffs.p;
     a.dense_base = EH;
     if (member) {
       a.member_src = member_src;
@@ -778,12 +779,10 @@ class Executor {
     DBuf<uint64_t> soffs(&pool_, o.nseg + 1);
     // segment offsets + rows emitted by the heavy kernel's segments, all rows, member words: one
     // workgroup, one host read
-    DBuf<uint64_t> wbuf(&pool_, 4);
-    launch_seg_totals(o.seg_count.p, o.nseg, nseg_h, soffs.p, member ? medges.p : nullptr, wbuf.p, s_);
-    HIP_CHECK(hipMemcpyAsync(g_.h_stage, wbuf.p, 4 * 8, hipMemcpyDeviceToHost, s_));
-    HIP_CHECK(hipStreamSynchronize(s_));
-    const uint64_t nh_n[3] = {g_.h_stage[0], g_.h_stage[1], g_.h_stage[2]};
-    const uint64_t probes = g_.h_stage[3];  // col[] probes of a fused closing check (4 B each, §8(d))
+    launch_seg_totals(o.seg_count.p, o.nseg, nseg_h, soffs.p, member ? medges.p : nullptr, mail(), s_);
+    const uint64_t *mt = wait_mail();
+    const uint64_t nh_n[3] = {mt[0], mt[1], mt[2]};
+    const uint64_t probes = mt[3];  // col[] probes of a fused closing check (4 B each, §8(d))
     o.E_member = nh_n[2];
     const uint64_t n = nh_n[1];
     // the probes are split between the kernels in proportion to their edges (one counter for both)
@@ -1031,9 +1030,8 @@ class Executor {
         launch_bfs_prep(fr.p, vis.p, V, while_bm, expand, adj, stats.p, cus(), s_);
         tm_.end(8ull * V);
         if (!expand) break;
-        unsigned long long h[3];
-        HIP_CHECK(hipMemcpyAsync(h, stats.p, sizeof(h), hipMemcpyDeviceToHost, s_));
-        HIP_CHECK(hipStreamSynchronize(s_));
+        launch_post_words(stats.p, 3, mail(), s_);
+        const uint64_t *h = wait_mail();
         tm_.amend(8ull * V + 24ull * h[2]);  // frontier scan + visited and row_ptr pair of the active vertices
         if (h[2] == 0) break;
         edges_ += h[0];

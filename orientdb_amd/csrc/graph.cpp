@@ -7,6 +7,7 @@
 #include <cstring>
 #include <thread>
 
+#include "kernels.h"
 #include "sql.h"
 
 namespace omx {
@@ -85,6 +86,7 @@ Graph::~Graph() {
     if (stream) (void)hipStreamDestroy(stream);
     if (stream2) (void)hipStreamDestroy(stream2);
     if (h_stage) (void)hipHostFree(h_stage);
+    if (h_mail) (void)hipHostFree(h_mail);
     for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
   }
 }
@@ -331,6 +333,8 @@ Graph *graph_create(const omx_graph_desc *d) {
     HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking));
     HIP_CHECK(hipHostMalloc((void **)&g->h_stage, Graph::kStageWords * sizeof(uint64_t), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void **)&g->h_mail, kMailWords * sizeof(uint64_t), hipHostMallocCoherent));
+    std::memset(g->h_mail, 0, kMailWords * sizeof(uint64_t));
     uint64_t &acc = g->device_bytes;
     g->d_vclass = upload(d->vertex_class, V, acc);
     g->d_rids = upload(d->rids, V, acc);

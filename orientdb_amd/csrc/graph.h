@@ -133,6 +133,8 @@ struct Graph {
   DevicePool pool;
   uint64_t *h_stage = nullptr;             // pinned host words for small device→host reads
   static constexpr int kStageWords = 512;
+  uint64_t *h_mail = nullptr;              // fine-grained pinned host mailbox (kernels.h Mail)
+  uint64_t mail_seq = 0;
   std::vector<hipEvent_t> event_pool;      // reusable timing events (OMX_FLAG_KERNEL_TIMING)
 
   // row pointers indexed by a global (owned) vertex id; dir 0 = out, 1 = in

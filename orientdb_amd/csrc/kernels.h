@@ -54,6 +54,16 @@ struct SliceChunk {
 };
 static_assert(sizeof(SliceChunk) == 16, "SliceChunk is one dwordx4");
 
+// host mailbox: Graph::h_mail is fine-grained pinned host memory; a kernel writes its payload words,
+// fences at system scope and then writes `seq` into the last word, which the host polls (no copy
+// kernel, no stream synchronisation on the small host reads between launches)
+constexpr int kMailWords = 64;
+constexpr int kMailSeq = kMailWords - 1;
+struct Mail {
+  uint64_t *p;
+  uint64_t seq;
+};
+
 struct ChunkDesc {
   uint64_t lo, hi;  // absolute col[] range of the chunk inside part `part` (one kChunk-aligned window)
   uint64_t dense;   // output index of edge lo in the dense (unfiltered) layout
@@ -86,7 +96,6 @@ struct ExpandArgs {
   const ChunkDesc *chunks;
   const SliceChunk *schunks;  // sliced kernel
   uint64_t nchunks;
-  const uint64_t *hoffs;    // [R+1] exclusive prefix of the heavy rows' full degree (dense mode)
   // fused closing check of a cyclic pattern (sorted-adjacency intersection): neighbour n of row r is
   // kept only if n ∈ N_member(member_src[r]); member_edges accumulates Σ |N_member(member_src[r])| over
   // the (row, n) pairs that reach the check, i.e. the edges the unfused check step traverses.
@@ -113,25 +122,25 @@ void launch_route_hash(int ncols, const uint32_t *const *cols, uint64_t R, uint3
                        hipStream_t s);
 
 void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t *deg, hipStream_t s);
-// per row: light degree (0 for heavy rows), heavy degree (0 for light rows), number of heavy chunks
-void launch_row_split(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint64_t *light,
-                      uint64_t *heavy, uint32_t *nchunks, hipStream_t s);
-void launch_fill_chunks(const uint32_t *src, uint64_t R, const DAdj &adj, const uint64_t *choffs,
-                        const uint64_t *hoffs, ChunkDesc *out, hipStream_t s);
 void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part,
                          hipStream_t s);
-// sliced chunks: nchq[q·(R+1) + r] = chunks of heavy row r inside slice q (layout slice-major so one
-// scan gives each slice a contiguous chunk range); light/heavy degrees as launch_row_split
 // rows [vlo, vhi) (the owned rows of a partition; rp indexed by global vertex id)
 void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t vlo, uint32_t vhi, uint32_t nslices,
                        uint32_t shift, uint32_t *cuts, hipStream_t s);
-void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint64_t heavy_deg,
-                             uint32_t nslices, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s);
-void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint32_t nslices,
-                               const uint64_t *choffs, const uint64_t *hoffs, SliceChunk *out, hipStream_t s);
-// meta = {loffs[R], hoffs[R], choffs[nchn-1], qb[0..P]}; qb[q] = choffs[q·(R+1)] (nslices = 0: unsliced)
-void launch_expand_meta(const uint64_t *loffs, const uint64_t *hoffs, const uint64_t *choffs, uint64_t R,
-                        uint64_t nchn, uint32_t nslices, uint64_t *qb, uint64_t *meta, hipStream_t s);
+// Degree binning of R rows in three launches (rows in tiles of kBinBlock): per tile, the sums of the
+// rows' light degrees, heavy degrees and heavy chunks per slice (blk[k·nb + b], k = 0 light, 1 heavy,
+// 2 + q chunks of slice q); one workgroup scans them (qb[q] = first chunk of slice q, qb[P] = chunks;
+// mail = {Σ light, Σ heavy, chunks, qb[0..P]}); then every tile redoes its rows and writes loffs
+// (light edge offsets, [R+1]) and the heavy rows' chunks. Unsliced: P = 1, kChunk-aligned ChunkDesc
+// windows; sliced: SliceChunk pieces cut at the slice boundaries (cuts).
+constexpr int kBinBlock = 256;
+inline unsigned bin_tiles(uint64_t R) { return (unsigned)((R + 1 + kBinBlock - 1) / kBinBlock); }
+void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
+                      uint64_t heavy_deg, uint32_t P, uint64_t *blk, hipStream_t s);
+void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s);
+void launch_bin_fill(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
+                     uint64_t heavy_deg, uint32_t P, const uint64_t *blk, const uint64_t *qb, uint64_t *loffs,
+                     ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s);
 // grid = sa.wg0[P] workgroups (one per CU); wave w appends to arena_base + w·arena_cap and reports
 // seg_count/seg_start[seg_base + w]
 void launch_expand_heavy_sliced(const ExpandArgs &a, const SliceArgs &sa, unsigned grid, bool write, hipStream_t s);
@@ -146,13 +155,13 @@ void launch_compact_segments(int ncols, uint32_t *const *in, uint32_t *const *ou
 // blk holds bitmap_list_blocks(nwords) words of scratch
 unsigned bitmap_list_blocks(uint64_t nwords);
 void launch_bitmap_list_2k(const uint64_t *words, uint64_t nwords, uint32_t V, int rank, int world, uint32_t lo,
-                           uint32_t hi, uint32_t *blk, uint32_t *out, uint64_t *count, hipStream_t s);
-// one workgroup: soffs = inclusive prefix of cnt (soffs[0] = 0); out = {soffs[nseg_h], soffs[nseg],
+                           uint32_t hi, uint32_t *blk, uint32_t *out, const Mail &count, hipStream_t s);
+// one workgroup: soffs = inclusive prefix of cnt (soffs[0] = 0); mail = {soffs[nseg_h], soffs[nseg],
 // member[0], member[1]} (member may be nullptr → 0)
 void launch_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h, uint64_t *soffs,
-                       const unsigned long long *member, uint64_t *out, hipStream_t s);
-// out[i] = *ptrs[i] (nullptr → 0), i < n ≤ 8: several device words for one host read
-void launch_gather_words(const uint64_t *const *ptrs, int n, uint64_t *out, hipStream_t s);
+                       const unsigned long long *member, const Mail &mail, hipStream_t s);
+// mail[i] = word i at p (words of `bytes` = 4 or 8, zero-extended), i < n < kMailSeq
+void launch_post_words(const void *p, int n, const Mail &mail, hipStream_t s, int bytes = 8);
 
 void launch_check(const uint32_t *src, const uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
                   uint8_t *flags, hipStream_t s);

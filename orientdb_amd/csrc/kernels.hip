@@ -268,65 +268,6 @@ void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_
   KCHECK("k_row_degree");
 }
 
-// degree binning: light rows go to the merge-path kernel, heavy rows (≥ kHeavyDeg) to chunks
-__global__ void k_row_split(const uint32_t *src, uint64_t R, DAdj adj, uint64_t heavy_deg, uint64_t *light,
-                            uint64_t *heavy, uint32_t *nch) {
-  uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > R) return;
-  if (r == R) {
-    light[R] = 0;
-    heavy[R] = 0;
-    nch[R] = 0;
-    return;
-  }
-  const uint32_t v = src[r];
-  const uint64_t d = adj_degree(adj, v);
-  if (d >= heavy_deg) {
-    uint32_t c = 0;
-    for (int p = 0; p < adj.n; ++p) {
-      const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
-      if (e > b) c += (uint32_t)((e - 1) / kChunk - b / kChunk + 1);
-    }
-    light[r] = 0;
-    heavy[r] = d;
-    nch[r] = c;
-  } else {
-    light[r] = d;
-    heavy[r] = 0;
-    nch[r] = 0;
-  }
-}
-void launch_row_split(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t heavy_deg, uint64_t *light,
-                      uint64_t *heavy, uint32_t *nch, hipStream_t s) {
-  hipLaunchKernelGGL(k_row_split, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, R, adj, heavy_deg, light, heavy,
-                     nch);
-  KCHECK("k_row_split");
-}
-
-__global__ void k_fill_chunks(const uint32_t *src, uint64_t R, DAdj adj, const uint64_t *choffs, const uint64_t *hoffs,
-                              ChunkDesc *out) {
-  uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  uint64_t o = choffs[r];
-  if (choffs[r + 1] == o) return;
-  const uint32_t v = src[r];
-  uint64_t pos = hoffs[r];  // dense output index of the row's first edge (parts in order)
-  for (int p = 0; p < adj.n; ++p) {
-    const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
-    for (uint64_t w = b / kChunk * kChunk; e > b && w < e; w += kChunk) {  // an empty part has no chunk
-      const uint64_t lo = w > b ? w : b, hi = w + kChunk < e ? w + kChunk : e;
-      out[o++] = ChunkDesc{lo, hi, pos + (lo - b), (uint32_t)r, (uint32_t)p};
-    }
-    pos += e - b;
-  }
-}
-void launch_fill_chunks(const uint32_t *src, uint64_t R, const DAdj &adj, const uint64_t *choffs,
-                        const uint64_t *hoffs, ChunkDesc *out, hipStream_t s) {
-  if (!R) return;
-  hipLaunchKernelGGL(k_fill_chunks, dim3(nblocks(R, 256)), dim3(256), 0, s, src, R, adj, choffs, hoffs, out);
-  KCHECK("k_fill_chunks");
-}
-
 // merge path over A = row ends (offs[r+1]) and B = edge indices 0..E-1; a row end is consumed
 // before edge j when offs[r+1] <= j.
 __global__ void k_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part) {
@@ -779,69 +720,6 @@ __device__ __forceinline__ void load_cuts(const uint32_t *c, uint32_t v, uint32_
   for (int q = 1; q <= MAXP; ++q) cut[q] = (uint32_t)q < P ? c[(uint64_t)v * (P - 1) + q - 1] : n;
 }
 
-template <int MAXP>
-__global__ __launch_bounds__(256) void k_row_split_sliced(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
-                                                          uint64_t heavy_deg, uint32_t P, uint64_t *light,
-                                                          uint64_t *heavy, uint32_t *nchq) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > R) return;
-  const uint64_t stride = R + 1;
-  if (r == R) {
-    light[R] = 0;
-    heavy[R] = 0;
-    for (uint32_t q = 0; q < P; ++q) nchq[q * stride + R] = 0;
-    nchq[P * stride] = 0;
-    return;
-  }
-  const uint32_t v = src[r];
-  const uint64_t d = adj_degree(adj, v);
-  if (d < heavy_deg) {
-    light[r] = d;
-    heavy[r] = 0;
-    for (uint32_t q = 0; q < P; ++q) nchq[q * stride + r] = 0;
-    return;
-  }
-  light[r] = 0;
-  heavy[r] = d;
-  uint32_t cnt[MAXP];
-#pragma unroll
-  for (int q = 0; q < MAXP; ++q) cnt[q] = 0;
-  for (int p = 0; p < adj.n; ++p) {
-    uint32_t cut[MAXP + 1];
-    load_cuts<MAXP>(cuts.c[p], v, (uint32_t)(adj.p[p].rp[v + 1] - adj.p[p].rp[v]), P, cut);
-#pragma unroll
-    for (int q = 0; q < MAXP; ++q) cnt[q] += chunk_pieces(cut[q], cut[q + 1]);
-  }
-#pragma unroll
-  for (int q = 0; q < MAXP; ++q)
-    if ((uint32_t)q < P) nchq[q * stride + r] = cnt[q];
-}
-
-template <int MAXP>
-__global__ __launch_bounds__(256) void k_fill_chunks_sliced(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
-                                                            uint32_t P, const uint64_t *choffs, const uint64_t *hoffs,
-                                                            SliceChunk *out) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R || hoffs[r + 1] == hoffs[r]) return;  // light row
-  const uint64_t stride = R + 1;
-  const uint32_t v = src[r];
-  uint64_t o[MAXP];
-#pragma unroll
-  for (int q = 0; q < MAXP; ++q) o[q] = (uint32_t)q < P ? choffs[q * stride + r] : 0;
-  for (int p = 0; p < adj.n; ++p) {
-    const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
-    uint32_t cut[MAXP + 1];
-    load_cuts<MAXP>(cuts.c[p], v, (uint32_t)(e - b), P, cut);
-#pragma unroll
-    for (int q = 0; q < MAXP; ++q) {
-      for (uint32_t clo = cut[q]; clo < cut[q + 1]; clo += kChunk) {  // as chunk_pieces
-        const uint32_t chi = clo + kChunk < cut[q + 1] ? clo + kChunk : cut[q + 1];
-        out[o[q]++] = SliceChunk{b + clo, (uint32_t)r, (uint16_t)(chi - clo), (uint16_t)p};
-      }
-    }
-  }
-}
-
 #define OMX_BY_MAXP(P, CALL) \
   do {                       \
     if ((P) <= 1) CALL(1);   \
@@ -861,45 +739,210 @@ void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t vlo, ui
   KCHECK("k_build_cuts");
 }
 
-void launch_row_split_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint64_t heavy_deg,
-                             uint32_t nslices, uint64_t *light, uint64_t *heavy, uint32_t *nchq, hipStream_t s) {
-#define OMX_RS(M) hipLaunchKernelGGL(k_row_split_sliced<M>, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, R, adj, \
-                                     cuts, heavy_deg, nslices, light, heavy, nchq)
-  OMX_BY_MAXP(nslices, OMX_RS);
-#undef OMX_RS
-  KCHECK("k_row_split_sliced");
-}
-
-void launch_fill_chunks_sliced(const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts, uint32_t nslices,
-                               const uint64_t *choffs, const uint64_t *hoffs, SliceChunk *out, hipStream_t s) {
-  if (!R) return;
-#define OMX_FC(M) hipLaunchKernelGGL(k_fill_chunks_sliced<M>, dim3(nblocks(R, 256)), dim3(256), 0, s, src, R, adj, \
-                                     cuts, nslices, choffs, hoffs, out)
-  OMX_BY_MAXP(nslices, OMX_FC);
-#undef OMX_FC
-  KCHECK("k_fill_chunks_sliced");
-}
-
-// the totals one host read needs after the binning scans: meta = {Σ light, Σ heavy, chunks,
-// qb[0..P]} and qb[q] = first chunk of slice q (P = 0: unsliced)
-__global__ void k_expand_meta(const uint64_t *loffs, const uint64_t *hoffs, const uint64_t *choffs, uint64_t R,
-                              uint64_t nchn, uint32_t P, uint64_t *qb, uint64_t *meta) {
-  const uint32_t t = threadIdx.x;
-  if (t == 0) {
-    meta[0] = loffs[R];
-    meta[1] = hoffs[R];
-    meta[2] = choffs[nchn - 1];
+// ---- degree binning ---------------------------------------------------------------------------------
+// x[0] = light degree, x[1] = heavy degree, x[2 + q] = heavy chunks in slice q of row r (all 0 for
+// r ≥ R). Unsliced (MAXP = 1): chunks are the kChunk-aligned windows the row's parts touch.
+template <bool SLICED, int MAXP>
+__device__ __forceinline__ void row_bins(const uint32_t *src, uint64_t r, uint64_t R, const DAdj &adj,
+                                         const DCuts &cuts, uint64_t heavy_deg, uint32_t P,
+                                         uint64_t (&x)[2 + MAXP]) {
+#pragma unroll
+  for (int k = 0; k < 2 + MAXP; ++k) x[k] = 0;
+  if (r >= R) return;
+  const uint32_t v = src[r];
+  const uint64_t d = adj_degree(adj, v);
+  if (d < heavy_deg) {
+    x[0] = d;
+    return;
   }
-  if (P && t <= P) {
-    const uint64_t x = choffs[(uint64_t)t * (R + 1)];
-    qb[t] = x;
-    meta[3 + t] = x;
+  x[1] = d;
+  for (int p = 0; p < adj.n; ++p) {
+    const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
+    if (SLICED) {
+      uint32_t cut[MAXP + 1];
+      load_cuts<MAXP>(cuts.c[p], v, (uint32_t)(e - b), P, cut);
+#pragma unroll
+      for (int q = 0; q < MAXP; ++q) x[2 + q] += chunk_pieces(cut[q], cut[q + 1]);
+    } else if (e > b) {
+      x[2] += (e - 1) / kChunk - b / kChunk + 1;
+    }
   }
 }
-void launch_expand_meta(const uint64_t *loffs, const uint64_t *hoffs, const uint64_t *choffs, uint64_t R,
-                        uint64_t nchn, uint32_t nslices, uint64_t *qb, uint64_t *meta, hipStream_t s) {
-  hipLaunchKernelGGL(k_expand_meta, dim3(1), dim3(64), 0, s, loffs, hoffs, choffs, R, nchn, nslices, qb, meta);
-  KCHECK("k_expand_meta");
+
+// block-wide exclusive scans of K u64 values per thread in one pass; x becomes exclusive, tot the sums
+template <int B, int K>
+__device__ __forceinline__ void block_excl_scan_k(uint64_t (&x)[K], uint64_t (&tot)[K], uint64_t *s_w) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t incl[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    incl[k] = x[k];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t y = __shfl_up(incl[k], off, 64);
+      if (lane >= (uint32_t)off) incl[k] += y;
+    }
+    if (lane == 63) s_w[k * (B / 64) + wave] = incl[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    uint64_t woff = 0, t = 0;
+#pragma unroll
+    for (int w = 0; w < B / 64; ++w) {
+      const uint64_t y = s_w[k * (B / 64) + w];
+      woff += w < (int)wave ? y : 0;
+      t += y;
+    }
+    tot[k] = t;
+    x[k] = woff + incl[k] - x[k];
+  }
+}
+
+template <bool SLICED, int MAXP>
+__global__ __launch_bounds__(kBinBlock) void k_bin_count(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
+                                                          uint64_t heavy_deg, uint32_t P, uint64_t *blk) {
+  constexpr int K = 2 + MAXP;
+  __shared__ uint64_t s_w[K * (kBinBlock / 64)];
+  const uint64_t r = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x;
+  uint64_t x[K], tot[K];
+  row_bins<SLICED, MAXP>(src, r, R, adj, cuts, heavy_deg, P, x);
+  block_excl_scan_k<kBinBlock, K>(x, tot, s_w);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if ((uint32_t)k < 2 + P) blk[(uint64_t)k * gridDim.x + blockIdx.x] = tot[k];
+  }
+}
+
+// one workgroup: exclusive scan of every key's tile sums in place, the slices' chunk bounds and the mail
+__global__ __launch_bounds__(1024) void k_bin_scan(uint64_t *blk, uint32_t nb, uint32_t P, uint64_t *qb, Mail mail) {
+  __shared__ unsigned long long s_w[16];
+  __shared__ uint64_t s_tot[2 + kMaxSlices];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t per = (nb + 1023) / 1024;
+  const uint32_t i0 = min(nb, threadIdx.x * per), i1 = min(nb, i0 + per);
+  for (uint32_t k = 0; k < 2 + P; ++k) {
+    uint64_t *a = blk + (uint64_t)k * nb;
+    unsigned long long c = 0;
+    for (uint32_t i = i0; i < i1; ++i) c += a[i];
+    unsigned long long incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned long long y = __shfl_up(incl, off, 64);
+      if (lane >= (uint32_t)off) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    unsigned long long run = 0, tot = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+      run += w < wave ? s_w[w] : 0;
+      tot += s_w[w];
+    }
+    run += incl - c;
+    for (uint32_t i = i0; i < i1; ++i) {
+      const uint64_t y = a[i];
+      a[i] = run;
+      run += y;
+    }
+    if (threadIdx.x == 0) s_tot[k] = tot;
+    __syncthreads();  // s_w is reused by the next key
+  }
+  if (threadIdx.x == 0) {
+    uint64_t q0 = 0;
+    mail.p[0] = s_tot[0];
+    mail.p[1] = s_tot[1];
+    for (uint32_t q = 0; q < P; ++q) {
+      qb[q] = q0;
+      mail.p[3 + q] = q0;
+      q0 += s_tot[2 + q];
+    }
+    qb[P] = q0;
+    mail.p[3 + P] = q0;
+    mail.p[2] = q0;
+    mail_post(mail);
+  }
+}
+
+template <bool SLICED, int MAXP>
+__global__ __launch_bounds__(kBinBlock) void k_bin_fill(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
+                                                         uint64_t heavy_deg, uint32_t P, const uint64_t *blk,
+                                                         const uint64_t *qb, uint64_t *loffs, ChunkDesc *chunks,
+                                                         SliceChunk *schunks) {
+  constexpr int K = 2 + MAXP;
+  __shared__ uint64_t s_w[K * (kBinBlock / 64)];
+  const uint64_t r = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x;
+  const uint32_t nb = gridDim.x;
+  uint64_t x[K], tot[K];
+  row_bins<SLICED, MAXP>(src, r, R, adj, cuts, heavy_deg, P, x);
+  const uint64_t heavy = x[1];
+  block_excl_scan_k<kBinBlock, K>(x, tot, s_w);
+  if (r > R) return;
+  loffs[r] = x[0] + blk[blockIdx.x];
+  if (!heavy) return;
+  const uint32_t v = src[r];
+  if (!SLICED) {
+    uint64_t o = x[2] + blk[2ull * nb + blockIdx.x];
+    uint64_t pos = x[1] + blk[(uint64_t)nb + blockIdx.x];  // dense output index of the row's first edge
+    for (int p = 0; p < adj.n; ++p) {
+      const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
+      for (uint64_t w = b / kChunk * kChunk; e > b && w < e; w += kChunk) {  // an empty part has no chunk
+        const uint64_t lo = w > b ? w : b, hi = w + kChunk < e ? w + kChunk : e;
+        chunks[o++] = ChunkDesc{lo, hi, pos + (lo - b), (uint32_t)r, (uint32_t)p};
+      }
+      pos += e - b;
+    }
+    return;
+  }
+  uint64_t o[MAXP];
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q)
+    o[q] = (uint32_t)q < P ? x[2 + q] + blk[(2ull + q) * nb + blockIdx.x] + qb[q] : 0;
+  for (int p = 0; p < adj.n; ++p) {
+    const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
+    uint32_t cut[MAXP + 1];
+    load_cuts<MAXP>(cuts.c[p], v, (uint32_t)(e - b), P, cut);
+#pragma unroll
+    for (int q = 0; q < MAXP; ++q) {
+      for (uint32_t clo = cut[q]; clo < cut[q + 1]; clo += kChunk) {  // as chunk_pieces
+        const uint32_t chi = clo + kChunk < cut[q + 1] ? clo + kChunk : cut[q + 1];
+        schunks[o[q]++] = SliceChunk{b + clo, (uint32_t)r, (uint16_t)(chi - clo), (uint16_t)p};
+      }
+    }
+  }
+}
+
+void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
+                      uint64_t heavy_deg, uint32_t P, uint64_t *blk, hipStream_t s) {
+  const unsigned nb = bin_tiles(R);
+  if (!sliced) {
+    hipLaunchKernelGGL((k_bin_count<false, 1>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, heavy_deg, 1u, blk);
+  } else {
+#define OMX_BN(M) hipLaunchKernelGGL((k_bin_count<true, M>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, \
+                                     heavy_deg, P, blk)
+    OMX_BY_MAXP(P, OMX_BN);
+#undef OMX_BN
+  }
+  KCHECK("k_bin_count");
+}
+void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s) {
+  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, blk, bin_tiles(R), P, qb, mail);
+  KCHECK("k_bin_scan");
+}
+void launch_bin_fill(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
+                     uint64_t heavy_deg, uint32_t P, const uint64_t *blk, const uint64_t *qb, uint64_t *loffs,
+                     ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s) {
+  const unsigned nb = bin_tiles(R);
+  if (!sliced) {
+    hipLaunchKernelGGL((k_bin_fill<false, 1>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, heavy_deg, 1u, blk,
+                       qb, loffs, chunks, schunks);
+  } else {
+#define OMX_BF(M) hipLaunchKernelGGL((k_bin_fill<true, M>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, \
+                                     heavy_deg, P, blk, qb, loffs, chunks, schunks)
+    OMX_BY_MAXP(P, OMX_BF);
+#undef OMX_BF
+  }
+  KCHECK("k_bin_fill");
 }
 
 // Workgroups [wg0[q], wg0[q+1]) own slice q (the host sizes each range by the slice's chunk count);
@@ -1307,7 +1350,7 @@ __global__ __launch_bounds__(kListB) void k_list_counts(const uint64_t *words, u
 }
 __global__ __launch_bounds__(kListB) void k_list_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank,
                                                          int world, uint32_t lo, uint32_t hi, const uint32_t *blk,
-                                                         uint32_t *out, unsigned long long *count) {
+                                                         uint32_t *out, Mail mail) {
   __shared__ uint32_t s_w[kListB / 64];
   __shared__ unsigned long long s_pre[kListB / 64];
   // prefix of the blocks before this one
@@ -1328,15 +1371,17 @@ __global__ __launch_bounds__(kListB) void k_list_scatter(const uint64_t *words, 
     out[o++] = (uint32_t)(i * 64 + __builtin_ctzll(w));
     w &= w - 1;
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *count = pre + tot;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the host only needs the count
+    mail.p[0] = pre + tot;
+    mail_post(mail);
+  }
 }
 void launch_bitmap_list_2k(const uint64_t *words, uint64_t n, uint32_t V, int rank, int world, uint32_t lo,
-                           uint32_t hi, uint32_t *blk, uint32_t *out, uint64_t *count, hipStream_t s) {
+                           uint32_t hi, uint32_t *blk, uint32_t *out, const Mail &mail, hipStream_t s) {
   const unsigned g = nblocks(n, kListB);
   hipLaunchKernelGGL(k_list_counts, dim3(g), dim3(kListB), 0, s, words, n, V, rank, world, lo, hi, blk);
   KCHECK("k_list_counts");
-  hipLaunchKernelGGL(k_list_scatter, dim3(g), dim3(kListB), 0, s, words, n, V, rank, world, lo, hi, blk, out,
-                     reinterpret_cast<unsigned long long *>(count));
+  hipLaunchKernelGGL(k_list_scatter, dim3(g), dim3(kListB), 0, s, words, n, V, rank, world, lo, hi, blk, out, mail);
   KCHECK("k_list_scatter");
 }
 unsigned bitmap_list_blocks(uint64_t nwords) { return nblocks(nwords, kListB); }
@@ -1345,7 +1390,7 @@ unsigned bitmap_list_blocks(uint64_t nwords) { return nblocks(nwords, kListB); }
 // words a filtered expansion reads back: rows of the first nseg_h segments, all rows, member words
 __global__ __launch_bounds__(1024) void k_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h,
                                                      uint64_t *soffs, const unsigned long long *member,
-                                                     uint64_t *out) {
+                                                     Mail mail) {
   __shared__ unsigned long long s_w[16];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t per = (nseg + 1023) / 1024;
@@ -1371,31 +1416,28 @@ __global__ __launch_bounds__(1024) void k_seg_totals(const uint32_t *cnt, uint64
   __threadfence_block();
   __syncthreads();
   if (threadIdx.x == 0) {
-    out[0] = soffs[nseg_h];
-    out[1] = soffs[nseg];
-    out[2] = member ? member[0] : 0;
-    out[3] = member ? member[1] : 0;
+    mail.p[0] = soffs[nseg_h];
+    mail.p[1] = soffs[nseg];
+    mail.p[2] = member ? member[0] : 0;
+    mail.p[3] = member ? member[1] : 0;
+    mail_post(mail);
   }
 }
 void launch_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h, uint64_t *soffs,
-                       const unsigned long long *member, uint64_t *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_seg_totals, dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, out);
+                       const unsigned long long *member, const Mail &mail, hipStream_t s) {
+  hipLaunchKernelGGL(k_seg_totals, dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, mail);
   KCHECK("k_seg_totals");
 }
 
 // ---- small host reads ------------------------------------------------------------------------------
-struct WordPtrs {
-  const unsigned long long *p[8];
-};
-__global__ void k_gather_words(WordPtrs w, int n, unsigned long long *out) {
-  const int i = threadIdx.x;
-  if (i < n) out[i] = w.p[i] ? *w.p[i] : 0ull;
+__global__ void k_post_words(const void *p, int n, int bytes, Mail mail) {
+  for (int i = 0; i < n; ++i) mail.p[i] = bytes == 8 ? ((const uint64_t *)p)[i] : (uint64_t)((const uint32_t *)p)[i];
+  mail_post(mail);
 }
-void launch_gather_words(const uint64_t *const *ptrs, int n, uint64_t *out, hipStream_t s) {
-  WordPtrs w{};
-  for (int i = 0; i < n && i < 8; ++i) w.p[i] = reinterpret_cast<const unsigned long long *>(ptrs[i]);
-  hipLaunchKernelGGL(k_gather_words, dim3(1), dim3(64), 0, s, w, n, reinterpret_cast<unsigned long long *>(out));
-  KCHECK("k_gather_words");
+void launch_post_words(const void *p, int n, const Mail &mail, hipStream_t s, int bytes) {
+  if (n <= 0 || n >= kMailSeq) fail(OMX_E_INVALID, "post_words: bad word count");
+  hipLaunchKernelGGL(k_post_words, dim3(1), dim3(1), 0, s, p, n, bytes, mail);
+  KCHECK("k_post_words");
 }
 
 // ---- helpers ----------------------------------------------------------------------------------------
