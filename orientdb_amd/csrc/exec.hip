@@ -143,6 +143,8 @@ class Executor {
     col_.resize(p.aliases.size());
     bound_.assign(p.aliases.size(), 0);
     if (const char *r = std::getenv("OMX_ROUTE_SELF")) route_self_ = std::strcmp(r, "0") != 0;
+    debug_expand_ = std::getenv("OMX_DEBUG_EXPAND") != nullptr;  // one stderr line per expansion
+    if (const char *ls = std::getenv("OMX_LIGHT_SLICED")) light_sliced_ = std::strcmp(ls, "0") != 0;
     dist_setup();
   }
 
@@ -259,6 +261,8 @@ class Executor {
   int cus_ = 0;
   uint64_t heavy_deg_ = kHeavyDeg;
   uint64_t heavy_deg_sliced_ = kHeavyDegSliced;
+  bool debug_expand_ = false;
+  bool light_sliced_ = true;  // LDS-sliced light kernel for sliced single-part hops (OMX_LIGHT_SLICED=0: merge path)
   bool sliced_ = true;  // LDS-sliced heavy kernel for filtered hops (OMX_SLICED=0 disables)
   uint32_t slice_shift_ = 20;  // log2 vertices per slice (OMX_SLICE_SHIFT, 6..20: tests cut small graphs)
   std::string varlen_mode_ = "auto";
@@ -368,12 +372,12 @@ class Executor {
     d.conj = conj < 0 ? 1 : conj;
   }
 
-  void eval_bitmap(int prog, int class_id, int64_t depth, uint64_t *words) {
+  void eval_bitmap(int prog, int class_id, int64_t depth, uint64_t *words, uint64_t nwords = 0) {
     tm_.begin("k_eval_bitmap");
     if (prog >= 0 && p_.progs[prog].const_false) {
-      HIP_CHECK(hipMemsetAsync(words, 0, nwords_ * 8, s_));
+      HIP_CHECK(hipMemsetAsync(words, 0, std::max(nwords, nwords_) * 8, s_));
     } else {
-      launch_eval_bitmap(make_pred(prog, class_id), g_.V, depth, words, s_);
+      launch_eval_bitmap(make_pred(prog, class_id), g_.V, depth, words, s_, nwords);
     }
     tm_.end((uint64_t)g_.V * 4 + nwords_ * 8);
     alg_bytes_ += (uint64_t)g_.V * 4;
@@ -382,8 +386,9 @@ class Executor {
   const uint64_t *bitmap(int id) {
     if (id < 0) return nullptr;
     if (!bms_[id].p) {
-      bms_[id] = DBuf<uint64_t>(&pool_, nwords_);
-      eval_bitmap(p_.bitmaps[id].prog, p_.bitmaps[id].class_id, 0, bms_[id].p);
+      const uint64_t padded = (nwords_ + kBitmapPadWords - 1) / kBitmapPadWords * kBitmapPadWords;
+      bms_[id] = DBuf<uint64_t>(&pool_, padded);
+      eval_bitmap(p_.bitmaps[id].prog, p_.bitmaps[id].class_id, 0, bms_[id].p, padded);
     }
     return bms_[id].p;
   }
@@ -620,13 +625,13 @@ class Executor {
     const DCuts cuts = sliced ? slice_cuts_of(adjs, P) : DCuts{};
     const uint64_t hd = sliced ? heavy_deg_sliced_ : heavy_deg_;
     // per-tile sums → one-workgroup scan (posts the totals to the host) → per-tile offsets and chunks
-    DBuf<uint64_t> blk(&pool_, (uint64_t)(2 + P) * bin_tiles(R)), qb(&pool_, P + 1), loffs(&pool_, R + 1);
+    DBuf<uint64_t> blk(&pool_, (uint64_t)(kBinKeys + P) * bin_tiles(R)), qb(&pool_, P + 1);
     tm_.begin("k_bin_rows");
     launch_bin_count(sliced, src, R, adj, cuts, hd, P, blk.p, s_);
     launch_bin_scan(blk.p, R, P, qb.p, mail(), s_);
     const uint64_t *m = wait_mail();
-    const uint64_t EL = m[0], EH = m[1], nchunks = m[2];
-    std::vector<uint64_t> hqb(m + 3, m + 4 + P);
+    const uint64_t EL = m[0], EH = m[1], nchunks = m[2], NL = m[3];
+    std::vector<uint64_t> hqb(m + 4, m + 5 + P);
     tm_.end(R * (4 + 16ull * adj.n + (sliced ? 4ull * (P - 1) * adj.n : 0)));
     const uint64_t E = EL + EH;
     o.E = E;
@@ -644,9 +649,33 @@ class Executor {
     if (sliced) schunks = DBuf<SliceChunk>(&pool_, std::max<uint64_t>(nchunks, 1));
     else chunks = DBuf<ChunkDesc>(&pool_, std::max<uint64_t>(nchunks, 1));
     tm_.begin("k_bin_fill");
-    launch_bin_fill(sliced, src, R, adj, cuts, hd, P, blk.p, qb.p, loffs.p, chunks.p, schunks.p, s_);
-    tm_.end(R * (4 + 16ull * adj.n + 8) + nchunks * (sliced ? sizeof(SliceChunk) : sizeof(ChunkDesc)));
-    const uint64_t ntiles = EL ? (R + EL + kExpandTile - 1) / kExpandTile : 0;
+    // light rows of a sliced single-part hop: the LDS-sliced light kernel over the compacted light rows
+    // (no merge-path partition); otherwise light data indexed by row for the merge-path kernel
+    const bool lsliced = sliced && adj.n == 1 && light_sliced_ && EL > 0;
+    DBuf<uint64_t> loffs(&pool_, (lsliced ? NL : R) + 1), lbase;
+    DBuf<uint32_t> lrow, lcuts;
+    std::vector<DBuf<uint32_t>> lcarry;
+    LightRows lr{};
+    if (lsliced) {
+      lbase = DBuf<uint64_t>(&pool_, NL);
+      lrow = DBuf<uint32_t>(&pool_, NL);
+      if (P > 1) lcuts = DBuf<uint32_t>(&pool_, (uint64_t)(P - 1) * NL);
+      lr = LightRows{lrow.p, lcuts.p, NL, 0, {}, {}};
+      if (write && carry.size() <= 4) {
+        lr.nc = (int)carry.size();
+        for (size_t c = 0; c < carry.size(); ++c) {
+          lcarry.emplace_back(&pool_, NL);
+          lr.cin[c] = carry[c];
+          lr.carry[c] = lcarry.back().p;
+        }
+      }
+    } else if (adj.n == 1) {
+      lbase = DBuf<uint64_t>(&pool_, R);
+    }
+    launch_bin_fill(sliced, src, R, adj, cuts, hd, P, blk.p, qb.p, loffs.p, lbase.p, lr, chunks.p, schunks.p, s_);
+    tm_.end(R * (4 + 16ull * adj.n + 8 + (adj.n == 1 ? 8 : 0)) +
+            nchunks * (sliced ? sizeof(SliceChunk) : sizeof(ChunkDesc)));
+    const uint64_t ntiles = EL && !lsliced ? (R + EL + kExpandTile - 1) / kExpandTile : 0;
     DBuf<uint64_t> part;
     if (ntiles) {
       part = DBuf<uint64_t>(&pool_, ntiles + 1);
@@ -687,16 +716,48 @@ class Executor {
     }
     const unsigned gh = !nchunks ? 0 : sliced ? sa.wg0[P] : (unsigned)std::min<uint64_t>(hblocks, sh);
     const unsigned gl = ntiles ? (unsigned)std::min<uint64_t>(ntiles, sl) : 0;
+    // sliced light kernel: one workgroup per CU, split evenly over the slices (light edges spread
+    // over V like the heavy ones); a wave's arena holds its share of EL plus one 64-row group
+    SliceArgs la{};
+    unsigned gls = 0;
+    uint64_t capls = 0;
+    if (lsliced) {
+      const uint32_t G = std::max<uint32_t>((uint32_t)cus(), P);
+      uint32_t w = 0, kmin = UINT32_MAX;
+      for (uint32_t q = 0; q < P; ++q) {
+        const uint32_t k = G / P + (q < G % P ? 1u : 0u);
+        la.wg0[q] = w;
+        w += k;
+        kmin = std::min(kmin, k);
+      }
+      la.wg0[P] = w;
+      la.V = g_.V;
+      la.nslices = P;
+      la.shift = slice_shift_;
+      la.lrow = lrow.p;
+      la.lcuts = lcuts.p;
+      for (int c = 0; c < lr.nc; ++c) la.lcarry[c] = lr.carry[c];
+      la.nl = NL;
+      gls = w;
+      const uint64_t wmin = (uint64_t)kmin * SWPB;
+      capls = (EL + wmin - 1) / wmin + 64 * hd;
+    }
+    const uint64_t lw = lsliced ? (uint64_t)gls * SWPB : gl;  // light workers (output segments)
+    if (debug_expand_)
+      std::fprintf(stderr, "[omx expand] R=%llu EL=%llu EH=%llu chunks=%llu P=%u ntiles=%llu gl=%u gls=%u gh=%u filt=%d\n",
+                   (unsigned long long)R, (unsigned long long)EL, (unsigned long long)EH,
+                   (unsigned long long)nchunks, P, (unsigned long long)ntiles, gl, gls, gh, (int)filt);
     // heavy output: one arena per wave, sized for the most chunks a wave of the launch owns
     const uint64_t wh = (uint64_t)gh * (sliced ? SWPB : WPB);
     const uint64_t caph = !gh ? 0 : sliced ? caph_sliced : (nchunks + wh - 1) / wh * (uint64_t)kChunk;
     const uint64_t nseg_h = wh;
     const uint64_t heavy_rows_cap = wh * caph;
-    const uint64_t capl = gl ? (ntiles + gl - 1) / gl * (uint64_t)kExpandTile : 0;
-    const uint64_t cap = filt ? heavy_rows_cap + gl * capl : E;
+    const uint64_t capl = lsliced ? capls : gl ? (ntiles + gl - 1) / gl * (uint64_t)kExpandTile : 0;
+    const uint64_t cap = filt ? heavy_rows_cap + lw * capl : E;
     ExpandArgs a{};
     a.src = src;
     a.offs = loffs.p;
+    a.lbase = lbase.p;
     a.part = part.p;
     a.R = R;
     a.E = EL;
@@ -726,7 +787,7 @@ class Executor {
       }
     }
     if (filt) {
-      o.nseg = (uint32_t)(nseg_h + gl);
+      o.nseg = (uint32_t)(nseg_h + lw);
       o.seg_start = DBuf<uint64_t>(&pool_, o.nseg);
       o.seg_count = DBuf<uint32_t>(&pool_, o.nseg);
       a.seg_start = o.seg_start.p;
@@ -754,12 +815,13 @@ class Executor {
       tm_.end(4 * EH + outw * (filt ? 0 : EH));
       rec_h = tm_.last();
     }
-    if (gl) {
+    if (gl || gls) {
       a.arena_base = heavy_rows_cap;
       a.arena_cap = capl;
       a.seg_base = (uint32_t)nseg_h;
       tm_.begin("k_expand_light");
-      launch_expand(a, gl, write, s_);
+      if (lsliced) launch_expand_light_sliced(a, la, gls, write, s_);
+      else launch_expand(a, gl, write, s_);
       tm_.end(8 * R + 4 * EL + outw * (filt ? 0 : EL));
       rec_l = tm_.last();
     }

@@ -42,6 +42,11 @@ struct SliceArgs {
   uint32_t V;
   uint32_t nslices;
   uint32_t shift;  // slice = 2^shift vertices (6 ≤ shift ≤ 20; tests shrink it to cut small graphs)
+  // sliced light kernel: the compacted light rows (k_bin_fill LightRows)
+  const uint32_t *lrow;
+  const uint32_t *lcuts;
+  const uint32_t *lcarry[4];  // carried values of the light rows (LightRows::carry), ≤ 4 columns
+  uint64_t nl;
 };
 
 // a chunk of the sliced kernel: ≤ kChunk edges of one row part inside one bitmap slice (16 B: one
@@ -74,6 +79,7 @@ struct ChunkDesc {
 struct ExpandArgs {
   const uint32_t *src;      // [R] source vertex of every binding row
   const uint64_t *offs;     // [R+1] exclusive prefix sum of the rows' LIGHT adjacency lengths
+  const uint64_t *lbase;    // [R] single-part adjacency: rp[src[r]] (k_bin_fill), so rows need no src load
   const uint64_t *part;     // [ntiles+1] merge-path split: rows consumed before tile t
   uint64_t R, E;            // rows, Σ light adjacency length
   uint64_t ntiles;
@@ -107,7 +113,12 @@ struct ExpandArgs {
 };
 
 // predicate VM → V-bit bitmap (u64 words); depth = value of $depth
-void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s);
+// nwords > ⌈V/64⌉ zero-fills the padding words (0: no padding)
+void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s,
+                        uint64_t nwords = 0);
+// filter bitmaps (Executor::bitmap) are padded to a multiple of the largest slice, so the sliced
+// kernels stage whole slices with unchecked 16-byte loads
+constexpr uint64_t kBitmapPadWords = kSliceBits / 64;
 void launch_bitmap_and(const uint64_t *a, uint64_t *b, uint64_t nwords, hipStream_t s);
 // per-word popcount of the bits v with lo <= v < hi (optionally also v % world == rank)
 void launch_word_popc(const uint64_t *words, uint64_t nwords, uint32_t V, int rank, int world, uint32_t lo,
@@ -128,22 +139,39 @@ void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t 
 void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t vlo, uint32_t vhi, uint32_t nslices,
                        uint32_t shift, uint32_t *cuts, hipStream_t s);
 // Degree binning of R rows in three launches (rows in tiles of kBinBlock): per tile, the sums of the
-// rows' light degrees, heavy degrees and heavy chunks per slice (blk[k·nb + b], k = 0 light, 1 heavy,
-// 2 + q chunks of slice q); one workgroup scans them (qb[q] = first chunk of slice q, qb[P] = chunks;
-// mail = {Σ light, Σ heavy, chunks, qb[0..P]}); then every tile redoes its rows and writes loffs
-// (light edge offsets, [R+1]) and the heavy rows' chunks. Unsliced: P = 1, kChunk-aligned ChunkDesc
-// windows; sliced: SliceChunk pieces cut at the slice boundaries (cuts).
+// rows' light degrees, heavy degrees, light rows and heavy chunks per slice (blk[k·nb + b]); one
+// workgroup scans them (qb[q] = first chunk of slice q, qb[P] = chunks; mail = {Σ light, Σ heavy,
+// chunks, light rows NL, qb[0..P]}); then every tile redoes its rows and writes the light offsets,
+// the light rows' first col index and the heavy rows' chunks. Unsliced: P = 1, kChunk-aligned
+// ChunkDesc windows; sliced: SliceChunk pieces cut at the slice boundaries (cuts).
+// LightRows::row == nullptr: loffs[R+1] / lbase[R] indexed by row (merge-path light kernel); else the
+// light rows are compacted in order: loffs[NL+1], lbase[NL], row[NL], cuts[(q−1)·NL + i] (the sliced
+// light kernel, single-part adjacency).
+struct LightRows {
+  uint32_t *row;
+  uint32_t *cuts;
+  uint64_t nl;
+  // the light rows' carried values, compacted alongside (carry[c][i] = cin[c][row i]) when ≤ 4 columns
+  int nc;
+  const uint32_t *cin[4];
+  uint32_t *carry[4];
+};
 constexpr int kBinBlock = 256;
+constexpr int kBinKeys = 3;  // keys before the per-slice chunk counts
 inline unsigned bin_tiles(uint64_t R) { return (unsigned)((R + 1 + kBinBlock - 1) / kBinBlock); }
 void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
                       uint64_t heavy_deg, uint32_t P, uint64_t *blk, hipStream_t s);
 void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s);
 void launch_bin_fill(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
                      uint64_t heavy_deg, uint32_t P, const uint64_t *blk, const uint64_t *qb, uint64_t *loffs,
-                     ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s);
+                     uint64_t *lbase, const LightRows &lr, ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s);
 // grid = sa.wg0[P] workgroups (one per CU); wave w appends to arena_base + w·arena_cap and reports
 // seg_count/seg_start[seg_base + w]
 void launch_expand_heavy_sliced(const ExpandArgs &a, const SliceArgs &sa, unsigned grid, bool write, hipStream_t s);
+// light rows of a sliced single-part hop (ExpandArgs: offs / lbase of the compacted light rows, E = Σ
+// light; sa.wg0 over the light grid, sa.lrow / lcuts / nl); wave w appends to arena_base + w·arena_cap, arena_cap ≥
+// ⌈E / waves of the smallest slice⌉ + 64·heavy_deg
+void launch_expand_light_sliced(const ExpandArgs &a, const SliceArgs &sa, unsigned grid, bool write, hipStream_t s);
 // persistent launches: `grid` blocks loop over the tiles / chunks
 void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);
 void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);

@@ -178,16 +178,20 @@ __host__ __device__ bool eval_pred(const DPred &P, uint32_t v, int64_t depth) {
 bool eval_pred_const(const DPred &pred, int64_t depth) { return eval_pred(pred, 0, depth); }
 
 // one lane per vertex, 64 vertices per wave → one u64 bitmap word per wave via ballot
-__global__ __launch_bounds__(256) void k_eval_bitmap(DPred P, uint32_t V, int64_t depth, uint64_t *words) {
+// words [⌈V/64⌉, nwords) (padding) are written as zero
+__global__ __launch_bounds__(256) void k_eval_bitmap(DPred P, uint32_t V, int64_t depth, uint64_t *words,
+                                                     uint64_t nwords) {
   uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool b = v < V && eval_pred(P, (uint32_t)v, depth);
   uint64_t m = __ballot(b);
-  if ((threadIdx.x & 63) == 0 && v < (uint64_t)V) words[v >> 6] = m;
+  if ((threadIdx.x & 63) == 0 && (v >> 6) < nwords) words[v >> 6] = m;
 }
 
-void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s) {
+void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s,
+                        uint64_t nwords) {
   if (!V) return;
-  hipLaunchKernelGGL(k_eval_bitmap, dim3(nblocks(V, 256)), dim3(256), 0, s, pred, V, depth, words);
+  if (!nwords) nwords = ((uint64_t)V + 63) / 64;
+  hipLaunchKernelGGL(k_eval_bitmap, dim3(nblocks(nwords * 64, 256)), dim3(256), 0, s, pred, V, depth, words, nwords);
   KCHECK("k_eval_bitmap");
 }
 
@@ -350,16 +354,16 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
       const uint64_t e = re < j1 ? (re > j0 ? re - j0 : 0) : ne;
       s_ls[lr] = (uint16_t)(s < ne ? s : ne);
       if (e > s && s < ne) s_seg[s] = (uint16_t)lr;
-      const uint32_t v = a.src[r];
       const uint64_t skip = rs < j0 ? j0 - rs : 0;
       if (MEMBER) {
         const uint32_t y = a.member_src[r];
         s_y[lr] = y;
         s_ydeg[lr] = (uint32_t)adj_degree(a.member_adj, y);
       }
-      if (SINGLE) {
-        s_base[lr] = a.adj.p[0].rp[v] + skip;
+      if (SINGLE) {  // the row's first col index, precomputed by k_bin_fill (no dependent rp[src] load)
+        s_base[lr] = a.lbase[r] + skip;
       } else {
+        const uint32_t v = a.src[r];
         s_vtx[lr] = v;
         if (lr == 0) s_base[0] = skip;
       }
@@ -740,19 +744,21 @@ void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t vlo, ui
 }
 
 // ---- degree binning ---------------------------------------------------------------------------------
-// x[0] = light degree, x[1] = heavy degree, x[2 + q] = heavy chunks in slice q of row r (all 0 for
-// r ≥ R). Unsliced (MAXP = 1): chunks are the kChunk-aligned windows the row's parts touch.
+// Keys of row r (all 0 for r ≥ R): x[0] = light degree (0 < d < heavy_deg), x[1] = heavy degree,
+// x[2] = 1 for a light row, x[3 + q] = heavy chunks in slice q. Unsliced (MAXP = 1): chunks are the
+// kChunk-aligned windows the row's parts touch.
 template <bool SLICED, int MAXP>
 __device__ __forceinline__ void row_bins(const uint32_t *src, uint64_t r, uint64_t R, const DAdj &adj,
                                          const DCuts &cuts, uint64_t heavy_deg, uint32_t P,
-                                         uint64_t (&x)[2 + MAXP]) {
+                                         uint64_t (&x)[kBinKeys + MAXP]) {
 #pragma unroll
-  for (int k = 0; k < 2 + MAXP; ++k) x[k] = 0;
+  for (int k = 0; k < kBinKeys + MAXP; ++k) x[k] = 0;
   if (r >= R) return;
   const uint32_t v = src[r];
   const uint64_t d = adj_degree(adj, v);
   if (d < heavy_deg) {
     x[0] = d;
+    x[2] = d > 0;
     return;
   }
   x[1] = d;
@@ -762,9 +768,9 @@ __device__ __forceinline__ void row_bins(const uint32_t *src, uint64_t r, uint64
       uint32_t cut[MAXP + 1];
       load_cuts<MAXP>(cuts.c[p], v, (uint32_t)(e - b), P, cut);
 #pragma unroll
-      for (int q = 0; q < MAXP; ++q) x[2 + q] += chunk_pieces(cut[q], cut[q + 1]);
+      for (int q = 0; q < MAXP; ++q) x[kBinKeys + q] += chunk_pieces(cut[q], cut[q + 1]);
     } else if (e > b) {
-      x[2] += (e - 1) / kChunk - b / kChunk + 1;
+      x[kBinKeys] += (e - 1) / kChunk - b / kChunk + 1;
     }
   }
 }
@@ -802,7 +808,7 @@ __device__ __forceinline__ void block_excl_scan_k(uint64_t (&x)[K], uint64_t (&t
 template <bool SLICED, int MAXP>
 __global__ __launch_bounds__(kBinBlock) void k_bin_count(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
                                                           uint64_t heavy_deg, uint32_t P, uint64_t *blk) {
-  constexpr int K = 2 + MAXP;
+  constexpr int K = kBinKeys + MAXP;
   __shared__ uint64_t s_w[K * (kBinBlock / 64)];
   const uint64_t r = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x;
   uint64_t x[K], tot[K];
@@ -811,84 +817,125 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_count(const uint32_t *src, ui
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      if ((uint32_t)k < 2 + P) blk[(uint64_t)k * gridDim.x + blockIdx.x] = tot[k];
+      if ((uint32_t)k < kBinKeys + P) blk[(uint64_t)k * gridDim.x + blockIdx.x] = tot[k];
   }
 }
 
-// one workgroup: exclusive scan of every key's tile sums in place, the slices' chunk bounds and the mail
+// one workgroup: exclusive scan of every key's tile sums in place (all keys' loads issued together),
+// the slices' chunk bounds and the mail {EL, EH, chunks, light rows, qb[0..P]}
+template <int MAXP>
 __global__ __launch_bounds__(1024) void k_bin_scan(uint64_t *blk, uint32_t nb, uint32_t P, uint64_t *qb, Mail mail) {
-  __shared__ unsigned long long s_w[16];
-  __shared__ uint64_t s_tot[2 + kMaxSlices];
+  constexpr int K = kBinKeys + MAXP;
+  __shared__ unsigned long long s_w[K][16];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t per = (nb + 1023) / 1024;
   const uint32_t i0 = min(nb, threadIdx.x * per), i1 = min(nb, i0 + per);
-  for (uint32_t k = 0; k < 2 + P; ++k) {
-    uint64_t *a = blk + (uint64_t)k * nb;
-    unsigned long long c = 0;
-    for (uint32_t i = i0; i < i1; ++i) c += a[i];
-    unsigned long long incl = c;
+  unsigned long long c[K], incl[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    c[k] = 0;
+    if ((uint32_t)k < kBinKeys + P)
+      for (uint32_t i = i0; i < i1; ++i) c[k] += blk[(uint64_t)k * nb + i];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    incl[k] = c[k];
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      const unsigned long long y = __shfl_up(incl, off, 64);
-      if (lane >= (uint32_t)off) incl += y;
+      const unsigned long long y = __shfl_up(incl[k], off, 64);
+      if (lane >= (uint32_t)off) incl[k] += y;
     }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    unsigned long long run = 0, tot = 0;
-    for (uint32_t w = 0; w < 16; ++w) {
-      run += w < wave ? s_w[w] : 0;
-      tot += s_w[w];
-    }
-    run += incl - c;
+    if (lane == 63) s_w[k][wave] = incl[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if ((uint32_t)k >= kBinKeys + P) continue;
+    unsigned long long run = 0;
+    for (uint32_t w = 0; w < wave; ++w) run += s_w[k][w];
+    run += incl[k] - c[k];
+    uint64_t *a = blk + (uint64_t)k * nb;
     for (uint32_t i = i0; i < i1; ++i) {
       const uint64_t y = a[i];
       a[i] = run;
       run += y;
     }
-    if (threadIdx.x == 0) s_tot[k] = tot;
-    __syncthreads();  // s_w is reused by the next key
   }
   if (threadIdx.x == 0) {
+    unsigned long long tot[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      tot[k] = 0;
+      for (int w = 0; w < 16; ++w) tot[k] += s_w[k][w];
+    }
     uint64_t q0 = 0;
-    mail.p[0] = s_tot[0];
-    mail.p[1] = s_tot[1];
-    for (uint32_t q = 0; q < P; ++q) {
+    mail.p[0] = tot[0];
+    mail.p[1] = tot[1];
+    mail.p[3] = tot[2];
+#pragma unroll
+    for (int q = 0; q < MAXP; ++q) {
+      if ((uint32_t)q >= P) break;
       qb[q] = q0;
-      mail.p[3 + q] = q0;
-      q0 += s_tot[2 + q];
+      mail.p[4 + q] = q0;
+      q0 += tot[kBinKeys + q];
     }
     qb[P] = q0;
-    mail.p[3 + P] = q0;
+    mail.p[4 + P] = q0;
     mail.p[2] = q0;
     mail_post(mail);
   }
 }
 
+// Every tile redoes its rows' keys, adds the tile prefixes and writes the light offsets, the light
+// rows' first col index and the heavy rows' chunks. lr.row == nullptr: light data indexed by row
+// (loffs[R+1], lbase[R]: merge-path kernel); else compacted to the light rows in order (loffs[NL+1],
+// lbase, lr.row, lr.cuts[(q−1)·NL + i] = slice cut q of light row i: sliced light kernel).
 template <bool SLICED, int MAXP>
 __global__ __launch_bounds__(kBinBlock) void k_bin_fill(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
                                                          uint64_t heavy_deg, uint32_t P, const uint64_t *blk,
-                                                         const uint64_t *qb, uint64_t *loffs, ChunkDesc *chunks,
-                                                         SliceChunk *schunks) {
-  constexpr int K = 2 + MAXP;
+                                                         const uint64_t *qb, uint64_t *loffs, uint64_t *lbase,
+                                                         LightRows lr, ChunkDesc *chunks, SliceChunk *schunks) {
+  constexpr int K = kBinKeys + MAXP;
   __shared__ uint64_t s_w[K * (kBinBlock / 64)];
   const uint64_t r = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x;
   const uint32_t nb = gridDim.x;
   uint64_t x[K], tot[K];
   row_bins<SLICED, MAXP>(src, r, R, adj, cuts, heavy_deg, P, x);
-  const uint64_t heavy = x[1];
+  const uint64_t heavy = x[1], light = x[2];
   block_excl_scan_k<kBinBlock, K>(x, tot, s_w);
   if (r > R) return;
-  loffs[r] = x[0] + blk[blockIdx.x];
+  const uint64_t lo = x[0] + blk[blockIdx.x];
+  if (lr.row) {
+    const uint64_t i = x[2] + blk[2ull * nb + blockIdx.x];  // compact index of a light row
+    if (r == R) {
+      loffs[i] = lo;  // i = NL
+      return;
+    }
+    if (light) {
+      const uint32_t v = src[r];
+      loffs[i] = lo;
+      lbase[i] = adj.p[0].rp[v];
+      lr.row[i] = (uint32_t)r;
+      for (int c = 0; c < lr.nc; ++c) lr.carry[c][i] = lr.cin[c][r];
+      if (SLICED)
+        for (uint32_t q = 1; q < P; ++q) lr.cuts[(uint64_t)(q - 1) * lr.nl + i] = cuts.c[0][(uint64_t)v * (P - 1) + q - 1];
+      return;
+    }
+  } else {
+    loffs[r] = lo;
+    if (r == R) return;
+    if (adj.n == 1) lbase[r] = adj.p[0].rp[src[r]];  // (an L1 hit: row_bins just read it)
+  }
   if (!heavy) return;
   const uint32_t v = src[r];
   if (!SLICED) {
-    uint64_t o = x[2] + blk[2ull * nb + blockIdx.x];
+    uint64_t o = x[kBinKeys] + blk[(uint64_t)kBinKeys * nb + blockIdx.x];
     uint64_t pos = x[1] + blk[(uint64_t)nb + blockIdx.x];  // dense output index of the row's first edge
     for (int p = 0; p < adj.n; ++p) {
       const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
       for (uint64_t w = b / kChunk * kChunk; e > b && w < e; w += kChunk) {  // an empty part has no chunk
-        const uint64_t lo = w > b ? w : b, hi = w + kChunk < e ? w + kChunk : e;
-        chunks[o++] = ChunkDesc{lo, hi, pos + (lo - b), (uint32_t)r, (uint32_t)p};
+        const uint64_t clo = w > b ? w : b, chi = w + kChunk < e ? w + kChunk : e;
+        chunks[o++] = ChunkDesc{clo, chi, pos + (clo - b), (uint32_t)r, (uint32_t)p};
       }
       pos += e - b;
     }
@@ -897,7 +944,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_fill(const uint32_t *src, uin
   uint64_t o[MAXP];
 #pragma unroll
   for (int q = 0; q < MAXP; ++q)
-    o[q] = (uint32_t)q < P ? x[2 + q] + blk[(2ull + q) * nb + blockIdx.x] + qb[q] : 0;
+    o[q] = (uint32_t)q < P ? x[kBinKeys + q] + blk[(uint64_t)(kBinKeys + q) * nb + blockIdx.x] + qb[q] : 0;
   for (int p = 0; p < adj.n; ++p) {
     const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
     uint32_t cut[MAXP + 1];
@@ -926,23 +973,55 @@ void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &
   KCHECK("k_bin_count");
 }
 void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s) {
-  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, blk, bin_tiles(R), P, qb, mail);
+#define OMX_BS(M) hipLaunchKernelGGL((k_bin_scan<M>), dim3(1), dim3(1024), 0, s, blk, bin_tiles(R), P, qb, mail)
+  OMX_BY_MAXP(P, OMX_BS);
+#undef OMX_BS
   KCHECK("k_bin_scan");
 }
 void launch_bin_fill(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
                      uint64_t heavy_deg, uint32_t P, const uint64_t *blk, const uint64_t *qb, uint64_t *loffs,
-                     ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s) {
+                     uint64_t *lbase, const LightRows &lr, ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s) {
   const unsigned nb = bin_tiles(R);
   if (!sliced) {
     hipLaunchKernelGGL((k_bin_fill<false, 1>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, heavy_deg, 1u, blk,
-                       qb, loffs, chunks, schunks);
+                       qb, loffs, lbase, lr, chunks, schunks);
   } else {
 #define OMX_BF(M) hipLaunchKernelGGL((k_bin_fill<true, M>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, \
-                                     heavy_deg, P, blk, qb, loffs, chunks, schunks)
+                                     heavy_deg, P, blk, qb, loffs, lbase, lr, chunks, schunks)
     OMX_BY_MAXP(P, OMX_BF);
 #undef OMX_BF
   }
   KCHECK("k_bin_fill");
+}
+
+// Copy bitmap slice q (2^shift bits) into LDS: 16-byte loads, eight per thread in flight before the
+// LDS stores (a plain loop waits for each load before its store: 32 serial round trips per thread)
+__device__ __forceinline__ void stage_slice(uint32_t *s_bm, const uint32_t *bm, uint32_t V, uint32_t q, uint32_t shift) {
+  const uint64_t nw = ((uint64_t)V + 63) / 64 * 2;  // u32 words of the bitmap (before the padding)
+  const uint32_t sw = (1u << shift) / 32;
+  const uint64_t w0 = (uint64_t)q * sw;
+  if (sw % (4 * kSliceBlock) == 0) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(bm + w0);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(s_bm);
+    const uint32_t n4 = sw / 4;
+    for (uint32_t i0 = 0; i0 < n4; i0 += 8 * kSliceBlock) {
+      u32x4 t[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // no range check: filter bitmaps are padded (kBitmapPadWords)
+        const uint32_t i = i0 + k * kSliceBlock + threadIdx.x;
+        t[k] = src[i < n4 ? i : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t i = i0 + k * kSliceBlock + threadIdx.x;
+        if (i < n4) dst[i] = t[k];
+      }
+    }
+  } else {  // small slices (tests)
+    for (uint32_t i = threadIdx.x; i < sw; i += kSliceBlock) s_bm[i] = w0 + i < nw ? bm[w0 + i] : 0u;
+  }
+  __syncthreads();
 }
 
 // Workgroups [wg0[q], wg0[q+1]) own slice q (the host sizes each range by the slice's chunk count);
@@ -993,14 +1072,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
   const uint32_t gw = blockIdx.x * WPB + wave;
   uint32_t qs = 0;
   while (qs + 1 < sa.nslices && blockIdx.x >= sa.wg0[qs + 1]) ++qs;
-  {  // stage the slice
-    const uint64_t nw = ((uint64_t)sa.V + 63) / 64 * 2;  // u32 words of the bitmap
-    const uint32_t sw = (1u << sa.shift) / 32;
-    const uint64_t w0 = (uint64_t)qs * sw;
-    const uint32_t *bm = reinterpret_cast<const uint32_t *>(a.filter);
-    for (uint32_t i = threadIdx.x; i < sw; i += kSliceBlock) s_bm[i] = w0 + i < nw ? bm[w0 + i] : 0u;
-  }
-  __syncthreads();
+  stage_slice(s_bm, reinterpret_cast<const uint32_t *>(a.filter), sa.V, qs, sa.shift);
   const uint64_t qend = sa.qb[qs + 1];
   const uint32_t nwq = (sa.wg0[qs + 1] - sa.wg0[qs]) * WPB;
   const uint64_t arena = a.arena_base + (uint64_t)gw * a.arena_cap;
@@ -1150,6 +1222,200 @@ void launch_expand_heavy_sliced(const ExpandArgs &a, const SliceArgs &sa, unsign
     }
   }
   KCHECK("k_expand_heavy_sliced");
+}
+
+// ---- LDS-sliced light rows ---------------------------------------------------------------------------
+// The merge-path kernel probes the target bitmap through L2: one L1→L2 request per edge (a light row's
+// few sorted neighbours spread over all of V), and that request rate bounds it. Here, as for the heavy
+// rows, workgroups [wg0[q], wg0[q+1]) hold slice q of the bitmap in LDS. The light rows come compacted
+// by k_bin_fill (offsets, first col index, row, slice cuts: coalesced, no dependent loads). Wave j of
+// slice q owns the 64-light-row groups whose first edge offset lies in [EL·j/W_q, EL·(j+1)/W_q) (a
+// 64-ary search over the offsets) and per group packs the 64 rows' slice-q pieces into 64-edge slots:
+// each lane finds the row owning its edge with a 6-step search over the wave's piece offsets
+// (cross-lane reads), loads the neighbour and probes LDS. U slots are in flight per step and the next
+// group's row data (with the carried values, compacted by k_bin_fill for ≤ 4 columns, so a survivor's
+// columns come from a cross-lane read, not a gather) is loaded while the current one is filtered. Survivors go to the wave's arena (cap
+// ⌈EL/W_q⌉ + 64·heavy_deg rows), compacted by ballot.
+constexpr int kLightStage = 320;  // staged survivors per wave (16 waves × 1.6 KiB beside the slice)
+template <bool WRITE, int U, int NC>
+__global__ __launch_bounds__(kSliceBlock) void k_expand_light_sliced(ExpandArgs a, SliceArgs sa) {
+  constexpr int NCV = NC > 0 ? NC : 1;
+  constexpr int WPB = kSliceBlock / 64;
+  __shared__ uint32_t s_bm[kSliceBits / 32];
+  __shared__ uint32_t s_stv[WRITE ? WPB * kLightStage : 1];
+  __shared__ uint8_t s_stj[WRITE ? WPB * kLightStage : 1];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t gw = blockIdx.x * WPB + wave;
+  uint32_t qs = 0;
+  while (qs + 1 < sa.nslices && blockIdx.x >= sa.wg0[qs + 1]) ++qs;
+  stage_slice(s_bm, reinterpret_cast<const uint32_t *>(a.filter), sa.V, qs, sa.shift);
+  const uint32_t P = sa.nslices, wbits = sa.shift - 5;
+  const uint64_t NL = sa.nl, EL = a.E, G = (NL + 63) / 64;
+  const uint32_t nwq = (sa.wg0[qs + 1] - sa.wg0[qs]) * WPB;
+  const uint32_t wq = (blockIdx.x - sa.wg0[qs]) * WPB + wave;
+  const uint64_t *offs = a.offs;
+  // first group g ∈ [0, G] whose first edge offset is ≥ target (offs[min(64g, NL)]; g = G → EL)
+  auto group_lb = [&](uint64_t target) -> uint64_t {
+    uint64_t lo = 0, hi = G;
+    while (lo < hi) {
+      const uint64_t step = (hi - lo + 63) / 64;
+      const uint64_t p = lo + (uint64_t)lane * step;
+      const bool f = p >= hi || offs[p * 64 < NL ? p * 64 : NL] >= target;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(f);
+      if (m == 0) {
+        lo += 63 * step + 1;
+      } else {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        if (l == 0) break;  // lo itself
+        hi = lo + (uint64_t)l * step;
+        lo += (uint64_t)(l - 1) * step + 1;
+      }
+    }
+    return lo;
+  };
+  const uint64_t g0 = group_lb(EL * wq / nwq);
+  const uint64_t g1 = wq + 1 == nwq ? G : group_lb(EL * (wq + 1) / nwq);
+  const uint64_t arena = a.arena_base + (uint64_t)gw * a.arena_cap;
+  const uint32_t *col = a.adj.p[0].col;
+  const uint32_t *clo_p = qs > 0 ? sa.lcuts + (uint64_t)(qs - 1) * NL : nullptr;
+  const uint32_t *chi_p = qs + 1 < P ? sa.lcuts + (uint64_t)qs * NL : nullptr;
+  const int nc = a.ncarry;
+  // row data of one group (loads unconditional, index clamped: a skipped load would make the waitcnt
+  // pass drain the prefetch at the join)
+  struct Grp {
+    uint64_t o0, o1, lb;
+    uint32_t clo, chi, row;
+    uint32_t cv[NCV];
+  };
+  auto gload = [&](uint64_t g, Grp &m) {
+    const uint64_t i = g * 64 + lane;
+    const uint64_t ii = i < NL ? i : NL - 1;
+    m.o0 = offs[ii];
+    m.o1 = i < NL ? offs[ii + 1] : m.o0;  // a lane past NL gets an empty piece
+    m.lb = a.lbase[ii];
+    m.clo = clo_p ? clo_p[ii] : 0u;
+    m.chi = chi_p ? chi_p[ii] : 0xffffffffu;
+    m.row = WRITE && NC < 0 ? sa.lrow[ii] : 0u;
+#pragma unroll
+    for (int c = 0; c < NCV; ++c) m.cv[c] = WRITE && c < NC ? sa.lcarry[c][ii] : 0u;
+  };
+  uint64_t acc = 0;
+  // per-wave LDS staging of the group's survivors (neighbour, owning lane), written out with
+  // full-wave coalesced stores once per group: no stores between the col[] loads of a group's steps
+  // (gfx9 counts stores on vmcnt, so each partial store would hold up the next step's load wait)
+  uint32_t *const stv = s_stv + wave * kLightStage;
+  uint8_t *const stj = s_stj + wave * kLightStage;
+  uint32_t st = 0;
+  auto flush = [&](const Grp &m) {
+    for (uint32_t k = 0; k < st; k += 64) {
+      const uint32_t idx = k + lane;
+      const uint32_t j = idx < st ? stj[idx] : 0u;
+      const uint32_t v = idx < st ? stv[idx] : 0u;
+      uint32_t cv[NCV];
+#pragma unroll
+      for (int c = 0; c < NCV; ++c) cv[c] = c < NC ? (uint32_t)__shfl(m.cv[c], (int)j, 64) : 0u;
+      const uint32_t rr = NC < 0 ? (uint32_t)__shfl(m.row, (int)j, 64) : 0u;
+      if (idx < st) {
+        const uint64_t o = arena + acc + idx;
+        a.out_dst[o] = v;
+        if (NC < 0) {
+          for (int c = 0; c < nc; ++c) a.carry_out[c][o] = a.carry_in[c][rr];
+        } else {
+#pragma unroll
+          for (int c = 0; c < NCV; ++c)
+            if (c < NC) a.carry_out[c][o] = cv[c];
+        }
+      }
+    }
+    acc += st;
+    st = 0;
+  };
+  auto process = [&](uint64_t g, const Grp &m) {
+    const uint32_t dl = (uint32_t)(m.o1 - m.o0);
+    const uint32_t clo = dl ? m.clo : 0u, chi = dl ? (m.chi < dl ? m.chi : dl) : 0u;
+    const uint32_t len = chi - clo;
+    const uint64_t start = m.lb + clo;
+    uint32_t incl = len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(incl, off, 64);
+      if (lane >= (uint32_t)off) incl += y;
+    }
+    const uint32_t pre = incl - len;
+    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    for (uint32_t base = 0; base < T; base += 64 * U) {
+      uint32_t nb[U], jj[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t e = base + u * 64 + lane;
+        // owner: the last lane j with pre_j ≤ e (zero-length pieces share their successor's offset)
+        uint32_t j = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+          if ((uint32_t)__shfl(pre, (int)(j + st), 64) <= e) j += st;
+        const uint64_t sj = ((uint64_t)(uint32_t)__shfl((uint32_t)(start >> 32), (int)j, 64) << 32) |
+                            (uint32_t)__shfl((uint32_t)start, (int)j, 64);
+        const uint32_t pj = (uint32_t)__shfl(pre, (int)j, 64);
+        jj[u] = j;
+        // unconditional load (lanes past T read the piece start and are masked below)
+        nb[u] = col[e < T ? sj + (e - pj) : sj];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t e = base + u * 64 + lane;
+        const uint32_t v = nb[u];
+        const bool bit = e < T && ((s_bm[__builtin_amdgcn_ubfe(v, 5, wbits)] >> (v & 31)) & 1u);
+        const uint64_t mk = __builtin_amdgcn_ballot_w64(bit);
+        if (WRITE) {
+          if (bit) {
+            const uint32_t o = st + lane_prefix(mk);
+            stv[o] = v;
+            stj[o] = (uint8_t)jj[u];
+          }
+          st += (uint32_t)__popcll(mk);
+          if (st > kLightStage - 64) flush(m);  // uniform: room for one more slot
+        } else {
+          acc += (uint64_t)__popcll(mk);
+        }
+      }
+    }
+    if (WRITE && st) flush(m);
+  };
+  if (g0 < g1) {
+    Grp A, B;
+    gload(g0, A);
+    for (uint64_t g = g0;; g += 2) {
+      gload(g + 1 < g1 ? g + 1 : g, B);
+      process(g, A);
+      if (g + 1 >= g1) break;
+      gload(g + 2 < g1 ? g + 2 : g + 1, A);
+      process(g + 1, B);
+      if (g + 2 >= g1) break;
+    }
+  }
+  if (lane == 0) {
+    a.seg_count[a.seg_base + gw] = (uint32_t)acc;
+    a.seg_start[a.seg_base + gw] = arena;
+  }
+}
+
+void launch_expand_light_sliced(const ExpandArgs &a, const SliceArgs &sa, unsigned grid, bool write, hipStream_t s) {
+  if (!grid) return;
+  const dim3 g(grid), b(kSliceBlock);
+  if (!write) {
+    hipLaunchKernelGGL((k_expand_light_sliced<false, 8, 0>), g, b, 0, s, a, sa);
+  } else {
+    switch (a.ncarry) {
+      case 0: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 0>), g, b, 0, s, a, sa); break;
+      case 1: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 1>), g, b, 0, s, a, sa); break;
+      case 2: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 2>), g, b, 0, s, a, sa); break;
+      case 3: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 3>), g, b, 0, s, a, sa); break;
+      case 4: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 4>), g, b, 0, s, a, sa); break;
+      default: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, -1>), g, b, 0, s, a, sa); break;
+    }
+  }
+  KCHECK("k_expand_light_sliced");
 }
 
 void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s) {

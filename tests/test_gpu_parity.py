@@ -185,6 +185,23 @@ def test_rmat_parity_sliced(rmat10, q, monkeypatch):
     assert c.info["edges_traversed"] >= 0
 
 
+@pytest.mark.parametrize("light_sliced", ["1", "0"], ids=["light_sliced", "light_merge_path"])
+@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in SLICED_IDS], ids=lambda q: q[0])
+def test_rmat_parity_sliced_light_rows(rmat10, q, light_sliced, monkeypatch):
+    """Rows of degree < 16 of a sliced hop through the LDS-sliced light kernel (16 slices of 64
+    vertices: each light row is cut into pieces, 64 rows' pieces packed per slot group), and through
+    the merge-path kernel."""
+    import orientdb_amd as o
+    monkeypatch.setenv("OMX_HEAVY_DEG", "16")
+    monkeypatch.setenv("OMX_SLICE_SHIFT", "6")
+    monkeypatch.setenv("OMX_LIGHT_SLICED", light_sliced)
+    g, ref = rmat10
+    _parity(g, ref, q[1], q[2])
+    m = o.OMatchStatement(q[1]).execute(g)
+    c = o.OMatchStatement(q[1]).execute(g, mode=o.OMX_MODE_COUNT)
+    assert c.info["n_rows"] == m.info["n_rows"]
+
+
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in SLICED_IDS], ids=lambda q: q[0])
 def test_rmat_parity_l2_probe_heavy(rmat10, q, monkeypatch):
     """The same cases through the L2-probe heavy kernel (slicing disabled)."""
