@@ -67,6 +67,7 @@ struct DPred {
   int64_t atom_i[4];
   double atom_d[4];
   int32_t atom_dbl[4];  // compare as double (double column or double constant)
+  DColumn atom_c[4];    // the atoms' column descriptors (kernel-argument copies: no dependent load)
 };
 
 }  // namespace omx

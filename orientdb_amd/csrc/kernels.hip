@@ -187,10 +187,84 @@ __global__ __launch_bounds__(256) void k_eval_bitmap(DPred P, uint32_t V, int64_
   if ((threadIdx.x & 63) == 0 && (v >> 6) < nwords) words[v >> 6] = m;
 }
 
+// "column OP constant" atoms (and the class test): EV bitmap words per wave, every load of the EV
+// vertices (class id, presence, value; column descriptors from the kernel arguments) issued before
+// any is used; loads are unconditional (index clamped) so none waits inside a branch
+constexpr int kEvalWords = 4;
+__device__ __forceinline__ uint64_t raw_col(const DColumn &c, uint64_t v) {
+  return (c.type == OMX_PROP_INT64 || c.type == OMX_PROP_DOUBLE) ? ((const uint64_t *)c.values)[v]
+                                                                 : (uint64_t)((const uint32_t *)c.values)[v];
+}
+__device__ __forceinline__ bool atom_true(const DPred &P, int k, uint64_t raw, bool present) {
+  const DColumn &c = P.atom_c[k];
+  if (!present || (c.type == OMX_PROP_STRING && (int32_t)(uint32_t)raw < 0)) return P.atom_op[k] == P_NE;
+  if (P.atom_dbl[k]) {
+    double a;
+    if (c.type == OMX_PROP_DOUBLE) a = __longlong_as_double((long long)raw);
+    else if (c.type == OMX_PROP_INT64) a = (double)(int64_t)raw;
+    else if (c.type == OMX_PROP_BOOL) a = (uint32_t)raw != 0;
+    else a = (double)(int32_t)(uint32_t)raw;
+    const double b = P.atom_d[k];
+    return atom_cmp(P.atom_op[k], a < b ? -1 : (a > b ? 1 : 0));
+  }
+  int64_t x;
+  if (c.type == OMX_PROP_INT64) x = (int64_t)raw;
+  else if (c.type == OMX_PROP_BOOL) x = (uint32_t)raw != 0;
+  else x = (int32_t)(uint32_t)raw;
+  const int64_t b = P.atom_i[k];
+  return atom_cmp(P.atom_op[k], x < b ? -1 : (x > b ? 1 : 0));
+}
+__global__ __launch_bounds__(256) void k_eval_atoms(DPred P, uint32_t V, uint64_t *words, uint64_t nwords) {
+  constexpr int EV = kEvalWords;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64 * EV;
+  uint64_t vv[EV];
+  uint32_t cls[EV];
+  uint64_t raw[4][EV];
+  uint32_t pres[4][EV];
+#pragma unroll
+  for (int e = 0; e < EV; ++e) {
+    const uint64_t v = (w0 + e) * 64 + lane;
+    vv[e] = v < V ? v : V - 1;
+    cls[e] = P.use_class ? P.vclass[vv[e]] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k >= P.n_atoms) break;  // uniform
+    const DColumn &c = P.atom_c[k];
+#pragma unroll
+    for (int e = 0; e < EV; ++e) {
+      raw[k][e] = raw_col(c, vv[e]);
+      pres[k][e] = c.present ? c.present[vv[e]] : 1u;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EV; ++e) {
+    const uint64_t v = (w0 + e) * 64 + lane;
+    bool b = v < V;
+    if (P.use_class) b = b && ((P.class_mask[cls[e] >> 6] >> (cls[e] & 63)) & 1ull);
+    bool acc = P.conj != 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= P.n_atoms) break;
+      const bool r = atom_true(P, k, raw[k][e], pres[k][e] != 0);
+      acc = P.conj ? (acc && r) : (acc || r);
+    }
+    const uint64_t m = __ballot(b && acc);
+    if (lane == 0 && w0 + e < nwords) words[w0 + e] = m;
+  }
+}
+
 void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s,
                         uint64_t nwords) {
   if (!V) return;
   if (!nwords) nwords = ((uint64_t)V + 63) / 64;
+  if (pred.n > 0 && pred.n_atoms > 0) {
+    const uint64_t waves = (nwords + kEvalWords - 1) / kEvalWords;
+    hipLaunchKernelGGL(k_eval_atoms, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s, pred, V, words, nwords);
+    KCHECK("k_eval_atoms");
+    return;
+  }
   hipLaunchKernelGGL(k_eval_bitmap, dim3(nblocks(nwords * 64, 256)), dim3(256), 0, s, pred, V, depth, words, nwords);
   KCHECK("k_eval_bitmap");
 }
@@ -823,19 +897,33 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_count(const uint32_t *src, ui
 
 // one workgroup: exclusive scan of every key's tile sums in place (all keys' loads issued together),
 // the slices' chunk bounds and the mail {EL, EH, chunks, light rows, qb[0..P]}
-template <int MAXP>
+// PER > 0: every thread owns PER consecutive tiles (nb ≤ 1024·PER), loaded all at once (clamped
+// indices, no branches) and kept in registers for the write-back; PER = 0: a loop per key
+template <int MAXP, int PER>
 __global__ __launch_bounds__(1024) void k_bin_scan(uint64_t *blk, uint32_t nb, uint32_t P, uint64_t *qb, Mail mail) {
-  constexpr int K = kBinKeys + MAXP;
+  constexpr int K = kBinKeys + MAXP, PV = PER > 0 ? PER : 1;
   __shared__ unsigned long long s_w[K][16];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t per = (nb + 1023) / 1024;
+  const uint32_t per = PER > 0 ? PER : (nb + 1023) / 1024;
   const uint32_t i0 = min(nb, threadIdx.x * per), i1 = min(nb, i0 + per);
   unsigned long long c[K], incl[K];
+  uint64_t v[K][PV];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     c[k] = 0;
-    if ((uint32_t)k < kBinKeys + P)
+    if (PER > 0) {
+#pragma unroll
+      for (int p = 0; p < PV; ++p) {
+        const uint32_t i = i0 + p;
+        const uint64_t x = blk[(uint64_t)((uint32_t)k < kBinKeys + P ? k : 0) * nb + (i < nb ? i : nb - 1)];
+        // a mask, not a select: the load stays unconditional (a select lets it sink into a branch,
+        // and every branch then waits for its load)
+        v[k][p] = x & (0ull - (uint64_t)(i < i1 && (uint32_t)k < kBinKeys + P));
+        c[k] += v[k][p];
+      }
+    } else if ((uint32_t)k < kBinKeys + P) {
       for (uint32_t i = i0; i < i1; ++i) c[k] += blk[(uint64_t)k * nb + i];
+    }
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -855,10 +943,18 @@ __global__ __launch_bounds__(1024) void k_bin_scan(uint64_t *blk, uint32_t nb, u
     for (uint32_t w = 0; w < wave; ++w) run += s_w[k][w];
     run += incl[k] - c[k];
     uint64_t *a = blk + (uint64_t)k * nb;
-    for (uint32_t i = i0; i < i1; ++i) {
-      const uint64_t y = a[i];
-      a[i] = run;
-      run += y;
+    if (PER > 0) {
+#pragma unroll
+      for (int p = 0; p < PV; ++p) {
+        if (i0 + p < i1) a[i0 + p] = run;
+        run += v[k][p];
+      }
+    } else {
+      for (uint32_t i = i0; i < i1; ++i) {
+        const uint64_t y = a[i];
+        a[i] = run;
+        run += y;
+      }
     }
   }
   if (threadIdx.x == 0) {
@@ -973,9 +1069,18 @@ void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &
   KCHECK("k_bin_count");
 }
 void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s) {
-#define OMX_BS(M) hipLaunchKernelGGL((k_bin_scan<M>), dim3(1), dim3(1024), 0, s, blk, bin_tiles(R), P, qb, mail)
-  OMX_BY_MAXP(P, OMX_BS);
+  const unsigned nb = bin_tiles(R);
+  if (nb <= 4096 && P <= 4) {  // registers for (3 + P) keys × 4 tiles
+#define OMX_BS(M) hipLaunchKernelGGL((k_bin_scan<M, 4>), dim3(1), dim3(1024), 0, s, blk, nb, P, qb, mail)
+    if (P <= 1) OMX_BS(1);
+    else if (P <= 2) OMX_BS(2);
+    else OMX_BS(4);
 #undef OMX_BS
+  } else {
+#define OMX_BS(M) hipLaunchKernelGGL((k_bin_scan<M, 0>), dim3(1), dim3(1024), 0, s, blk, nb, P, qb, mail)
+    OMX_BY_MAXP(P, OMX_BS);
+#undef OMX_BS
+  }
   KCHECK("k_bin_scan");
 }
 void launch_bin_fill(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
@@ -1404,15 +1509,15 @@ void launch_expand_light_sliced(const ExpandArgs &a, const SliceArgs &sa, unsign
   if (!grid) return;
   const dim3 g(grid), b(kSliceBlock);
   if (!write) {
-    hipLaunchKernelGGL((k_expand_light_sliced<false, 8, 0>), g, b, 0, s, a, sa);
+    hipLaunchKernelGGL((k_expand_light_sliced<false, 16, 0>), g, b, 0, s, a, sa);
   } else {
     switch (a.ncarry) {
-      case 0: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 0>), g, b, 0, s, a, sa); break;
-      case 1: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 1>), g, b, 0, s, a, sa); break;
-      case 2: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 2>), g, b, 0, s, a, sa); break;
-      case 3: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 3>), g, b, 0, s, a, sa); break;
-      case 4: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 4>), g, b, 0, s, a, sa); break;
-      default: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, -1>), g, b, 0, s, a, sa); break;
+      case 0: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 0>), g, b, 0, s, a, sa); break;
+      case 1: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 1>), g, b, 0, s, a, sa); break;
+      case 2: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 2>), g, b, 0, s, a, sa); break;
+      case 3: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 3>), g, b, 0, s, a, sa); break;
+      case 4: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 4>), g, b, 0, s, a, sa); break;
+      default: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, -1>), g, b, 0, s, a, sa); break;
     }
   }
   KCHECK("k_expand_light_sliced");
@@ -1654,15 +1759,29 @@ unsigned bitmap_list_blocks(uint64_t nwords) { return nblocks(nwords, kListB); }
 
 // inclusive prefix of the segments' row counts (soffs[0] = 0, soffs[i+1] = Σ_{j<=i}) and the four
 // words a filtered expansion reads back: rows of the first nseg_h segments, all rows, member words
+// PER > 0: PER consecutive segments per thread (nseg ≤ 1024·PER), loaded at once and kept in registers
+template <int PER>
 __global__ __launch_bounds__(1024) void k_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h,
                                                      uint64_t *soffs, const unsigned long long *member,
                                                      Mail mail) {
+  constexpr int PV = PER > 0 ? PER : 1;
   __shared__ unsigned long long s_w[16];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t per = (nseg + 1023) / 1024;
+  const uint64_t per = PER > 0 ? PER : (nseg + 1023) / 1024;
   const uint64_t i0 = min(nseg, (uint64_t)threadIdx.x * per), i1 = min(nseg, i0 + per);
   unsigned long long c = 0;
-  for (uint64_t i = i0; i < i1; ++i) c += cnt[i];
+  uint32_t v[PV];
+  if (PER > 0) {
+#pragma unroll
+    for (int p = 0; p < PV; ++p) {
+      const uint64_t i = i0 + p;
+      const uint32_t x = cnt[i < nseg ? i : nseg - 1];
+      v[p] = x & (0u - (uint32_t)(i < i1));  // mask, not select (see k_bin_scan)
+      c += v[p];
+    }
+  } else {
+    for (uint64_t i = i0; i < i1; ++i) c += cnt[i];
+  }
   unsigned long long incl = c;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -1675,9 +1794,17 @@ __global__ __launch_bounds__(1024) void k_seg_totals(const uint32_t *cnt, uint64
   for (uint32_t w = 0; w < wave; ++w) base += s_w[w];
   unsigned long long run = base + incl - c;
   if (threadIdx.x == 0) soffs[0] = 0;
-  for (uint64_t i = i0; i < i1; ++i) {
-    run += cnt[i];
-    soffs[i + 1] = run;
+  if (PER > 0) {
+#pragma unroll
+    for (int p = 0; p < PV; ++p) {
+      run += v[p];
+      if (i0 + p < i1) soffs[i0 + p + 1] = run;
+    }
+  } else {
+    for (uint64_t i = i0; i < i1; ++i) {
+      run += cnt[i];
+      soffs[i + 1] = run;
+    }
   }
   __threadfence_block();
   __syncthreads();
@@ -1691,7 +1818,13 @@ __global__ __launch_bounds__(1024) void k_seg_totals(const uint32_t *cnt, uint64
 }
 void launch_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h, uint64_t *soffs,
                        const unsigned long long *member, const Mail &mail, hipStream_t s) {
-  hipLaunchKernelGGL(k_seg_totals, dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, mail);
+  if (nseg == 0) {
+    hipLaunchKernelGGL((k_seg_totals<0>), dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, mail);
+  } else if (nseg <= 8 * 1024) {
+    hipLaunchKernelGGL((k_seg_totals<8>), dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, mail);
+  } else {
+    hipLaunchKernelGGL((k_seg_totals<0>), dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, mail);
+  }
   KCHECK("k_seg_totals");
 }
 
