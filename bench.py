@@ -37,7 +37,7 @@ PARTITIONED = {"c5"}  # queries whose graph is 1-D partitioned across the ranks 
 COUNT_MODE = {"c5"}   # the last hop counts its rows (count mode)
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # ≈7e4 Person, ≈2e6 Knows
 # kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)
-HOT_KERNELS = ("k_expand_heavy", "k_expand_light", "k_check", "k_bfs_pull", "k_bfs_push", "k_bfs_prep", "k_bfs_emit",
+HOT_KERNELS = ("k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light", "k_expand_light_sliced", "k_check", "k_bfs_pull", "k_bfs_push", "k_bfs_prep", "k_bfs_emit",
                "k_gather_cols", "k_compact_segments")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md §Chip-level parameters)
 
@@ -126,6 +126,16 @@ def with_heartbeat(label, fn, every=20.0):
     finally:
         hb.kill()
         hb.wait()
+
+
+def measured_traffic(args, dom, default_scale, world):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes (tools/pmc_traffic.py
+    writes profiles/traffic.json) — only for the exact default workload they were collected on."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
+    if world != 1 or args.count or str(args.scale) != str(default_scale) or not os.path.exists(path):
+        return None
+    rec = json.load(open(path)).get(args.query)
+    return rec if rec and rec.get("kernel") == dom else None
 
 
 def main():
@@ -257,6 +267,10 @@ def main():
                     for k, v in sorted(kst.items(), key=lambda kv: -kv[1]["ms"])},
         "cpu_baseline": None,
     }
+    tr = measured_traffic(args, dom, default_scale, world)
+    if tr is not None:
+        out["roofline"]["traffic"] = tr["bytes_per_launch"]
+        out["roofline"]["traffic_source"] = tr["source"] + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(g, query, args.cpu_seconds)
     print(json.dumps(out))

@@ -40,7 +40,8 @@ class Timer {
   }
   // the traversal kernels (what OMX_FLAG_TIME_HOT keeps)
   static bool hot(const char *name) {
-    static const char *const kHot[] = {"k_expand_heavy", "k_expand_light", "k_check", "k_bfs_pull", "k_bfs_push",
+    static const char *const kHot[] = {"k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light",
+                                       "k_expand_light_sliced", "k_check", "k_bfs_pull", "k_bfs_push",
                                        "k_bfs_emit"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
@@ -836,7 +837,7 @@ class Executor {
       a.arena_cap = caph;
       a.seg_base = 0;
       if (sliced) {
-        tm_.begin("k_expand_heavy");
+        tm_.begin("k_expand_heavy_sliced");
         launch_expand_heavy_sliced(a, sa, gh, write, s_);
       } else {
         tm_.begin("k_expand_heavy");
@@ -849,7 +850,7 @@ class Executor {
       a.arena_base = heavy_rows_cap;
       a.arena_cap = capl;
       a.seg_base = (uint32_t)nseg_h;
-      tm_.begin("k_expand_light");
+      tm_.begin(lsliced ? "k_expand_light_sliced" : "k_expand_light");
       if (lsliced) launch_expand_light_sliced(a, la, gls, write, s_);
       else launch_expand(a, gl, write, s_);
       tm_.end(8 * R + 4 * EL + outw * (filt ? 0 : EL));
@@ -1136,7 +1137,8 @@ class Executor {
               launch_bfs_pull_partition(radj.p[p].rp, V, pull_E[p], pull_part[p].p, s_);
             }
             tm_.begin("k_bfs_pull");
-            launch_bfs_pull(V, radj.p[p].rp, radj.p[p].col, pull_part[p].p, pull_E[p], lanes, fr.p, vis.p, nx.p, cus(), s_);
+            launch_bfs_pull(V, radj.p[p].rp, radj.p[p].col, pull_part[p].p, pull_E[p], lanes, fr.p, vis.p, nx.p,
+                            cus(), s_);
             // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask
             tm_.end(16ull * V + 12ull * pull_E[p]);
           }
@@ -1184,9 +1186,16 @@ class Executor {
       select_rows(bflags.p, R);
       return;
     }
-    DBuf<uint32_t> rrow(&pool_, std::max<uint64_t>(ntotal, 1)), rv(&pool_, std::max<uint64_t>(ntotal, 1));
+    DBuf<uint32_t> rrow, rv;
+    if (on.size() == 1) {  // one batch: its output is already the table
+      rrow = std::move(orow[0]);
+      rv = std::move(ov[0]);
+    } else {
+      rrow = DBuf<uint32_t>(&pool_, std::max<uint64_t>(ntotal, 1));
+      rv = DBuf<uint32_t>(&pool_, std::max<uint64_t>(ntotal, 1));
+    }
     uint64_t off = 0;
-    for (size_t i = 0; i < on.size(); ++i) {
+    for (size_t i = 0; on.size() > 1 && i < on.size(); ++i) {
       HIP_CHECK(hipMemcpyAsync(rrow.p + off, orow[i].p, on[i] * 4, hipMemcpyDeviceToDevice, s_));
       HIP_CHECK(hipMemcpyAsync(rv.p + off, ov[i].p, on[i] * 4, hipMemcpyDeviceToDevice, s_));
       off += on[i];

@@ -300,7 +300,7 @@ def test_kernel_timing_reports_expand(rmat10):
     g, _ = rmat10
     rs = o.OMatchStatement(RMAT_QUERIES[0][1]).execute(g, flags=o.OMX_FLAG_KERNEL_TIMING)
     names = {k["name"] for k in rs.kernel_stats}
-    assert ("k_expand_light" in names or "k_expand_heavy" in names) and "k_eval_bitmap" in names
+    assert any(n.startswith("k_expand_") for n in names) and "k_eval_bitmap" in names
 
 
 def test_empty_and_edge_cases(rmat10):
