@@ -5,7 +5,8 @@ Default workload = BASELINE.json configs[1]: RMAT scale-22 (V = 4,194,304, 16·V
 one "step" = one full execution of that MATCH (root scan → two expansions → distinct rows in HBM;
 inputs resident in HBM before the timed region). N GPUs: one process per GPU (torch.distributed.run),
 graph replicated (it is 0.6 GB at scale 22), roots sharded v % N == rank, no data-path collective —
-rows with different roots are distinct, so no cross-rank dedup is needed for RETURN a,b,c. The barrier
+rows with different roots are distinct, so no cross-rank dedup is needed for RETURN a,b,c. Scaling is
+weak: at N ranks the root window is `age < N` (N % of the vertices), so each rank keeps ≈ the N=1 share. The barrier
 and the max-over-ranks reduction go over gloo (CPU); torch never touches the GPU here (libomx owns it).
 
 Prints ONE JSON line (rank 0).
@@ -33,6 +34,21 @@ QUERIES = {
     "c5": ("C5: RMAT 3-hop MATCH (COUNT), 1-D partitioned graph, per-hop all-to-all row exchange (RCCL)",
            "MATCH {class:Person,as:a,where:(uid < 64)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d", 26),
 }
+# Weak scaling over roots on the replicated graph (each root's DFS subtree is independent):
+# at N ranks the root window widens N-fold and every rank keeps ≈ the N=1 share (roots v % N == rank),
+# so per-GPU work is fixed as N grows. At N=1 the query is exactly configs[1]'s.
+WEAK_ROOTS = {"c2": ("age < 1", "age < %d")}
+
+
+def scaled_query(name, query, world, partitioned):
+    """The query a run at `world` ranks executes, and its scaling kind."""
+    if name in WEAK_ROOTS and not partitioned:
+        old, new = WEAK_ROOTS[name]
+        assert old in query
+        return query.replace(old, new % world), "weak"
+    return query, "strong"
+
+
 PARTITIONED = {"c5"}  # queries whose graph is 1-D partitioned across the ranks (SURVEY §8(e))
 COUNT_MODE = {"c5"}   # the last hop counts its rows (SURVEY §8(d) C5: count mode)
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # SURVEY §8(d): ≈7e4 Person, ≈2e6 Knows
@@ -155,6 +171,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of N ranks on a one-GPU box: every rank on that device (the driver's runs leave it unset)
+    local = int(os.environ.get("OMX_BENCH_DEVICE", local))
     import orientdb_amd as o  # loads libomx (and the system HIP runtime) before torch
 
     dist = None
@@ -171,6 +189,7 @@ def main():
     if args.scale is None:
         args.scale = default_scale
     partitioned = (args.partitioned or args.query in PARTITIONED) and args.scale != "ldbc"
+    query, scaling = scaled_query(args.query, query, world, partitioned)
     t_build = time.perf_counter()
     keep = rank == 0 and world == 1 and not args.no_cpu_baseline
     comm = None
@@ -242,7 +261,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt_max / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (%s, deterministic splitmix64 generator in libomx)" % graph_desc["graph"],

@@ -13,7 +13,11 @@
 // masks.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <vector>
+
 #include "devutil.h"
+#include "graph.h"
 #include "kernels.h"
 
 namespace omx {
@@ -49,19 +53,22 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
   __shared__ uint64_t s_r[3][kB / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint64_t te = 0, td = 0, tn = 0;
-  for (uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x; v < V; v += (uint64_t)gridDim.x * kB) {
-    const uint64_t f = frontier[v];
-    if (!f) continue;
-    const uint64_t vis = visited[v];
-    uint64_t m = f & ~vis;
-    if (m) visited[v] = vis | m;
-    if (expand && while_bm && !bm_test(while_bm, (uint32_t)v)) m = 0;
-    if (m != f) frontier[v] = m;
-    if (m && expand) {
-      const uint64_t d = adj_degree(adj, (uint32_t)v);
-      te += (uint64_t)__popcll(m) * d;
-      td += d;
-      tn += 1;
+  for (uint64_t v0 = (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
+    const uint64_t v = v0 + threadIdx.x;
+    const uint64_t f = v < V ? frontier[v] : 0;
+    uint64_t m = 0;
+    if (f) {
+      const uint64_t vis = visited[v];
+      m = f & ~vis;
+      if (m) visited[v] = vis | m;
+      if (expand && while_bm && !bm_test(while_bm, (uint32_t)v)) m = 0;
+      if (m != f) frontier[v] = m;
+      if (m && expand) {
+        const uint64_t d = adj_degree(adj, (uint32_t)v);
+        te += (uint64_t)__popcll(m) * d;
+        td += d;
+        tn += 1;
+      }
     }
   }
   if (!expand) return;
@@ -153,9 +160,12 @@ __global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, u
 
 // Bottom-up over one reversed adjacency part: merge-path tiles of kPullTile items over (vertices +
 // in-edges), partitioned once per traversal from the part's row_ptr (k_pull_partition with offs = rp). Consecutive lanes take consecutive in-edges (coalesced col[] loads); the in-edges of a
-// vertex whose lanes are all visited are skipped; each edge gathers its source's frontier mask. (A
-// one-bit "frontier non-empty" probe before that gather was measured 10% slower at C3: at pull levels
-// the sources of most in-edges are hubs, which are in the frontier.)
+// vertex whose lanes are all visited are skipped; each edge gathers its source's frontier mask. The
+// col array is the hub-annotated copy (k_pull_annotate): in RMAT most in-edges come from a few
+// hundred thousand high-degree sources, whose masks scattered over the V·8-B frontier cost one cache
+// line each; their copies in the dense hub array (k_hub_gather, ≤ 2 MiB) stay in L2 (C3: pull
+// 7.5 → 5.6 ms). A one-bit "frontier non-empty" probe before the gather of a non-hub mask was
+// measured 10-15% slower, with or without the hub array.
 // Masks are OR-reduced per vertex by a segmented wave scan, merged in LDS (ds_or_b64) and written
 // with one atomicOr per vertex and tile (next[] is zeroed first; k_bfs_prep masks out visited lanes).
 constexpr int kPullB = 256, kPullIPT = 4, kPullTile = kPullB * kPullIPT;
@@ -163,12 +173,12 @@ constexpr int kPullB = 256, kPullIPT = 4, kPullTile = kPullB * kPullIPT;
 __global__ __launch_bounds__(kPullB) void k_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col,
                                                      const uint64_t *part, uint64_t E, uint64_t ntiles,
                                                      uint64_t lanes, const uint64_t *frontier,
-                                                     const uint64_t *visited, uint64_t *next) {
+                                                     const uint64_t *hub_fr, const uint64_t *visited, uint64_t *next) {
   constexpr int B = kPullB, IPT = kPullIPT, T = kPullTile, W = B / 64;
-  __shared__ uint64_t s_base[T + 1];
+  // tile item jl is in-edge j0 + jl (merge-path tiles cover consecutive edges), so a row needs only
+  // its lane mask and accumulator here: 18 B per row + 2 B per item → 8 workgroups per CU
   __shared__ uint64_t s_need[T + 1];
   __shared__ unsigned long long s_acc[T + 1];
-  __shared__ uint16_t s_ls[T + 1];
   __shared__ uint16_t s_seg[T];
   __shared__ uint32_t s_wmax[W];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -188,9 +198,7 @@ __global__ __launch_bounds__(kPullB) void k_bfs_pull(uint32_t V, const uint64_t 
       const uint64_t rs = rp[r], re = rp[r + 1];
       const uint64_t s = rs > j0 ? rs - j0 : 0;
       const uint64_t e = re < j1 ? (re > j0 ? re - j0 : 0) : ne;
-      s_ls[lr] = (uint16_t)(s < ne ? s : ne);
       if (e > s && s < ne) s_seg[s] = (uint16_t)lr;
-      s_base[lr] = rs + (rs < j0 ? j0 - rs : 0);
       s_need[lr] = (e > s) ? (lanes & ~visited[r]) : 0;
       s_acc[lr] = 0;
     }
@@ -225,6 +233,10 @@ __global__ __launch_bounds__(kPullB) void k_bfs_pull(uint32_t V, const uint64_t 
       }
     }
     __syncthreads();
+    // all IPT gathers are issued before the first reduction consumes one (IPT independent
+    // col → frontier chains in flight per lane)
+    uint64_t fk[IPT];
+    uint32_t lrk[IPT];
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const uint32_t jl = k * B + tid;
@@ -233,8 +245,19 @@ __global__ __launch_bounds__(kPullB) void k_bfs_pull(uint32_t V, const uint64_t 
       uint64_t f = 0;
       if (valid) {
         const uint64_t need = s_need[lr];
-        if (need) f = frontier[col[s_base[lr] + (jl - s_ls[lr])]] & need;
+        if (need) {
+          const uint32_t x = col[j0 + jl];
+          f = (x >> 31 ? hub_fr[x & 0x7FFFFFFFu] : frontier[x]) & need;
+        }
       }
+      fk[k] = f;
+      lrk[k] = lr;
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const bool valid = k * B + tid < ne;
+      const uint32_t lr = lrk[k];
+      uint64_t f = fk[k];
       // segmented inclusive OR over the wave (a vertex's edges are consecutive lanes)
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
@@ -262,15 +285,22 @@ void launch_bfs_pull_partition(const uint64_t *rp, uint32_t V, uint64_t E, uint6
   KCHECK("k_pull_partition");
 }
 void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const uint64_t *part, uint64_t E,
-                     uint64_t lanes, const uint64_t *frontier, const uint64_t *visited, uint64_t *next, int cus,
-                     hipStream_t s) {
+                     uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *visited,
+                     uint64_t *next, int cus, hipStream_t s) {
   const uint64_t ntiles = bfs_pull_tiles(V, E);
   if (!ntiles) return;
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bfs_pull, kPullB, 0) != hipSuccess || per < 1) per = 2;
+  // resident workgroups per CU: 7 of the 8 that fit measured fastest at C3 (4.26 ms against 5.54 ms
+  // at 8 and 4.60 at 5: with a full CU the random gathers thrash L2); OMX_PULL_PER overrides
+  static const int cap = [] {
+    const char *e = std::getenv("OMX_PULL_PER");
+    return e ? std::atoi(e) : 7;
+  }();
+  if (cap > 0 && cap < per) per = cap;
   const unsigned g = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * per);
-  hipLaunchKernelGGL(k_bfs_pull, dim3(g), dim3(kPullB), 0, s, V, rp, col, part, E, ntiles, lanes, frontier, visited,
-                     next);
+  hipLaunchKernelGGL(k_bfs_pull, dim3(g), dim3(kPullB), 0, s, V, rp, col, part, E, ntiles, lanes, frontier, hub_fr,
+                     visited, next);
   KCHECK("k_bfs_pull");
 }
 
@@ -360,6 +390,88 @@ void launch_bfs_bound(const uint32_t *dst, uint64_t row0, int nl, const uint64_t
                       uint8_t *flags, hipStream_t s) {
   hipLaunchKernelGGL(k_bfs_bound, dim3(1), dim3(64), 0, s, dst, row0, nl, visited, emit_bm, flags);
   KCHECK("k_bfs_bound");
+}
+
+// ---- hub annotation (once per CSR) -------------------------------------------------------------------
+constexpr int kHist = 4096;  // degree histogram buckets (degrees ≥ 4095 share the last one)
+
+__global__ __launch_bounds__(kB) void k_deg_hist(const uint64_t *rp, uint32_t V, uint32_t *hist) {
+  __shared__ uint32_t s_h[kHist];
+  for (int i = threadIdx.x; i < kHist; i += kB) s_h[i] = 0;
+  __syncthreads();
+  for (uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x; v < V; v += (uint64_t)gridDim.x * kB) {
+    const uint64_t d = rp[v + 1] - rp[v];
+    atomicAdd(&s_h[d < kHist - 1 ? d : kHist - 1], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHist; i += kB)
+    if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
+
+// hub_idx[v] = its hub index when deg(v) ≥ t (order of discovery; any order is a valid labelling)
+__global__ __launch_bounds__(kB) void k_hub_mark(const uint64_t *rp, uint32_t V, uint64_t t, uint32_t *hub_idx,
+                                                 uint32_t *hubs, unsigned long long *count) {
+  __shared__ uint32_t s_w[kB / 64];
+  __shared__ uint32_t s_base;
+  for (uint64_t v0 = (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
+    const uint64_t v = v0 + threadIdx.x;
+    const bool hub = v < V && rp[v + 1] - rp[v] >= t;
+    uint32_t tot;
+    const uint32_t off = block_excl_scan<kB>(hub ? 1u : 0u, s_w, &tot);
+    if (threadIdx.x == 0 && tot) s_base = (uint32_t)atomicAdd(count, (unsigned long long)tot);
+    __syncthreads();
+    if (v < V) hub_idx[v] = hub ? s_base + off : 0xFFFFFFFFu;
+    if (hub) hubs[s_base + off] = (uint32_t)v;
+    __syncthreads();
+  }
+}
+
+__global__ void k_pull_annotate(const uint32_t *col, uint64_t E, const uint32_t *hub_idx, uint32_t *out) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = col[e];
+    const uint32_t h = hub_idx[c];
+    out[e] = h != 0xFFFFFFFFu ? (0x80000000u | h) : c;
+  }
+}
+
+uint32_t build_pull_col(const uint64_t *rp_other, const uint32_t *col, uint32_t V, uint64_t E, uint32_t max_hubs,
+                        uint32_t *hub_idx, uint32_t *hist, unsigned long long *count, uint32_t *hubs,
+                        uint32_t *out, int cus, hipStream_t s) {
+  HIP_CHECK(hipMemsetAsync(hist, 0, kHist * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(count, 0, sizeof(unsigned long long), s));
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 4);
+  hipLaunchKernelGGL(k_deg_hist, dim3(g), dim3(kB), 0, s, rp_other, V, hist);
+  KCHECK("k_deg_hist");
+  std::vector<uint32_t> h(kHist);
+  HIP_CHECK(hipMemcpyAsync(h.data(), hist, kHist * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  // the lowest degree threshold t ≥ 2 whose vertices (deg ≥ t) number at most max_hubs
+  uint64_t cum = 0, t = kHist;
+  for (int d = kHist - 1; d >= 2; --d) {
+    if (cum + h[d] > max_hubs) break;
+    cum += h[d];
+    t = d;
+  }
+  if (cum == 0) t = ~0ull;  // no hubs: the copy is the plain col
+  hipLaunchKernelGGL(k_hub_mark, dim3(g), dim3(kB), 0, s, rp_other, V, (uint64_t)t, hub_idx, hubs, count);
+  KCHECK("k_hub_mark");
+  if (E) {
+    const unsigned ge = (unsigned)std::min<uint64_t>(nblocks(E, kB), (uint64_t)cus * 16);
+    hipLaunchKernelGGL(k_pull_annotate, dim3(ge), dim3(kB), 0, s, col, E, hub_idx, out);
+    KCHECK("k_pull_annotate");
+  }
+  return (uint32_t)cum;
+}
+
+// per pull level: the hubs' frontier masks, packed
+__global__ void k_hub_gather(const uint32_t *hubs, uint32_t n, const uint64_t *frontier, uint64_t *hub_fr) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) hub_fr[i] = frontier[hubs[i]];
+}
+void launch_hub_gather(const uint32_t *hubs, uint32_t n, const uint64_t *frontier, uint64_t *hub_fr, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_hub_gather, dim3(nblocks(n, kB)), dim3(kB), 0, s, hubs, n, frontier, hub_fr);
+  KCHECK("k_hub_gather");
 }
 
 }  // namespace omx

@@ -139,6 +139,7 @@ class Executor {
     if (const char *sh = std::getenv("OMX_SLICE_SHIFT"))
       slice_shift_ = (uint32_t)std::min<long>(20, std::max<long>(6, std::strtol(sh, nullptr, 10)));
     if (const char *f = std::getenv("OMX_FUSE_CHECK")) fuse_mode_ = f;  // "0" disables the intersection
+    if (const char *hb = std::getenv("OMX_PULL_HUBS")) pull_hubs_ = (uint32_t)std::strtoul(hb, nullptr, 10);
     if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max<uint64_t>(1, std::strtoull(d, nullptr, 10));
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
@@ -297,6 +298,7 @@ class Executor {
   uint32_t slice_shift_ = 20;  // log2 vertices per slice (OMX_SLICE_SHIFT, 6..20: tests cut small graphs)
   std::string varlen_mode_ = "auto";
   std::string fuse_mode_ = "1";
+  uint32_t pull_hubs_ = 1u << 18;  // hub masks packed for the pull kernel (2 MiB); 0 = plain col
   uint64_t pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
 
@@ -609,6 +611,27 @@ class Executor {
       cus_ = prop.multiProcessorCount;
     }
     return cus_;
+  }
+
+  // the hub-annotated col of one CSR for the bottom-up BFS (built once per CSR, bfs.hip)
+  const uint32_t *pull_col_of(int eset, int dir, uint32_t *nhubs, const uint32_t **hubs) {
+    EdgeSet &es = g_.esets[eset];
+    *nhubs = 0;
+    *hubs = nullptr;
+    if (pull_hubs_ == 0 || g_.partitioned() || g_.V >= 0x80000000u) return g_.col(es, dir);
+    if (!es.d_pull_col[dir]) {
+      const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
+      HIP_CHECK(hipMalloc((void **)&es.d_pull_col[dir], std::max<size_t>(E * 4, 4)));
+      HIP_CHECK(hipMalloc((void **)&es.d_hubs[dir], std::max<size_t>((size_t)pull_hubs_ * 4, 4)));
+      g_.device_bytes += E * 4 + (uint64_t)pull_hubs_ * 4;
+      DBuf<uint32_t> hub_idx(&pool_, g_.V), hist(&pool_, 4096);
+      DBuf<unsigned long long> cnt(&pool_, 1);
+      es.n_hubs[dir] = build_pull_col(g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, pull_hubs_, hub_idx.p, hist.p,
+                                      cnt.p, es.d_hubs[dir], es.d_pull_col[dir], cus(), s_);
+    }
+    *nhubs = es.n_hubs[dir];
+    *hubs = es.d_hubs[dir];
+    return es.d_pull_col[dir];
   }
 
   // the slice-cut index of every part of an adjacency (built once per CSR and slice size)
@@ -1097,7 +1120,9 @@ class Executor {
     DBuf<uint32_t> list;
     DBuf<unsigned long long> stats(&pool_, 4);
     // bottom-up partitions of every reversed part (once per traversal; built on the first pull level)
-    std::vector<DBuf<uint64_t>> pull_part(radj.n);
+    std::vector<DBuf<uint64_t>> pull_part(radj.n), hub_fr(radj.n);
+    std::vector<const uint32_t *> pull_col(radj.n, nullptr), pull_hubs(radj.n, nullptr);
+    std::vector<uint32_t> pull_nh(radj.n, 0);
     std::vector<uint64_t> pull_E(radj.n);
     for (int p = 0; p < radj.n; ++p) pull_E[p] = g_.esets[rspec.parts[p].first].n_edges;
     DBuf<uint8_t> bflags;
@@ -1135,10 +1160,13 @@ class Executor {
             if (!pull_part[p].p) {
               pull_part[p] = DBuf<uint64_t>(&pool_, nt + 1);
               launch_bfs_pull_partition(radj.p[p].rp, V, pull_E[p], pull_part[p].p, s_);
+              pull_col[p] = pull_col_of(rspec.parts[p].first, rspec.parts[p].second, &pull_nh[p], &pull_hubs[p]);
+              hub_fr[p] = DBuf<uint64_t>(&pool_, std::max<uint32_t>(pull_nh[p], 1));
             }
+            launch_hub_gather(pull_hubs[p], pull_nh[p], fr.p, hub_fr[p].p, s_);
             tm_.begin("k_bfs_pull");
-            launch_bfs_pull(V, radj.p[p].rp, radj.p[p].col, pull_part[p].p, pull_E[p], lanes, fr.p, vis.p, nx.p,
-                            cus(), s_);
+            launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p].p, pull_E[p], lanes, fr.p, hub_fr[p].p, vis.p,
+                            nx.p, cus(), s_);
             // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask
             tm_.end(16ull * V + 12ull * pull_E[p]);
           }

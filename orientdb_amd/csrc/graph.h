@@ -90,6 +90,13 @@ struct EdgeSet {
   // its sorted row where neighbours reach q·2^shift (q = 1…P−1); built on the first filtered hop
   // that uses the CSR (a property of the immutable snapshot, like the sort order)
   std::map<uint32_t, uint32_t *> d_cuts[2];
+  // hub-annotated copy of a CSR's col (0 = out, 1 = in) for the bottom-up BFS (bfs.hip k_bfs_pull):
+  // a neighbour that is one of the n_hubs vertices of highest degree in the opposite CSR is stored as
+  // 0x80000000 | its hub index, so its frontier mask is read from a small L2-resident hub array;
+  // built on the first pull level over the CSR
+  uint32_t *d_pull_col[2] = {nullptr, nullptr};
+  uint32_t *d_hubs[2] = {nullptr, nullptr};
+  uint32_t n_hubs[2] = {0, 0};
 };
 
 struct Property {

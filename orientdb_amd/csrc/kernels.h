@@ -224,8 +224,13 @@ void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, u
 uint64_t bfs_pull_tiles(uint32_t V, uint64_t E);
 void launch_bfs_pull_partition(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t *part, hipStream_t s);
 void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const uint64_t *part, uint64_t E,
-                     uint64_t lanes, const uint64_t *frontier, const uint64_t *visited, uint64_t *next, int cus,
-                     hipStream_t s);
+                     uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *visited,
+                     uint64_t *next, int cus, hipStream_t s);
+// hub-annotated col of a CSR for k_bfs_pull (returns the hub count; hub_idx u32[V], hist u32[4096] scratch)
+uint32_t build_pull_col(const uint64_t *rp_other, const uint32_t *col, uint32_t V, uint64_t E, uint32_t max_hubs,
+                        uint32_t *hub_idx, uint32_t *hist, unsigned long long *count, uint32_t *hubs,
+                        uint32_t *out, int cus, hipStream_t s);
+void launch_hub_gather(const uint32_t *hubs, uint32_t n, const uint64_t *frontier, uint64_t *hub_fr, hipStream_t s);
 unsigned bfs_blocks(uint32_t V);
 void launch_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, uint32_t *blk, hipStream_t s);
 void launch_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, const uint64_t *blk_offs,

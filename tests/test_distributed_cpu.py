@@ -89,3 +89,13 @@ def test_reduce_single_process_is_identity():
     sys.path.insert(0, ROOT)
     import bench
     assert bench.reduce_over_ranks(None, 0.5, 10, 20, 3) == (0.5, 10.0, 20.0, 3.0)
+
+
+def test_bench_weak_root_window():
+    """bench.py at N ranks widens C2's root window N-fold (weak scaling); N=1 is configs[1] verbatim."""
+    import bench
+    q = bench.QUERIES["c2"][1]
+    assert bench.scaled_query("c2", q, 1, False) == (q, "weak")
+    q8, kind = bench.scaled_query("c2", q, 8, False)
+    assert kind == "weak" and "age < 8" in q8 and "age >= 90" in q8
+    assert bench.scaled_query("c5", bench.QUERIES["c5"][1], 8, True) == (bench.QUERIES["c5"][1], "strong")
