@@ -332,19 +332,25 @@ __global__ __launch_bounds__(kB) void k_bfs_emit_count(const uint64_t *visited, 
 // The block's output range is written through LDS in windows of kEmitWin entries: every thread
 // drops its (lane, vertex) pairs that fall in the window into LDS, then the block flushes the window
 // with coalesced stores (the same order as a thread-by-thread write: vertex-major, lanes ascending).
+// With carried columns (cc.n > 0) the pair's binding row is written as its columns' values
+// (cc.in[c][row0 + lane], staged once per block in LDS) instead of as a row index, so no row gather
+// follows the emission.
 constexpr uint32_t kEmitWin = 4096;
 __global__ __launch_bounds__(kB) void k_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V,
                                                        const uint64_t *blk_offs, uint32_t row0, uint32_t *out_row,
-                                                       uint32_t *out_v) {
+                                                       uint32_t *out_v, BfsCarry cc) {
   __shared__ uint32_t s_w[kB / 64];
   __shared__ uint32_t s_row[kEmitWin];
   __shared__ uint32_t s_v[kEmitWin];
+  __shared__ uint32_t s_cv[BfsCarry::kMax][64];
   const uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  for (int c = 0; c < cc.n; ++c)
+    if (threadIdx.x < cc.nl) s_cv[c][threadIdx.x] = cc.in[c][row0 + threadIdx.x];
   uint64_t m = 0;
   if (v < V && (!emit_bm || bm_test(emit_bm, (uint32_t)v))) m = visited[v];
   uint32_t tot;
   const uint32_t c = (uint32_t)__popcll(m);
-  const uint32_t off = block_excl_scan<kB>(c, s_w, &tot);
+  const uint32_t off = block_excl_scan<kB>(c, s_w, &tot);  // (its barrier also publishes s_cv)
   const uint64_t base = blk_offs[blockIdx.x];
   for (uint32_t w0 = 0; w0 < tot; w0 += kEmitWin) {
     const uint32_t w1 = min(w0 + kEmitWin, tot);
@@ -353,14 +359,16 @@ __global__ __launch_bounds__(kB) void k_bfs_emit_write(const uint64_t *visited, 
       uint32_t o = off;
       for (; o < w0; ++o) mm &= mm - 1;  // entries that belong to an earlier window
       for (; mm && o < w1; ++o) {
-        s_row[o - w0] = row0 + (uint32_t)__builtin_ctzll(mm);
+        s_row[o - w0] = (uint32_t)__builtin_ctzll(mm);
         s_v[o - w0] = (uint32_t)v;
         mm &= mm - 1;
       }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < w1 - w0; i += kB) {
-      out_row[base + w0 + i] = s_row[i];
+      const uint32_t l = s_row[i];
+      if (cc.n == 0) out_row[base + w0 + i] = row0 + l;
+      for (int k = 0; k < cc.n; ++k) cc.out[k][base + w0 + i] = s_cv[k][l];
       out_v[base + w0 + i] = s_v[i];
     }
     __syncthreads();
@@ -371,9 +379,9 @@ void launch_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uin
   KCHECK("k_bfs_emit_count");
 }
 void launch_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, const uint64_t *blk_offs,
-                           uint32_t row0, uint32_t *out_row, uint32_t *out_v, hipStream_t s) {
+                           uint32_t row0, uint32_t *out_row, uint32_t *out_v, const BfsCarry &cc, hipStream_t s) {
   hipLaunchKernelGGL(k_bfs_emit_write, dim3(nblocks(V, kB)), dim3(kB), 0, s, visited, emit_bm, V, blk_offs, row0,
-                     out_row, out_v);
+                     out_row, out_v, cc);
   KCHECK("k_bfs_emit_write");
 }
 unsigned bfs_blocks(uint32_t V) { return nblocks(V, kB); }

@@ -1132,6 +1132,10 @@ class Executor {
     DBuf<uint64_t> blk_offs(&pool_, nb + 1);
     std::vector<DBuf<uint32_t>> orow, ov;
     std::vector<uint64_t> on;
+    // up to BfsCarry::kMax bound columns are written by the emission itself (no row gather after it)
+    const std::vector<int> bcols = bound_cols();
+    const bool carry = bcols.size() <= (size_t)BfsCarry::kMax;
+    std::vector<std::vector<DBuf<uint32_t>>> oc(carry ? bcols.size() : 0);
     uint64_t ntotal = 0;
     for (uint64_t row0 = 0; row0 < R; row0 += 64) {
       const int nl = (int)std::min<uint64_t>(64, R - row0);
@@ -1202,36 +1206,52 @@ class Executor {
       cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, bit, blk_offs.p + 1, (int64_t)nb, s_); });
       const uint64_t n = read1(blk_offs.p + nb);
       if (n) {
-        orow.emplace_back(&pool_, n);
+        BfsCarry cc;
+        cc.nl = (uint32_t)nl;
+        if (carry) {
+          cc.n = (int)bcols.size();
+          for (size_t k = 0; k < bcols.size(); ++k) {
+            oc[k].emplace_back(&pool_, n);
+            cc.in[k] = col_[bcols[k]].p;
+            cc.out[k] = oc[k].back().p;
+          }
+        } else {
+          orow.emplace_back(&pool_, n);
+        }
         ov.emplace_back(&pool_, n);
         on.push_back(n);
-        launch_bfs_emit_write(vis.p, emit_bm, V, blk_offs.p, (uint32_t)row0, orow.back().p, ov.back().p, s_);
+        launch_bfs_emit_write(vis.p, emit_bm, V, blk_offs.p, (uint32_t)row0, carry ? nullptr : orow.back().p,
+                              ov.back().p, cc, s_);
         ntotal += n;
       }
-      tm_.end(16ull * V + 8ull * n);
+      // visited + emission bitmap scans (two passes) + 4 B per written column per row
+      tm_.end(16ull * V + 4ull * n * (carry ? bcols.size() + 1 : 2));
     }
     if (st.mode == T_BOUND) {
       select_rows(bflags.p, R);
       return;
     }
-    DBuf<uint32_t> rrow, rv;
-    if (on.size() == 1) {  // one batch: its output is already the table
-      rrow = std::move(orow[0]);
-      rv = std::move(ov[0]);
+    if (carry) {
+      for (size_t k = 0; k < bcols.size(); ++k) col_[bcols[k]] = concat_batches(oc[k], on, ntotal);
+      R_ = ntotal;
     } else {
-      rrow = DBuf<uint32_t>(&pool_, std::max<uint64_t>(ntotal, 1));
-      rv = DBuf<uint32_t>(&pool_, std::max<uint64_t>(ntotal, 1));
+      DBuf<uint32_t> rrow = concat_batches(orow, on, ntotal);
+      gather_rows(rrow.p, ntotal);
     }
+    col_[st.dst] = concat_batches(ov, on, ntotal);
+  }
+
+  // one column from per-batch pieces (moved when there is one piece)
+  DBuf<uint32_t> concat_batches(std::vector<DBuf<uint32_t>> &parts, const std::vector<uint64_t> &n, uint64_t total) {
+    if (parts.size() == 1) return std::move(parts[0]);
+    DBuf<uint32_t> out(&pool_, std::max<uint64_t>(total, 1));
     uint64_t off = 0;
-    for (size_t i = 0; on.size() > 1 && i < on.size(); ++i) {
-      HIP_CHECK(hipMemcpyAsync(rrow.p + off, orow[i].p, on[i] * 4, hipMemcpyDeviceToDevice, s_));
-      HIP_CHECK(hipMemcpyAsync(rv.p + off, ov[i].p, on[i] * 4, hipMemcpyDeviceToDevice, s_));
-      off += on[i];
+    for (size_t i = 0; i < parts.size(); ++i) {
+      HIP_CHECK(hipMemcpyAsync(out.p + off, parts[i].p, n[i] * 4, hipMemcpyDeviceToDevice, s_));
+      off += n[i];
     }
-    orow.clear();
-    ov.clear();
-    gather_rows(rrow.p, ntotal);
-    col_[st.dst] = std::move(rv);
+    parts.clear();
+    return out;
   }
 
   // (row, vertex) pairs level by level: the general form (any $depth use)
