@@ -199,6 +199,7 @@ class Executor {
           case S_NEWROOT:
           case S_CARTESIAN: cross_step(st); break;
           case S_KILL: R_ = 0; break;
+          case S_ROWCMP: rowcmp_step(st); break;
         }
       }
       if (p_.steps.empty()) R_ = 0;
@@ -948,6 +949,14 @@ class Executor {
     segmented_ = o.segmented;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
     col_[st.dst] = std::move(o.dst);
+  }
+
+  // WHERE conjunct `$matched.X op $currentMatch` of the alias the previous step bound
+  void rowcmp_step(const Step &st) {
+    if (R_ == 0) return;
+    DBuf<uint8_t> flags(&pool_, R_);
+    launch_flag_colcmp(col_[st.src].p, col_[st.dst].p, R_, st.row_eq, flags.p, s_);
+    select_rows(flags.p, R_);
   }
 
   // keep the rows whose flag is set (all bound columns)

@@ -1888,6 +1888,17 @@ void launch_flag_bitmap(const uint32_t *v, uint64_t n, const uint64_t *bm, uint8
   KCHECK("k_flag_bitmap");
 }
 
+// S_ROWCMP: flags[i] = (a[i] == b[i]) == eq (record identity of two bound aliases)
+__global__ void k_flag_colcmp(const uint32_t *a, const uint32_t *b, uint64_t n, int eq, uint8_t *flags) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flags[i] = (a[i] == b[i]) == (eq != 0);
+}
+void launch_flag_colcmp(const uint32_t *a, const uint32_t *b, uint64_t n, bool eq, uint8_t *flags, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_flag_colcmp, dim3(nblocks(n, 256)), dim3(256), 0, s, a, b, n, (int)eq, flags);
+  KCHECK("k_flag_colcmp");
+}
+
 __global__ void k_iota(uint32_t *out, uint64_t n) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = (uint32_t)i;

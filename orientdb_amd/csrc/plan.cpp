@@ -176,6 +176,7 @@ class Planner {
         if (n.in.empty()) fail(OMX_E_PARSE, "In current MATCH version, optional nodes must have at least one incoming pattern edge");
       }
   }
+  // the alias's whole WHERE (AND of its fragments): what the estimates see (OWhereClause.estimate)
   ExprP where_of(const std::string &alias) const {
     auto it = alias_where_.find(alias);
     if (it == alias_where_.end()) return nullptr;
@@ -183,6 +184,58 @@ class Planner {
     a->kind = Expr::AND;
     a->kids = it->second;
     return a;
+  }
+
+  // `$matched.X op $currentMatch` (either order, op = / == / != / <>): a row-level conjunct
+  static bool row_cmp(const ExprP &e, std::string *alias, bool *eq) {
+    if (!e || e->kind != Expr::CMP) return false;
+    const std::string &op = e->name;
+    if (op != "=" && op != "==" && op != "!=" && op != "<>") return false;
+    auto is_cur = [](const ExprP &x) { return x->kind == Expr::VAR && ieq(x->name, "$currentMatch"); };
+    auto matched = [](const ExprP &x, std::string *a) {
+      if (x->kind != Expr::CHAIN || x->suffixes.size() != 1 || x->suffixes[0].kind != Suffix::FIELD) return false;
+      if (x->kids[0]->kind != Expr::VAR || !ieq(x->kids[0]->name, "$matched")) return false;
+      *a = x->suffixes[0].name;
+      return true;
+    };
+    const ExprP &L = e->kids[0], &R = e->kids[1];
+    if (!((is_cur(R) && matched(L, alias)) || (is_cur(L) && matched(R, alias)))) return false;
+    *eq = op == "=" || op == "==";
+    return true;
+  }
+  static void flatten_and(const ExprP &e, std::vector<ExprP> &out) {
+    if (e->kind == Expr::AND) {
+      for (auto &k : e->kids) flatten_and(k, out);
+    } else {
+      out.push_back(e);
+    }
+  }
+  // the alias's WHERE without its row-level conjuncts (what a per-vertex bitmap can hold), and those
+  // conjuncts as (alias, equal)
+  ExprP vertex_where_of(const std::string &alias, std::vector<std::pair<std::string, bool>> *rows = nullptr) const {
+    ExprP w = where_of(alias);
+    if (!w) return nullptr;
+    std::vector<ExprP> conj, keep;
+    flatten_and(w, conj);
+    for (auto &c : conj) {
+      std::string a;
+      bool eq;
+      if (row_cmp(c, &a, &eq)) {
+        if (rows) rows->emplace_back(a, eq);
+      } else {
+        keep.push_back(c);
+      }
+    }
+    if (keep.empty()) return nullptr;
+    auto a = std::make_shared<Expr>();
+    a->kind = Expr::AND;
+    a->kids = keep;
+    return a;
+  }
+  bool has_row_conds(const std::string &alias) const {
+    std::vector<std::pair<std::string, bool>> r;
+    vertex_where_of(alias, &r);
+    return !r.empty();
   }
 
   // ---- estimates -------------------------------------------------------------------------------
@@ -649,7 +702,9 @@ class Planner {
     auto it = bm_cache_.find(key);
     if (it != bm_cache_.end()) return it->second;
     BitmapSpec s;
-    s.prog = add_prog(where_of(alias), false);
+    if (kind == 1 && has_row_conds(alias))
+      unsupported("$matched in the WHERE of a root, prefetched or cartesian alias (" + alias + ")");
+    s.prog = add_prog(vertex_where_of(alias), false);
     if (kind == 1) {
       auto c = alias_class_.find(alias);
       if (c == alias_class_.end()) fail(OMX_E_EXECUTION, "Cannot execute MATCH statement on alias " + alias + ": class not defined");
@@ -712,6 +767,17 @@ class Planner {
       bool varlen = it.filter.while_ || it.filter.has_max_depth;
       std::string m = lower(it.method);
       if (m != "out" && m != "in" && m != "both") unsupported("traversal method " + it.method + "() on the device");
+      std::vector<std::pair<std::string, bool>> rconds;
+      vertex_where_of(nodes_[t].alias, &rconds);
+      if (!rconds.empty()) {
+        if (varlen || st.mode != T_FREE)
+          unsupported("$matched in the WHERE of a variable-length, bound or prefetched target (" + nodes_[t].alias + ")");
+        for (auto &rc : rconds) {
+          auto ai = alias_idx_.find(rc.first);
+          if (ai == alias_idx_.end() || !bound[ai->second] || ai->second == t)
+            unsupported("$matched." + rc.first + " is not bound when " + nodes_[t].alias + " is matched");
+        }
+      }
       if (varlen) {
         st.kind = S_VARLEN;
         st.adj = adjacency(m, it.labels);
@@ -736,6 +802,15 @@ class Planner {
                 (st.mode == T_BOUND ? " [bound]" : st.mode == T_CAND ? " [candidates]" : " [free]");
       plan_->steps.push_back(st);
       bound[t] = true;
+      for (auto &rc : rconds) {
+        Step c;
+        c.kind = S_ROWCMP;
+        c.src = alias_idx_.at(rc.first);
+        c.dst = t;
+        c.row_eq = rc.second;
+        c.desc = "rows where $matched." + rc.first + (rc.second ? " = " : " != ") + nodes_[t].alias;
+        plan_->steps.push_back(c);
+      }
     }
     for (size_t a = 0; a < nodes_.size(); ++a)
       if (!bound[a]) {  // expandCartesianProduct (:620-650)

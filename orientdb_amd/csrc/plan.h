@@ -37,7 +37,10 @@ struct BitmapSpec {
   int class_id = -1;  // polymorphic class test (-1 = none)
 };
 
-enum StepKind { S_ROOT, S_EXPAND, S_CHECK, S_VARLEN, S_NEWROOT, S_CARTESIAN, S_KILL };
+// S_ROWCMP: keep the rows where col[src] (=|!=) col[dst]: a WHERE conjunct `$matched.X op $currentMatch`
+// of the alias the previous step bound (OMatchPathItem.executeTraversal evaluates it per neighbour
+// with $matched = the row's bindings, P/OMatchPathItem.java:49-78; identity comparison of records)
+enum StepKind { S_ROOT, S_EXPAND, S_CHECK, S_VARLEN, S_NEWROOT, S_CARTESIAN, S_KILL, S_ROWCMP };
 enum TargetMode { T_FREE, T_CAND, T_BOUND };
 
 struct Step {
@@ -50,6 +53,7 @@ struct Step {
   int where_prog = -1, while_prog = -1;  // S_VARLEN
   bool has_max_depth = false;
   int max_depth = 0;
+  bool row_eq = false;     // S_ROWCMP: = (true) or != (false)
   std::string desc;
 };
 

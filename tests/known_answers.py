@@ -67,10 +67,10 @@ KNOWN = [
      ("names", "friend"), (1, {"n4"}), True),
     ("testFriendsOfFriends2", 438,
      "match {class:Person, where:(name = 'n1'), as: me}.both('Friend').both('Friend'){as:friend, where: ($matched.me != $currentMatch)} return $matches",
-     None, ("names_not", "friend"), (None, {"n1"}), False),
+     None, ("names_not", "friend"), (None, {"n1"}), True),
     ("testFriendsOfFriends2Arrows", 452,
      "match {class:Person, where:(name = 'n1'), as: me}-Friend-{}-Friend-{as:friend, where: ($matched.me != $currentMatch)} return $matches",
-     None, ("names_not", "friend"), (None, {"n1"}), False),
+     None, ("names_not", "friend"), (None, {"n1"}), True),
     ("testFriendsWithName", 466,
      "match {class:Person, where:(name = 'n1' and 1 + 1 = 2)}.out('Friend'){as:friend, where:(name = 'n2' and 1 + 1 = 2)} return friend",
      None, ("names", "friend"), (1, {"n2"}), True),

@@ -141,6 +141,13 @@ RMAT_QUERIES = [
     ("varlen_while_prop", "MATCH {class:Person,as:s,where:(uid < 3)}-Knows->{as:v, maxDepth: 3, while:(age < 60)} RETURN s, v",
      ["s", "v"]),
     ("cartesian", "MATCH {class:Person,as:a,where:(uid < 3)},{class:Person,as:b,where:(uid > 1020)} RETURN a,b", ["a", "b"]),
+    # WHERE conjuncts on the row's bindings ($matched.X op $currentMatch, OMatchPathItem.java:49-78)
+    ("fof_not_me", "MATCH {class:Person,as:me,where:(age < 10)}-Knows->{}-Knows->{as:f, where:($matched.me != $currentMatch)} RETURN me, f",
+     ["me", "f"]),
+    ("fof_is_me", "MATCH {class:Person,as:me,where:(age < 30)}-Knows->{}-Knows->{as:f, where:($currentMatch = $matched.me)} RETURN me, f",
+     ["me", "f"]),
+    ("matched_and_filter", "MATCH {class:Person,as:me,where:(age < 20)}<-Knows-{as:x}-Knows->{as:f, where:($matched.me <> $currentMatch and age < 50)} RETURN me, x, f",
+     ["me", "x", "f"]),
     ("bound_candidate", "MATCH {class:Person,as:a,where:(uid = 1)}-Knows->{as:b},{class:Person,as:b,where:(uid < 600)} RETURN a,b",
      ["a", "b"]),
 ]
