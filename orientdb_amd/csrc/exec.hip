@@ -901,6 +901,10 @@ class Executor {
     const uint64_t nh_n[3] = {mt[0], mt[1], mt[2]};
     const uint64_t probes = mt[3];  // col[] probes of a fused closing check (4 B each, §8(d))
     o.E_member = nh_n[2];
+    if (debug_expand_)
+      std::fprintf(stderr, "[omx expand] rows out=%llu (heavy %llu) member edges=%llu probes=%llu\n",
+                   (unsigned long long)nh_n[1], (unsigned long long)nh_n[0], (unsigned long long)nh_n[2],
+                   (unsigned long long)mt[3]);
     const uint64_t n = nh_n[1];
     // the probes are split between the kernels in proportion to their edges (one counter for both)
     const uint64_t ph = E ? (uint64_t)((double)probes * (double)EH / (double)E) : 0;
