@@ -139,6 +139,7 @@ class Executor {
     if (const char *sh = std::getenv("OMX_SLICE_SHIFT"))
       slice_shift_ = (uint32_t)std::min<long>(20, std::max<long>(6, std::strtol(sh, nullptr, 10)));
     if (const char *f = std::getenv("OMX_FUSE_CHECK")) fuse_mode_ = f;  // "0" disables the intersection
+    if (const char *sw = std::getenv("OMX_SWAP_CHECK")) swap_ = std::strcmp(sw, "0") != 0;
     if (const char *hb = std::getenv("OMX_PULL_HUBS")) pull_hubs_ = (uint32_t)std::strtoul(hb, nullptr, 10);
     if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max<uint64_t>(1, std::strtoull(d, nullptr, 10));
     bms_.resize(p.bitmaps.size());
@@ -299,6 +300,7 @@ class Executor {
   uint32_t slice_shift_ = 20;  // log2 vertices per slice (OMX_SLICE_SHIFT, 6..20: tests cut small graphs)
   std::string varlen_mode_ = "auto";
   std::string fuse_mode_ = "1";
+  bool swap_ = true;  // fused closing check iterates the shorter of the two lists (OMX_SWAP_CHECK=0: off)
   uint32_t pull_hubs_ = 1u << 18;  // hub masks packed for the pull kernel (2 MiB); 0 = plain col
   uint64_t pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
@@ -938,6 +940,10 @@ class Executor {
   // fused: the following S_CHECK closes a cycle on this step's new column (sorted-
   // adjacency intersection instead of materialising the wedges and probing each)
   void expand_step(const Step &st, bool write, bool allow_segmented, const Step *check = nullptr) {
+    if (check && swap_ok(st, *check)) {
+      expand_check_swapped(st, *check, write);
+      return;
+    }
     route_owner(st.src);
     std::vector<int> cols = bound_cols();  // the carried columns (st.dst is not bound yet)
     bound_[st.dst] = 1;
@@ -961,6 +967,74 @@ class Executor {
     DBuf<uint8_t> flags(&pool_, R_);
     launch_flag_colcmp(col_[st.src].p, col_[st.dst].p, R_, st.row_eq, flags.p, s_);
     select_rows(flags.p, R_);
+  }
+
+  // The fused intersection N_x(x) ∩ N_y(y) of an expansion x → t and a closing check y → t iterates
+  // the shorter list and binary-searches the longer one. On simple adjacencies with no target filter
+  // on the expansion the result rows are the same either way (no multiplicity, the check's own filter
+  // applies to t on both sides), so rows are split by which list is shorter and each group runs the
+  // fused kernel with its roles in that order. E_t stays the reference's: Σ|N_x(x)| for the hop and
+  // Σ|N_x(x)|·|N_y(y)| for the check (k_swap_flags).
+  bool swap_ok(const Step &ex, const Step &ck) const {
+    return swap_ && !dist_ && ex.filter_bm < 0 && ex.adj.parts.size() == 1 && ck.adj.parts.size() == 1 &&
+           ex.adj.dup_free && ck.adj.dup_free && ex.adj.sorted && ck.adj.sorted;
+  }
+  void expand_check_swapped(const Step &ex, const Step &ck, bool write) {
+    const std::vector<int> cols = bound_cols();  // carried columns (ex.dst is not bound yet)
+    bound_[ex.dst] = 1;
+    const uint64_t R = R_;
+    const int ix = (int)(std::find(cols.begin(), cols.end(), ex.src) - cols.begin());
+    const int iy = (int)(std::find(cols.begin(), cols.end(), ck.src) - cols.begin());
+    DBuf<uint8_t> fl(&pool_, R);
+    DBuf<unsigned long long> sums(&pool_, 2);
+    HIP_CHECK(hipMemsetAsync(sums.p, 0, 2 * sizeof(unsigned long long), s_));
+    launch_swap_flags(col_[ex.src].p, col_[ck.src].p, R, make_adj(ex.adj), make_adj(ck.adj), fl.p, sums.p, cus(), s_);
+    // swapped rows first, the others after them (reversed: order is irrelevant)
+    DBuf<uint32_t> idx(&pool_, R);
+    DBuf<uint64_t> nsel(&pool_, 1);
+    hipcub::CountingInputIterator<uint32_t> cnt(0);
+    cub([&](void *t, size_t &b) { return hipcub::DevicePartition::Flagged(t, b, cnt, fl.p, idx.p, nsel.p, (int64_t)R, s_); });
+    launch_post_words(sums.p, 2, mail(), s_);
+    const uint64_t *h = wait_mail();
+    edges_ += h[0] + h[1];
+    const uint64_t nsw = read1(nsel.p);
+    ExpandOut og[2];
+    const uint64_t gn[2] = {nsw, R - nsw};
+    const uint32_t *gi[2] = {idx.p, idx.p + nsw};
+    const uint64_t *cfilter = bitmap(ck.filter_bm);
+    for (int g = 0; g < 2; ++g) {
+      if (gn[g] == 0) continue;
+      std::vector<DBuf<uint32_t>> gc;
+      std::vector<const uint32_t *> in, carry;
+      std::vector<uint32_t *> out;
+      for (int c : cols) {
+        gc.emplace_back(&pool_, gn[g]);
+        in.push_back(col_[c].p);
+        out.push_back(gc.back().p);
+      }
+      launch_gather_cols(gi[g], gn[g], (int)cols.size(), in.data(), out.data(), s_);
+      for (auto &b : gc) carry.push_back(b.p);
+      if (g == 0)  // |N_x(x)| > |N_y(y)|: iterate N_y(y), probe N_x(x)
+        og[g] = expand_core(gc[iy].p, gn[g], ck.adj, nullptr, carry, write, false, gc[ix].p, &ex.adj, cfilter);
+      else
+        og[g] = expand_core(gc[ix].p, gn[g], ex.adj, nullptr, carry, write, false, gc[iy].p, &ck.adj, cfilter);
+    }
+    R_ = og[0].n + og[1].n;
+    if (!write || R_ == 0) return;
+    segmented_ = false;
+    auto cat = [&](DBuf<uint32_t> &a, uint64_t na, DBuf<uint32_t> &b, uint64_t nb) {
+      if (nb == 0) return std::move(a);
+      if (na == 0) return std::move(b);
+      DBuf<uint32_t> o(&pool_, na + nb);
+      HIP_CHECK(hipMemcpyAsync(o.p, a.p, na * 4, hipMemcpyDeviceToDevice, s_));
+      HIP_CHECK(hipMemcpyAsync(o.p + na, b.p, nb * 4, hipMemcpyDeviceToDevice, s_));
+      return o;
+    };
+    for (size_t i = 0; i < cols.size(); ++i) {
+      DBuf<uint32_t> e0, e1;
+      col_[cols[i]] = cat(og[0].n ? og[0].carry[i] : e0, og[0].n, og[1].n ? og[1].carry[i] : e1, og[1].n);
+    }
+    col_[ex.dst] = cat(og[0].dst, og[0].n, og[1].dst, og[1].n);
   }
 
   // keep the rows whose flag is set (all bound columns)

@@ -198,6 +198,8 @@ void launch_gather_cols(const uint32_t *idx, uint64_t n, int ncols, const uint32
 void launch_cross(uint64_t R, int ncols, const uint32_t *const *in, uint32_t *const *out, const uint32_t *cand,
                   uint64_t ncand, uint32_t *out_dst, hipStream_t s);
 void launch_flag_bitmap(const uint32_t *v, uint64_t n, const uint64_t *bm, uint8_t *flags, hipStream_t s);
+void launch_swap_flags(const uint32_t *xs, const uint32_t *ys, uint64_t R, const DAdj &ax, const DAdj &ay,
+                       uint8_t *flags, unsigned long long *sums, int cus, hipStream_t s);
 void launch_flag_colcmp(const uint32_t *a, const uint32_t *b, uint64_t n, bool eq, uint8_t *flags, hipStream_t s);
 void launch_iota(uint32_t *out, uint64_t n, hipStream_t s);
 void launch_pack_pairs(const uint32_t *hi, const uint32_t *lo, uint64_t n, uint64_t *keys, hipStream_t s);

@@ -1888,6 +1888,45 @@ void launch_flag_bitmap(const uint32_t *v, uint64_t n, const uint64_t *bm, uint8
   KCHECK("k_flag_bitmap");
 }
 
+// Fused closing check, shorter side first: row r (x = xs[r] expanded over ax, y = ys[r] whose list ay
+// is probed) is flagged when |ax(x)| > |ay(y)|, so the intersection iterates ay(y) and probes ax(x)
+// instead. sums[0] += Σ |ax(x)| (the hop's E_t), sums[1] += Σ |ax(x)|·|ay(y)| (the check's E_t: every
+// wedge (x, y, n) traverses ay(y)); one atomic per wave.
+__global__ __launch_bounds__(256) void k_swap_flags(const uint32_t *xs, const uint32_t *ys, uint64_t R, DAdj ax,
+                                                    DAdj ay, uint8_t *flags, unsigned long long *sums) {
+  __shared__ uint64_t s_p[2][4];
+  uint64_t dx = 0, dxy = 0;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t a = adj_degree(ax, xs[r]);
+    const uint64_t b = adj_degree(ay, ys[r]);
+    flags[r] = a > b;
+    dx += a;
+    dxy += a * b;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    dx += __shfl_xor(dx, off, 64);
+    dxy += __shfl_xor(dxy, off, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_p[0][w] = dx;
+    s_p[1][w] = dxy;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {  // one atomic per block and sum: a few hundred, not one per wave
+    const uint64_t t = s_p[threadIdx.x][0] + s_p[threadIdx.x][1] + s_p[threadIdx.x][2] + s_p[threadIdx.x][3];
+    if (t) atomicAdd(&sums[threadIdx.x], (unsigned long long)t);
+  }
+}
+void launch_swap_flags(const uint32_t *xs, const uint32_t *ys, uint64_t R, const DAdj &ax, const DAdj &ay,
+                       uint8_t *flags, unsigned long long *sums, int cus, hipStream_t s) {
+  if (!R) return;
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(R, 256), (uint64_t)cus * 2);
+  hipLaunchKernelGGL(k_swap_flags, dim3(g), dim3(256), 0, s, xs, ys, R, ax, ay, flags, sums);
+  KCHECK("k_swap_flags");
+}
+
 // S_ROWCMP: flags[i] = (a[i] == b[i]) == eq (record identity of two bound aliases)
 __global__ void k_flag_colcmp(const uint32_t *a, const uint32_t *b, uint64_t n, int eq, uint8_t *flags) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
