@@ -602,9 +602,23 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
     acc += s_total;
     __syncthreads();  // LDS reuse by the next tile
   }
-  if (MEMBER) {
-    wave_add_u64(a.member_edges, medges);
-    wave_add_u64(a.member_edges + 1, mprobes);
+  if (MEMBER) {  // one atomic per block and counter (per-wave atomics on one address serialise)
+    __shared__ uint64_t s_mc[2][W];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      medges += __shfl_xor(medges, off, 64);
+      mprobes += __shfl_xor(mprobes, off, 64);
+    }
+    if (lane == 0) {
+      s_mc[0][wave] = medges;
+      s_mc[1][wave] = mprobes;
+    }
+    __syncthreads();
+    if (tid < 2) {
+      uint64_t t = 0;
+      for (int w = 0; w < W; ++w) t += s_mc[tid][w];
+      if (t) atomicAdd(a.member_edges + tid, (unsigned long long)t);
+    }
   }
   if (FILTER && tid == 0) {
     a.seg_count[a.seg_base + blockIdx.x] = (uint32_t)acc;
