@@ -46,6 +46,21 @@ def test_fused_counts_equal_unfused(rmat10, q, monkeypatch):
         assert info["1"][k] == info["0"][k], k
 
 
+@pytest.mark.parametrize("q", CYCLES, ids=[q[0] for q in CYCLES])
+def test_shorter_list_first_equals_plain_fused(rmat10, q, monkeypatch):
+    """The fused check iterates the shorter of N_x(x), N_y(y) (exec.hip expand_check_swapped); with
+    that disabled (OMX_SWAP_CHECK=0) every row expands N_x(x): same rows, bindings and E_t."""
+    import orientdb_amd as o
+    g, ref = rmat10
+    info = {}
+    for sw in ("1", "0"):
+        monkeypatch.setenv("OMX_SWAP_CHECK", sw)
+        rs = _parity(g, ref, q[1], _cols(q[1]))
+        info[sw] = rs.info
+    for k in ("n_rows", "bindings", "edges_traversed"):
+        assert info["1"][k] == info["0"][k], k
+
+
 @pytest.mark.parametrize("q", CYCLES[:3], ids=[q[0] for q in CYCLES[:3]])
 def test_cycle_parity_heavy_and_multigraph(rmat10, rmat10_raw, q, monkeypatch):
     """every row of degree ≥ 2 through the chunked kernel's fused path; parallel edges kept."""
