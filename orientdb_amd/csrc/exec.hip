@@ -616,6 +616,17 @@ class Executor {
     return cus_;
   }
 
+  // the pull tiles' merge-path split of one CSR (built once per CSR: the snapshot is immutable)
+  const uint64_t *pull_part_of(int eset, int dir, const uint64_t *rp, uint64_t E, uint64_t ntiles) {
+    EdgeSet &es = g_.esets[eset];
+    if (!es.d_pull_part[dir]) {
+      HIP_CHECK(hipMalloc((void **)&es.d_pull_part[dir], (ntiles + 1) * sizeof(uint64_t)));
+      g_.device_bytes += (ntiles + 1) * sizeof(uint64_t);
+      launch_bfs_pull_partition(rp, g_.V, E, es.d_pull_part[dir], s_);
+    }
+    return es.d_pull_part[dir];
+  }
+
   // the hub-annotated col of one CSR for the bottom-up BFS (built once per CSR, bfs.hip)
   const uint32_t *pull_col_of(int eset, int dir, uint32_t *nhubs, const uint32_t **hubs) {
     EdgeSet &es = g_.esets[eset];
@@ -1207,7 +1218,8 @@ class Executor {
     DBuf<uint32_t> list;
     DBuf<unsigned long long> stats(&pool_, 4);
     // bottom-up partitions of every reversed part (once per traversal; built on the first pull level)
-    std::vector<DBuf<uint64_t>> pull_part(radj.n), hub_fr(radj.n);
+    std::vector<DBuf<uint64_t>> hub_fr(radj.n);
+    std::vector<const uint64_t *> pull_part(radj.n, nullptr);
     std::vector<const uint32_t *> pull_col(radj.n, nullptr), pull_hubs(radj.n, nullptr);
     std::vector<uint32_t> pull_nh(radj.n, 0);
     std::vector<uint64_t> pull_E(radj.n);
@@ -1248,15 +1260,14 @@ class Executor {
         if (h[1] * pull_div_ > eadj) {
           for (int p = 0; p < radj.n; ++p) {
             const uint64_t nt = bfs_pull_tiles(V, pull_E[p]);
-            if (!pull_part[p].p) {
-              pull_part[p] = DBuf<uint64_t>(&pool_, nt + 1);
-              launch_bfs_pull_partition(radj.p[p].rp, V, pull_E[p], pull_part[p].p, s_);
+            if (!pull_part[p]) {
+              pull_part[p] = pull_part_of(rspec.parts[p].first, rspec.parts[p].second, radj.p[p].rp, pull_E[p], nt);
               pull_col[p] = pull_col_of(rspec.parts[p].first, rspec.parts[p].second, &pull_nh[p], &pull_hubs[p]);
               hub_fr[p] = DBuf<uint64_t>(&pool_, std::max<uint32_t>(pull_nh[p], 1));
             }
             launch_hub_gather(pull_hubs[p], pull_nh[p], fr.p, hub_fr[p].p, s_);
             tm_.begin("k_bfs_pull");
-            launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p].p, pull_E[p], lanes, fr.p, hub_fr[p].p, vis.p,
+            launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p], pull_E[p], lanes, fr.p, hub_fr[p].p, vis.p,
                             nx.p, cus(), s_);
             // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask
             tm_.end(16ull * V + 12ull * pull_E[p]);

@@ -97,6 +97,8 @@ struct EdgeSet {
   uint32_t *d_pull_col[2] = {nullptr, nullptr};
   uint32_t *d_hubs[2] = {nullptr, nullptr};
   uint32_t n_hubs[2] = {0, 0};
+  // merge-path split of the CSR into pull tiles (bfs.hip k_pull_partition), built with d_pull_col
+  uint64_t *d_pull_part[2] = {nullptr, nullptr};
 };
 
 struct Property {

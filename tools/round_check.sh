@@ -14,7 +14,7 @@ for q in c3 c4; do
 done
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp && cd "$R" || exit 1
-for q in c2 c3; do
+for q in c2 c3 c4; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$q" -o run --output-format csv \
     -- python3 bench.py --query $q --no-cpu-baseline > "$OUT/prof_$q.log" 2>&1 || { tail -20 "$OUT/prof_$q.log"; exit 1; }
 done
