@@ -41,7 +41,8 @@ class Timer {
   // the traversal kernels (what OMX_FLAG_TIME_HOT keeps)
   static bool hot(const char *name) {
     static const char *const kHot[] = {"k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light",
-                                       "k_expand_light_sliced", "k_check", "k_bfs_pull", "k_bfs_push",
+                                       "k_expand_light_sliced", "k_expand_light_check", "k_expand_heavy_check",
+                                       "k_check", "k_bfs_pull", "k_bfs_push",
                                        "k_bfs_emit"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
@@ -877,7 +878,7 @@ class Executor {
         tm_.begin("k_expand_heavy_sliced");
         launch_expand_heavy_sliced(a, sa, gh, write, s_);
       } else {
-        tm_.begin("k_expand_heavy");
+        tm_.begin(member ? "k_expand_heavy_check" : "k_expand_heavy");
         launch_expand_heavy(a, gh, write, s_);
       }
       tm_.end(4 * EH + outw * (filt ? 0 : EH));
@@ -887,7 +888,7 @@ class Executor {
       a.arena_base = heavy_rows_cap;
       a.arena_cap = capl;
       a.seg_base = (uint32_t)nseg_h;
-      tm_.begin(lsliced ? "k_expand_light_sliced" : "k_expand_light");
+      tm_.begin(lsliced ? "k_expand_light_sliced" : member ? "k_expand_light_check" : "k_expand_light");
       if (lsliced) launch_expand_light_sliced(a, la, gls, write, s_);
       else launch_expand(a, gl, write, s_);
       tm_.end(8 * R + 4 * EL + outw * (filt ? 0 : EL));
