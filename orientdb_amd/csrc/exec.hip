@@ -633,7 +633,9 @@ class Executor {
     EdgeSet &es = g_.esets[eset];
     *nhubs = 0;
     *hubs = nullptr;
-    if (pull_hubs_ == 0 || g_.partitioned() || g_.V >= 0x80000000u) return g_.col(es, dir);
+    // k_bfs_pull reads bit 31 of a col entry as the hub tag: vertex ids must stay below 2^31
+    if (g_.V >= 0x80000000u) unsupported("variable-length traversal over 2^31 or more vertices");
+    if (pull_hubs_ == 0 || g_.partitioned()) return g_.col(es, dir);
     if (!es.d_pull_col[dir]) {
       const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
       HIP_CHECK(hipMalloc((void **)&es.d_pull_col[dir], std::max<size_t>(E * 4, 4)));
