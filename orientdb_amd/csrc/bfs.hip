@@ -168,7 +168,14 @@ __global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, u
 // measured 10-15% slower, with or without the hub array.
 // Masks are OR-reduced per vertex by a segmented wave scan, merged in LDS (ds_or_b64) and written
 // with one atomicOr per vertex and tile (next[] is zeroed first; k_bfs_prep masks out visited lanes).
-constexpr int kPullB = 256, kPullIPT = 4, kPullTile = kPullB * kPullIPT;
+#ifndef OMX_PULL_B
+#define OMX_PULL_B 256
+#endif
+#ifndef OMX_PULL_IPT
+#define OMX_PULL_IPT 4
+#endif
+constexpr int kPullB = OMX_PULL_B, kPullIPT = OMX_PULL_IPT, kPullTile = kPullB * kPullIPT;
+static_assert(kPullTile <= 65535, "s_seg holds tile-local row indices in 16 bits");
 
 __global__ __launch_bounds__(kPullB) void k_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col,
                                                      const uint64_t *part, uint64_t E, uint64_t ntiles,
