@@ -1,13 +1,20 @@
 """Benchmark: MATCH edges traversed/sec (GTEPS) + bindings/sec on a synthetic RMAT Person/Knows graph.
 
-Default workload = BASELINE.json configs[1]: RMAT scale-22 (V = 4,194,304, 16·V raw edges, simple),
+Default workload = BASELINE.json's metric config, "RMAT-24 2-hop" (`--query m1`): RMAT scale-24
+(V = 16,777,216, 16·V raw edges, simple: 263 M edges) with configs[1]'s 2-hop query,
   MATCH {class:Person,as:a,where:(age < 1)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a,b,c
-one "step" = one full execution of that MATCH (root scan → two expansions → distinct rows in HBM;
-inputs resident in HBM before the timed region). N GPUs: one process per GPU (torch.distributed.run),
-graph replicated (it is 0.6 GB at scale 22), roots sharded v % N == rank, no data-path collective —
-rows with different roots are distinct, so no cross-rank dedup is needed for RETURN a,b,c. Scaling is
-weak: at N ranks the root window is `age < N` (N % of the vertices), so each rank keeps ≈ the N=1 share. The barrier
-and the max-over-ranks reduction go over gloo (CPU); torch never touches the GPU here (libomx owns it).
+(root window 1 %, target window 10 %: 168 K roots, E_t ≈ 1.03e10 edges, ≈ 1.03e9 distinct rows per step,
+SURVEY §8(d) "adjust to keep ≤ ~1e9 rows"). `--query c2` is configs[1] itself (the same query at scale 22);
+c1/c3/c4/c5 are the other configs. One "step" = one full execution of the MATCH (root scan → expansions
+→ distinct rows in HBM; inputs resident in HBM before the timed region).
+
+N GPUs (one process per GPU, torch.distributed.run): by default the graph is 1-D PARTITIONED (SURVEY
+§8(e), BASELINE north_star): rank r generates and holds the CSR rows of the vertices [r·B, (r+1)·B),
+starts from the roots it owns, and binding rows travel to the owner of the vertex whose adjacency the
+next hop reads (RCCL all-to-all over xGMI). The query is the same at every N: scaling is "strong".
+`--replicated`: the graph is replicated, roots sharded v % N == rank, no data-path collective, and the
+root window widens to `age < N` so per-GPU work is fixed ("weak"). The barrier and the max-over-ranks
+reduction go over gloo (CPU); torch never touches the GPU here (libomx owns it).
 
 Prints ONE JSON line (rank 0).
 """
@@ -24,6 +31,8 @@ sys.path.insert(0, ROOT)
 METRIC = "MATCH edges traversed/sec (GTEPS) + bindings/sec, RMAT-24 2-hop, 1-8 GPUs"
 # name → (workload, query, default RMAT scale)
 QUERIES = {
+    "m1": ("M1: RMAT-24 2-hop MATCH with WHERE on both ends (the metric's own config; configs[1]'s query at scale 24)",
+           "MATCH {class:Person,as:a,where:(age < 1)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a,b,c", 24),
     "c2": ("C2: RMAT 2-hop MATCH with WHERE property filter on both ends",
            "MATCH {class:Person,as:a,where:(age < 1)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a,b,c", 22),
     "c1": ("C1: RMAT 2-hop MATCH friends-of-friends", "MATCH {class:Person}-Knows->{}-Knows->{as:fof} RETURN fof", 16),
@@ -37,19 +46,19 @@ QUERIES = {
 # Weak scaling over roots on the replicated graph (each root's DFS subtree is independent):
 # at N ranks the root window widens N-fold and every rank keeps ≈ the N=1 share (roots v % N == rank),
 # so per-GPU work is fixed as N grows. At N=1 the query is exactly configs[1]'s.
-WEAK_ROOTS = {"c2": ("age < 1", "age < %d")}
+WEAK_ROOTS = {"c2": ("age < 1", "age < %d"), "m1": ("age < 1", "age < %d")}
 
 
 def scaled_query(name, query, world, partitioned):
     """The query a run at `world` ranks executes, and its scaling kind."""
-    if name in WEAK_ROOTS and not partitioned:
+    if world > 1 and name in WEAK_ROOTS and not partitioned:
         old, new = WEAK_ROOTS[name]
         assert old in query
         return query.replace(old, new % world), "weak"
     return query, "strong"
 
 
-PARTITIONED = {"c5"}  # queries whose graph is 1-D partitioned across the ranks (SURVEY §8(e))
+REPLICATED_ONLY = {"c1", "c3", "c4"}  # partitioned snapshots reject these plans (varlen, LDBC replicas, SURVEY §8(e))
 COUNT_MODE = {"c5"}   # the last hop counts its rows (SURVEY §8(d) C5: count mode)
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # SURVEY §8(d): ≈7e4 Person, ≈2e6 Knows
 # kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)
@@ -85,14 +94,28 @@ def cpu_baseline_varlen(g, nroots, depth, target_s, threads):
             "bindings_per_s": pairs / secs}
 
 
+def host_threads():
+    """Threads for the CPU baseline: the host cores this job may use. On the GPU box that is its CPU
+    share per GPU, which the harness exports as OMP_NUM_THREADS (16); os.cpu_count() there reports the
+    whole machine, whose other cores belong to other jobs. Returns (threads, cores visible)."""
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:
+        visible = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(share, visible) if share > 0 else visible), visible
+
+
 def cpu_baseline(g, query, target_s=12.0):
     """The oracle's C DFS restatement (oracle/dfs_ref.c) on the host cores, on a bounded sample of
     the same workload's roots; GTEPS over the sampled roots."""
     import numpy as np
     from oracle import dfs
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads, visible = host_threads()
     if "while:($depth < 4)" in query:
-        return cpu_baseline_varlen(g, 64, 4, target_s, threads)
+        r = cpu_baseline_varlen(g, 64, 4, target_s, threads)
+        r["cores_visible"] = visible
+        return r
     rp, col = g.csr
     cg = dfs.CsrGraph(rp, col, {"uid": np.arange(g.V, dtype=np.int64), "age": g.age})
     probe = dfs.run(cg, query, nthreads=threads, emit=False, root_sample=64)
@@ -112,9 +135,10 @@ def cpu_baseline(g, query, target_s=12.0):
         secs += r["seconds"]
         reps += 1
     return {"value": edges / secs / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
-            "sample": "%d of %d roots x %d repetitions (%.1f s, %d edges, %d bindings; oracle/dfs_ref.c DFS, %d threads)" % (
-                sample, nroots_total, reps, secs, edges, bindings, threads),
-            "bindings_per_s": bindings / secs}
+            "sample": "%d of %d roots x %d repetitions (%.1f s, %d edges, %d bindings; oracle/dfs_ref.c DFS, %d threads "
+                      "= the job's host-core share (OMP_NUM_THREADS), %d cores visible)" % (
+                sample, nroots_total, reps, secs, edges, bindings, threads, visible),
+            "bindings_per_s": bindings / secs, "cores_visible": visible}
 
 
 def reduce_over_ranks(dist, dt, edges, bindings, rows):
@@ -161,12 +185,12 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scale", default=None, help="RMAT scale or 'ldbc' (default: the query's config)")
-    ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
+    ap.add_argument("--query", default="m1", choices=sorted(QUERIES))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--count", action="store_true", help="COUNT mode (the last hop counts its rows)")
-    ap.add_argument("--partitioned", action="store_true",
-                    help="1-D partition the graph across the ranks and exchange rows per hop (default for c5)")
+    ap.add_argument("--replicated", action="store_true",
+                    help="N > 1: replicate the graph and shard roots (weak scaling) instead of 1-D partitioning it")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -189,7 +213,7 @@ def main():
     workload, query, default_scale = QUERIES[args.query]
     if args.scale is None:
         args.scale = default_scale
-    partitioned = (args.partitioned or args.query in PARTITIONED) and args.scale != "ldbc"
+    partitioned = world > 1 and not args.replicated and args.query not in REPLICATED_ONLY and args.scale != "ldbc"
     query, scaling = scaled_query(args.query, query, world, partitioned)
     t_build = time.perf_counter()
     keep = rank == 0 and world == 1 and not args.no_cpu_baseline
@@ -269,12 +293,14 @@ def main():
         "config": {"workload": workload, "query": query, **graph_desc,
                    "V": g.V, "E": g.n_edges, "rows_per_step": int(rows_all),
                    "edges_per_step": int(edges_all / args.steps), "bindings_per_step": int(bindings_all / args.steps),
-                   # edges whose neighbour ids a kernel read; a COUNT run sums an unfiltered last hop
-                   # from degrees (E_t per SURVEY §8(d) still counts those edges)
+                   # adjacency entries a kernel iterated (omx_result_info.edges_read): E_t minus a COUNT
+                   # run's unfiltered last hop (summed from degrees) and minus the E_t of cycle-closing
+                   # checks answered by binary search (E_t per SURVEY §8(d) still counts both)
                    "edges_read_per_step": int(edges_read_all / args.steps),
-                   "parallelism": ("1-D partitioned graph over %d GPU(s), rows exchanged per hop (RCCL all-to-all)"
+                   "parallelism": ("1-D partitioned graph over %d GPUs, rows exchanged per hop (RCCL all-to-all)"
                                    % world) if comm is not None else
-                                  ("roots sharded v%%N across %d GPU(s), graph replicated" % world),
+                                  ("1 GPU" if world == 1 else
+                                   "roots sharded v%%N across %d GPUs, graph replicated" % world),
                    "mode": "count" if mode == o.OMX_MODE_COUNT else "materialize (rows kept in HBM)",
                    "graph_build_s": round(t_build, 2)},
         "bindings_per_s": bindings_all / dt_max,

@@ -154,6 +154,8 @@ int omx_statement_explain(omx_statement *s, const omx_graph *g, const omx_value 
 #define OMX_FLAG_KEEP_DEVICE   4 /* do not copy rows to the host (benchmarking; rows stay in HBM)   */
 #define OMX_FLAG_TIME_HOT      8 /* with KERNEL_TIMING: time only the traversal kernels (expansion,  */
                                  /* check, BFS levels), so the events do not stretch a timed step     */
+#define OMX_FLAG_DIGEST       16 /* compute omx_result_info.digest on the device (works with         */
+                                 /* KEEP_DEVICE: whole-result parity checks without a host copy)      */
 
 typedef struct omx_exec_options {
   int32_t mode;          /* OMX_MODE_*                                                            */
@@ -178,8 +180,13 @@ typedef struct omx_result_info {
   uint64_t alg_bytes;        /* algorithmic HBM bytes, SURVEY §8(d)                                */
   double device_ms;          /* wall time of the device part (root scan → last kernel)             */
   double total_ms;           /* wall time of omx_execute                                           */
-  uint64_t edges_read;       /* edges whose neighbour ids were read: edges_traversed minus the hops */
-                             /* a COUNT run sums from degrees (an unfiltered last hop)              */
+  uint64_t edges_read;       /* adjacency entries a kernel iterated one by one: edges_traversed     */
+                             /* minus the hops a COUNT run sums from degrees (an unfiltered last    */
+                             /* hop) and minus the E_t a cycle-closing check stands for (answered   */
+                             /* by binary searches into the sorted adjacency, never iterated)       */
+  uint64_t digest;           /* OMX_FLAG_DIGEST: Σ over the distinct rows of h(row) mod 2^64, h =   */
+                             /* splitmix64 chained over the row's RIDs in column order (h0 =        */
+                             /* 0x9E3779B97F4A7C15, h = mix(h ^ rid)); 0 otherwise                  */
 } omx_result_info;
 
 int omx_result_info_get(const omx_result *r, omx_result_info *info);

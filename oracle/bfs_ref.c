@@ -34,13 +34,22 @@ static void push_pair(pairs *p, uint32_t a, uint32_t b) {
 
 /* Returns the number of (root index, v) results; pairs in *out when emit != 0 (malloc'ed, 2 u32 per
  * pair). max_depth < 0 = unbounded. where_bm may be NULL. */
-int64_t bfs_varlen(const uint64_t *rp, const uint32_t *col, uint32_t V, const uint32_t *roots, int64_t nroots,
-                   int32_t max_depth, const uint64_t *where_bm, int32_t nthreads, int32_t emit, uint32_t **out,
-                   uint64_t *out_pairs, uint64_t *edges) {
+static inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+/* *digest (may be NULL): Σ over the (root, v) results of the row hash of (rid_base | roots[i],
+ * rid_base | v) — the device's OMX_FLAG_DIGEST of `RETURN s, v` (oracle/dfs.py row_digest). */
+int64_t bfs_varlen_ex(const uint64_t *rp, const uint32_t *col, uint32_t V, const uint32_t *roots, int64_t nroots,
+                      int32_t max_depth, const uint64_t *where_bm, int32_t nthreads, int32_t emit, uint32_t **out,
+                      uint64_t *out_pairs, uint64_t *edges, uint64_t rid_base, uint64_t *digest) {
   if (nthreads < 1) nthreads = 1;
   pairs *sinks = (pairs *)calloc(nthreads, sizeof(pairs));
   uint64_t *tedges = (uint64_t *)calloc(nthreads, sizeof(uint64_t));
   uint64_t *tcount = (uint64_t *)calloc(nthreads, sizeof(uint64_t));
+  uint64_t *tdig = (uint64_t *)calloc(nthreads, sizeof(uint64_t));
 #pragma omp parallel num_threads(nthreads)
   {
     const int t = omp_get_thread_num();
@@ -58,6 +67,7 @@ int64_t bfs_varlen(const uint64_t *rp, const uint32_t *col, uint32_t V, const ui
           const uint32_t v = queue[q];
           if (!where_bm || bm(where_bm, v)) {
             tcount[t]++;
+            if (digest) tdig[t] += mix64(mix64(0x9E3779B97F4A7C15ull ^ (rid_base | roots[i])) ^ (rid_base | v));
             if (emit) push_pair(&sinks[t], (uint32_t)i, v);
           }
         }
@@ -80,11 +90,13 @@ int64_t bfs_varlen(const uint64_t *rp, const uint32_t *col, uint32_t V, const ui
     free(stamp);
     free(queue);
   }
-  uint64_t total = 0, ed = 0;
+  uint64_t total = 0, ed = 0, dg = 0;
   for (int t = 0; t < nthreads; ++t) {
     total += tcount[t];
     ed += tedges[t];
+    dg += tdig[t];
   }
+  if (digest) *digest = dg;
   if (emit) {
     uint32_t *buf = (uint32_t *)malloc((total ? total : 1) * 2 * sizeof(uint32_t));
     uint64_t off = 0;
@@ -100,5 +112,12 @@ int64_t bfs_varlen(const uint64_t *rp, const uint32_t *col, uint32_t V, const ui
   free(sinks);
   free(tedges);
   free(tcount);
+  free(tdig);
   return (int64_t)total;
+}
+
+int64_t bfs_varlen(const uint64_t *rp, const uint32_t *col, uint32_t V, const uint32_t *roots, int64_t nroots,
+                   int32_t max_depth, const uint64_t *where_bm, int32_t nthreads, int32_t emit, uint32_t **out,
+                   uint64_t *out_pairs, uint64_t *edges) {
+  return bfs_varlen_ex(rp, col, V, roots, nroots, max_depth, where_bm, nthreads, emit, out, out_pairs, edges, 0, NULL);
 }

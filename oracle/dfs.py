@@ -42,31 +42,52 @@ def lib():
         L.dfs_run.restype = C.c_int64
         L.dfs_run.argtypes = [C.POINTER(dfs_plan), C.c_int32, C.POINTER(C.c_uint32), C.c_int64, C.c_int32, C.c_int32,
                               C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.dfs_run_ex.restype = C.c_int64
+        L.dfs_run_ex.argtypes = L.dfs_run.argtypes + [C.POINTER(C.c_int32), C.c_int32, C.c_uint64,
+                                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.dfs_free.argtypes = [C.c_void_p]
         L.bfs_varlen.restype = C.c_int64
         L.bfs_varlen.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
                                  C.c_int64, C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                  C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.bfs_varlen_ex.restype = C.c_int64
+        L.bfs_varlen_ex.argtypes = L.bfs_varlen.argtypes + [C.c_uint64, C.POINTER(C.c_uint64)]
         _lib = L
     return _lib
 
 
+MIX_H0 = 0x9E3779B97F4A7C15
+RID_BASE = 11 << 48  # the synthetic Person cluster (GraphSnapshot.rmat: RID #11:v)
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+    return z ^ (z >> np.uint64(31))
+
+
+def row_digest(rows):
+    """Σ over rows of the splitmix64 chain of the row's RIDs mod 2^64 (rows: u64 [n, k], distinct) — the
+    same function as the device's OMX_FLAG_DIGEST (kernels.hip k_digest)."""
+    rows = np.asarray(rows, np.uint64)
+    if rows.ndim == 1:
+        rows = rows[:, None]
+    with np.errstate(over="ignore"):
+        h = np.full(rows.shape[0], MIX_H0, np.uint64)
+        for c in range(rows.shape[1]):
+            h = _mix64(h ^ rows[:, c])
+        return int(h.sum(dtype=np.uint64)) if len(h) else 0
+
+
 class CsrGraph:
-    """Person/Knows graph as arrays: out CSR, in CSR, property columns (name → numpy array)."""
+    """Person/Knows graph as arrays: out CSR, in CSR (built on first use), property columns."""
 
     def __init__(self, rp, col, columns, trp=None, tcol=None, simple=True):
         self.V = len(rp) - 1
         self.rp = np.ascontiguousarray(rp, np.uint64)
         self.col = np.ascontiguousarray(col, np.uint32)
-        if trp is None:
-            src = np.repeat(np.arange(self.V, dtype=np.uint32), np.diff(self.rp).astype(np.int64))
-            order = np.lexsort((src, self.col))
-            tcol = src[order]
-            cnt = np.bincount(self.col, minlength=self.V)
-            trp = np.zeros(self.V + 1, np.uint64)
-            trp[1:] = np.cumsum(cnt)
-        self.trp = np.ascontiguousarray(trp, np.uint64)
-        self.tcol = np.ascontiguousarray(tcol, np.uint32)
+        self._trp = None if trp is None else np.ascontiguousarray(trp, np.uint64)
+        self._tcol = None if tcol is None else np.ascontiguousarray(tcol, np.uint32)
         self.columns = columns
         self.simple = simple
         # a schema-only RefDB for the planner (class counts; no records are traversed through it)
@@ -78,6 +99,26 @@ class CsrGraph:
         self._count = self.V
         db.count = lambda c: self.V if c in ("Person", "V") else 0
         self.schema = db
+
+    def _transpose(self):
+        src = np.repeat(np.arange(self.V, dtype=np.uint32), np.diff(self.rp).astype(np.int64))
+        order = np.lexsort((src, self.col))
+        self._tcol = np.ascontiguousarray(src[order], np.uint32)
+        cnt = np.bincount(self.col, minlength=self.V)
+        self._trp = np.zeros(self.V + 1, np.uint64)
+        self._trp[1:] = np.cumsum(cnt)
+
+    @property
+    def trp(self):
+        if self._trp is None:
+            self._transpose()
+        return self._trp
+
+    @property
+    def tcol(self):
+        if self._tcol is None:
+            self._transpose()
+        return self._tcol
 
 
 def np_eval(e, cols, params):
@@ -124,9 +165,11 @@ def _bm_from_mask(mask):
     return words
 
 
-def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=None):
+def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=None, digest=None, distinct=None):
     """Returns dict(rows=np.uint32[n, k] (distinct, sorted; None when emit=False), aliases, bindings,
-    edges, seconds, nroots)."""
+    edges, seconds, nroots). digest = RETURN aliases: every binding's projection is hashed (row_digest of
+    RIDs #11:v) into r["digest"] — the digest of the result when its rows are distinct by construction.
+    distinct = one RETURN alias: r["distinct"] = its distinct vertex ids (sorted), via a V-bit set."""
     mo = MatchOracle(g.schema, query)
     pmap = MatchOracle._param_map(params)
     est = mo.estimate_root_entries(Ctx(pmap))
@@ -169,7 +212,8 @@ def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=No
         m = it.method.lower()
         if not fwd:
             m = {"out": "in", "in": "out", "both": "both"}[m]
-        parts = {"out": [(g.rp, g.col)], "in": [(g.trp, g.tcol)], "both": [(g.rp, g.col), (g.trp, g.tcol)]}[m]
+        parts = {"out": lambda: [(g.rp, g.col)], "in": lambda: [(g.trp, g.tcol)],
+                 "both": lambda: [(g.rp, g.col), (g.trp, g.tcol)]}[m]()
         if it.labels and not any(lab.lower() in ("knows", "e") for lab in it.labels):
             parts = []
         st.nparts = len(parts)
@@ -199,9 +243,14 @@ def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=No
     out = C.POINTER(C.c_uint32)()
     nrows = C.c_uint64()
     edges = C.c_uint64()
+    proj = [aidx[a] for a in (digest or ([distinct] if distinct else []))]
+    parr = (C.c_int32 * max(1, len(proj)))(*proj)
+    dg = C.c_uint64()
+    seen = np.zeros((g.V + 63) // 64, np.uint64) if distinct else None
     t0 = time.perf_counter()
-    b = lib().dfs_run(C.byref(plan), aidx[root], roots.ctypes.data_as(C.POINTER(C.c_uint32)), len(roots), nthreads,
-                      int(emit), C.byref(out), C.byref(nrows), C.byref(edges))
+    b = lib().dfs_run_ex(C.byref(plan), aidx[root], roots.ctypes.data_as(C.POINTER(C.c_uint32)), len(roots), nthreads,
+                         int(emit), C.byref(out), C.byref(nrows), C.byref(edges), parr, len(proj), RID_BASE,
+                         C.byref(dg), seen.ctypes.data_as(C.POINTER(C.c_uint64)) if seen is not None else None)
     dt = time.perf_counter() - t0
     rows = None
     if emit:
@@ -209,13 +258,19 @@ def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=No
         arr = np.ctypeslib.as_array(out, shape=(max(n, 1) * len(aliases),))[:n * len(aliases)].copy()
         lib().dfs_free(C.cast(out, C.c_void_p))
         rows = np.unique(arr.reshape(n, len(aliases)), axis=0) if n else arr.reshape(0, len(aliases))
-    return {"rows": rows, "aliases": aliases, "bindings": b, "edges": edges.value, "seconds": dt, "nroots": len(roots)}
+    res = {"rows": rows, "aliases": aliases, "bindings": b, "edges": edges.value, "seconds": dt, "nroots": len(roots)}
+    if digest:
+        res["digest"] = dg.value
+    if distinct:
+        bits = np.unpackbits(seen.view(np.uint8), bitorder="little")[:g.V]
+        res["distinct"] = np.nonzero(bits)[0].astype(np.uint32)
+    return res
 
 
 def bfs_varlen(rp, col, roots, max_depth=-1, where_mask=None, nthreads=1, emit=True):
     """oracle/bfs_ref.c: variable-length item with depth-free WHERE and a depth-only while (the result
     is the BFS ball of radius max_depth; -1 = unbounded). Returns dict(pairs=np.uint32[n, 2] of
-    (root index, v) or None, n, edges, seconds)."""
+    (root index, v) or None, n, edges, seconds, digest = row_digest of the (RID(root), RID(v)) rows)."""
     rp = np.ascontiguousarray(rp, np.uint64)
     col = np.ascontiguousarray(col, np.uint32)
     roots = np.ascontiguousarray(roots, np.uint32)
@@ -225,13 +280,14 @@ def bfs_varlen(rp, col, roots, max_depth=-1, where_mask=None, nthreads=1, emit=T
     npairs = C.c_uint64()
     edges = C.c_uint64()
     t0 = time.perf_counter()
-    n = lib().bfs_varlen(rp.ctypes.data_as(C.POINTER(C.c_uint64)), col.ctypes.data_as(C.POINTER(C.c_uint32)), V,
-                         roots.ctypes.data_as(C.POINTER(C.c_uint32)), len(roots), int(max_depth),
-                         wb.ctypes.data_as(C.POINTER(C.c_uint64)) if wb is not None else None, int(nthreads),
-                         int(emit), C.byref(out), C.byref(npairs), C.byref(edges))
+    dg = C.c_uint64()
+    n = lib().bfs_varlen_ex(rp.ctypes.data_as(C.POINTER(C.c_uint64)), col.ctypes.data_as(C.POINTER(C.c_uint32)), V,
+                            roots.ctypes.data_as(C.POINTER(C.c_uint32)), len(roots), int(max_depth),
+                            wb.ctypes.data_as(C.POINTER(C.c_uint64)) if wb is not None else None, int(nthreads),
+                            int(emit), C.byref(out), C.byref(npairs), C.byref(edges), RID_BASE, C.byref(dg))
     dt = time.perf_counter() - t0
     pairs = None
     if emit:
         pairs = np.ctypeslib.as_array(out, shape=(max(1, npairs.value) * 2,))[:npairs.value * 2].reshape(-1, 2).copy()
         lib().dfs_free(C.cast(out, C.c_void_p))
-    return {"pairs": pairs, "n": int(n), "edges": int(edges.value), "seconds": dt}
+    return {"pairs": pairs, "n": int(n), "edges": int(edges.value), "seconds": dt, "digest": dg.value}

@@ -52,12 +52,36 @@ typedef struct {
   uint64_t bindings;
   int emit;
   int k;
+  /* whole-result checks at sizes where rows cannot be kept: the projected columns of every binding are
+     hashed (digest of a result whose rows are distinct by construction), or, for a one-column
+     projection, marked in a V-bit set (the distinct set, OBasicCommandContext.addToUniqueResult) */
+  const int32_t *proj;
+  int32_t nproj;
+  uint64_t rid_base;
+  uint64_t digest;
+  uint64_t *seen;
 } sink;
+
+/* splitmix64 finalizer; the row hash chains it over the RIDs (same function as the device's
+   OMX_FLAG_DIGEST and oracle/dfs.py row_digest) */
+static inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
 
 static inline int bm(const uint64_t *b, uint32_t v) { return (int)((b[v >> 6] >> (v & 63)) & 1ull); }
 
 static void emit_row(sink *s, const uint32_t *bind) {
   s->bindings++;
+  if (s->seen) {
+    const uint32_t v = bind[s->proj[0]];
+    __atomic_fetch_or(&s->seen[v >> 6], 1ull << (v & 63), __ATOMIC_RELAXED);
+  } else if (s->nproj) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int c = 0; c < s->nproj; ++c) h = mix64(h ^ (s->rid_base | bind[s->proj[c]]));
+    s->digest += h;
+  }
   if (!s->emit) return;
   if (s->n == s->cap) {
     s->cap = s->cap ? s->cap * 2 : 1024;
@@ -140,13 +164,21 @@ done:
 
 /* Runs the DFS from every root (bound to alias `root_alias`) on `nthreads` threads.
  * Returns complete bindings; rows (naliases u32 per row) when emit != 0, in *out (malloc'ed). */
-int64_t dfs_run(const dfs_plan *p, int32_t root_alias, const uint32_t *roots, int64_t nroots, int32_t nthreads,
-                int32_t emit, uint32_t **out, uint64_t *out_rows, uint64_t *edges) {
+/* dfs_run_ex: proj[0..nproj) = the RETURN columns (alias indices); with nproj > 0 every binding's
+ * projection is hashed into *digest (RIDs = rid_base | dense id), or, when seen != NULL (nproj == 1),
+ * set in the V-bit set `seen` instead. */
+int64_t dfs_run_ex(const dfs_plan *p, int32_t root_alias, const uint32_t *roots, int64_t nroots, int32_t nthreads,
+                   int32_t emit, uint32_t **out, uint64_t *out_rows, uint64_t *edges, const int32_t *proj,
+                   int32_t nproj, uint64_t rid_base, uint64_t *digest, uint64_t *seen) {
   if (nthreads < 1) nthreads = 1;
   sink *sinks = (sink *)calloc(nthreads, sizeof(sink));
   for (int t = 0; t < nthreads; ++t) {
     sinks[t].emit = emit;
     sinks[t].k = p->naliases;
+    sinks[t].proj = proj;
+    sinks[t].nproj = nproj;
+    sinks[t].rid_base = rid_base;
+    sinks[t].seen = nproj == 1 ? seen : NULL;
   }
 #pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads)
   for (int64_t i = 0; i < nroots; ++i) {
@@ -156,8 +188,9 @@ int64_t dfs_run(const dfs_plan *p, int32_t root_alias, const uint32_t *roots, in
     bind[root_alias] = roots[i];
     process(p, 0, bind, s);
   }
-  uint64_t total = 0, rows = 0, ed = 0;
+  uint64_t total = 0, rows = 0, ed = 0, dg = 0;
   for (int t = 0; t < nthreads; ++t) {
+    dg += sinks[t].digest;
     total += sinks[t].bindings;
     rows += sinks[t].n;
     ed += sinks[t].edges;
@@ -174,8 +207,14 @@ int64_t dfs_run(const dfs_plan *p, int32_t root_alias, const uint32_t *roots, in
     *out_rows = rows;
   }
   if (edges) *edges = ed;
+  if (digest) *digest = dg;
   free(sinks);
   return (int64_t)total;
+}
+
+int64_t dfs_run(const dfs_plan *p, int32_t root_alias, const uint32_t *roots, int64_t nroots, int32_t nthreads,
+                int32_t emit, uint32_t **out, uint64_t *out_rows, uint64_t *edges) {
+  return dfs_run_ex(p, root_alias, roots, nroots, nthreads, emit, out, out_rows, edges, NULL, 0, 0, NULL, NULL);
 }
 
 void dfs_free(void *p) { free(p); }

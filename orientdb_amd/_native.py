@@ -13,7 +13,7 @@ OMX_OK, OMX_E_UNSUPPORTED, OMX_E_INVALID, OMX_E_OOM, OMX_E_DEVICE, OMX_E_PARSE, 
 OMX_PROP_INT32, OMX_PROP_INT64, OMX_PROP_DOUBLE, OMX_PROP_STRING, OMX_PROP_BOOL = 1, 2, 3, 4, 5
 OMX_VAL_NULL, OMX_VAL_INT, OMX_VAL_DOUBLE, OMX_VAL_STRING, OMX_VAL_BOOL = 0, 1, 2, 3, 4
 OMX_MODE_MATERIALIZE, OMX_MODE_COUNT = 0, 1
-OMX_FLAG_KERNEL_TIMING, OMX_FLAG_NO_RID_MAP, OMX_FLAG_KEEP_DEVICE, OMX_FLAG_TIME_HOT = 1, 2, 4, 8
+OMX_FLAG_KERNEL_TIMING, OMX_FLAG_NO_RID_MAP, OMX_FLAG_KEEP_DEVICE, OMX_FLAG_TIME_HOT, OMX_FLAG_DIGEST = 1, 2, 4, 8, 16
 
 
 class omx_class_desc(C.Structure):
@@ -59,7 +59,8 @@ class omx_exec_options(C.Structure):
 class omx_result_info(C.Structure):
     _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_int32), ("deduplicated", C.c_int32),
                 ("edges_traversed", C.c_uint64), ("bindings", C.c_uint64), ("alg_bytes", C.c_uint64),
-                ("device_ms", C.c_double), ("total_ms", C.c_double), ("edges_read", C.c_uint64)]
+                ("device_ms", C.c_double), ("total_ms", C.c_double), ("edges_read", C.c_uint64),
+                ("digest", C.c_uint64)]
 
 
 # every exported symbol of include/omx/match.h: name -> (restype, argtypes)

@@ -180,14 +180,15 @@ class Executor {
         // the last expansion of a plan whose rows are distinct by construction may stay block-
         // segmented in HBM when the rows are not copied to the host
         bool seg_ok = last && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES &&
-                      (o_.flags & OMX_FLAG_KEEP_DEVICE);
+                      (o_.flags & OMX_FLAG_KEEP_DEVICE) && !(o_.flags & OMX_FLAG_DIGEST);
         // expansion + closing check fused into one intersection pass
         const Step *fuse = nullptr;
         if (st.kind == S_EXPAND && i + 1 < p_.steps.size() && fuse_ok(st, p_.steps[i + 1])) {
           fuse = &p_.steps[i + 1];
           const bool last2 = i + 2 == p_.steps.size();
           count_only = last2 && o_.mode == OMX_MODE_COUNT && p_.unique_by_construction;
-          seg_ok = last2 && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES && (o_.flags & OMX_FLAG_KEEP_DEVICE);
+          seg_ok = last2 && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES &&
+                   (o_.flags & OMX_FLAG_KEEP_DEVICE) && !(o_.flags & OMX_FLAG_DIGEST);
           expand_step(st, !count_only, seg_ok, fuse);
           counted_only = count_only;
           ++i;
@@ -223,6 +224,14 @@ class Executor {
     }
     int64_t limit = p_.limit >= 0 ? p_.limit : o_.limit;
     if (limit > -1 && n > (uint64_t)std::max<int64_t>(limit, 1)) n = (uint64_t)std::max<int64_t>(limit, 1);
+    if (n > 0 && !counted_only && (o_.flags & OMX_FLAG_DIGEST)) {
+      std::vector<const uint32_t *> cp;
+      for (auto &c : out) cp.push_back(c.p);
+      DBuf<unsigned long long> d(&pool_, 1);
+      HIP_CHECK(hipMemsetAsync(d.p, 0, 8, s_));
+      launch_digest(ncols, cp.data(), n, (o_.flags & OMX_FLAG_NO_RID_MAP) ? nullptr : g_.d_rids, d.p, cus(), s_);
+      digest_ = read1(reinterpret_cast<const uint64_t *>(d.p));
+    }
     if (n > 0 && !counted_only && !(o_.flags & OMX_FLAG_KEEP_DEVICE)) {
       DBuf<uint64_t> rids(&pool_, n * ncols);
       std::vector<const uint32_t *> cp;
@@ -253,7 +262,8 @@ class Executor {
     res->info.n_cols = n ? ncols : 0;
     res->info.deduplicated = dedup_ran_;
     res->info.edges_traversed = edges_;
-    res->info.edges_read = edges_ - degree_counted_;
+    res->info.edges_read = edges_iter_;
+    res->info.digest = digest_;
     res->info.bindings = bindings_;
     res->info.alg_bytes = alg_bytes_;
     res->info.device_ms = dms;
@@ -290,7 +300,10 @@ class Executor {
   std::vector<DBuf<uint32_t>> col_;
   uint64_t R_ = 1;
   uint64_t edges_ = 0, alg_bytes_ = 0, bindings_ = 0;
-  uint64_t degree_counted_ = 0;  // edges of count-only unfiltered hops (summed from degrees, not read)
+  // adjacency entries iterated one by one (omx_result_info.edges_read): E_t minus count-only hops summed
+  // from degrees and minus the E_t of closing checks answered by binary search
+  uint64_t edges_iter_ = 0;
+  uint64_t digest_ = 0;  // OMX_FLAG_DIGEST
   int dedup_ran_ = 0;
   int cus_ = 0;
   uint64_t heavy_deg_ = kHeavyDeg;
@@ -967,7 +980,7 @@ class Executor {
                               check ? col_[check->src].p : nullptr, check ? &check->adj : nullptr,
                               check ? bitmap(check->filter_bm) : nullptr);
     edges_ += o.E + o.E_member;
-    if (o.counted_from_degrees) degree_counted_ += o.E;
+    if (!o.counted_from_degrees) edges_iter_ += o.E;
     R_ = o.n;
     if (!write || R_ == 0) return;
     segmented_ = o.segmented;
@@ -1033,6 +1046,7 @@ class Executor {
       else
         og[g] = expand_core(gc[ix].p, gn[g], ex.adj, nullptr, carry, write, false, gc[iy].p, &ck.adj, cfilter);
     }
+    edges_iter_ += og[0].E + og[1].E;  // the iterated lists (the probed ones are binary-searched)
     R_ = og[0].n + og[1].n;
     if (!write || R_ == 0) return;
     segmented_ = false;
@@ -1259,6 +1273,7 @@ class Executor {
         tm_.amend(8ull * V + 24ull * h[2]);  // frontier scan + visited and row_ptr pair of the active vertices
         if (h[2] == 0) break;
         edges_ += h[0];
+        edges_iter_ += h[0];
         HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
         if (h[1] * pull_div_ > eadj) {
           for (int p = 0; p < radj.n; ++p) {
@@ -1428,6 +1443,7 @@ class Executor {
       if (ng == 0) break;
       ExpandOut ex = expand_core(gvp, ng, st.adj, nullptr, {gr}, true);
       edges_ += ex.E;
+      edges_iter_ += ex.E;
       if (ex.n == 0) break;
       DBuf<uint64_t> keys(&pool_, ex.n);
       launch_pack_pairs(ex.carry[0].p, ex.dst.p, ex.n, keys.p, s_);

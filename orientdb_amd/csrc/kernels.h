@@ -211,6 +211,9 @@ void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uin
 void launch_flag_row_change(int ncols, const uint32_t *const *cols, uint64_t n, uint8_t *flags, hipStream_t s);
 void launch_map_rids(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, uint64_t *out,
                      hipStream_t s);
+// *out += Σ_rows splitmix64-chain(RIDs of the row) (OMX_FLAG_DIGEST; rids == nullptr: dense ids)
+void launch_digest(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, unsigned long long *out,
+                   int cus, hipStream_t s);
 // host evaluation of a predicate program that reads no vertex data (constants and $depth only)
 bool eval_pred_const(const DPred &pred, int64_t depth);
 

@@ -2056,4 +2056,38 @@ void launch_map_rids(int ncols, const uint32_t *const *cols, uint64_t n, const u
   KCHECK("k_map_rids");
 }
 
+// ---- order-independent digest of a result table (OMX_FLAG_DIGEST) --------------------------------------
+// digest = Σ_rows h(row) mod 2^64, h = splitmix64 chained over the row's RIDs in column order (the same
+// function as oracle/dfs.py row_digest): the parity tests compare whole result sets of ~1e9 rows
+// without copying them to the host.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void k_digest(int ncols, ColPtrs cp, uint64_t n, const uint64_t *rids,
+                                                unsigned long long *out) {
+  uint64_t acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (int c = 0; c < ncols; ++c) {
+      const uint32_t v = cp.in[c][i];
+      h = mix64(h ^ (rids ? rids[v] : (uint64_t)v));
+    }
+    acc += h;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+void launch_digest(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, unsigned long long *out,
+                   int cus, hipStream_t s) {
+  if (!n || !ncols) return;
+  ColPtrs cp;
+  for (int c = 0; c < ncols; ++c) cp.in[c] = cols[c];
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(n, 256), (uint64_t)cus * 8);
+  hipLaunchKernelGGL(k_digest, dim3(g), dim3(256), 0, s, ncols, cp, n, rids, out);
+  KCHECK("k_digest");
+}
+
 }  // namespace omx

@@ -91,11 +91,21 @@ def test_reduce_single_process_is_identity():
     assert bench.reduce_over_ranks(None, 0.5, 10, 20, 3) == (0.5, 10.0, 20.0, 3.0)
 
 
-def test_bench_weak_root_window():
-    """bench.py at N ranks widens C2's root window N-fold (weak scaling); N=1 is configs[1] verbatim."""
+def test_bench_scaling_modes():
+    """bench.py: N=1 runs the config verbatim; N > 1 on the (default) partitioned graph keeps the query
+    (strong scaling); --replicated widens the root window N-fold (weak scaling)."""
     import bench
-    q = bench.QUERIES["c2"][1]
-    assert bench.scaled_query("c2", q, 1, False) == (q, "weak")
-    q8, kind = bench.scaled_query("c2", q, 8, False)
-    assert kind == "weak" and "age < 8" in q8 and "age >= 90" in q8
+    assert bench.QUERIES["m1"][1] == bench.QUERIES["c2"][1] and bench.QUERIES["m1"][2] == 24
+    for name in ("m1", "c2"):
+        q = bench.QUERIES[name][1]
+        assert bench.scaled_query(name, q, 1, False) == (q, "strong")
+        assert bench.scaled_query(name, q, 8, True) == (q, "strong")
+        q8, kind = bench.scaled_query(name, q, 8, False)
+        assert kind == "weak" and "age < 8" in q8 and "age >= 90" in q8
     assert bench.scaled_query("c5", bench.QUERIES["c5"][1], 8, True) == (bench.QUERIES["c5"][1], "strong")
+
+
+def test_bench_host_threads():
+    import bench
+    threads, visible = bench.host_threads()
+    assert 1 <= threads <= visible

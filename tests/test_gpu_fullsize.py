@@ -1,0 +1,113 @@
+"""Full-size parity of BASELINE.json's configs against the C oracle restatements.
+
+Every config is run verbatim at its own scale through the C-ABI and compared with oracle/dfs_ref.c
+(OMatchStatement.processContext, P/OMatchStatement.java:412-568) or oracle/bfs_ref.c (the
+variable-length item, P/OMatchPathItem.java:79-105):
+
+* C1  RMAT-16, all 65,536 roots, `RETURN fof`: the distinct set, bit-exact (≤ 65,536 RIDs);
+* C2  RMAT-22 2-hop with WHERE on both ends: row count, E_t and the order-independent digest of all
+      155 M (a, b, c) RID tuples (OMX_FLAG_DIGEST: Σ splitmix64-chain(row) mod 2^64, kernels.hip k_digest
+      = oracle/dfs.py row_digest), rows left in HBM;
+* M1  the metric's own workload, RMAT-24 2-hop (C2's query at scale 24, ≈1.0e9 rows): the same;
+* C3  RMAT-24, 64 roots, `while:($depth < 4)`: row count, E_t (Σ frontier degrees) and digest;
+* C5  the 3-hop COUNT shape on a 4-rank 1-D partition of RMAT-16 (thread transport): the ranks' bindings
+      and edges add up to the oracle's, and the ranks' digests of the materialized rows add up to it.
+
+The oracle's digest sums every binding's hash; for these queries the rows are distinct by construction
+(simple graph, every alias returned), so that is the digest of the result set.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, os.cpu_count() or 1)  # the GPU box's CPU share
+C2_QUERY = "MATCH {class:Person,as:a,where:(age < 1)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a,b,c"
+
+
+def _cg(g):
+    from oracle import dfs
+    return dfs.CsrGraph(g.csr[0], g.csr[1], {"uid": np.arange(g.V, dtype=np.int64), "age": g.age})
+
+
+def _digest_run(g, query):
+    import orientdb_amd as o
+    return o.OMatchStatement(query).execute(g, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST, documents=False)
+
+
+def test_c1_fof_all_roots_rmat16():
+    """configs[0] verbatim: every Person is a root; 4e8 pre-dedup bindings collapse to the distinct fof set."""
+    import orientdb_amd as o
+    from oracle import dfs
+    g = o.GraphSnapshot.rmat(16, device=0, keep_csr=True)
+    q = "MATCH {class:Person}-Knows->{}-Knows->{as:fof} RETURN fof"
+    ref = dfs.run(_cg(g), q, nthreads=THREADS, emit=False, distinct="fof")
+    rs = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_NO_RID_MAP, documents=False)
+    assert ref["nroots"] == g.V
+    assert rs.info["bindings"] == ref["bindings"]
+    assert rs.info["edges_traversed"] == ref["edges"]
+    assert rs.info["n_rows"] == len(ref["distinct"])
+    assert np.array_equal(np.sort(rs.rows[:, 0].astype(np.uint32)), ref["distinct"])
+
+
+def test_c2_rmat22_digest():
+    """configs[1] verbatim at RMAT-22."""
+    import orientdb_amd as o
+    from oracle import dfs
+    g = o.GraphSnapshot.rmat(22, device=0, keep_csr=True)
+    ref = dfs.run(_cg(g), C2_QUERY, nthreads=THREADS, emit=False, digest=["a", "b", "c"])
+    rs = _digest_run(g, C2_QUERY)
+    assert rs.info["n_rows"] == rs.info["bindings"] == ref["bindings"] > 1e8
+    assert rs.info["edges_traversed"] == ref["edges"]
+    assert rs.info["digest"] == ref["digest"]
+
+
+@pytest.fixture(scope="module")
+def rmat24():
+    import orientdb_amd as o
+    g = o.GraphSnapshot.rmat(24, device=0, keep_csr=True)
+    yield g
+    g.close()
+
+
+def test_m1_rmat24_two_hop_digest(rmat24):
+    """The metric's own config (BASELINE.json: RMAT-24 2-hop): C2's query at scale 24, ≈1e9 distinct rows."""
+    from oracle import dfs
+    g = rmat24
+    ref = dfs.run(_cg(g), C2_QUERY, nthreads=THREADS, emit=False, digest=["a", "b", "c"])
+    rs = _digest_run(g, C2_QUERY)
+    assert rs.info["n_rows"] == rs.info["bindings"] == ref["bindings"] > 5e8
+    assert rs.info["edges_traversed"] == ref["edges"]
+    assert rs.info["digest"] == ref["digest"]
+
+
+def test_c3_rmat24_varlen_digest(rmat24):
+    """configs[2] verbatim: 64 roots, while:($depth < 4) (BFS ball of radius 4 per root)."""
+    from oracle import dfs
+    g = rmat24
+    q = "MATCH {class:Person,as:s,where:(uid < 64)}-Knows->{as:v, while:($depth < 4)} RETURN s, v"
+    ref = dfs.bfs_varlen(g.csr[0], g.csr[1], np.arange(64, dtype=np.uint32), max_depth=4, nthreads=THREADS,
+                         emit=False)
+    rs = _digest_run(g, q)
+    assert rs.info["n_rows"] == ref["n"] > 1e8
+    assert rs.info["edges_traversed"] == ref["edges"]
+    assert rs.info["digest"] == ref["digest"]
+
+
+def test_c5_shape_partitioned_rmat16():
+    """configs[4]'s 3-hop shape on a 4-rank 1-D partition of RMAT-16 (rows exchanged per hop)."""
+    import orientdb_amd as o
+    from oracle import dfs
+    from tests.test_gpu_dist import run_ranks
+    q = "MATCH {class:Person,as:a,where:(uid < 64)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d"
+    full = o.GraphSnapshot.rmat(16, device=0, keep_csr=True)
+    ref = dfs.run(_cg(full), q, nthreads=THREADS, emit=False, digest=["a", "b", "c", "d"])
+    parts = [o.GraphSnapshot.rmat(16, device=0, partition=(r, 4)) for r in range(4)]
+    cnt = run_ranks(parts, q, mode=o.OMX_MODE_COUNT)
+    assert sum(r.info["bindings"] for r in cnt) == ref["bindings"] > 1e6
+    assert sum(r.info["edges_traversed"] for r in cnt) == ref["edges"]
+    mat = run_ranks(parts, q, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST)
+    assert sum(r.info["n_rows"] for r in mat) == ref["bindings"]
+    assert sum(r.info["digest"] for r in mat) % (1 << 64) == ref["digest"]
