@@ -21,8 +21,9 @@
  * Conventions: plain C types only; every function returns an int status (OMX_OK = 0) unless it is
  * a getter; on failure omx_last_error() (thread-local) describes the error. OMX_E_UNSUPPORTED means
  * "valid MATCH, but not executable by this engine": the host (the Java OMatchStatement strategy) falls
- * back to the reference executor. Handles are not thread-safe; a graph may be shared read-only by
- * several statements executed one at a time per host thread.
+ * back to the reference executor. A graph may be executed from several host threads: omx_execute
+ * serialises the executions of one graph (its stream, scratch pool and adjacency caches are per graph).
+ * A statement handle belongs to one thread at a time (it caches its compiled plan).
  */
 #ifndef OMX_MATCH_H
 #define OMX_MATCH_H

@@ -2,6 +2,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 
 #include "dist.h"
@@ -12,6 +13,9 @@
 
 struct omx_graph {
   std::unique_ptr<omx::Graph> g;
+  // a snapshot may be executed from several host threads (OrientDB sessions): its stream, scratch pool,
+  // host mailbox and lazily built adjacency caches are per graph, so executions are serialised
+  std::mutex m;
 };
 struct omx_statement {
   std::unique_ptr<omx::Statement> st;
@@ -152,7 +156,7 @@ void omx_exec_options_init(omx_exec_options *o) {
 }
 
 int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, omx_result **out) {
-  return guard([&] {
+  const int rc = guard([&] {
     if (!g || !s || !out) omx::fail(OMX_E_INVALID, "null argument");
     omx_exec_options o;
     omx_exec_options_init(&o);
@@ -166,8 +170,12 @@ int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, om
       s->plan_graph = g->g->uid;
       s->plan_key = key;
     }
+    std::lock_guard<std::mutex> lk(g->m);
     *out = omx::execute_plan(*g->g, *s->plan, o, o.comm ? o.comm->t.get() : nullptr);
   });
+  // a rank that fails (planning included) releases the peers waiting for it in an exchange
+  if (rc != OMX_OK && opts && opts->comm) opts->comm->t->abort();
+  return rc;
 }
 
 int omx_comm_unique_id(uint8_t *id) {

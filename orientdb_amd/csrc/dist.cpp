@@ -27,14 +27,22 @@ ThreadHub::ThreadHub(int w) : world(w), counts(w, std::vector<uint64_t>(w, 0)), 
 
 void ThreadHub::barrier() {
   std::unique_lock<std::mutex> lk(m);
+  if (aborted) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: another rank failed");
   const uint64_t gen = generation;
   if (++arrived == world) {
     arrived = 0;
     ++generation;
     cv.notify_all();
   } else {
-    cv.wait(lk, [&] { return generation != gen; });
+    cv.wait(lk, [&] { return generation != gen || aborted; });
+    if (generation == gen) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: another rank failed");
   }
+}
+
+void ThreadHub::abort() {
+  std::lock_guard<std::mutex> lk(m);
+  aborted = true;
+  cv.notify_all();
 }
 
 namespace {
@@ -87,6 +95,8 @@ class ThreadTransport : public Transport {
     hub_->barrier();  // peers are done reading this rank's send buffers
   }
 
+  void abort() override { hub_->abort(); }
+
  private:
   std::shared_ptr<ThreadHub> hub_;
   int rank_;
@@ -109,11 +119,17 @@ class RcclTransport : public Transport {
     if (d_recv_) (void)hipFree(d_recv_);
     if (comm_) (void)ncclCommDestroy(comm_);
   }
+  // peers inside a collective with this rank are released with an error (ncclCommAbort)
+  void abort() override {
+    if (comm_) (void)ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
   int rank() const override { return rank_; }
   int world() const override { return world_; }
 
   void counts(const uint64_t *d_send, std::vector<uint64_t> &send, std::vector<uint64_t> &recv,
               hipStream_t s) override {
+    if (!comm_) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: the communicator was aborted");
     NCCL_OK(ncclAllToAll(d_send, d_recv_, 1, ncclUint64, comm_, s));
     send.assign(world_, 0);
     recv.assign(world_, 0);
@@ -125,6 +141,7 @@ class RcclTransport : public Transport {
   void alltoallv(const std::vector<const uint32_t *> &sbuf, const std::vector<uint64_t> &send,
                  const std::vector<uint64_t> &sdispl, const std::vector<uint32_t *> &rbuf,
                  const std::vector<uint64_t> &recv, const std::vector<uint64_t> &rdispl, hipStream_t s) override {
+    if (!comm_) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: the communicator was aborted");
     std::vector<size_t> sc(send.begin(), send.end()), sd(sdispl.begin(), sdispl.end()), rc(recv.begin(), recv.end()),
         rd(rdispl.begin(), rdispl.end());
     NCCL_OK(ncclGroupStart());

@@ -38,13 +38,18 @@ class Transport {
   virtual void alltoallv(const std::vector<const uint32_t *> &sbuf, const std::vector<uint64_t> &send,
                          const std::vector<uint64_t> &sdispl, const std::vector<uint32_t *> &rbuf,
                          const std::vector<uint64_t> &recv, const std::vector<uint64_t> &rdispl, hipStream_t s) = 0;
+  // called when this rank's execute fails: peers blocked in (or later entering) an exchange fail too
+  // instead of waiting forever. The communicator is unusable afterwards.
+  virtual void abort() = 0;
 };
 
 // threads of one process as ranks
 struct ThreadHub {
   explicit ThreadHub(int w);
-  void barrier();
+  void barrier();  // throws OmxError once a rank has aborted
+  void abort();
   const int world;
+  bool aborted = false;
   std::mutex m;
   std::condition_variable cv;
   int arrived = 0;

@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 
 #include "dist.h"
 #include "kernels.h"
@@ -149,6 +150,8 @@ class Executor {
     if (const char *r = std::getenv("OMX_ROUTE_SELF")) route_self_ = std::strcmp(r, "0") != 0;
     debug_expand_ = std::getenv("OMX_DEBUG_EXPAND") != nullptr;  // one stderr line per expansion
     if (const char *ls = std::getenv("OMX_LIGHT_SLICED")) light_sliced_ = std::strcmp(ls, "0") != 0;
+    if (const char *ae = std::getenv("OMX_ARENA_ESTIMATE")) arena_estimate_ = std::strcmp(ae, "0") != 0;
+    if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
     dist_setup();
   }
 
@@ -203,6 +206,7 @@ class Executor {
           case S_CARTESIAN: cross_step(st); break;
           case S_KILL: R_ = 0; break;
           case S_ROWCMP: rowcmp_step(st); break;
+          case S_MULTI: multi_step(st); break;
         }
       }
       if (p_.steps.empty()) R_ = 0;
@@ -318,6 +322,11 @@ class Executor {
   uint32_t pull_hubs_ = 1u << 18;  // hub masks packed for the pull kernel (2 MiB); 0 = plain col
   uint64_t pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
+  // sliced hops size their arenas from the target bitmap's density (OMX_ARENA_ESTIMATE=0: exact bound;
+  // OMX_ARENA_MARGIN scales the estimate, 0 forces the short-arena re-run in tests)
+  bool arena_estimate_ = true;
+  double arena_margin_ = 1.25;
+  uint64_t arena_retries_ = 0;
 
   // ---- helpers -----------------------------------------------------------------------------------
   template <class F>
@@ -511,8 +520,8 @@ class Executor {
       fail(OMX_E_INVALID, "snapshot rows [" + std::to_string(g_.part_lo) + ", " + std::to_string(g_.part_hi) +
                               ") are not rank " + std::to_string(r) + "'s block of " + std::to_string(W));
     for (const Step &st : p_.steps)
-      if (st.kind == S_VARLEN || st.kind == S_NEWROOT || st.kind == S_CARTESIAN)
-        unsupported("variable-length items and disconnected patterns are not supported on a partitioned snapshot");
+      if (st.kind == S_VARLEN || st.kind == S_MULTI || st.kind == S_NEWROOT || st.kind == S_CARTESIAN)
+        unsupported("variable-length and multi-step items and disconnected patterns are not supported on a partitioned snapshot");
     for (const PredProgram &pp : p_.progs)
       for (const DPredInstr &in : pp.code)
         if (in.op == P_PUSH_DEG) unsupported("out()/in()/both().size() in WHERE is not supported on a partitioned snapshot");
@@ -633,10 +642,18 @@ class Executor {
   // the pull tiles' merge-path split of one CSR (built once per CSR: the snapshot is immutable)
   const uint64_t *pull_part_of(int eset, int dir, const uint64_t *rp, uint64_t E, uint64_t ntiles) {
     EdgeSet &es = g_.esets[eset];
-    if (!es.d_pull_part[dir]) {
-      HIP_CHECK(hipMalloc((void **)&es.d_pull_part[dir], (ntiles + 1) * sizeof(uint64_t)));
+    if (!es.d_pull_part[dir]) {  // built into a local buffer, published once complete
+      uint64_t *part = nullptr;
+      HIP_CHECK(hipMalloc((void **)&part, (ntiles + 1) * sizeof(uint64_t)));
+      try {
+        launch_bfs_pull_partition(rp, g_.V, E, part, s_);
+        HIP_CHECK(hipStreamSynchronize(s_));
+      } catch (...) {
+        (void)hipFree(part);
+        throw;
+      }
+      es.d_pull_part[dir] = part;
       g_.device_bytes += (ntiles + 1) * sizeof(uint64_t);
-      launch_bfs_pull_partition(rp, g_.V, E, es.d_pull_part[dir], s_);
     }
     return es.d_pull_part[dir];
   }
@@ -649,15 +666,26 @@ class Executor {
     // k_bfs_pull reads bit 31 of a col entry as the hub tag: vertex ids must stay below 2^31
     if (g_.V >= 0x80000000u) unsupported("variable-length traversal over 2^31 or more vertices");
     if (pull_hubs_ == 0 || g_.partitioned()) return g_.col(es, dir);
-    if (!es.d_pull_col[dir]) {
+    if (!es.d_pull_col[dir]) {  // built into local buffers, published once complete
       const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
-      HIP_CHECK(hipMalloc((void **)&es.d_pull_col[dir], std::max<size_t>(E * 4, 4)));
-      HIP_CHECK(hipMalloc((void **)&es.d_hubs[dir], std::max<size_t>((size_t)pull_hubs_ * 4, 4)));
+      uint32_t *pcol = nullptr, *hubs = nullptr, nh = 0;
+      try {
+        HIP_CHECK(hipMalloc((void **)&pcol, std::max<size_t>(E * 4, 4)));
+        HIP_CHECK(hipMalloc((void **)&hubs, std::max<size_t>((size_t)pull_hubs_ * 4, 4)));
+        DBuf<uint32_t> hub_idx(&pool_, g_.V), hist(&pool_, 4096);
+        DBuf<unsigned long long> cnt(&pool_, 1);
+        nh = build_pull_col(g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, pull_hubs_, hub_idx.p, hist.p, cnt.p, hubs,
+                            pcol, cus(), s_);
+        HIP_CHECK(hipStreamSynchronize(s_));
+      } catch (...) {
+        if (pcol) (void)hipFree(pcol);
+        if (hubs) (void)hipFree(hubs);
+        throw;
+      }
+      es.d_pull_col[dir] = pcol;
+      es.d_hubs[dir] = hubs;
+      es.n_hubs[dir] = nh;
       g_.device_bytes += E * 4 + (uint64_t)pull_hubs_ * 4;
-      DBuf<uint32_t> hub_idx(&pool_, g_.V), hist(&pool_, 4096);
-      DBuf<unsigned long long> cnt(&pool_, 1);
-      es.n_hubs[dir] = build_pull_col(g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, pull_hubs_, hub_idx.p, hist.p,
-                                      cnt.p, es.d_hubs[dir], es.d_pull_col[dir], cus(), s_);
     }
     *nhubs = es.n_hubs[dir];
     *hubs = es.d_hubs[dir];
@@ -710,12 +738,26 @@ class Executor {
     const uint64_t hd = sliced ? heavy_deg_sliced_ : heavy_deg_;
     // per-tile sums → one-workgroup scan (posts the totals to the host) → per-tile offsets and chunks
     DBuf<uint64_t> blk(&pool_, (uint64_t)(kBinKeys + P) * bin_tiles(R)), qb(&pool_, P + 1);
+    // a sliced hop that writes rows sizes its arenas from the target bitmap's density per slice
+    // (posted with the binning totals); an arena found short re-runs the hop with the exact bound
+    const bool estimate = sliced && write && arena_estimate_;
+    DBuf<unsigned long long> spop;
+    if (estimate) {
+      spop = DBuf<unsigned long long>(&pool_, P);
+      launch_slice_popc(filter, g_.V, slice_shift_, P, spop.p, s_);
+    }
     tm_.begin("k_bin_rows");
     launch_bin_count(sliced, src, R, adj, cuts, hd, P, blk.p, s_);
-    launch_bin_scan(blk.p, R, P, qb.p, mail(), s_);
+    launch_bin_scan(blk.p, R, P, qb.p, mail(), s_, spop.p, estimate ? P : 0);
     const uint64_t *m = wait_mail();
     const uint64_t EL = m[0], EH = m[1], nchunks = m[2], NL = m[3];
     std::vector<uint64_t> hqb(m + 4, m + 5 + P);
+    std::vector<double> dens(P, 1.0);  // fraction of each slice's vertices the target bitmap holds
+    if (estimate)
+      for (uint32_t q = 0; q < P; ++q) {
+        const uint64_t lo = (uint64_t)q << slice_shift_, hi = std::min<uint64_t>(g_.V, (uint64_t)(q + 1) << slice_shift_);
+        dens[q] = hi > lo ? std::min(1.0, (double)m[5 + P + q] / (double)(hi - lo)) : 0.0;
+      }
     tm_.end(R * (4 + 16ull * adj.n + (sliced ? 4ull * (P - 1) * adj.n : 0)));
     const uint64_t E = EL + EH;
     o.E = E;
@@ -780,6 +822,7 @@ class Executor {
     // sliced: one workgroup per CU, split over the slices in proportion to their chunk counts
     SliceArgs sa{};
     uint64_t caph_sliced = 0;
+    double caph_est = 0;  // expected rows of the fullest heavy wave (estimate mode)
     if (sliced && nchunks) {
       const uint64_t G = std::min<uint64_t>((uint64_t)cus(), (nchunks + SWPB - 1) / SWPB);
       sa.qb = qb.p;
@@ -794,7 +837,11 @@ class Executor {
         sa.wg0[q] = w;
         w += (uint32_t)k;
         // + a 64-row tail pad (k_expand_heavy_sliced may write one dropped row past a wave's count)
-        if (k) caph_sliced = std::max<uint64_t>(caph_sliced, (nq + k * SWPB - 1) / (k * SWPB) * (uint64_t)kChunk + 64);
+        if (k) {
+          const uint64_t cpw = (nq + k * SWPB - 1) / (k * SWPB);  // chunks of the fullest wave of slice q
+          caph_sliced = std::max<uint64_t>(caph_sliced, cpw * (uint64_t)kChunk + 64);
+          caph_est = std::max(caph_est, (double)cpw * ((double)EH / (double)nchunks) * dens[q]);
+        }
       }
       sa.wg0[P] = w;
     }
@@ -833,11 +880,20 @@ class Executor {
                    (unsigned long long)nchunks, P, (unsigned long long)ntiles, gl, gls, gh, (int)filt);
     // heavy output: one arena per wave, sized for the most chunks a wave of the launch owns
     const uint64_t wh = (uint64_t)gh * (sliced ? SWPB : WPB);
-    const uint64_t caph = !gh ? 0 : sliced ? caph_sliced : (nchunks + wh - 1) / wh * (uint64_t)kChunk;
+    const uint64_t caph_exact = !gh ? 0 : sliced ? caph_sliced : (nchunks + wh - 1) / wh * (uint64_t)kChunk;
     const uint64_t nseg_h = wh;
-    const uint64_t heavy_rows_cap = wh * caph;
-    const uint64_t capl = lsliced ? capls : gl ? (ntiles + gl - 1) / gl * (uint64_t)kExpandTile : 0;
-    const uint64_t cap = filt ? heavy_rows_cap + lw * capl : E;
+    const uint64_t capl_exact = lsliced ? capls : gl ? (ntiles + gl - 1) / gl * (uint64_t)kExpandTile : 0;
+    double capl_est = 0;
+    if (lsliced) {
+      double dmax = 0;
+      for (double d : dens) dmax = std::max(dmax, d);
+      capl_est = (double)(capls - 64 * hd) * dmax;
+    }
+    // estimated arenas: 25 % over the expected rows plus 4096 (binomial spread of a wave's survivors)
+    const double margin = arena_margin_;
+    auto est_cap = [margin](double expect, uint64_t exact) {
+      return std::min<uint64_t>(exact, (uint64_t)(expect * margin) + (margin > 0 ? 4096 : 0));
+    };
     ExpandArgs a{};
     a.src = src;
     a.offs = loffs.p;
@@ -861,17 +917,10 @@ class Executor {
     }
     std::vector<DBuf<uint32_t>> outc;
     DBuf<uint32_t> odst;
-    if (write) {
-      odst = DBuf<uint32_t>(&pool_, std::max<uint64_t>(cap, 1));
-      a.out_dst = odst.p;
-      for (size_t c = 0; c < carry.size(); ++c) {
-        outc.emplace_back(&pool_, std::max<uint64_t>(cap, 1));
-        a.carry_in[c] = carry[c];
-        a.carry_out[c] = outc.back().p;
-      }
-    }
+    DBuf<uint64_t> soffs;
     if (filt) {
       o.nseg = (uint32_t)(nseg_h + lw);
+      soffs = DBuf<uint64_t>(&pool_, o.nseg + 1);
       o.seg_start = DBuf<uint64_t>(&pool_, o.nseg);
       o.seg_count = DBuf<uint32_t>(&pool_, o.nseg);
       a.seg_start = o.seg_start.p;
@@ -880,34 +929,63 @@ class Executor {
     // algorithmic bytes: 8 B row_ptr pair per row + 4 B col per edge (+ 4 B × columns
     // per emitted row, added below)
     uint64_t kb = 8 * R + 4 * E;
-    // per-kernel algorithmic bytes: heavy rows carry EH edges, light rows EL (+ 8 B per row each)
     // per-kernel algorithmic bytes (amended below once the emitted rows are known): heavy = 4·EH + out,
     // light = 8·R + 4·EL + out, out = 4 B × written columns × rows the kernel emitted
     const uint64_t outw = write ? 4ull * (carry.size() + 1) : 0;
     size_t rec_h = SIZE_MAX, rec_l = SIZE_MAX;
-    if (gh) {
-      a.arena_base = 0;
-      a.arena_cap = caph;
-      a.seg_base = 0;
-      if (sliced) {
-        tm_.begin("k_expand_heavy_sliced");
-        launch_expand_heavy_sliced(a, sa, gh, write, s_);
-      } else {
-        tm_.begin(member ? "k_expand_heavy_check" : "k_expand_heavy");
-        launch_expand_heavy(a, gh, write, s_);
+    uint64_t caph = caph_exact, capl = capl_exact, heavy_rows_cap = 0;
+    const uint64_t *mt = nullptr;
+    for (int attempt = 0;; ++attempt) {
+      const bool est = estimate && attempt == 0;
+      caph = est ? est_cap(caph_est, caph_exact) : caph_exact;
+      capl = est && lsliced ? est_cap(capl_est, capl_exact) : capl_exact;
+      heavy_rows_cap = wh * caph;
+      const uint64_t cap = filt ? heavy_rows_cap + lw * capl : E;
+      if (write) {
+        odst = DBuf<uint32_t>(&pool_, std::max<uint64_t>(cap, 1));
+        a.out_dst = odst.p;
+        outc.clear();
+        for (size_t c = 0; c < carry.size(); ++c) {
+          outc.emplace_back(&pool_, std::max<uint64_t>(cap, 1));
+          a.carry_in[c] = carry[c];
+          a.carry_out[c] = outc.back().p;
+        }
       }
-      tm_.end(4 * EH + outw * (filt ? 0 : EH));
-      rec_h = tm_.last();
-    }
-    if (gl || gls) {
-      a.arena_base = heavy_rows_cap;
-      a.arena_cap = capl;
-      a.seg_base = (uint32_t)nseg_h;
-      tm_.begin(lsliced ? "k_expand_light_sliced" : member ? "k_expand_light_check" : "k_expand_light");
-      if (lsliced) launch_expand_light_sliced(a, la, gls, write, s_);
-      else launch_expand(a, gl, write, s_);
-      tm_.end(8 * R + 4 * EL + outw * (filt ? 0 : EL));
-      rec_l = tm_.last();
+      if (gh) {
+        a.arena_base = 0;
+        a.arena_cap = caph;
+        a.seg_base = 0;
+        if (sliced) {
+          tm_.begin("k_expand_heavy_sliced");
+          launch_expand_heavy_sliced(a, sa, gh, write, s_);
+        } else {
+          tm_.begin(member ? "k_expand_heavy_check" : "k_expand_heavy");
+          launch_expand_heavy(a, gh, write, s_);
+        }
+        tm_.end(4 * EH + outw * (filt ? 0 : EH));
+        rec_h = tm_.last();
+      }
+      if (gl || gls) {
+        a.arena_base = heavy_rows_cap;
+        a.arena_cap = capl;
+        a.seg_base = (uint32_t)nseg_h;
+        tm_.begin(lsliced ? "k_expand_light_sliced" : member ? "k_expand_light_check" : "k_expand_light");
+        if (lsliced) launch_expand_light_sliced(a, la, gls, write, s_);
+        else launch_expand(a, gl, write, s_);
+        tm_.end(8 * R + 4 * EL + outw * (filt ? 0 : EL));
+        rec_l = tm_.last();
+      }
+      if (!filt) break;
+      // rows per block segment → total (and dense compaction when required); segment offsets + rows
+      // emitted by the heavy kernel's segments, all rows, member words, arena overflow: one workgroup,
+      // one host read
+      launch_seg_totals(o.seg_count.p, o.nseg, nseg_h, soffs.p, member ? medges.p : nullptr,
+                        gh ? caph : UINT64_MAX, (gl || gls) ? capl : UINT64_MAX, mail(), s_);
+      mt = wait_mail();
+      if (!mt[4]) break;
+      if (!est) fail(OMX_E_INVALID, "internal: an exact expansion arena overflowed");
+      ++arena_retries_;
+      if (debug_expand_) std::fprintf(stderr, "[omx expand] estimated arena short: re-running with exact caps\n");
     }
     tm_.begin("expand_total");
     if (!filt) {
@@ -921,12 +999,7 @@ class Executor {
       }
       return o;
     }
-    // filtered: rows per block segment → total (and dense compaction when required)
-    DBuf<uint64_t> soffs(&pool_, o.nseg + 1);
-    // segment offsets + rows emitted by the heavy kernel's segments, all rows, member words: one
-    // workgroup, one host read
-    launch_seg_totals(o.seg_count.p, o.nseg, nseg_h, soffs.p, member ? medges.p : nullptr, mail(), s_);
-    const uint64_t *mt = wait_mail();
+    // filtered: rows per block segment (mt: the seg-totals mail of the final attempt)
     const uint64_t nh_n[3] = {mt[0], mt[1], mt[2]};
     const uint64_t probes = mt[3];  // col[] probes of a fused closing check (4 B each, §8(d))
     o.E_member = nh_n[2];
@@ -1007,6 +1080,7 @@ class Executor {
            ex.adj.dup_free && ck.adj.dup_free && ex.adj.sorted && ck.adj.sorted;
   }
   void expand_check_swapped(const Step &ex, const Step &ck, bool write) {
+    require_u32_rows("a cycle-closing intersection");
     const std::vector<int> cols = bound_cols();  // carried columns (ex.dst is not bound yet)
     bound_[ex.dst] = 1;
     const uint64_t R = R_;
@@ -1067,6 +1141,7 @@ class Executor {
 
   // keep the rows whose flag is set (all bound columns)
   void select_rows(const uint8_t *flags, uint64_t R) {
+    require_u32_rows("a row selection");
     DBuf<uint32_t> idx(&pool_, R);
     DBuf<uint64_t> nsel(&pool_, 1);
     hipcub::CountingInputIterator<uint32_t> cnt(0);
@@ -1198,8 +1273,15 @@ class Executor {
     return true;
   }
 
+  // binding-row indices are u32 in the gathers, selects and (row, vertex) pair keys
+  void require_u32_rows(const char *what) const {
+    if (R_ >= (1ull << 32))
+      unsupported(std::string(what) + " over 2^32 or more binding rows (u32 row indices)");
+  }
+
   // Multi-source BFS over 64-row batches (bfs.hip). Rows (row, v) come out distinct per row.
   void varlen_msbfs(const Step &st, bool depth_only_while) {
+    require_u32_rows("a variable-length item");
     const uint64_t R = R_;
     const uint32_t V = g_.V;
     const DAdj adj = make_adj(st.adj);
@@ -1370,104 +1452,146 @@ class Executor {
     return out;
   }
 
-  // (row, vertex) pairs level by level: the general form (any $depth use)
-  void varlen_pairs(const Step &st) {
-    const uint64_t R = R_;
-    const bool dep_where = st.where_prog >= 0 && p_.progs[st.where_prog].uses_depth;
-    const bool dep_while = st.while_prog >= 0 && p_.progs[st.while_prog].uses_depth;
-    const bool use_visited = !dep_where && !dep_while;
-    const int vbits = bits_for(g_.V);
-    const int key_bits = 32 + vbits;
-    DBuf<uint32_t> frow(&pool_, R), fv(&pool_, R);
-    launch_iota(frow.p, R, s_);
-    HIP_CHECK(hipMemcpyAsync(fv.p, col_[st.src].p, R * 4, hipMemcpyDeviceToDevice, s_));
-    uint64_t nf = R;
+  // ---- (row, vertex) pair sets: the general traversal (any $depth use, multi items) -----------------
+  // A pair set holds, per binding row, the set of vertices an item's executeTraversal returned so far
+  // (P/OMatchPathItem.java:49-107): distinct (row, v) pairs, kept as two u32 columns. Sets of rows with
+  // the same start vertex are the same, so per-row sets equal the reference's per-start-vertex HashSets.
+  struct PairSet {
+    DBuf<uint32_t> row, v;
+    uint64_t n = 0;
+  };
+
+  int pair_key_bits() const { return 32 + bits_for(g_.V); }
+
+  // distinct (row, v) pairs of n packed keys (sorted)
+  PairSet pairs_from_keys(DBuf<uint64_t> &keys, uint64_t n, bool unique_sorted = false) {
+    PairSet o;
+    if (!unique_sorted) n = sort_unique_keys(keys, n, pair_key_bits());
+    o.n = n;
+    o.row = DBuf<uint32_t>(&pool_, std::max<uint64_t>(n, 1));
+    o.v = DBuf<uint32_t>(&pool_, std::max<uint64_t>(n, 1));
+    if (n) launch_unpack_pairs(keys.p, n, o.row.p, o.v.p, s_);
+    return o;
+  }
+  DBuf<uint64_t> pair_keys(const PairSet &p) {
+    DBuf<uint64_t> k(&pool_, std::max<uint64_t>(p.n, 1));
+    if (p.n) launch_pack_pairs(p.row.p, p.v.p, p.n, k.p, s_);
+    return k;
+  }
+  // the pairs whose vertex is in bitmap bm
+  PairSet filter_pairs(const PairSet &in, const uint64_t *bm) {
+    if (!bm || in.n == 0) {
+      DBuf<uint64_t> k = pair_keys(in);
+      return pairs_from_keys(k, in.n, true);
+    }
+    DBuf<uint8_t> flags(&pool_, in.n);
+    launch_flag_bitmap(in.v.p, in.n, bm, flags.p, s_);
+    DBuf<uint64_t> all = pair_keys(in), sel(&pool_, in.n), nsel(&pool_, 1);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, all.p, flags.p, sel.p, nsel.p, (int64_t)in.n, s_); });
+    return pairs_from_keys(sel, read1(nsel.p), true);  // a subsequence of sorted keys stays sorted
+  }
+  // bitmap of a predicate program at $depth = depth (cached when it does not read $depth)
+  std::map<int, DBuf<uint64_t>> prog_bms_;
+  const uint64_t *prog_bitmap(int prog, int64_t depth, DBuf<uint64_t> &scratch) {
+    if (prog < 0) return nullptr;
+    if (p_.progs[prog].uses_depth) {
+      if (!scratch.p) scratch = DBuf<uint64_t>(&pool_, nwords_);
+      eval_bitmap(prog, -1, depth, scratch.p);
+      return scratch.p;
+    }
+    DBuf<uint64_t> &b = prog_bms_[prog];
+    if (!b.p) {
+      b = DBuf<uint64_t>(&pool_, nwords_);
+      eval_bitmap(prog, -1, 0, b.p);
+    }
+    return b.p;
+  }
+
+  // one hop of a single-method item over a pair set (target bitmap optional), distinct pairs out
+  PairSet hop_pairs(const PairSet &in, const AdjSpec &adj, const uint64_t *filter) {
+    if (in.n == 0) return PairSet{};
+    ExpandOut ex = expand_core(in.v.p, in.n, adj, filter, {in.row.p}, true);
+    edges_ += ex.E;
+    edges_iter_ += ex.E;
+    if (ex.n == 0) return PairSet{};
+    DBuf<uint64_t> keys(&pool_, ex.n);
+    launch_pack_pairs(ex.carry[0].p, ex.dst.p, ex.n, keys.p, s_);
+    return pairs_from_keys(keys, ex.n);
+  }
+
+  // traversePatternEdge of an item (P/OMatchPathItem.java:109-126): the neighbour set without the
+  // item's own filter; a multi item composes its sub-items (P/OMultiMatchPathItem.java:41-61)
+  PairSet pattern_edge(const TravSpec &t, const PairSet &in) {
+    if (!t.multi) return hop_pairs(in, t.adj, nullptr);
+    PairSet cur;
+    {
+      DBuf<uint64_t> k = pair_keys(in);
+      cur = pairs_from_keys(k, in.n, true);
+    }
+    for (const TravSpec &sub : t.subs) {
+      if (cur.n == 0) break;
+      cur = traverse(sub, cur);
+    }
+    return cur;
+  }
+
+  // executeTraversal (P/OMatchPathItem.java:49-107) from every pair's vertex at depth 0
+  PairSet traverse(const TravSpec &t, const PairSet &in) {
+    DBuf<uint64_t> where_scratch, while_scratch;
+    if (!t.varlen) {  // one level; the item's WHERE filters the neighbours (a HashSet, :63-78)
+      const uint64_t *w = prog_bitmap(t.where_prog, 0, where_scratch);
+      if (!t.multi) return hop_pairs(in, t.adj, w);
+      PairSet n = pattern_edge(t, in);
+      return filter_pairs(n, w);
+    }
+    // level-synchronous: level d keeps F_d ∩ where_d and expands F_d ∩ while_d while d < maxDepth.
+    // Without $depth in where/while the per-row visited set is exact and terminates on cycles.
+    const bool dep = (t.where_prog >= 0 && p_.progs[t.where_prog].uses_depth) ||
+                     (t.while_prog >= 0 && p_.progs[t.while_prog].uses_depth);
+    const int kb = pair_key_bits();
+    PairSet F;
+    {
+      DBuf<uint64_t> k = pair_keys(in);
+      F = pairs_from_keys(k, in.n, true);
+    }
     DBuf<uint64_t> visited;
     uint64_t nvisited = 0;
-    if (use_visited) {
-      visited = DBuf<uint64_t>(&pool_, R);
-      launch_pack_pairs(frow.p, fv.p, R, visited.p, s_);
-      nvisited = sort_unique_keys(visited, R, key_bits);
+    if (!dep) {
+      visited = pair_keys(F);
+      nvisited = F.n;
     }
     std::vector<DBuf<uint64_t>> res_parts;
     std::vector<uint64_t> res_n;
-    DBuf<uint64_t> where_bm(&pool_, nwords_), while_bm(&pool_, nwords_);
-    bool where_ready = false, while_ready = false;
-    for (int64_t d = 0;; ++d) {
+    for (int64_t d = 0; F.n; ++d) {
       if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate (the reference recurses without bound)");
-      // include F_d ∩ where_d
-      {
-        DBuf<uint64_t> keys(&pool_, std::max<uint64_t>(nf, 1));
-        uint64_t nk = nf;
-        if (st.where_prog >= 0) {
-          if (!where_ready || dep_where) {
-            eval_bitmap(st.where_prog, -1, d, where_bm.p);
-            where_ready = true;
-          }
-          DBuf<uint8_t> flags(&pool_, nf);
-          launch_flag_bitmap(fv.p, nf, where_bm.p, flags.p, s_);
-          DBuf<uint64_t> all(&pool_, nf), nsel(&pool_, 1);
-          launch_pack_pairs(frow.p, fv.p, nf, all.p, s_);
-          cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, all.p, flags.p, keys.p, nsel.p, (int64_t)nf, s_); });
-          nk = read1(nsel.p);
-        } else {
-          launch_pack_pairs(frow.p, fv.p, nf, keys.p, s_);
-        }
-        if (nk) {
-          res_parts.push_back(std::move(keys));
-          res_n.push_back(nk);
+      {  // include F_d ∩ where_d
+        PairSet inc = filter_pairs(F, prog_bitmap(t.where_prog, d, where_scratch));
+        if (inc.n) {
+          res_parts.push_back(pair_keys(inc));
+          res_n.push_back(inc.n);
         }
       }
-      if (st.has_max_depth && d >= st.max_depth) break;
-      // G = F_d ∩ while_d
-      uint64_t ng = nf;
-      DBuf<uint32_t> grow, gv;
-      const uint32_t *gr = frow.p, *gvp = fv.p;
-      if (st.while_prog >= 0) {
-        if (!while_ready || dep_while) {
-          eval_bitmap(st.while_prog, -1, d, while_bm.p);
-          while_ready = true;
-        }
-        DBuf<uint8_t> flags(&pool_, nf);
-        launch_flag_bitmap(fv.p, nf, while_bm.p, flags.p, s_);
-        DBuf<uint64_t> all(&pool_, nf), sel(&pool_, nf), nsel(&pool_, 1);
-        launch_pack_pairs(frow.p, fv.p, nf, all.p, s_);
-        cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, all.p, flags.p, sel.p, nsel.p, (int64_t)nf, s_); });
-        ng = read1(nsel.p);
-        grow = DBuf<uint32_t>(&pool_, std::max<uint64_t>(ng, 1));
-        gv = DBuf<uint32_t>(&pool_, std::max<uint64_t>(ng, 1));
-        launch_unpack_pairs(sel.p, ng, grow.p, gv.p, s_);
-        gr = grow.p;
-        gvp = gv.p;
-      }
-      if (ng == 0) break;
-      ExpandOut ex = expand_core(gvp, ng, st.adj, nullptr, {gr}, true);
-      edges_ += ex.E;
-      edges_iter_ += ex.E;
-      if (ex.n == 0) break;
-      DBuf<uint64_t> keys(&pool_, ex.n);
-      launch_pack_pairs(ex.carry[0].p, ex.dst.p, ex.n, keys.p, s_);
-      uint64_t nk = sort_unique_keys(keys, ex.n, key_bits);
-      if (use_visited) {
-        DBuf<uint8_t> flags(&pool_, nk);
-        launch_flag_not_in(visited.p, nvisited, keys.p, nk, flags.p, s_);
-        DBuf<uint64_t> fresh(&pool_, nk), nsel(&pool_, 1);
-        cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, keys.p, flags.p, fresh.p, nsel.p, (int64_t)nk, s_); });
-        nk = read1(nsel.p);
+      if (t.has_max_depth && d >= t.max_depth) break;
+      PairSet G = filter_pairs(F, prog_bitmap(t.while_prog, d, while_scratch));  // F_d ∩ while_d
+      if (G.n == 0) break;
+      PairSet N = pattern_edge(t, G);
+      if (!dep && N.n) {  // drop the pairs seen at an earlier level
+        DBuf<uint64_t> keys = pair_keys(N);
+        DBuf<uint8_t> flags(&pool_, N.n);
+        launch_flag_not_in(visited.p, nvisited, keys.p, N.n, flags.p, s_);
+        DBuf<uint64_t> fresh(&pool_, N.n), nsel(&pool_, 1);
+        cub([&](void *tt, size_t &b) { return hipcub::DeviceSelect::Flagged(tt, b, keys.p, flags.p, fresh.p, nsel.p, (int64_t)N.n, s_); });
+        const uint64_t nk = read1(nsel.p);
         if (nk) {
           DBuf<uint64_t> merged(&pool_, nvisited + nk);
           HIP_CHECK(hipMemcpyAsync(merged.p, visited.p, nvisited * 8, hipMemcpyDeviceToDevice, s_));
           HIP_CHECK(hipMemcpyAsync(merged.p + nvisited, fresh.p, nk * 8, hipMemcpyDeviceToDevice, s_));
-          nvisited = sort_unique_keys(merged, nvisited + nk, key_bits);
+          nvisited = sort_unique_keys(merged, nvisited + nk, kb);
           visited = std::move(merged);
         }
-        keys = std::move(fresh);
+        N = pairs_from_keys(fresh, nk, true);
       }
-      if (nk == 0) break;
-      frow = DBuf<uint32_t>(&pool_, nk);
-      fv = DBuf<uint32_t>(&pool_, nk);
-      launch_unpack_pairs(keys.p, nk, frow.p, fv.p, s_);
-      nf = nk;
+      F = std::move(N);
     }
     // union of the levels' results (HashSet union, P/OMatchPathItem.java:61,96-101)
     uint64_t total = 0;
@@ -1478,33 +1602,58 @@ class Executor {
       HIP_CHECK(hipMemcpyAsync(res.p + off, res_parts[i].p, res_n[i] * 8, hipMemcpyDeviceToDevice, s_));
       off += res_n[i];
     }
-    res_parts.clear();
-    uint64_t nres = sort_unique_keys(res, total, key_bits);
-    DBuf<uint32_t> rrow(&pool_, std::max<uint64_t>(nres, 1)), rv(&pool_, std::max<uint64_t>(nres, 1));
-    launch_unpack_pairs(res.p, nres, rrow.p, rv.p, s_);
-    if (st.mode == T_BOUND) {
+    return pairs_from_keys(res, total);
+  }
+
+  // the binding rows' start pairs (row index, source vertex)
+  PairSet start_pairs(int src) {
+    require_u32_rows("a variable-length or multi-step item");
+    PairSet p;
+    p.n = R_;
+    p.row = DBuf<uint32_t>(&pool_, std::max<uint64_t>(R_, 1));
+    p.v = DBuf<uint32_t>(&pool_, std::max<uint64_t>(R_, 1));
+    launch_iota(p.row.p, R_, s_);
+    HIP_CHECK(hipMemcpyAsync(p.v.p, col_[src].p, R_ * 4, hipMemcpyDeviceToDevice, s_));
+    return p;
+  }
+
+  // processContext's three branches (:468-497) over an item's (row, v) result set
+  void bind_pairs(const Step &st, PairSet &res) {
+    const uint64_t R = R_;
+    if (st.mode == T_BOUND) {  // keep a row iff its bound target is in its set (existence)
+      DBuf<uint64_t> rk = pair_keys(res);
       DBuf<uint32_t> idx(&pool_, std::max<uint64_t>(R, 1));
       launch_iota(idx.p, R, s_);
       DBuf<uint64_t> keys(&pool_, std::max<uint64_t>(R, 1));
       launch_pack_pairs(idx.p, col_[st.dst].p, R, keys.p, s_);
-      DBuf<uint8_t> flags(&pool_, std::max<uint64_t>(R, 1));
-      launch_flag_not_in(res.p, nres, keys.p, R, flags.p, s_);
-      // flags = "not in" → invert by selecting on the complement
-      DBuf<uint8_t> keep(&pool_, std::max<uint64_t>(R, 1));
+      DBuf<uint8_t> flags(&pool_, std::max<uint64_t>(R, 1)), keep(&pool_, std::max<uint64_t>(R, 1));
+      launch_flag_not_in(rk.p, res.n, keys.p, R, flags.p, s_);
       invert_flags(flags.p, keep.p, R);
       select_rows(keep.p, R);
       return;
     }
-    if (st.mode == T_CAND && nres) {
-      DBuf<uint8_t> flags(&pool_, nres);
-      launch_flag_bitmap(rv.p, nres, bitmap(st.cand_bm), flags.p, s_);
-      DBuf<uint64_t> sel(&pool_, nres), nsel(&pool_, 1);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, res.p, flags.p, sel.p, nsel.p, (int64_t)nres, s_); });
-      nres = read1(nsel.p);
-      launch_unpack_pairs(sel.p, nres, rrow.p, rv.p, s_);
-    }
-    gather_rows(rrow.p, nres);
-    col_[st.dst] = std::move(rv);
+    if (st.mode == T_CAND) res = filter_pairs(res, bitmap(st.cand_bm));
+    gather_rows(res.row.p, res.n);
+    col_[st.dst] = std::move(res.v);
+  }
+
+  // variable-length item over (row, vertex) pairs (any $depth use)
+  void varlen_pairs(const Step &st) {
+    TravSpec t;
+    t.adj = st.adj;
+    t.varlen = true;
+    t.where_prog = st.where_prog;
+    t.while_prog = st.while_prog;
+    t.has_max_depth = st.has_max_depth;
+    t.max_depth = st.max_depth;
+    PairSet res = traverse(t, start_pairs(st.src));
+    bind_pairs(st, res);
+  }
+
+  // multi-step item .( ... ) (OMultiMatchPathItem)
+  void multi_step(const Step &st) {
+    PairSet res = traverse(st.trav, start_pairs(st.src));
+    bind_pairs(st, res);
   }
 
   void invert_flags(const uint8_t *in, uint8_t *out, uint64_t n) {
@@ -1618,8 +1767,13 @@ void Executor::unpack_tuple(const uint64_t *keys, uint64_t n, std::vector<DBuf<u
 omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts, Transport *tr) {
   if (!g.on_device()) fail(OMX_E_DEVICE, "graph snapshot is host-only (device = -1)");
   HIP_CHECK(hipSetDevice(g.device));
-  Executor ex(g, p, opts, tr);
-  return ex.run();
+  try {
+    Executor ex(g, p, opts, tr);
+    return ex.run();
+  } catch (...) {
+    if (tr) tr->abort();  // release the peers waiting in an exchange with this rank
+    throw;
+  }
 }
 
 }  // namespace omx

@@ -161,7 +161,12 @@ constexpr int kBinKeys = 3;  // keys before the per-slice chunk counts
 inline unsigned bin_tiles(uint64_t R) { return (unsigned)((R + 1 + kBinBlock - 1) / kBinBlock); }
 void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
                       uint64_t heavy_deg, uint32_t P, uint64_t *blk, hipStream_t s);
-void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s);
+// extra[0..nextra) (device words) are posted after the totals: mail[5 + P + i]
+void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s,
+                     const unsigned long long *extra = nullptr, uint32_t nextra = 0);
+// out[q] = set bits of slice q (2^shift vertices) of a V-bit bitmap, q < P
+void launch_slice_popc(const uint64_t *bm, uint32_t V, uint32_t shift, uint32_t P, unsigned long long *out,
+                       hipStream_t s);
 void launch_bin_fill(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
                      uint64_t heavy_deg, uint32_t P, const uint64_t *blk, const uint64_t *qb, uint64_t *loffs,
                      uint64_t *lbase, const LightRows &lr, ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s);
@@ -185,9 +190,11 @@ unsigned bitmap_list_blocks(uint64_t nwords);
 void launch_bitmap_list_2k(const uint64_t *words, uint64_t nwords, uint32_t V, int rank, int world, uint32_t lo,
                            uint32_t hi, uint32_t *blk, uint32_t *out, const Mail &count, hipStream_t s);
 // one workgroup: soffs = inclusive prefix of cnt (soffs[0] = 0); mail = {soffs[nseg_h], soffs[nseg],
-// member[0], member[1]} (member may be nullptr → 0)
+// member[0], member[1], overflow} (member may be nullptr → 0; overflow = some segment below nseg_h
+// counted more than cap_h rows, or one above it more than cap_l)
 void launch_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h, uint64_t *soffs,
-                       const unsigned long long *member, const Mail &mail, hipStream_t s);
+                       const unsigned long long *member, uint64_t cap_h, uint64_t cap_l, const Mail &mail,
+                       hipStream_t s);
 // mail[i] = word i at p (words of `bytes` = 4 or 8, zero-extended), i < n < kMailSeq
 void launch_post_words(const void *p, int n, const Mail &mail, hipStream_t s, int bytes = 8);
 

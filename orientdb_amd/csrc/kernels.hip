@@ -914,7 +914,8 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_count(const uint32_t *src, ui
 // PER > 0: every thread owns PER consecutive tiles (nb ≤ 1024·PER), loaded all at once (clamped
 // indices, no branches) and kept in registers for the write-back; PER = 0: a loop per key
 template <int MAXP, int PER>
-__global__ __launch_bounds__(1024) void k_bin_scan(uint64_t *blk, uint32_t nb, uint32_t P, uint64_t *qb, Mail mail) {
+__global__ __launch_bounds__(1024) void k_bin_scan(uint64_t *blk, uint32_t nb, uint32_t P, uint64_t *qb, Mail mail,
+                                                   const unsigned long long *extra, uint32_t nextra) {
   constexpr int K = kBinKeys + MAXP, PV = PER > 0 ? PER : 1;
   __shared__ unsigned long long s_w[K][16];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -992,6 +993,7 @@ __global__ __launch_bounds__(1024) void k_bin_scan(uint64_t *blk, uint32_t nb, u
     qb[P] = q0;
     mail.p[4 + P] = q0;
     mail.p[2] = q0;
+    for (uint32_t i = 0; i < nextra; ++i) mail.p[5 + P + i] = extra[i];
     mail_post(mail);
   }
 }
@@ -1082,16 +1084,18 @@ void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &
   }
   KCHECK("k_bin_count");
 }
-void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s) {
+void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s,
+                     const unsigned long long *extra, uint32_t nextra) {
   const unsigned nb = bin_tiles(R);
+  if (5 + P + nextra >= (uint32_t)kMailSeq) fail(OMX_E_INVALID, "internal: bin-scan mail overflows");
   if (nb <= 4096 && P <= 4) {  // registers for (3 + P) keys × 4 tiles
-#define OMX_BS(M) hipLaunchKernelGGL((k_bin_scan<M, 4>), dim3(1), dim3(1024), 0, s, blk, nb, P, qb, mail)
+#define OMX_BS(M) hipLaunchKernelGGL((k_bin_scan<M, 4>), dim3(1), dim3(1024), 0, s, blk, nb, P, qb, mail, extra, nextra)
     if (P <= 1) OMX_BS(1);
     else if (P <= 2) OMX_BS(2);
     else OMX_BS(4);
 #undef OMX_BS
   } else {
-#define OMX_BS(M) hipLaunchKernelGGL((k_bin_scan<M, 0>), dim3(1), dim3(1024), 0, s, blk, nb, P, qb, mail)
+#define OMX_BS(M) hipLaunchKernelGGL((k_bin_scan<M, 0>), dim3(1), dim3(1024), 0, s, blk, nb, P, qb, mail, extra, nextra)
     OMX_BY_MAXP(P, OMX_BS);
 #undef OMX_BS
   }
@@ -1111,6 +1115,28 @@ void launch_bin_fill(bool sliced, const uint32_t *src, uint64_t R, const DAdj &a
 #undef OMX_BF
   }
   KCHECK("k_bin_fill");
+}
+
+// out[q] = set bits of bitmap slice q (2^shift vertices): the slices' densities size the arenas of the
+// sliced expansion kernels (Executor::expand_core)
+__global__ __launch_bounds__(256) void k_slice_popc(const uint64_t *bm, uint64_t nwords, uint32_t shift,
+                                                    unsigned long long *out) {
+  const uint64_t wps = shift >= 6 ? (1ull << (shift - 6)) : 1;
+  const uint64_t w0 = (uint64_t)blockIdx.x * wps, w1 = min(nwords, w0 + wps);
+  unsigned long long c = 0;
+  for (uint64_t w = w0 + threadIdx.x; w < w1; w += blockDim.x) c += __popcll(bm[w]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  __shared__ unsigned long long s_c[4];
+  if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+}
+void launch_slice_popc(const uint64_t *bm, uint32_t V, uint32_t shift, uint32_t P, unsigned long long *out,
+                       hipStream_t s) {
+  if (!P) return;
+  hipLaunchKernelGGL(k_slice_popc, dim3(P), dim3(256), 0, s, bm, ((uint64_t)V + 63) / 64, shift, out);
+  KCHECK("k_slice_popc");
 }
 
 // Copy bitmap slice q (2^shift bits) into LDS: 16-byte loads, eight per thread in flight before the
@@ -1240,11 +1266,14 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
   uint32_t *const stage = s_stage + wave * (kStage + 1);
   auto cvk = [](const Cur &x, int k) { return k < NCV ? x.cv[k < NCV ? k : 0] : 0u; };
   // writes the `n` staged rows (neighbour from LDS, carried columns constant) at the arena's acc
+  // an estimated arena may be short (Executor::expand_core): rows past arena_cap are counted, not
+  // written (an explicit bound: the buffer range check does not cover the scalar offset)
+  const uint64_t cap = a.arena_cap;
   auto flush = [&](const Cur &x, uint32_t n) {
     const int32_t so = (int32_t)(acc * 4);
     for (uint32_t k = 0; k < n; k += 64) {
       const uint32_t idx = k + lane;
-      if (idx < n) {
+      if (idx < n && acc + idx < cap) {
         const uint32_t off = idx * 4;
         __builtin_amdgcn_raw_buffer_store_b32(stage[idx], od, off, so, 0);
         if (nc > 0) __builtin_amdgcn_raw_buffer_store_b32(cvk(x, 0), oc0, off, so, 0);
@@ -1283,7 +1312,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_heavy_sliced(ExpandArgs 
             flush(x, st);
             st = 0;
           }
-        } else if (bit) {  // more than 4 carried columns: direct stores
+        } else if (bit && acc + lane_prefix(m) < cap) {  // more than 4 carried columns: direct stores
           const uint32_t pre = lane_prefix(m);
           const uint32_t off = pre * 4;
           const int32_t so = (int32_t)(acc * 4);
@@ -1435,7 +1464,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_light_sliced(ExpandArgs 
 #pragma unroll
       for (int c = 0; c < NCV; ++c) cv[c] = c < NC ? (uint32_t)__shfl(m.cv[c], (int)j, 64) : 0u;
       const uint32_t rr = NC < 0 ? (uint32_t)__shfl(m.row, (int)j, 64) : 0u;
-      if (idx < st) {
+      if (idx < st && acc + idx < a.arena_cap) {  // an estimated arena may be short: counted, not written
         const uint64_t o = arena + acc + idx;
         a.out_dst[o] = v;
         if (NC < 0) {
@@ -1777,14 +1806,17 @@ unsigned bitmap_list_blocks(uint64_t nwords) { return nblocks(nwords, kListB); }
 template <int PER>
 __global__ __launch_bounds__(1024) void k_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h,
                                                      uint64_t *soffs, const unsigned long long *member,
-                                                     Mail mail) {
+                                                     uint64_t cap_h, uint64_t cap_l, Mail mail) {
   constexpr int PV = PER > 0 ? PER : 1;
   __shared__ unsigned long long s_w[16];
+  __shared__ uint32_t s_over;
+  if (threadIdx.x == 0) s_over = 0;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t per = PER > 0 ? PER : (nseg + 1023) / 1024;
   const uint64_t i0 = min(nseg, (uint64_t)threadIdx.x * per), i1 = min(nseg, i0 + per);
   unsigned long long c = 0;
   uint32_t v[PV];
+  uint32_t over = 0;  // a segment counted more rows than its arena holds (estimated caps)
   if (PER > 0) {
 #pragma unroll
     for (int p = 0; p < PV; ++p) {
@@ -1792,10 +1824,15 @@ __global__ __launch_bounds__(1024) void k_seg_totals(const uint32_t *cnt, uint64
       const uint32_t x = cnt[i < nseg ? i : nseg - 1];
       v[p] = x & (0u - (uint32_t)(i < i1));  // mask, not select (see k_bin_scan)
       c += v[p];
+      over |= (uint32_t)(v[p] > (i < nseg_h ? cap_h : cap_l));
     }
   } else {
-    for (uint64_t i = i0; i < i1; ++i) c += cnt[i];
+    for (uint64_t i = i0; i < i1; ++i) {
+      c += cnt[i];
+      over |= (uint32_t)(cnt[i] > (i < nseg_h ? cap_h : cap_l));
+    }
   }
+  if (over) atomicOr(&s_over, 1u);
   unsigned long long incl = c;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -1827,17 +1864,19 @@ __global__ __launch_bounds__(1024) void k_seg_totals(const uint32_t *cnt, uint64
     mail.p[1] = soffs[nseg];
     mail.p[2] = member ? member[0] : 0;
     mail.p[3] = member ? member[1] : 0;
+    mail.p[4] = s_over;
     mail_post(mail);
   }
 }
 void launch_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h, uint64_t *soffs,
-                       const unsigned long long *member, const Mail &mail, hipStream_t s) {
+                       const unsigned long long *member, uint64_t cap_h, uint64_t cap_l, const Mail &mail,
+                       hipStream_t s) {
   if (nseg == 0) {
-    hipLaunchKernelGGL((k_seg_totals<0>), dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, mail);
+    hipLaunchKernelGGL((k_seg_totals<0>), dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, cap_h, cap_l, mail);
   } else if (nseg <= 8 * 1024) {
-    hipLaunchKernelGGL((k_seg_totals<8>), dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, mail);
+    hipLaunchKernelGGL((k_seg_totals<8>), dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, cap_h, cap_l, mail);
   } else {
-    hipLaunchKernelGGL((k_seg_totals<0>), dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, mail);
+    hipLaunchKernelGGL((k_seg_totals<0>), dim3(1), dim3(1024), 0, s, cnt, nseg, nseg_h, soffs, member, cap_h, cap_l, mail);
   }
   KCHECK("k_seg_totals");
 }

@@ -723,8 +723,6 @@ class Planner {
   void compile_steps() {
     for (auto &n : nodes_)
       if (n.optional) unsupported("optional pattern nodes");
-    for (auto &e : edges_)
-      if (e.item->is_multi) unsupported("multi-step path items .( ... )");
     // candidate sets that must be non-empty (calculateMatch :340-357, :359-367)
     for (int a : prefetched_) plan_->must_be_nonempty.push_back(bitmap(nodes_[a].alias, 1));
     if (!prefetched_.count(root_))
@@ -766,19 +764,31 @@ class Planner {
       st.mode = bound[t] ? T_BOUND : prefetched_.count(t) ? T_CAND : T_FREE;
       bool varlen = it.filter.while_ || it.filter.has_max_depth;
       std::string m = lower(it.method);
-      if (m != "out" && m != "in" && m != "both") unsupported("traversal method " + it.method + "() on the device");
+      if (!it.is_multi && m != "out" && m != "in" && m != "both")
+        unsupported("traversal method " + it.method + "() on the device");
       std::vector<std::pair<std::string, bool>> rconds;
       vertex_where_of(nodes_[t].alias, &rconds);
       if (!rconds.empty()) {
-        if (varlen || st.mode != T_FREE)
-          unsupported("$matched in the WHERE of a variable-length, bound or prefetched target (" + nodes_[t].alias + ")");
+        if (varlen || it.is_multi || st.mode != T_FREE)
+          unsupported("$matched in the WHERE of a variable-length, multi-step, bound or prefetched target (" +
+                      nodes_[t].alias + ")");
         for (auto &rc : rconds) {
           auto ai = alias_idx_.find(rc.first);
           if (ai == alias_idx_.end() || !bound[ai->second] || ai->second == t)
             unsupported("$matched." + rc.first + " is not bound when " + nodes_[t].alias + " is matched");
         }
       }
-      if (varlen) {
+      if (it.is_multi) {  // never reversed: OMultiMatchPathItem.isBidirectional is false
+        st.kind = S_MULTI;
+        st.trav.multi = true;
+        st.trav.subs = compile_subs(it.multi);
+        st.trav.varlen = varlen;
+        st.trav.where_prog = add_prog(where_of(nodes_[t].alias), varlen);  // the rebound alias filter (:185-195)
+        st.trav.while_prog = add_prog(it.filter.while_, true);
+        st.trav.has_max_depth = it.filter.has_max_depth;
+        st.trav.max_depth = it.filter.max_depth;
+        if (st.mode == T_CAND) st.cand_bm = bitmap(nodes_[t].alias, 1);
+      } else if (varlen) {
         st.kind = S_VARLEN;
         st.adj = adjacency(m, it.labels);
         st.where_prog = add_prog(where_of(nodes_[t].alias), true);
@@ -797,7 +807,7 @@ class Planner {
           st.filter_bm = st.mode == T_CAND ? bitmap(nodes_[t].alias, 1) : bitmap(nodes_[t].alias, 0);
         }
       }
-      st.desc = std::string(st.kind == S_VARLEN ? "varlen " : st.kind == S_CHECK ? "check " : "expand ") +
+      st.desc = std::string(st.kind == S_VARLEN ? "varlen " : st.kind == S_MULTI ? "multi " : st.kind == S_CHECK ? "check " : "expand ") +
                 nodes_[s].alias + (fwd ? " -" : " <-") + it.method + "- " + nodes_[t].alias +
                 (st.mode == T_BOUND ? " [bound]" : st.mode == T_CAND ? " [candidates]" : " [free]");
       plan_->steps.push_back(st);
@@ -822,6 +832,44 @@ class Planner {
         plan_->steps.push_back(c);
         bound[a] = true;
       }
+  }
+
+  // The sub-items of a multi item .( ... ): their own filters (not rebound: they are not pattern nodes),
+  // `outE('L').inV()` and `inE('L').outV()` pairs as the vertex sets of out('L') / in('L')
+  std::vector<TravSpec> compile_subs(const std::vector<PathItem> &items) {
+    std::vector<TravSpec> out;
+    for (size_t i = 0; i < items.size(); ++i) {
+      const PathItem &s = items[i];
+      const PathItem *fi = &s;  // the item whose filter applies
+      TravSpec t;
+      if (s.is_multi) {
+        t.multi = true;
+        t.subs = compile_subs(s.multi);
+      } else {
+        const std::string m = lower(s.method);
+        if (m == "oute" || m == "ine") {
+          if (s.filter.where || s.filter.while_ || s.filter.has_max_depth || s.filter.optional)
+            unsupported("a filter on the edge step " + s.method + "() inside .( ... )");
+          const std::string v = i + 1 < items.size() && !items[i + 1].is_multi ? lower(items[i + 1].method) : "";
+          if (!((m == "oute" && v == "inv") || (m == "ine" && v == "outv")) || !items[i + 1].labels.empty())
+            unsupported("edge step " + s.method + "() not followed by its vertex step inside .( ... )");
+          t.adj = adjacency(m == "oute" ? "out" : "in", s.labels);
+          fi = &items[++i];
+        } else {
+          if (m != "out" && m != "in" && m != "both") unsupported("traversal method " + s.method + "() inside .( ... )");
+          t.adj = adjacency(m, s.labels);
+        }
+      }
+      const MatchFilter &f = fi->filter;
+      if (f.optional) unsupported("optional inside .( ... )");
+      t.varlen = f.while_ || f.has_max_depth;
+      t.where_prog = add_prog(f.where, t.varlen);
+      t.while_prog = add_prog(f.while_, true);
+      t.has_max_depth = f.has_max_depth;
+      t.max_depth = f.max_depth;
+      out.push_back(std::move(t));
+    }
+    return out;
   }
 
   void compile_projection() {

@@ -40,8 +40,26 @@ struct BitmapSpec {
 // S_ROWCMP: keep the rows where col[src] (=|!=) col[dst]: a WHERE conjunct `$matched.X op $currentMatch`
 // of the alias the previous step bound (OMatchPathItem.executeTraversal evaluates it per neighbour
 // with $matched = the row's bindings, P/OMatchPathItem.java:49-78; identity comparison of records)
-enum StepKind { S_ROOT, S_EXPAND, S_CHECK, S_VARLEN, S_NEWROOT, S_CARTESIAN, S_KILL, S_ROWCMP };
+// S_MULTI: a multi-step item .( ... ) (OMultiMatchPathItem, P/OMultiMatchPathItem.java:41-61), over
+// (row, vertex) pair sets (Step::trav)
+enum StepKind { S_ROOT, S_EXPAND, S_CHECK, S_VARLEN, S_NEWROOT, S_CARTESIAN, S_KILL, S_ROWCMP, S_MULTI };
 enum TargetMode { T_FREE, T_CAND, T_BOUND };
+
+// One item's traversal as a set-valued function of a start vertex, OMatchPathItem.executeTraversal
+// (P/OMatchPathItem.java:49-107): single-hop items expand `adj` and keep the neighbours passing `where`
+// (a HashSet); variable-length items (while / maxDepth) run level by level from the start vertex with
+// $depth; multi items compose `subs`, each applied to every vertex of the previous step's set (a set
+// per step, OMultiMatchPathItem.traversePatternEdge). `outE('L').inV()` / `inE('L').outV()` pairs
+// inside a multi item are the vertex sets of out('L') / in('L').
+struct TravSpec {
+  bool multi = false;
+  AdjSpec adj;                  // single-method item
+  std::vector<TravSpec> subs;   // multi item
+  bool varlen = false;          // while or maxDepth given
+  int where_prog = -1, while_prog = -1;
+  bool has_max_depth = false;
+  int max_depth = 0;
+};
 
 struct Step {
   StepKind kind = S_EXPAND;
@@ -54,6 +72,7 @@ struct Step {
   bool has_max_depth = false;
   int max_depth = 0;
   bool row_eq = false;     // S_ROWCMP: = (true) or != (false)
+  TravSpec trav;           // S_MULTI
   std::string desc;
 };
 

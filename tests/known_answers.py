@@ -246,14 +246,13 @@ for _p, _m in [("p10", "c"), ("p12", "c"), ("p6", "b"), ("p11", "b")]:
         for _multi in (False, True):
             KNOWN.append(("testManager%s%s.%s" % ("2" if _multi else "", "Arrows" if _arrows else "", _p),
                           660 if not _multi else 710, _manager(_p, _arrows, _multi), None, ("names", "manager"),
-                          (1, {_m}), not _multi))
+                          (1, {_m}), True))
 for _arrows in (False, True):
     for _multi in (False, True):
         tag = "testManaged%s%s" % ("2" if _multi else "", "Arrows" if _arrows else "")
-        KNOWN.append((tag + ".a", 734, _managed("a", _arrows, _multi), None, ("names", "managed"), (1, {"p1"}),
-                      not _multi))
+        KNOWN.append((tag + ".a", 734, _managed("a", _arrows, _multi), None, ("names", "managed"), (1, {"p1"}), True))
         KNOWN.append((tag + ".b", 734, _managed("b", _arrows, _multi), None, ("names", "managed"),
-                      (5, {"p2", "p3", "p6", "p7", "p11"}), not _multi))
+                      (5, {"p2", "p3", "p6", "p7", "p11"}), True))
 KNOWN.append(("testManagedElements", 1264, _managed("b", True, False, "$elements"), None, ("record_names", None),
               (6, {"b", "p2", "p3", "p6", "p7", "p11"}), True))
 KNOWN.append(("testManagedPathElements", 1299, _managed("b", True, False, "$pathElements"), None,

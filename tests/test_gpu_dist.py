@@ -114,6 +114,32 @@ def test_rccl_one_rank_routes_through_itself(rmat10_full, monkeypatch):
         comm.close()
 
 
+def test_failing_rank_releases_its_peers(rmat10_full):
+    """A rank whose execute fails (here: a missing query parameter on rank 0 only) aborts the thread
+    communicator; its peer fails with an error instead of waiting forever in the exchange."""
+    import orientdb_amd as o
+    parts = _parts(2)
+    comms = o.Comm.threads(2)
+    q = RMAT_QUERIES[0][1]
+    errs = [None, None]
+
+    def work(r):
+        try:
+            o.OMatchStatement(q.replace("age < 5", "age < ?") if r == 0 else q).execute(parts[r], comm=comms[r])
+        except o.OmxError as e:
+            errs[r] = e
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in th), "the surviving rank hung in the exchange"
+    assert errs[0] is not None and errs[1] is not None
+    for c in comms:
+        c.close()
+
+
 def test_partition_errors(rmat10_full):
     import orientdb_amd as o
     parts = _parts(2)

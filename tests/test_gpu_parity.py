@@ -218,6 +218,19 @@ def test_rmat_parity_l2_probe_heavy(rmat10, q, monkeypatch):
     _parity(g, ref, q[1], q[2])
 
 
+@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in ("c2_both_ends", "in_dir", "three_hop", "matches")],
+                         ids=lambda q: q[0])
+def test_rmat_parity_short_arena_rerun(rmat10, q, monkeypatch):
+    """Sliced hops size their output arenas from the target bitmap's density; with the margin at 0 the
+    estimate is short, the kernels count the rows they could not write, and the hop re-runs with the
+    exact bound (Executor::expand_core) — same rows."""
+    monkeypatch.setenv("OMX_HEAVY_DEG", "2")
+    monkeypatch.setenv("OMX_SLICE_SHIFT", "6")
+    monkeypatch.setenv("OMX_ARENA_MARGIN", "0")
+    g, ref = rmat10
+    _parity(g, ref, q[1], q[2])
+
+
 def test_sliced_count_mode_and_segments(rmat10, monkeypatch):
     """Count mode and the KEEP_DEVICE block-segmented result of the sliced kernel agree with the
     materialized rows."""
