@@ -188,7 +188,13 @@ typedef struct omx_result_info {
   uint64_t digest;           /* OMX_FLAG_DIGEST: Σ over the distinct rows of h(row) mod 2^64, h =   */
                              /* splitmix64 chained over the row's RIDs in column order (h0 =        */
                              /* 0x9E3779B97F4A7C15, h = mix(h ^ rid)); 0 otherwise                  */
+  int32_t documents;         /* 1: rows are documents of RETURN expressions / JSON (omx_result_cell); */
+                             /* 0: rows are RID tuples (omx_result_rows)                             */
+  int32_t reserved;
 } omx_result_info;
+
+/* A null binding (an unmatched optional node, P/OMatchStatement.java:448-458) in omx_result_rows. */
+#define OMX_NULL_RID UINT64_MAX
 
 int omx_result_info_get(const omx_result *r, omx_result_info *info);
 const char *omx_result_column_name(const omx_result *r, int32_t col);
@@ -200,6 +206,27 @@ const uint64_t *omx_result_rows(const omx_result *r);
 int omx_result_kernel_stat(const omx_result *r, int32_t i, const char **name, int64_t *launches, double *total_ms,
                            uint64_t *alg_bytes);
 void omx_result_free(omx_result *r);
+
+/* One field of a result document (info.documents = 1): the value of RETURN item `col` (or of JSON key
+ * `col`) in row `row`, as ODocument.field would hold it. LIST / MAP values come as JSON text in `s`
+ * (records as "#cluster:position" strings); `s` stays valid until omx_result_free. */
+#define OMX_CELL_NULL   0
+#define OMX_CELL_INT    1
+#define OMX_CELL_DOUBLE 2
+#define OMX_CELL_STRING 3
+#define OMX_CELL_BOOL   4
+#define OMX_CELL_RID    5
+#define OMX_CELL_LIST   6
+#define OMX_CELL_MAP    7
+typedef struct omx_cell {
+  int32_t type;   /* OMX_CELL_*                                                                     */
+  int32_t n;      /* LIST / MAP: elements                                                           */
+  int64_t i;      /* INT, BOOL (0/1)                                                                */
+  double d;       /* DOUBLE                                                                         */
+  uint64_t rid;   /* RID: (cluster << 48) | position                                                */
+  const char *s;  /* STRING (UTF-8), LIST / MAP (JSON)                                              */
+} omx_cell;
+int omx_result_cell(const omx_result *r, uint64_t row, int32_t col, omx_cell *out);
 
 const char *omx_last_error(void);
 const char *omx_version(void);

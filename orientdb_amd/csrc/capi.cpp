@@ -241,6 +241,23 @@ int omx_result_kernel_stat(const omx_result *r, int32_t i, const char **name, in
 
 void omx_result_free(omx_result *r) { delete r; }
 
+int omx_result_cell(const omx_result *r, uint64_t row, int32_t col, omx_cell *out) {
+  if (!r || !out || row >= r->docs.size() || col < 0 || (size_t)col >= r->docs[row].size()) return OMX_E_INVALID;
+  const omx::HVal &v = r->docs[row][col];
+  std::memset(out, 0, sizeof(*out));
+  switch (v.k) {
+    case omx::HVal::NUL: out->type = OMX_CELL_NULL; break;
+    case omx::HVal::INT: out->type = OMX_CELL_INT; out->i = v.i; break;
+    case omx::HVal::DBL: out->type = OMX_CELL_DOUBLE; out->d = v.d; break;
+    case omx::HVal::STR: out->type = OMX_CELL_STRING; out->s = v.s.c_str(); break;
+    case omx::HVal::BOOL: out->type = OMX_CELL_BOOL; out->i = v.i; break;
+    case omx::HVal::RID: out->type = OMX_CELL_RID; out->rid = v.rid; break;
+    case omx::HVal::LIST: out->type = OMX_CELL_LIST; out->n = (int32_t)v.items.size(); out->s = v.json.c_str(); break;
+    case omx::HVal::MAP: out->type = OMX_CELL_MAP; out->n = (int32_t)v.items.size(); out->s = v.json.c_str(); break;
+  }
+  return OMX_OK;
+}
+
 const char *omx_last_error(void) { return g_last_error.c_str(); }
 
 const char *omx_version(void) { return "omx 0.1 (gfx950)"; }

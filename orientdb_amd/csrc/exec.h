@@ -5,11 +5,13 @@
 
 #include "graph.h"
 #include "plan.h"
+#include "project.h"
 
 struct omx_result {
   omx_result_info info{};
   std::vector<std::string> names;
   std::vector<uint64_t> rows;  // row-major n_rows × n_cols
+  std::vector<omx::Document> docs;  // RETURN expressions / JSON: one document per row (info.documents)
   struct KStat {
     std::string name;
     int64_t launches = 0;

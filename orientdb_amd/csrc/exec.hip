@@ -21,6 +21,7 @@
 
 #include "dist.h"
 #include "kernels.h"
+#include "project.h"
 
 namespace omx {
 namespace {
@@ -219,7 +220,22 @@ class Executor {
     std::vector<DBuf<uint32_t>> out;
     // partitioned + distinct projection: equal tuples meet on one rank first
     if (dist_ && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
-    if (R_ > 0 && !counted_only) {
+    const bool docs = p_.proj == Plan::PROJ_EXPR || p_.proj == Plan::PROJ_JSON;
+    if (R_ > 0 && !counted_only && docs) {
+      // RETURN expressions / JSON: distinct tuples of the aliases they read (device), then one document
+      // per tuple, de-duplicated by content (project.cpp: the OResultSet fill of addResult :698-719)
+      if (!p_.out_aliases.empty()) project_dedup(out, n);
+      else n = 1;  // constant expressions: the same document for every binding
+      std::vector<const uint32_t *> cp;
+      for (auto &c : out) cp.push_back(c.p);
+      int64_t lim = p_.limit >= 0 ? p_.limit : o_.limit;
+      tm_.begin("documents");
+      res->docs = build_documents(g_, p_, cp, n, lim, s_);
+      tm_.end();
+      n = res->docs.size();
+      ncols = (int)p_.out_names.size();
+      dedup_ran_ = 1;
+    } else if (R_ > 0 && !counted_only) {
       project_dedup(out, n);
       ncols = (int)out.size();
     } else if (counted_only) {
@@ -228,20 +244,20 @@ class Executor {
     }
     int64_t limit = p_.limit >= 0 ? p_.limit : o_.limit;
     if (limit > -1 && n > (uint64_t)std::max<int64_t>(limit, 1)) n = (uint64_t)std::max<int64_t>(limit, 1);
-    if (n > 0 && !counted_only && (o_.flags & OMX_FLAG_DIGEST)) {
+    if (n > 0 && !counted_only && !docs && (o_.flags & OMX_FLAG_DIGEST)) {
       std::vector<const uint32_t *> cp;
       for (auto &c : out) cp.push_back(c.p);
       DBuf<unsigned long long> d(&pool_, 1);
       HIP_CHECK(hipMemsetAsync(d.p, 0, 8, s_));
-      launch_digest(ncols, cp.data(), n, (o_.flags & OMX_FLAG_NO_RID_MAP) ? nullptr : g_.d_rids, d.p, cus(), s_);
+      launch_digest(ncols, cp.data(), n, (o_.flags & OMX_FLAG_NO_RID_MAP) ? nullptr : g_.d_rids, g_.V, d.p, cus(), s_);
       digest_ = read1(reinterpret_cast<const uint64_t *>(d.p));
     }
-    if (n > 0 && !counted_only && !(o_.flags & OMX_FLAG_KEEP_DEVICE)) {
+    if (n > 0 && !counted_only && !docs && !(o_.flags & OMX_FLAG_KEEP_DEVICE)) {
       DBuf<uint64_t> rids(&pool_, n * ncols);
       std::vector<const uint32_t *> cp;
       for (auto &c : out) cp.push_back(c.p);
       tm_.begin("k_map_rids");
-      launch_map_rids(ncols, cp.data(), n, (o_.flags & OMX_FLAG_NO_RID_MAP) ? nullptr : g_.d_rids, rids.p, s_);
+      launch_map_rids(ncols, cp.data(), n, (o_.flags & OMX_FLAG_NO_RID_MAP) ? nullptr : g_.d_rids, rids.p, g_.V, s_);
       tm_.end(n * ncols * 12);
       res->rows.resize(n * ncols);
       HIP_CHECK(hipMemcpyAsync(res->rows.data(), rids.p, n * ncols * sizeof(uint64_t), hipMemcpyDeviceToHost, s_));
@@ -268,6 +284,7 @@ class Executor {
     res->info.edges_traversed = edges_;
     res->info.edges_read = edges_iter_;
     res->info.digest = digest_;
+    res->info.documents = docs ? 1 : 0;
     res->info.bindings = bindings_;
     res->info.alg_bytes = alg_bytes_;
     res->info.device_ms = dms;
@@ -525,7 +542,10 @@ class Executor {
     for (const PredProgram &pp : p_.progs)
       for (const DPredInstr &in : pp.code)
         if (in.op == P_PUSH_DEG) unsupported("out()/in()/both().size() in WHERE is not supported on a partitioned snapshot");
-    if (p_.proj == Plan::PROJ_ELEMENTS) unsupported("$elements / $pathElements are not supported on a partitioned snapshot");
+    if (p_.proj != Plan::PROJ_ALIASES)
+      unsupported("$elements, $pathElements and RETURN expressions are not supported on a partitioned snapshot");
+    for (char opt : p_.optional)
+      if (opt) unsupported("optional nodes are not supported on a partitioned snapshot");
     if (p_.limit >= 0 || o_.limit >= 0) unsupported("LIMIT is not supported on a partitioned snapshot");
     dist_ = true;
   }
@@ -1045,6 +1065,23 @@ class Executor {
       return;
     }
     route_owner(st.src);
+    // optional target: rows whose traversal returns nothing continue with the target null (dense id V);
+    // taken before the expansion replaces the columns (P/OMatchStatement.java:448-458)
+    std::vector<DBuf<uint32_t>> empty_rows;
+    uint64_t n_empty = 0;
+    if (st.optional && R_) {
+      DBuf<uint8_t> fl(&pool_, R_);
+      launch_flag_no_neighbor(col_[st.src].p, R_, make_adj(st.adj), bitmap(st.where_bm), fl.p, s_);
+      DBuf<uint32_t> idx(&pool_, R_);
+      DBuf<uint64_t> nsel(&pool_, 1);
+      hipcub::CountingInputIterator<uint32_t> cnt(0);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cnt, fl.p, idx.p, nsel.p, (int64_t)R_, s_); });
+      n_empty = read1(nsel.p);
+      for (int c : bound_cols()) {
+        empty_rows.emplace_back(&pool_, std::max<uint64_t>(n_empty, 1));
+        if (n_empty) launch_gather_u32(col_[c].p, idx.p, n_empty, empty_rows.back().p, s_);
+      }
+    }
     std::vector<int> cols = bound_cols();  // the carried columns (st.dst is not bound yet)
     bound_[st.dst] = 1;
     std::vector<const uint32_t *> carry;
@@ -1055,6 +1092,21 @@ class Executor {
     edges_ += o.E + o.E_member;
     if (!o.counted_from_degrees) edges_iter_ += o.E;
     R_ = o.n;
+    if (n_empty) {  // append the null-target rows
+      const uint64_t n = R_ + n_empty;
+      auto cat = [&](DBuf<uint32_t> *a, const uint32_t *b) {
+        DBuf<uint32_t> o2(&pool_, n);
+        if (a && R_) HIP_CHECK(hipMemcpyAsync(o2.p, a->p, R_ * 4, hipMemcpyDeviceToDevice, s_));
+        if (b) HIP_CHECK(hipMemcpyAsync(o2.p + R_, b, n_empty * 4, hipMemcpyDeviceToDevice, s_));
+        else launch_fill_u32(o2.p + R_, n_empty, g_.V, s_);
+        return o2;
+      };
+      for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = cat(R_ ? &o.carry[i] : nullptr, empty_rows[i].p);
+      col_[st.dst] = cat(R_ ? &o.dst : nullptr, nullptr);
+      R_ = n;
+      segmented_ = false;
+      return;
+    }
     if (!write || R_ == 0) return;
     segmented_ = o.segmented;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
@@ -1172,6 +1224,7 @@ class Executor {
   bool fuse_ok(const Step &ex, const Step &ck) const {
     if (fuse_mode_ == "0" || dist_) return false;  // partitioned: N(y) of the check may live on another rank
     if (ck.kind != S_CHECK || ck.dst != ex.dst || ck.src == ex.dst || !col_[ck.src].p) return false;
+    if (ex.optional || ck.optional) return false;
     if (!ck.adj.sorted || ck.adj.parts.empty()) return false;
     return true;
   }
@@ -1191,6 +1244,14 @@ class Executor {
     const uint64_t R = R_;
     const uint64_t E = degree_sum(col_[st.src].p, R, st.adj);
     edges_ += E;
+    if (st.optional) {  // a bound optional target not reached becomes null; no row is dropped
+      DBuf<unsigned int> npe(&pool_, 1);
+      HIP_CHECK(hipMemsetAsync(npe.p, 0, 4, s_));
+      launch_check_optional(col_[st.src].p, col_[st.dst].p, R, make_adj(st.adj), bitmap(st.where_bm), g_.V, npe.p, s_);
+      if (read1(npe.p))
+        fail(OMX_E_EXECUTION, "NullPointerException: optional alias " + p_.aliases[st.dst] + " is null and reached again");
+      return;
+    }
     DBuf<uint8_t> flags(&pool_, R);
     tm_.begin("k_check");
     launch_check(col_[st.src].p, col_[st.dst].p, R, make_adj(st.adj), bitmap(st.filter_bm), flags.p, s_);
@@ -1667,7 +1728,7 @@ class Executor {
       DBuf<uint64_t> bm(&pool_, nwords_);
       HIP_CHECK(hipMemsetAsync(bm.p, 0, nwords_ * 8, s_));
       tm_.begin("k_mark_bitmap");
-      for (int a : p_.out_aliases) launch_mark_bitmap(col_[a].p, R_, bm.p, s_);
+      for (int a : p_.out_aliases) launch_mark_bitmap(col_[a].p, R_, bm.p, g_.V, s_);
       tm_.end(R_ * 4 * p_.out_aliases.size());
       uint64_t m = 0;
       out.push_back(bitmap_list(bm.p, 0, 1, m));

@@ -132,7 +132,8 @@ struct Graph {
   std::vector<EdgeSet> esets;
   std::vector<Property> props;
   std::vector<IndexInfo> indexes;
-  std::vector<uint16_t> h_vclass;  // kept only when indexes exist
+  std::vector<uint16_t> h_vclass;  // kept when indexes exist, or copied on the first RETURN expression
+  std::vector<uint64_t> h_rids;    // copied on the first RETURN expression (project.cpp)
   uint16_t *d_vclass = nullptr;
   uint64_t *d_rids = nullptr;
   DColumn *d_cols = nullptr;

@@ -209,18 +209,27 @@ void launch_swap_flags(const uint32_t *xs, const uint32_t *ys, uint64_t R, const
                        uint8_t *flags, unsigned long long *sums, int cus, hipStream_t s);
 void launch_flag_colcmp(const uint32_t *a, const uint32_t *b, uint64_t n, bool eq, uint8_t *flags, hipStream_t s);
 void launch_iota(uint32_t *out, uint64_t n, hipStream_t s);
+void launch_fill_u32(uint32_t *out, uint64_t n, uint32_t x, hipStream_t s);
 void launch_pack_pairs(const uint32_t *hi, const uint32_t *lo, uint64_t n, uint64_t *keys, hipStream_t s);
 void launch_unpack_pairs(const uint64_t *keys, uint64_t n, uint32_t *hi, uint32_t *lo, hipStream_t s);
 void launch_flag_not_in(const uint64_t *sorted, uint64_t nsorted, const uint64_t *keys, uint64_t n, uint8_t *flags,
                         hipStream_t s);
-void launch_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, hipStream_t s);
+// v ≥ V (a null binding) is skipped
+void launch_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, uint32_t V, hipStream_t s);
+// optional targets (exec.hip Executor::expand_step / check_step)
+void launch_flag_no_neighbor(const uint32_t *src, uint64_t R, const DAdj &adj, const uint64_t *filter, uint8_t *flags,
+                             hipStream_t s);
+void launch_check_optional(const uint32_t *src, uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
+                           uint32_t V, unsigned int *npe, hipStream_t s);
 void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out, hipStream_t s);
 void launch_flag_row_change(int ncols, const uint32_t *const *cols, uint64_t n, uint8_t *flags, hipStream_t s);
+// a null binding (dense id ≥ V: an unmatched optional node) maps to kNullRid
+constexpr uint64_t kNullRid = ~0ull;
 void launch_map_rids(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, uint64_t *out,
-                     hipStream_t s);
+                     uint32_t V, hipStream_t s);
 // *out += Σ_rows splitmix64-chain(RIDs of the row) (OMX_FLAG_DIGEST; rids == nullptr: dense ids)
-void launch_digest(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, unsigned long long *out,
-                   int cus, hipStream_t s);
+void launch_digest(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, uint32_t V,
+                   unsigned long long *out, int cus, hipStream_t s);
 // host evaluation of a predicate program that reads no vertex data (constants and $depth only)
 bool eval_pred_const(const DPred &pred, int64_t depth);
 

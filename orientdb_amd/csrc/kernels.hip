@@ -1654,6 +1654,52 @@ void launch_compact_segments(int ncols, uint32_t *const *in, uint32_t *const *ou
   KCHECK("k_compact_segments");
 }
 
+// ---- optional targets (P/OMatchStatement.java:448-458) ------------------------------------------------
+// flags[r] = 1 iff no neighbour of src[r] passes `filter` (the traversal returned nothing)
+__global__ void k_flag_no_neighbor(const uint32_t *src, uint64_t R, DAdj adj, const uint64_t *filter, uint8_t *flags) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint32_t v = src[r];
+  bool any = false;
+  for (int p = 0; p < adj.n && !any; ++p)
+    for (uint64_t e = adj.p[p].rp[v], h = adj.p[p].rp[v + 1]; e < h && !any; ++e)
+      any = !filter || bm_test(filter, adj.p[p].col[e]);
+  flags[r] = any ? 0 : 1;
+}
+void launch_flag_no_neighbor(const uint32_t *src, uint64_t R, const DAdj &adj, const uint64_t *filter, uint8_t *flags,
+                             hipStream_t s) {
+  if (!R) return;
+  hipLaunchKernelGGL(k_flag_no_neighbor, dim3(nblocks(R, 256)), dim3(256), 0, s, src, R, adj, filter, flags);
+  KCHECK("k_flag_no_neighbor");
+}
+// A bound optional target t of row r: t ∉ traversal(src[r]) → t := null (V). A null t with a non-empty
+// traversal is the reference's NullPointerException (matched.get(t).getIdentity(), :468): *npe = 1.
+__global__ void k_check_optional(const uint32_t *src, uint32_t *dst, uint64_t R, DAdj adj, const uint64_t *filter,
+                                 uint32_t V, unsigned int *npe) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint32_t v = src[r], t = dst[r];
+  bool found = false, any = false;
+  for (int p = 0; p < adj.n; ++p)
+    for (uint64_t e = adj.p[p].rp[v], h = adj.p[p].rp[v + 1]; e < h; ++e) {
+      const uint32_t x = adj.p[p].col[e];
+      if (filter && !bm_test(filter, x)) continue;
+      any = true;
+      found = found || x == t;
+    }
+  if (t >= V) {
+    if (any) atomicOr(npe, 1u);
+  } else if (!found) {
+    dst[r] = V;
+  }
+}
+void launch_check_optional(const uint32_t *src, uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
+                           uint32_t V, unsigned int *npe, hipStream_t s) {
+  if (!R) return;
+  hipLaunchKernelGGL(k_check_optional, dim3(nblocks(R, 256)), dim3(256), 0, s, src, dst, R, adj, filter, V, npe);
+  KCHECK("k_check_optional");
+}
+
 // ---- bound-target check (existence of dst[r] in N(src[r]); P/OMatchStatement.java:468-477) ----------
 
 __global__ void k_check(const uint32_t *src, const uint32_t *dst, uint64_t R, DAdj adj, const uint64_t *filter,
@@ -1991,6 +2037,16 @@ void launch_flag_colcmp(const uint32_t *a, const uint32_t *b, uint64_t n, bool e
   KCHECK("k_flag_colcmp");
 }
 
+__global__ void k_fill_u32(uint32_t *out, uint64_t n, uint32_t x) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = x;
+}
+void launch_fill_u32(uint32_t *out, uint64_t n, uint32_t x, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_fill_u32, dim3(nblocks(n, 256)), dim3(256), 0, s, out, n, x);
+  KCHECK("k_fill_u32");
+}
+
 __global__ void k_iota(uint32_t *out, uint64_t n) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = (uint32_t)i;
@@ -2043,13 +2099,13 @@ void launch_flag_not_in(const uint64_t *sorted, uint64_t ns, const uint64_t *key
   KCHECK("k_flag_not_in");
 }
 
-__global__ void k_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm) {
+__global__ void k_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, uint32_t V) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) atomicOr((unsigned long long *)&bm[v[i] >> 6], 1ull << (v[i] & 63));
+  if (i < n && v[i] < V) atomicOr((unsigned long long *)&bm[v[i] >> 6], 1ull << (v[i] & 63));
 }
-void launch_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, hipStream_t s) {
+void launch_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, uint32_t V, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_mark_bitmap, dim3(nblocks(n, 256)), dim3(256), 0, s, v, n, bm);
+  hipLaunchKernelGGL(k_mark_bitmap, dim3(nblocks(n, 256)), dim3(256), 0, s, v, n, bm, V);
   KCHECK("k_mark_bitmap");
 }
 
@@ -2078,20 +2134,21 @@ void launch_flag_row_change(int ncols, const uint32_t *const *cols, uint64_t n, 
   KCHECK("k_flag_row_change");
 }
 
-__global__ void k_map_rids(int ncols, ColPtrs cp, uint64_t n, const uint64_t *rids, uint64_t *out) {
+// a null binding (an unmatched optional node: dense id V) maps to kNullRid
+__device__ __forceinline__ uint64_t rid_of(const uint64_t *rids, uint32_t v, uint32_t V) {
+  return v >= V ? kNullRid : rids ? rids[v] : (uint64_t)v;
+}
+__global__ void k_map_rids(int ncols, ColPtrs cp, uint64_t n, const uint64_t *rids, uint64_t *out, uint32_t V) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  for (int c = 0; c < ncols; ++c) {
-    uint32_t v = cp.in[c][i];
-    out[i * ncols + c] = rids ? rids[v] : (uint64_t)v;
-  }
+  for (int c = 0; c < ncols; ++c) out[i * ncols + c] = rid_of(rids, cp.in[c][i], V);
 }
 void launch_map_rids(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, uint64_t *out,
-                     hipStream_t s) {
+                     uint32_t V, hipStream_t s) {
   if (!n || !ncols) return;
   ColPtrs cp;
   for (int c = 0; c < ncols; ++c) cp.in[c] = cols[c];
-  hipLaunchKernelGGL(k_map_rids, dim3(nblocks(n, 256)), dim3(256), 0, s, ncols, cp, n, rids, out);
+  hipLaunchKernelGGL(k_map_rids, dim3(nblocks(n, 256)), dim3(256), 0, s, ncols, cp, n, rids, out, V);
   KCHECK("k_map_rids");
 }
 
@@ -2104,14 +2161,13 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
 }
-__global__ __launch_bounds__(256) void k_digest(int ncols, ColPtrs cp, uint64_t n, const uint64_t *rids,
+__global__ __launch_bounds__(256) void k_digest(int ncols, ColPtrs cp, uint64_t n, const uint64_t *rids, uint32_t V,
                                                 unsigned long long *out) {
   uint64_t acc = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t h = 0x9E3779B97F4A7C15ull;
     for (int c = 0; c < ncols; ++c) {
-      const uint32_t v = cp.in[c][i];
-      h = mix64(h ^ (rids ? rids[v] : (uint64_t)v));
+      h = mix64(h ^ rid_of(rids, cp.in[c][i], V));
     }
     acc += h;
   }
@@ -2119,13 +2175,13 @@ __global__ __launch_bounds__(256) void k_digest(int ncols, ColPtrs cp, uint64_t 
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
   if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
 }
-void launch_digest(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, unsigned long long *out,
-                   int cus, hipStream_t s) {
+void launch_digest(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, uint32_t V,
+                   unsigned long long *out, int cus, hipStream_t s) {
   if (!n || !ncols) return;
   ColPtrs cp;
   for (int c = 0; c < ncols; ++c) cp.in[c] = cols[c];
   const unsigned g = (unsigned)std::min<uint64_t>(nblocks(n, 256), (uint64_t)cus * 8);
-  hipLaunchKernelGGL(k_digest, dim3(g), dim3(256), 0, s, ncols, cp, n, rids, out);
+  hipLaunchKernelGGL(k_digest, dim3(g), dim3(256), 0, s, ncols, cp, n, rids, V, out);
   KCHECK("k_digest");
 }
 

@@ -94,6 +94,7 @@ class Planner {
     sort_edges();
     choose_prefetch_and_root();
     if (logical_only) return std::move(plan_);
+    plan_->params = params_;
     compile_steps();
     compile_projection();
     plan_->limit = st_.has_limit ? st_.limit : -1;
@@ -721,8 +722,7 @@ class Planner {
 
   // ---- steps -----------------------------------------------------------------------------------
   void compile_steps() {
-    for (auto &n : nodes_)
-      if (n.optional) unsupported("optional pattern nodes");
+    for (auto &n : nodes_) plan_->optional.push_back(n.optional);
     // candidate sets that must be non-empty (calculateMatch :340-357, :359-367)
     for (int a : prefetched_) plan_->must_be_nonempty.push_back(bitmap(nodes_[a].alias, 1));
     if (!prefetched_.count(root_))
@@ -763,13 +763,20 @@ class Planner {
       st.dst = t;
       st.mode = bound[t] ? T_BOUND : prefetched_.count(t) ? T_CAND : T_FREE;
       bool varlen = it.filter.while_ || it.filter.has_max_depth;
+      if (nodes_[s].optional) unsupported("a traversal starting from the optional node " + nodes_[s].alias);
+      if (nodes_[t].optional) {
+        if (varlen || it.is_multi) unsupported("an optional variable-length or multi-step item");
+        if (!fwd) unsupported("a reversed traversal into an optional node");
+        st.optional = true;
+        st.where_bm = bitmap(nodes_[t].alias, 0);
+      }
       std::string m = lower(it.method);
       if (!it.is_multi && m != "out" && m != "in" && m != "both")
         unsupported("traversal method " + it.method + "() on the device");
       std::vector<std::pair<std::string, bool>> rconds;
       vertex_where_of(nodes_[t].alias, &rconds);
       if (!rconds.empty()) {
-        if (varlen || it.is_multi || st.mode != T_FREE)
+        if (varlen || it.is_multi || st.mode != T_FREE || st.optional)
           unsupported("$matched in the WHERE of a variable-length, multi-step, bound or prefetched target (" +
                       nodes_[t].alias + ")");
         for (auto &rc : rconds) {
@@ -872,6 +879,69 @@ class Planner {
     return out;
   }
 
+  // OExpression.getDefaultAlias: the item's text without spaces, every run of other characters than
+  // letters, digits, '_' and '$' → '_' ('friend.name' → 'friend_name')
+  static std::string default_alias(const std::string &raw) {
+    std::string s, o;
+    for (char c : raw)
+      if (c != ' ') s += c;
+    bool run = false;
+    for (char c : s) {
+      if (std::isalnum((unsigned char)c) || c == '_' || c == '$') {
+        o += c;
+        run = false;
+      } else if (!run) {
+        o += '_';
+        run = true;
+      }
+    }
+    size_t a = o.find_first_not_of('_'), b = o.find_last_not_of('_');
+    return a == std::string::npos ? std::string() : o.substr(a, b - a + 1);
+  }
+
+  // what the result builder (project.cpp) evaluates: literals, parameters, aliases and their fields,
+  // arithmetic / string concatenation, comparisons, JSON and arrays, out()/in()/both() of a vertex,
+  // size() / toUpperCase() / toLowerCase(), and [i] / [a-b] / [i, j] / [condition] selectors
+  void check_return(const ExprP &e, std::vector<int> &refs) {
+    if (!e) return;
+    switch (e->kind) {
+      case Expr::LIT:
+      case Expr::PARAM: return;
+      case Expr::FIELD: {
+        auto it = alias_idx_.find(e->name);
+        if (it != alias_idx_.end() && std::find(refs.begin(), refs.end(), it->second) == refs.end())
+          refs.push_back(it->second);
+        return;
+      }
+      case Expr::VAR: unsupported("context variable " + e->name + " in a RETURN expression");
+      case Expr::CALL: unsupported("function call " + e->name + "() in a RETURN expression");
+      case Expr::CHAIN:
+        check_return(e->kids[0], refs);
+        for (auto &s : e->suffixes) {
+          if (s.kind == Suffix::METHOD) {
+            const std::string m = lower(s.name);
+            if (m == "out" || m == "in" || m == "both") {
+              std::vector<std::string> labels;
+              for (auto &a : s.args) {
+                auto v = fold(a);
+                if (!v || v->kind != Value::STR) unsupported("non-constant edge label in a RETURN expression");
+                labels.push_back(v->s);
+              }
+              plan_->ret_adj[&s] = adjacency(m, labels);
+            } else if (!((m == "size" || m == "touppercase" || m == "tolowercase") && s.args.empty())) {
+              unsupported("method " + s.name + "() in a RETURN expression");
+            }
+          } else if (s.kind == Suffix::INDEX) {
+            for (const ExprP &x : {s.index, s.index2}) check_return(x, refs);
+            for (auto &x : s.items) check_return(x, refs);
+          }
+        }
+        return;
+      default:
+        for (auto &k : e->kids) check_return(k, refs);
+    }
+  }
+
   void compile_projection() {
     auto has = [&](const char *name) {
       for (auto &r : st_.returns)
@@ -893,14 +963,31 @@ class Planner {
           p.out_names.push_back(nodes_[a].alias);
         }
     } else {
-      for (auto &r : st_.returns) {
-        if (r.expr->kind != Expr::FIELD || !alias_idx_.count(r.expr->name))
-          unsupported("RETURN item " + r.text + " (only aliases, $matches, $patterns, $paths, $elements, $pathElements)");
-        p.out_aliases.push_back(alias_idx_.at(r.expr->name));
-        p.out_names.push_back(r.alias.empty() ? r.expr->name : r.alias);
+      bool plain = true;
+      for (auto &r : st_.returns)
+        plain = plain && r.expr->kind == Expr::FIELD && alias_idx_.count(r.expr->name);
+      if (plain) {
+        for (auto &r : st_.returns) {
+          p.out_aliases.push_back(alias_idx_.at(r.expr->name));
+          p.out_names.push_back(r.alias.empty() ? r.expr->name : r.alias);
+        }
+      } else {
+        // expressions / JSON (addResult :698-719, jsonToDoc :791-806): evaluated per distinct tuple of the
+        // aliases they read
+        const bool json = st_.returns.size() == 1 && st_.returns[0].expr->kind == Expr::JSON && st_.returns[0].alias.empty();
+        p.proj = json ? Plan::PROJ_JSON : Plan::PROJ_EXPR;
+        p.returns = st_.returns;
+        std::vector<int> refs;
+        for (auto &r : st_.returns) check_return(r.expr, refs);
+        p.out_aliases = refs;
+        if (json) {
+          p.out_names = st_.returns[0].expr->json_keys;
+        } else {
+          for (auto &r : st_.returns) p.out_names.push_back(r.alias.empty() ? default_alias(r.raw) : r.alias);
+        }
       }
     }
-    bool dup_free = true;
+    bool dup_free = !std::any_of(p.optional.begin(), p.optional.end(), [](char o) { return o != 0; });
     for (auto &s : p.steps)
       if (s.kind == S_EXPAND && !s.adj.dup_free) dup_free = false;
     std::set<int> cover(p.out_aliases.begin(), p.out_aliases.end());

@@ -1,5 +1,6 @@
 // plan.h — logical MATCH plan (the reference's planner) and its compilation to device steps.
 #pragma once
+#include <map>
 #include <memory>
 #include <string>
 #include <utility>
@@ -44,6 +45,8 @@ struct BitmapSpec {
 // (row, vertex) pair sets (Step::trav)
 enum StepKind { S_ROOT, S_EXPAND, S_CHECK, S_VARLEN, S_NEWROOT, S_CARTESIAN, S_KILL, S_ROWCMP, S_MULTI };
 enum TargetMode { T_FREE, T_CAND, T_BOUND };
+// an optional target (OMatchStatement.java:448-458): no match → the row continues with the alias null
+// (dense id V); a bound optional target that is not reached is overwritten with null
 
 // One item's traversal as a set-valued function of a start vertex, OMatchPathItem.executeTraversal
 // (P/OMatchPathItem.java:49-107): single-hop items expand `adj` and keep the neighbours passing `where`
@@ -73,6 +76,8 @@ struct Step {
   int max_depth = 0;
   bool row_eq = false;     // S_ROWCMP: = (true) or != (false)
   TravSpec trav;           // S_MULTI
+  bool optional = false;   // S_EXPAND / S_CHECK into an optional node
+  int where_bm = -1;       // optional target: the node's WHERE alone (the emptiness test of the traversal)
   std::string desc;
 };
 
@@ -91,9 +96,15 @@ struct Plan {
   std::vector<BitmapSpec> bitmaps;
   std::vector<int> must_be_nonempty;  // candidate bitmaps of prefetched aliases (calculateMatch :340-357)
   std::vector<Step> steps;
-  enum Projection { PROJ_ALIASES, PROJ_ELEMENTS } proj = PROJ_ALIASES;
+  // PROJ_EXPR: RETURN expressions (addResult :700-720), PROJ_JSON: one JSON RETURN (:791-806). Both are
+  // evaluated per distinct tuple of the aliases they read (out_aliases), then de-duplicated by content
+  enum Projection { PROJ_ALIASES, PROJ_ELEMENTS, PROJ_EXPR, PROJ_JSON } proj = PROJ_ALIASES;
   std::vector<int> out_aliases;
   std::vector<std::string> out_names;
+  std::vector<ReturnItem> returns;                 // PROJ_EXPR / PROJ_JSON
+  std::map<const Suffix *, AdjSpec> ret_adj;       // out()/in()/both() suffixes inside RETURN expressions
+  std::vector<char> optional;                      // per alias: an optional pattern node (null when unmatched)
+  Params params;                                   // the query parameters (RETURN expressions read them)
   bool unique_by_construction = false;
   int64_t limit = -1;  // LIMIT clause (-1 = none)
 };

@@ -117,8 +117,10 @@ class Parser {
     ++i_;
     for (;;) {
       ReturnItem ri;
+      const size_t start = i_;
       ri.expr = expr();
       ri.text = expr_text(ri.expr);
+      for (size_t k = start; k < i_; ++k) ri.raw += (k > start ? " " : "") + t_[k].v;
       if (kw("as")) {
         ++i_;
         ri.alias = next().v;
@@ -372,8 +374,36 @@ class Parser {
         ++i_;
         Suffix s;
         s.kind = Suffix::INDEX;
-        s.index = or_expr();
-        while (!op("]")) next();  // range / multi selectors: kept opaque (unsupported on the device)
+        if (peek().kind == Tok::NUM && peek(1).kind == Tok::OP && peek(1).v == "-" && peek(2).kind == Tok::NUM &&
+            peek(3).kind == Tok::OP && peek(3).v == "]") {  // [a-b]: a range, not a subtraction
+          s.sel = Suffix::SEL_RANGE;
+          s.index = mk(Expr::LIT);
+          s.index->value = Value::Int(std::strtoll(next().v.c_str(), nullptr, 10));
+          ++i_;
+          s.index2 = mk(Expr::LIT);
+          s.index2->value = Value::Int(std::strtoll(next().v.c_str(), nullptr, 10));
+        } else {
+          ExprP sel = or_expr();
+          if (op("-")) {
+            ++i_;
+            s.sel = Suffix::SEL_RANGE;
+            s.index = sel->kind == Expr::TRUTH ? sel->kids[0] : sel;
+            s.index2 = expr();
+          } else if (op(",")) {
+            s.sel = Suffix::SEL_MULTI;
+            s.items.push_back(sel->kind == Expr::TRUTH ? sel->kids[0] : sel);
+            while (op(",")) {
+              ++i_;
+              s.items.push_back(expr());
+            }
+          } else if (sel->kind == Expr::TRUTH) {
+            s.sel = Suffix::SEL_ONE;
+            s.index = sel->kids[0];
+          } else {
+            s.sel = Suffix::SEL_COND;
+            s.index = sel;
+          }
+        }
         expect("]");
         sfx.push_back(s);
       } else {

@@ -30,7 +30,11 @@ struct Suffix {
   enum Kind { FIELD, METHOD, INDEX } kind;
   std::string name;
   std::vector<ExprP> args;
-  ExprP index;
+  // INDEX selectors (OArraySelector / OArrayRangeSelector / OArraySingleValuesSelector / a condition):
+  // [i] → index; [a-b] → index..index2 (exclusive); [i, j, …] → items; [cond] → index (a condition)
+  enum Sel { SEL_ONE, SEL_RANGE, SEL_MULTI, SEL_COND } sel = SEL_ONE;
+  ExprP index, index2;
+  std::vector<ExprP> items;
 };
 
 struct Expr {
@@ -84,7 +88,8 @@ struct MatchExpression {
 struct ReturnItem {
   ExprP expr;
   std::string alias;  // AS alias ("" if none)
-  std::string text;   // canonical text, for $matches/$paths detection and default aliases
+  std::string text;   // canonical text, for $matches/$paths detection
+  std::string raw;    // the item's tokens joined by spaces (string literals unquoted): its default alias
 };
 
 struct Statement {
