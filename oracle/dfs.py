@@ -184,6 +184,12 @@ def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=No
         root = aliases[0]
     cols = g.columns
     keep = []
+    if any(n.optional for n in mo.nodes.values()):
+        raise NotImplementedError("oracle C path: optional nodes")
+    if not all(e[0] == "field" and e[1] in aidx for e, _, _ in mo.st.return_items) and not any(
+            t.replace(" ", "").lower() in ("$matches", "$patterns", "$paths", "$elements", "$pathelements")
+            for _, _, t in mo.st.return_items):
+        raise NotImplementedError("oracle C path: RETURN expressions")
 
     def where_mask(alias):
         w = mo.where_of(alias)

@@ -60,7 +60,17 @@ class omx_result_info(C.Structure):
     _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_int32), ("deduplicated", C.c_int32),
                 ("edges_traversed", C.c_uint64), ("bindings", C.c_uint64), ("alg_bytes", C.c_uint64),
                 ("device_ms", C.c_double), ("total_ms", C.c_double), ("edges_read", C.c_uint64),
-                ("digest", C.c_uint64)]
+                ("digest", C.c_uint64), ("documents", C.c_int32), ("reserved", C.c_int32)]
+
+
+OMX_NULL_RID = (1 << 64) - 1  # a null binding (unmatched optional node)
+OMX_CELL_NULL, OMX_CELL_INT, OMX_CELL_DOUBLE, OMX_CELL_STRING, OMX_CELL_BOOL, OMX_CELL_RID, OMX_CELL_LIST, \
+    OMX_CELL_MAP = range(8)
+
+
+class omx_cell(C.Structure):
+    _fields_ = [("type", C.c_int32), ("n", C.c_int32), ("i", C.c_int64), ("d", C.c_double), ("rid", C.c_uint64),
+                ("s", C.c_char_p)]
 
 
 # every exported symbol of include/omx/match.h: name -> (restype, argtypes)
@@ -81,6 +91,7 @@ SIGNATURES = {
     "omx_result_kernel_stat": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_char_p), C.POINTER(C.c_int64),
                                          C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "omx_result_free": (None, [C.c_void_p]),
+    "omx_result_cell": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int32, C.POINTER(omx_cell)]),
     "omx_last_error": (C.c_char_p, []),
     "omx_version": (C.c_char_p, []),
     "omx_rmat_generate": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int32,

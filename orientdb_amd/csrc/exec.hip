@@ -135,6 +135,7 @@ class Executor {
     if (const char *h = std::getenv("OMX_HEAVY_DEG")) {
       heavy_deg_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
       heavy_deg_sliced_ = heavy_deg_;
+      heavy_deg_fixed_ = true;
     }
     // variable-length strategy: "bfs" (multi-source BFS whenever exact), "pairs" ((row, v) levels), auto
     if (const char *v = std::getenv("OMX_VARLEN")) varlen_mode_ = v;
@@ -329,6 +330,7 @@ class Executor {
   int cus_ = 0;
   uint64_t heavy_deg_ = kHeavyDeg;
   uint64_t heavy_deg_sliced_ = kHeavyDegSliced;
+  bool heavy_deg_fixed_ = false;  // OMX_HEAVY_DEG given
   bool debug_expand_ = false;
   bool light_sliced_ = true;  // LDS-sliced light kernel for sliced single-part hops (OMX_LIGHT_SLICED=0: merge path)
   bool sliced_ = true;  // LDS-sliced heavy kernel for filtered hops (OMX_SLICED=0 disables)
@@ -755,7 +757,10 @@ class Executor {
                         (uint64_t)g_.V <= ((uint64_t)kMaxSlices << slice_shift_);
     const uint32_t P = sliced ? (uint32_t)(((uint64_t)g_.V + (1ull << slice_shift_) - 1) >> slice_shift_) : 1;
     const DCuts cuts = sliced ? slice_cuts_of(adjs, P) : DCuts{};
-    const uint64_t hd = sliced ? heavy_deg_sliced_ : heavy_deg_;
+    // sliced: a heavy row is cut into P pieces, one chunk each; below ~128 edges per piece a chunk issues
+    // its 16 loads for a few live slots, so the cut grows with P (RMAT-24, P = 16: 2048 measured best of
+    // 256…4096, profiles/r02/hd_sweep)
+    const uint64_t hd = !sliced ? heavy_deg_ : heavy_deg_fixed_ || P <= 4 ? heavy_deg_sliced_ : 128ull * P;
     // per-tile sums → one-workgroup scan (posts the totals to the host) → per-tile offsets and chunks
     DBuf<uint64_t> blk(&pool_, (uint64_t)(kBinKeys + P) * bin_tiles(R)), qb(&pool_, P + 1);
     // a sliced hop that writes rows sizes its arenas from the target bitmap's density per slice

@@ -15,11 +15,14 @@ strategy falls back to OMatchStatement).
 """
 import ctypes as C
 import json
+import re
 
 import numpy as np
 
 from . import _native as N
 from .graph import unpack_rid
+
+_RID_RE = re.compile(r"^#(-?\d+):(\d+)$")
 
 
 class ORecordId(tuple):
@@ -30,7 +33,16 @@ class ORecordId(tuple):
 
     @classmethod
     def from_packed(cls, r):
+        """None for a null binding (an unmatched optional node, OMX_NULL_RID)."""
+        if int(r) == N.OMX_NULL_RID:
+            return None
         return cls(*unpack_rid(r))
+
+    @classmethod
+    def parse(cls, s):
+        """'#cluster:position' → ORecordId, or None if s is not a RID string."""
+        m = _RID_RE.match(s)
+        return cls(int(m.group(1)), int(m.group(2))) if m else None
 
     @property
     def cluster(self):
@@ -88,6 +100,35 @@ def _value(a, index=0, name=None):
     else:
         v.type, v.s = N.OMX_VAL_STRING, str(a).encode()
     return v
+
+
+def _json_value(x):
+    """A LIST / MAP cell (JSON text): record links come as '#cluster:position' strings."""
+    if isinstance(x, str):
+        r = ORecordId.parse(x)
+        return r if r is not None else x
+    if isinstance(x, list):
+        return [_json_value(y) for y in x]
+    if isinstance(x, dict):
+        return ODocument((k, _json_value(v)) for k, v in x.items())
+    return x
+
+
+def _cell_value(cell):
+    t = cell.type
+    if t == N.OMX_CELL_NULL:
+        return None
+    if t == N.OMX_CELL_INT:
+        return int(cell.i)
+    if t == N.OMX_CELL_DOUBLE:
+        return float(cell.d)
+    if t == N.OMX_CELL_STRING:
+        return cell.s.decode("utf-8")
+    if t == N.OMX_CELL_BOOL:
+        return bool(cell.i)
+    if t == N.OMX_CELL_RID:
+        return ORecordId.from_packed(cell.rid)
+    return _json_value(json.loads(cell.s.decode("utf-8")))
 
 
 class OMatchStatement:
@@ -169,6 +210,16 @@ class OMatchStatement:
             i += 1
         rs.kernel_stats = stats
         nrows, ncols = info.n_rows, info.n_cols
+        if info.documents:  # RETURN expressions / JSON: one document per row (omx_result_cell)
+            rs.rows = np.zeros((0, 0), np.uint64)
+            cell = N.omx_cell()
+            for i in range(nrows):
+                doc = ODocument()
+                for c, name in enumerate(cols):
+                    N.check(L.omx_result_cell(r, i, c, C.byref(cell)))
+                    doc[name] = _cell_value(cell)
+                rs.append(doc)
+            return rs
         p = L.omx_result_rows(r)
         if p and nrows and ncols:
             rs.rows = np.ctypeslib.as_array(p, shape=(nrows * ncols,)).reshape(nrows, ncols).copy()

@@ -37,28 +37,28 @@ KNOWN = [
      None, ("names", "friend"), (1, {"n2"}), True),
     ("testCommonFriends2", 324,
      "match {class:Person, where:(name = 'n1')}.both('Friend'){as:friend}.both('Friend'){class: Person, where:(name = 'n4')} return friend.name as name",
-     None, ("field", "name"), (1, {"n2"}), False),
+     None, ("field", "name"), (1, {"n2"}), True),
     ("testCommonFriends2Arrows", 336,
      "match {class:Person, where:(name = 'n1')}-Friend-{as:friend}-Friend-{class: Person, where:(name = 'n4')} return friend.name as name",
-     None, ("field", "name"), (1, {"n2"}), False),
+     None, ("field", "name"), (1, {"n2"}), True),
     ("testReturnMethod", 348,
      "match {class:Person, where:(name = 'n1')}.both('Friend'){as:friend}.both('Friend'){class: Person, where:(name = 'n4')} return friend.name.toUppercase() as name",
-     None, ("field", "name"), (1, {"N2"}), False),
+     None, ("field", "name"), (1, {"N2"}), True),
     ("testReturnMethodArrows", 360,
      "match {class:Person, where:(name = 'n1')}-Friend-{as:friend}-Friend-{class: Person, where:(name = 'n4')} return friend.name.toUppercase() as name",
-     None, ("field", "name"), (1, {"N2"}), False),
+     None, ("field", "name"), (1, {"N2"}), True),
     ("testReturnExpression", 372,
      "match {class:Person, where:(name = 'n1')}.both('Friend'){as:friend}.both('Friend'){class: Person, where:(name = 'n4')} return friend.name + ' ' +friend.name as name",
-     None, ("field", "name"), (1, {"n2 n2"}), False),
+     None, ("field", "name"), (1, {"n2 n2"}), True),
     ("testReturnExpressionArrows", 384,
      "match {class:Person, where:(name = 'n1')}-Friend-{as:friend}-Friend-{class: Person, where:(name = 'n4')} return friend.name + ' ' +friend.name as name",
-     None, ("field", "name"), (1, {"n2 n2"}), False),
+     None, ("field", "name"), (1, {"n2 n2"}), True),
     ("testReturnDefaultAlias", 396,
      "match {class:Person, where:(name = 'n1')}.both('Friend'){as:friend}.both('Friend'){class: Person, where:(name = 'n4')} return friend.name",
-     None, ("field", "friend_name"), (1, {"n2"}), False),
+     None, ("field", "friend_name"), (1, {"n2"}), True),
     ("testReturnDefaultAliasArrows", 408,
      "match {class:Person, where:(name = 'n1')}-Friend-{as:friend}-Friend-{class: Person, where:(name = 'n4')} return friend.name",
-     None, ("field", "friend_name"), (1, {"n2"}), False),
+     None, ("field", "friend_name"), (1, {"n2"}), True),
     ("testFriendsOfFriends", 414,
      "match {class:Person, where:(name = 'n1')}.out('Friend').out('Friend'){as:friend} return $matches", None,
      ("names", "friend"), (1, {"n4"}), True),
@@ -163,22 +163,22 @@ KNOWN = [
      None, ("uid_of", "friend1"), (1, {1}), True),
     ("testArrayNumber", 1078,
      "match {class:TriangleV, as: friend1, where: (uid = 0)}return friend1.out('TriangleE')[0] as foo", None,
-     ("field_kind", "foo"), (1, "vertex"), False),
+     ("field_kind", "foo"), (1, "vertex"), True),
     ("testArraySingleSelectors2", 1092,
      "match {class:TriangleV, as: friend1, where: (uid = 0)}return friend1.out('TriangleE')[0,1] as foo", None,
-     ("field_len", "foo"), (1, 2), False),
+     ("field_len", "foo"), (1, 2), True),
     ("testArrayRangeSelectors1", 1107,
      "match {class:TriangleV, as: friend1, where: (uid = 0)}return friend1.out('TriangleE')[0-1] as foo", None,
-     ("field_len", "foo"), (1, 1), False),
+     ("field_len", "foo"), (1, 1), True),
     ("testArrayRange2", 1122,
      "match {class:TriangleV, as: friend1, where: (uid = 0)}return friend1.out('TriangleE')[0-2] as foo", None,
-     ("field_len", "foo"), (1, 2), False),
+     ("field_len", "foo"), (1, 2), True),
     ("testArrayRange3", 1137,
      "match {class:TriangleV, as: friend1, where: (uid = 0)}return friend1.out('TriangleE')[0-3] as foo", None,
-     ("field_len", "foo"), (1, 2), False),
+     ("field_len", "foo"), (1, 2), True),
     ("testConditionInSquareBrackets", 1152,
      "match {class:TriangleV, as: friend1, where: (uid = 0)}return friend1.out('TriangleE')[uid = 2] as foo", None,
-     ("field_len", "foo"), (1, 1), False),
+     ("field_len", "foo"), (1, 1), True),
     ("testIndexedEdge", 1175,
      "match {class:IndexedVertex, as: one, where: (uid = 0)}.out('IndexedEdge'){class:IndexedVertex, as: two, where: (uid = 1)}return one, two",
      None, None, (1, None), True),
@@ -186,30 +186,30 @@ KNOWN = [
      "match {class:IndexedVertex, as: one, where: (uid = 0)}-IndexedEdge->{class:IndexedVertex, as: two, where: (uid = 1)}return one, two",
      None, None, (1, None), True),
     ("testJson", 1199, "match {class:IndexedVertex, as: one, where: (uid = 0)} return {'name':'foo', 'uuid':one.uid}",
-     None, None, (1, None), False),
+     None, None, (1, None), True),
     ("testJson2", 1213,
      "match {class:IndexedVertex, as: one, where: (uid = 0)} return {'name':'foo', 'sub': {'uuid':one.uid}}", None,
-     None, (1, None), False),
+     None, (1, None), True),
     ("testJson3", 1227,
      "match {class:IndexedVertex, as: one, where: (uid = 0)} return {'name':'foo', 'sub': [{'uuid':one.uid}]}", None,
-     None, (1, None), False),
+     None, (1, None), True),
     ("testUnique.1", 1241,
      "match {class:DiamondV, as: one, where: (uid = 0)}.out('DiamondE').out('DiamondE'){as: two} return one, two",
      None, None, (1, None), True),
     ("testUnique.2", 1250,
      "match {class:DiamondV, as: one, where: (uid = 0)}.out('DiamondE').out('DiamondE'){as: two} return one.uid, two.uid",
-     None, None, (1, None), False),
+     None, None, (1, None), True),
     ("testOptional", 1323,
      "match {class:Person, as: person} -NonExistingEdge-> {as:b, optional:true} return person, b.name", None, None,
-     (6, None), False),
+     (6, None), True),
     ("testOptional2", 1336,
      "match {class:Person, as: person} --> {as:b, optional:true, where:(nonExisting = 12)} return person, b.name",
-     None, None, (6, None), False),
+     None, None, (6, None), True),
     ("testOptional3", 1349,
      "match {class:Person, as:a, where:(name = 'n1' and 1 + 1 = 2)}.out('Friend'){as:friend, where:(name = 'n2' and 1 + 1 = 2)},{as:a}.out(){as:b, where:(nonExisting = 12), optional:true},{as:friend}.out(){as:b, optional:true} return friend",
-     None, ("names", "friend"), (1, {"n2"}), False),
+     None, ("names", "friend"), (1, {"n2"}), True),
     ("testAliasesWithSubquery", 1365, "match {class:Person, as:A} return A.name as namexx", None,
-     ("field_prefix", "namexx"), (6, "n"), False),
+     ("field_prefix", "namexx"), (6, "n"), True),
 ]
 
 

@@ -19,13 +19,16 @@ def oracle_rows(db, query, params=None, limit=None):
     return MatchOracle(db, query).execute(params, limit)
 
 
+NULL_RID = (1 << 64) - 1  # an unmatched optional node (include/omx/match.h OMX_NULL_RID)
+
+
 def oracle_set(rows, cols):
     out = set()
     for r in rows:
         if isinstance(r, Record):
             out.add(((r.rid[0] << 48) | r.rid[1],))
         else:
-            out.add(tuple((r[c].rid[0] << 48) | r[c].rid[1] for c in cols))
+            out.add(tuple(NULL_RID if r[c] is None else (r[c].rid[0] << 48) | r[c].rid[1] for c in cols))
     return out
 
 
@@ -59,8 +62,30 @@ def test_known_answers_on_device(refdb, gdb, case):
     assert rs.info["n_rows"] == len(ref)
     if "limit" in query.lower():
         return  # LIMIT picks HashSet-order-dependent rows (OMatchStatement.java:404): count only
+    if rs.info["documents"]:  # RETURN expressions / JSON: documents equal by content
+        assert doc_set(rs) == doc_set(ref)
+        return
     cols = rs.columns if rs.columns[0] not in ("$elements", "$pathElements") else None
     assert gpu_set(rs) == oracle_set(ref, cols)
+
+
+def _norm(x):
+    """Content of a result value: records by RID, documents by their fields (ODocumentEqualityWrapper)."""
+    if isinstance(x, Record):
+        return ("r", tuple(x.rid))
+    if x is not None and type(x).__name__ == "ORecordId":
+        return ("r", tuple(x))
+    if isinstance(x, dict):
+        return ("d", tuple(sorted((k, _norm(v)) for k, v in x.items())))
+    if isinstance(x, (list, tuple)):
+        return ("l", tuple(_norm(v) for v in x))
+    return ("v", x)
+
+
+def doc_set(rows):
+    out = {_norm(r) for r in rows}
+    assert len(out) == len(rows), "duplicate documents"
+    return out
 
 
 # ------------------------------------------------------------------------------------------------
@@ -150,7 +175,58 @@ RMAT_QUERIES = [
      ["me", "x", "f"]),
     ("bound_candidate", "MATCH {class:Person,as:a,where:(uid = 1)}-Knows->{as:b},{class:Person,as:b,where:(uid < 600)} RETURN a,b",
      ["a", "b"]),
+    # optional nodes (P/OMatchStatement.java:448-458): unmatched → the row continues with a null alias
+    ("optional_free", "MATCH {class:Person,as:a,where:(uid < 80)}-Knows->{as:b, where:(age < 3), optional:true} RETURN a, b",
+     ["a", "b"]),
+    ("optional_bound", "MATCH {class:Person,as:a,where:(uid < 40)}-Knows->{as:c, optional:true},"
+                       "{as:a}-Knows->{as:b}-Knows->{as:c, optional:true} RETURN a, b, c", ["a", "b", "c"]),
+    # multi-step items .( ... ) (P/OMultiMatchPathItem.java:41-61)
+    ("multi_two_hops", "MATCH {class:Person,as:a,where:(uid < 20)}.(out('Knows').out('Knows')){as:c, where:(age < 30)} RETURN a, c",
+     ["a", "c"]),
+    ("multi_varlen", "MATCH {class:Person,as:a,where:(uid < 6)}.(out('Knows'){where:(age < 70)}.in('Knows')){as:c, while:($depth < 2)} RETURN a, c",
+     ["a", "c"]),
+    ("multi_edge_pair", "MATCH {class:Person,as:a,where:(uid < 12)}.(outE('Knows').inV()){as:b, where:(age > 50)} RETURN a, b",
+     ["a", "b"]),
 ]
+
+
+DOC_QUERIES = [
+    ("alias_fields", "MATCH {class:Person,as:a,where:(age < 3)}-Knows->{as:b} RETURN a.uid, b.age"),
+    ("field_dedup", "MATCH {class:Person,as:a,where:(age < 10)}-Knows->{as:b} RETURN b.age as age"),
+    ("expr_math", "MATCH {class:Person,as:a,where:(uid < 30)}-Knows->{as:b} RETURN a.uid * 1000 + b.age as k, a"),
+    ("json", "MATCH {class:Person,as:a,where:(uid < 20)}-Knows->{as:b} RETURN {'a': a.uid, 'n': b.age + 1, 'r': b}"),
+    ("out_list", "MATCH {class:Person,as:a,where:(uid < 15)} RETURN a.out('Knows').size() as d, a.out('Knows')[0-2] as f"),
+    ("optional_expr", "MATCH {class:Person,as:a,where:(uid < 60)}-Knows->{as:b, where:(age < 4), optional:true} RETURN a, b.uid"),
+]
+
+
+@pytest.mark.parametrize("q", DOC_QUERIES, ids=[q[0] for q in DOC_QUERIES])
+def test_rmat_documents(rmat10, q):
+    """RETURN expressions / JSON (addResult :698-719, jsonToDoc :791-806): documents equal by content."""
+    import orientdb_amd as o
+    g, ref = rmat10
+    want = oracle_rows(ref.db, q[1])
+    rs = o.OMatchStatement(q[1]).execute(g)
+    assert rs.info["documents"] == 1
+    assert len(rs) == len(want)
+    if "[0-2]" in q[1]:  # list order = ridbag order (unpinned): compare as multisets of lengths and sizes
+        assert sorted((d["d"], len(d["f"])) for d in rs) == sorted((d["d"], len(d["f"])) for d in want)
+        return
+    assert doc_set(rs) == doc_set(want)
+
+
+def test_optional_null_reached_again_raises(rmat10):
+    """A null optional alias reached again by a non-empty traversal is the reference's
+    NullPointerException (matched.get(alias).getIdentity(), P/OMatchStatement.java:468): an execution error."""
+    import orientdb_amd as o
+    from oracle.match_ref import OracleError
+    g, ref = rmat10
+    q = ("MATCH {class:Person,as:a,where:(uid < 40)}-Knows->{as:b}-Knows->{as:c, where:(age < 30), optional:true},"
+         "{as:a}-Knows->{as:c, optional:true} RETURN a, b, c")
+    with pytest.raises(OracleError):
+        oracle_rows(ref.db, q)
+    with pytest.raises(o.OmxExecutionError):
+        o.OMatchStatement(q).execute(g)
 
 
 def _parity(g, ref, query, cols, **kw):
