@@ -231,6 +231,59 @@ int omx_result_cell(const omx_result *r, uint64_t row, int32_t col, omx_cell *ou
 const char *omx_last_error(void);
 const char *omx_version(void);
 
+/* ---- pointer-free variants (JNI / Panama: one caller-owned direct buffer) ---------------------- */
+/* The same snapshot and parameters as omx_graph_desc / omx_value, laid out in ONE buffer the Java side
+ * fills (a direct ByteBuffer, native byte order) with every pointer replaced by a byte offset from the
+ * start of the buffer (0 = none). Arrays are naturally aligned; strings are NUL-terminated UTF-8. omx
+ * validates every offset and length against `size` (OMX_E_INVALID otherwise) and copies what it keeps. */
+#define OMX_BLOB_MAGIC   0x47584D4Fu /* "OMXG" */
+#define OMX_BLOB_VERSION 1u
+typedef struct omx_graph_blob {       /* at offset 0 of the buffer                                       */
+  uint32_t magic, version;
+  uint32_t n_vertices;
+  int32_t n_classes, n_edge_sets, n_properties, n_indexes;
+  int32_t device;
+  uint32_t part_lo, part_hi;
+  uint64_t classes_off;      /* omx_class_rec[n_classes]                                               */
+  uint64_t vertex_class_off; /* uint16_t[V]                                                            */
+  uint64_t rids_off;         /* uint64_t[V]                                                            */
+  uint64_t edge_sets_off;    /* omx_edge_set_rec[n_edge_sets]                                          */
+  uint64_t properties_off;   /* omx_property_rec[n_properties]                                         */
+  uint64_t indexes_off;      /* omx_index_rec[n_indexes]                                               */
+} omx_graph_blob;
+typedef struct omx_class_rec {
+  uint64_t name_off;
+  int32_t superclass, is_edge_class, cluster_id, reserved;
+} omx_class_rec;
+typedef struct omx_edge_set_rec {
+  int32_t edge_class, reserved;
+  uint64_t n_edges, out_row_ptr_off, out_col_off, in_row_ptr_off, in_col_off, n_in_edges;
+} omx_edge_set_rec;
+typedef struct omx_property_rec {
+  uint64_t name_off;
+  int32_t type, dict_size;
+  uint64_t values_off, present_off;
+  uint64_t dict_off;         /* uint64_t[dict_size] offsets of the dictionary strings                  */
+} omx_property_rec;
+typedef struct omx_index_rec {
+  uint64_t property_off;
+  int32_t class_id, unique;
+} omx_index_rec;
+int omx_graph_create_blob(const void *blob, uint64_t size, omx_graph **out);
+
+/* Parameters as one buffer: uint32_t n, uint32_t reserved, omx_param_rec[n], then the strings. */
+typedef struct omx_param_rec {
+  int32_t type, index;       /* OMX_VAL_*, positional index (when name_off == 0)                       */
+  int64_t i;
+  double d;
+  uint64_t name_off;         /* named parameter (without ':'), 0 = positional                          */
+  uint64_t s_off;            /* OMX_VAL_STRING                                                          */
+} omx_param_rec;
+/* omx_execute with plain option fields and the parameter buffer (param_blob may be NULL: none). */
+int omx_execute_packed(omx_graph *g, omx_statement *s, int32_t mode, int32_t flags, int64_t limit, int32_t shard_rank,
+                       int32_t shard_world, omx_comm *comm, const void *param_blob, uint64_t param_blob_size,
+                       omx_result **out);
+
 /* ---- multi-GPU: communicator of a 1-D partitioned MATCH ------------------------ */
 /* With a partitioned snapshot, omx_execute routes binding rows to the rank owning the vertex whose
  * adjacency the next step reads (an all-to-all of counts, then of every bound column), and before a

@@ -95,9 +95,158 @@ std::string params_key(const omx_value *vals, int32_t n) {
   }
   return k;
 }
+// ---- pointer-free buffers (omx_graph_create_blob / omx_execute_packed) ------------------------------
+static_assert(sizeof(omx_graph_blob) == 88, "omx_graph_blob layout");
+static_assert(sizeof(omx_class_rec) == 24 && sizeof(omx_edge_set_rec) == 56 && sizeof(omx_property_rec) == 40 &&
+                  sizeof(omx_index_rec) == 16 && sizeof(omx_param_rec) == 40,
+              "blob record layouts");
+
+class Blob {
+ public:
+  Blob(const void *p, uint64_t size) : p_(static_cast<const uint8_t *>(p)), size_(size) {
+    if (!p_) omx::fail(OMX_E_INVALID, "null buffer");
+  }
+  // `count` elements of T at byte offset `off` (nullptr when off == 0 and optional)
+  template <class T>
+  const T *array(uint64_t off, uint64_t count, const char *what, bool optional = false) const {
+    if (off == 0) {
+      if (optional || count == 0) return nullptr;
+      omx::fail(OMX_E_INVALID, std::string("buffer: missing ") + what);
+    }
+    if (off % alignof(T) != 0) omx::fail(OMX_E_INVALID, std::string("buffer: misaligned ") + what);
+    if (off > size_ || count > (size_ - off) / sizeof(T)) omx::fail(OMX_E_INVALID, std::string("buffer: ") + what + " out of range");
+    return reinterpret_cast<const T *>(p_ + off);
+  }
+  const char *str(uint64_t off, const char *what, bool optional = false) const {
+    if (off == 0) {
+      if (optional) return nullptr;
+      omx::fail(OMX_E_INVALID, std::string("buffer: missing ") + what);
+    }
+    if (off >= size_) omx::fail(OMX_E_INVALID, std::string("buffer: ") + what + " out of range");
+    const void *z = std::memchr(p_ + off, 0, size_ - off);
+    if (!z) omx::fail(OMX_E_INVALID, std::string("buffer: unterminated ") + what);
+    return reinterpret_cast<const char *>(p_ + off);
+  }
+
+ private:
+  const uint8_t *p_;
+  uint64_t size_;
+};
+
 }  // namespace
 
 extern "C" {
+
+int omx_graph_create_blob(const void *blob, uint64_t size, omx_graph **out) {
+  return guard([&] {
+    if (!out) omx::fail(OMX_E_INVALID, "null out pointer");
+    const Blob b(blob, size);
+    if (size < sizeof(omx_graph_blob)) omx::fail(OMX_E_INVALID, "buffer smaller than its header");
+    if (reinterpret_cast<uintptr_t>(blob) % 8) omx::fail(OMX_E_INVALID, "buffer not 8-byte aligned");
+    const omx_graph_blob *h = static_cast<const omx_graph_blob *>(blob);
+    if (h->magic != OMX_BLOB_MAGIC || h->version != OMX_BLOB_VERSION) omx::fail(OMX_E_INVALID, "buffer: bad magic/version");
+    if (h->n_classes < 0 || h->n_edge_sets < 0 || h->n_properties < 0 || h->n_indexes < 0)
+      omx::fail(OMX_E_INVALID, "buffer: negative count");
+    const uint64_t V = h->n_vertices;
+    const uint32_t VL = (h->part_lo == 0 && h->part_hi == 0) ? h->n_vertices : h->part_hi - h->part_lo;
+    if (h->part_hi < h->part_lo) omx::fail(OMX_E_INVALID, "buffer: bad partition range");
+    omx_graph_desc d{};
+    d.n_vertices = h->n_vertices;
+    d.device = h->device;
+    d.part_lo = h->part_lo;
+    d.part_hi = h->part_hi;
+    d.vertex_class = b.array<uint16_t>(h->vertex_class_off, V, "vertex_class");
+    d.rids = b.array<uint64_t>(h->rids_off, V, "rids");
+    std::vector<omx_class_desc> cls(h->n_classes);
+    const omx_class_rec *cr = b.array<omx_class_rec>(h->classes_off, h->n_classes, "classes");
+    for (int i = 0; i < h->n_classes; ++i)
+      cls[i] = omx_class_desc{b.str(cr[i].name_off, "class name"), cr[i].superclass, cr[i].is_edge_class, cr[i].cluster_id};
+    d.n_classes = h->n_classes;
+    d.classes = cls.data();
+    std::vector<omx_edge_set_desc> es(h->n_edge_sets);
+    const omx_edge_set_rec *er = b.array<omx_edge_set_rec>(h->edge_sets_off, h->n_edge_sets, "edge sets");
+    for (int i = 0; i < h->n_edge_sets; ++i) {
+      const omx_edge_set_rec &r = er[i];
+      const uint64_t nin = r.n_in_edges ? r.n_in_edges : r.n_edges;
+      es[i].edge_class = r.edge_class;
+      es[i].n_edges = r.n_edges;
+      es[i].out_row_ptr = b.array<uint64_t>(r.out_row_ptr_off, (uint64_t)VL + 1, "out_row_ptr");
+      es[i].out_col = b.array<uint32_t>(r.out_col_off, r.n_edges, "out_col");
+      es[i].in_row_ptr = b.array<uint64_t>(r.in_row_ptr_off, (uint64_t)VL + 1, "in_row_ptr", true);
+      es[i].in_col = es[i].in_row_ptr ? b.array<uint32_t>(r.in_col_off, nin, "in_col") : nullptr;
+      es[i].n_in_edges = r.n_in_edges;
+      if (es[i].out_row_ptr && es[i].out_row_ptr[VL] != r.n_edges) omx::fail(OMX_E_INVALID, "buffer: out_row_ptr[V] != n_edges");
+      if (es[i].in_row_ptr && es[i].in_row_ptr[VL] != nin) omx::fail(OMX_E_INVALID, "buffer: in_row_ptr[V] != n_in_edges");
+    }
+    d.n_edge_sets = h->n_edge_sets;
+    d.edge_sets = es.data();
+    std::vector<omx_property_desc> pr(h->n_properties);
+    std::vector<std::vector<const char *>> dicts(h->n_properties);
+    const omx_property_rec *prr = b.array<omx_property_rec>(h->properties_off, h->n_properties, "properties");
+    for (int i = 0; i < h->n_properties; ++i) {
+      const omx_property_rec &r = prr[i];
+      pr[i].name = b.str(r.name_off, "property name");
+      pr[i].type = r.type;
+      const size_t w = r.type == OMX_PROP_INT64 || r.type == OMX_PROP_DOUBLE ? 8 : 4;
+      pr[i].values = w == 8 ? (const void *)b.array<uint64_t>(r.values_off, V, "property values")
+                            : (const void *)b.array<uint32_t>(r.values_off, V, "property values");
+      pr[i].present = b.array<uint8_t>(r.present_off, V, "present", true);
+      if (r.dict_size < 0) omx::fail(OMX_E_INVALID, "buffer: negative dictionary size");
+      if (r.type == OMX_PROP_STRING) {
+        const uint64_t *doff = b.array<uint64_t>(r.dict_off, (uint64_t)r.dict_size, "dictionary");
+        for (int k = 0; k < r.dict_size; ++k) dicts[i].push_back(b.str(doff[k], "dictionary string"));
+      }
+      pr[i].dict_size = r.dict_size;
+      pr[i].dict = dicts[i].empty() ? nullptr : dicts[i].data();
+    }
+    d.n_properties = h->n_properties;
+    d.properties = pr.data();
+    std::vector<omx_index_desc> ix(h->n_indexes);
+    const omx_index_rec *ir = b.array<omx_index_rec>(h->indexes_off, h->n_indexes, "indexes");
+    for (int i = 0; i < h->n_indexes; ++i) ix[i] = omx_index_desc{ir[i].class_id, b.str(ir[i].property_off, "index property"), ir[i].unique};
+    d.n_indexes = h->n_indexes;
+    d.indexes = ix.data();
+    auto g = std::make_unique<omx_graph>();
+    g->g.reset(omx::graph_create(&d));
+    *out = g.release();
+  });
+}
+
+int omx_execute_packed(omx_graph *g, omx_statement *s, int32_t mode, int32_t flags, int64_t limit, int32_t shard_rank,
+                       int32_t shard_world, omx_comm *comm, const void *param_blob, uint64_t param_blob_size,
+                       omx_result **out) {
+  std::vector<omx_value> vals;
+  const int rc = guard([&] {
+    if (!param_blob) return;
+    const Blob b(param_blob, param_blob_size);
+    if (param_blob_size < 8) omx::fail(OMX_E_INVALID, "parameter buffer smaller than its header");
+    if (reinterpret_cast<uintptr_t>(param_blob) % 8) omx::fail(OMX_E_INVALID, "parameter buffer not 8-byte aligned");
+    const uint32_t *n = static_cast<const uint32_t *>(param_blob);
+    const omx_param_rec *r = b.array<omx_param_rec>(8, n[0], "parameters");
+    for (uint32_t i = 0; i < n[0]; ++i) {
+      omx_value v{};
+      v.type = r[i].type;
+      v.index = r[i].index;
+      v.i = r[i].i;
+      v.d = r[i].d;
+      v.name = b.str(r[i].name_off, "parameter name", true);
+      v.s = r[i].type == OMX_VAL_STRING ? b.str(r[i].s_off, "parameter string") : nullptr;
+      vals.push_back(v);
+    }
+  });
+  if (rc != OMX_OK) return rc;
+  omx_exec_options o;
+  omx_exec_options_init(&o);
+  o.mode = mode;
+  o.flags = flags;
+  o.limit = limit;
+  o.shard_rank = shard_rank;
+  o.shard_world = shard_world;
+  o.comm = comm;
+  o.params = vals.empty() ? nullptr : vals.data();
+  o.n_params = (int32_t)vals.size();
+  return omx_execute(g, s, &o, out);
+}
 
 int omx_graph_create(const omx_graph_desc *desc, omx_graph **out) {
   return guard([&] {

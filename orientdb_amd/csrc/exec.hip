@@ -189,6 +189,7 @@ class Executor {
         // expansion + closing check fused into one intersection pass
         const Step *fuse = nullptr;
         if (st.kind == S_EXPAND && i + 1 < p_.steps.size() && fuse_ok(st, p_.steps[i + 1])) {
+          prune(p_.live_before[i]);
           fuse = &p_.steps[i + 1];
           const bool last2 = i + 2 == p_.steps.size();
           count_only = last2 && o_.mode == OMX_MODE_COUNT && p_.unique_by_construction;
@@ -199,6 +200,7 @@ class Executor {
           ++i;
           continue;
         }
+        prune(p_.live_before[i]);
         switch (st.kind) {
           case S_ROOT: root(st); break;
           case S_EXPAND: expand_step(st, !count_only, seg_ok); counted_only = count_only; break;
@@ -515,6 +517,15 @@ class Executor {
     return true;
   }
 
+  // drop the bound columns no later step reads and the projection does not return
+  void prune(const std::vector<char> &live) {
+    for (size_t a = 0; a < col_.size(); ++a)
+      if (!live[a] && (dist_ ? bound_[a] != 0 : col_[a].p != nullptr)) {
+        col_[a].reset();
+        bound_[a] = 0;
+      }
+  }
+
   std::vector<int> bound_cols() const {
     std::vector<int> c;
     for (size_t a = 0; a < col_.size(); ++a)
@@ -688,6 +699,13 @@ class Executor {
     // k_bfs_pull reads bit 31 of a col entry as the hub tag: vertex ids must stay below 2^31
     if (g_.V >= 0x80000000u) unsupported("variable-length traversal over 2^31 or more vertices");
     if (pull_hubs_ == 0 || g_.partitioned()) return g_.col(es, dir);
+    if (es.d_pull_col[dir] && es.hubs_requested[dir] != pull_hubs_) {  // another hub budget (OMX_PULL_HUBS)
+      HIP_CHECK(hipStreamSynchronize(s_));
+      (void)hipFree(es.d_pull_col[dir]);
+      (void)hipFree(es.d_hubs[dir]);
+      es.d_pull_col[dir] = nullptr;
+      es.d_hubs[dir] = nullptr;
+    }
     if (!es.d_pull_col[dir]) {  // built into local buffers, published once complete
       const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
       uint32_t *pcol = nullptr, *hubs = nullptr, nh = 0;
@@ -707,6 +725,7 @@ class Executor {
       es.d_pull_col[dir] = pcol;
       es.d_hubs[dir] = hubs;
       es.n_hubs[dir] = nh;
+      es.hubs_requested[dir] = pull_hubs_;
       g_.device_bytes += E * 4 + (uint64_t)pull_hubs_ * 4;
     }
     *nhubs = es.n_hubs[dir];
@@ -759,8 +778,8 @@ class Executor {
     const DCuts cuts = sliced ? slice_cuts_of(adjs, P) : DCuts{};
     // sliced: a heavy row is cut into P pieces, one chunk each; below ~128 edges per piece a chunk issues
     // its 16 loads for a few live slots, so the cut grows with P (RMAT-24, P = 16: 2048 measured best of
-    // 256…4096, profiles/r02/hd_sweep)
-    const uint64_t hd = !sliced ? heavy_deg_ : heavy_deg_fixed_ || P <= 4 ? heavy_deg_sliced_ : 128ull * P;
+    // 256…4096, profiles/r02/hd_sweep; RMAT-22, P = 4: 512 against 256, 1.80 against 1.83 ms per step)
+    const uint64_t hd = !sliced ? heavy_deg_ : heavy_deg_fixed_ ? heavy_deg_sliced_ : std::max<uint64_t>(heavy_deg_sliced_, 128ull * P);
     // per-tile sums → one-workgroup scan (posts the totals to the host) → per-tile offsets and chunks
     DBuf<uint64_t> blk(&pool_, (uint64_t)(kBinKeys + P) * bin_tiles(R)), qb(&pool_, P + 1);
     // a sliced hop that writes rows sizes its arenas from the target bitmap's density per slice
@@ -1757,6 +1776,20 @@ class Executor {
     dedup_ran_ = 1;
     tm_.begin("dedup");
     const int vbits = bits_for(g_.V);
+    bool may_null = false;
+    for (int a : p_.out_aliases) may_null = may_null || p_.optional[a];
+    if (k == 1 && !may_null) {
+      // one column: the distinct vertices are the set bits of a V-bit bitmap (no sort)
+      DBuf<uint64_t> bm(&pool_, nwords_);
+      HIP_CHECK(hipMemsetAsync(bm.p, 0, nwords_ * 8, s_));
+      launch_mark_bitmap(out[0].p, R_, bm.p, g_.V, s_);
+      uint64_t m = 0;
+      DBuf<uint32_t> lst = bitmap_list(bm.p, 0, 1, m);
+      out[0] = std::move(lst);
+      n = m;
+      tm_.end(R_ * 4 + nwords_ * 16 + m * 4);
+      return;
+    }
     if (k <= 3 && k * vbits <= 64) {
       // pack the tuple into one u64 key
       DBuf<uint64_t> keys(&pool_, R_);

@@ -993,6 +993,28 @@ class Planner {
     std::set<int> cover(p.out_aliases.begin(), p.out_aliases.end());
     p.unique_by_construction = p.proj == Plan::PROJ_ALIASES && dup_free && cover.size() == nodes_.size() &&
                                p.out_aliases.size() == nodes_.size();
+    // liveness of the binding columns, backwards from the projection
+    std::vector<char> live(nodes_.size(), 0);
+    for (int a : p.out_aliases) live[a] = 1;
+    p.live_before.assign(p.steps.size(), {});
+    for (size_t i = p.steps.size(); i-- > 0;) {
+      const Step &s = p.steps[i];
+      auto use = [&](int a) {
+        if (a >= 0) live[a] = 1;
+      };
+      switch (s.kind) {
+        case S_EXPAND: use(s.src); break;
+        case S_CHECK:
+        case S_ROWCMP: use(s.src); use(s.dst); break;
+        case S_VARLEN:
+        case S_MULTI:
+          use(s.src);
+          if (s.mode == T_BOUND) use(s.dst);
+          break;
+        default: break;
+      }
+      p.live_before[i] = live;
+    }
   }
 };
 

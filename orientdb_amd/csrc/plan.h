@@ -106,6 +106,9 @@ struct Plan {
   std::vector<char> optional;                      // per alias: an optional pattern node (null when unmatched)
   Params params;                                   // the query parameters (RETURN expressions read them)
   bool unique_by_construction = false;
+  // live_before[i][a]: alias a is read by step i or a later step, or projected; a bound column that is
+  // not live is dropped before step i (expansions then carry only what is still read)
+  std::vector<std::vector<char>> live_before;
   int64_t limit = -1;  // LIMIT clause (-1 = none)
 };
 

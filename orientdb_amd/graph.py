@@ -117,71 +117,27 @@ class GraphSnapshot:
 
     # ---------------------------------------------------------------------------------------------
     @classmethod
+    def from_blob(cls, buf):
+        """omx_graph_create_blob: a snapshot from one pointer-free buffer (include/omx/match.h), as a
+        Java builder fills it (buf: an 8-byte aligned numpy array)."""
+        L = N.lib()
+        h = C.c_void_p()
+        N.check(L.omx_graph_create_blob(buf.ctypes.data_as(C.c_void_p), buf.nbytes, C.byref(h)))
+        g = cls.__new__(cls)
+        g._h = h
+        g.V = int(np.frombuffer(buf.tobytes()[8:12], np.uint32)[0])
+        g.part = (0, g.V)
+        return g
+
+    @classmethod
     def from_records(cls, db, device=0):
         """Snapshot of a record-level description (the JSON of tests/golden/make_match_test_db.py):
         classes in creation order, one cluster per class (ids from 11), vertices in insertion order."""
-        if isinstance(db, str):
-            with open(db) as f:
-                db = json.load(f)
-        names = [c["name"] for c in db["classes"]]
-        classes = []
-        for i, c in enumerate(db["classes"]):
-            sup = names.index(c["superclass"]) if c["superclass"] is not None else -1
-            classes.append((c["name"], sup, bool(c["is_edge"]), 11 + i))
-        V = len(db["vertices"])
-        vclass = np.zeros(V, np.uint16)
-        rids = np.zeros(V, np.uint64)
-        per_class = {}
-        for v, rec in enumerate(db["vertices"]):
-            ci = names.index(rec["class"])
-            vclass[v] = ci
-            pos = per_class.get(ci, 0)
-            per_class[ci] = pos + 1
-            rids[v] = pack_rid(classes[ci][3], pos)
-        # adjacency: one CSR per edge class, rows in insertion order (ridbag order)
-        edge_sets = []
-        for ci, (name, _, is_edge, _) in enumerate(classes):
-            if not is_edge:
-                continue
-            es = [(e["out"], e["in"]) for e in db["edges"] if e["class"] == name]
-            if not es:
-                continue
-            src = np.array([a for a, _ in es], np.int64)
-            dst = np.array([b for _, b in es], np.uint32)
-            order = np.argsort(src, kind="stable")
-            rp = np.zeros(V + 1, np.uint64)
-            np.add.at(rp, src + 1, 1)
-            rp = np.cumsum(rp).astype(np.uint64)
-            edge_sets.append({"cls": ci, "out_rp": rp, "out_col": dst[order]})
-        # properties: one column per field name over all vertices
-        fields = []
-        for rec in db["vertices"]:
-            for k in rec["props"]:
-                if k not in fields:
-                    fields.append(k)
-        props = []
-        for f in fields:
-            vals = [rec["props"].get(f) for rec in db["vertices"]]
-            present = np.array([x is not None for x in vals], np.uint8)
-            nonnull = [x for x in vals if x is not None]
-            if all(isinstance(x, str) for x in nonnull):
-                d = sorted(set(nonnull), key=lambda s: s.encode())
-                code = {s: i for i, s in enumerate(d)}
-                col = np.array([code[x] if x is not None else -1 for x in vals], np.int32)
-                props.append({"name": f, "type": N.OMX_PROP_STRING, "values": col, "present": present, "dict": d})
-            elif all(isinstance(x, bool) for x in nonnull):
-                col = np.array([int(x) if x is not None else 0 for x in vals], np.int32)
-                props.append({"name": f, "type": N.OMX_PROP_BOOL, "values": col, "present": present})
-            elif all(isinstance(x, int) and not isinstance(x, bool) for x in nonnull):
-                col = np.array([x if x is not None else 0 for x in vals], np.int64)
-                props.append({"name": f, "type": N.OMX_PROP_INT64, "values": col, "present": present})
-            else:
-                col = np.array([float(x) if x is not None else 0.0 for x in vals], np.float64)
-                props.append({"name": f, "type": N.OMX_PROP_DOUBLE, "values": col, "present": present})
-        indexes = [(names.index(ix["class"]), ix["property"], bool(ix["unique"])) for ix in db.get("indexes", [])]
-        g = cls(V, classes, vclass, rids, edge_sets, props, indexes, device)
+        g = cls(*records_arrays(db), device)
         g.records = db
         return g
+
+
 
     @classmethod
     def person_knows(cls, rp, col, seed, device=0, keep_csr=False):
@@ -235,6 +191,72 @@ class GraphSnapshot:
             g.csr = (rp, col)
         g.age = props[1]["values"]
         return g
+
+
+
+def records_arrays(db):
+    """(V, classes, vertex_class, rids, edge_sets, properties, indexes) of a record-level description
+    (GraphSnapshot.from_records)."""
+    if isinstance(db, str):
+        with open(db) as f:
+            db = json.load(f)
+    names = [c["name"] for c in db["classes"]]
+    classes = []
+    for i, c in enumerate(db["classes"]):
+        sup = names.index(c["superclass"]) if c["superclass"] is not None else -1
+        classes.append((c["name"], sup, bool(c["is_edge"]), 11 + i))
+    V = len(db["vertices"])
+    vclass = np.zeros(V, np.uint16)
+    rids = np.zeros(V, np.uint64)
+    per_class = {}
+    for v, rec in enumerate(db["vertices"]):
+        ci = names.index(rec["class"])
+        vclass[v] = ci
+        pos = per_class.get(ci, 0)
+        per_class[ci] = pos + 1
+        rids[v] = pack_rid(classes[ci][3], pos)
+    # adjacency: one CSR per edge class, rows in insertion order (ridbag order)
+    edge_sets = []
+    for ci, (name, _, is_edge, _) in enumerate(classes):
+        if not is_edge:
+            continue
+        es = [(e["out"], e["in"]) for e in db["edges"] if e["class"] == name]
+        if not es:
+            continue
+        src = np.array([a for a, _ in es], np.int64)
+        dst = np.array([b for _, b in es], np.uint32)
+        order = np.argsort(src, kind="stable")
+        rp = np.zeros(V + 1, np.uint64)
+        np.add.at(rp, src + 1, 1)
+        rp = np.cumsum(rp).astype(np.uint64)
+        edge_sets.append({"cls": ci, "out_rp": rp, "out_col": dst[order]})
+    # properties: one column per field name over all vertices
+    fields = []
+    for rec in db["vertices"]:
+        for k in rec["props"]:
+            if k not in fields:
+                fields.append(k)
+    props = []
+    for f in fields:
+        vals = [rec["props"].get(f) for rec in db["vertices"]]
+        present = np.array([x is not None for x in vals], np.uint8)
+        nonnull = [x for x in vals if x is not None]
+        if all(isinstance(x, str) for x in nonnull):
+            d = sorted(set(nonnull), key=lambda s: s.encode())
+            code = {s: i for i, s in enumerate(d)}
+            col = np.array([code[x] if x is not None else -1 for x in vals], np.int32)
+            props.append({"name": f, "type": N.OMX_PROP_STRING, "values": col, "present": present, "dict": d})
+        elif all(isinstance(x, bool) for x in nonnull):
+            col = np.array([int(x) if x is not None else 0 for x in vals], np.int32)
+            props.append({"name": f, "type": N.OMX_PROP_BOOL, "values": col, "present": present})
+        elif all(isinstance(x, int) and not isinstance(x, bool) for x in nonnull):
+            col = np.array([x if x is not None else 0 for x in vals], np.int64)
+            props.append({"name": f, "type": N.OMX_PROP_INT64, "values": col, "present": present})
+        else:
+            col = np.array([float(x) if x is not None else 0.0 for x in vals], np.float64)
+            props.append({"name": f, "type": N.OMX_PROP_DOUBLE, "values": col, "present": present})
+    indexes = [(names.index(ix["class"]), ix["property"], bool(ix["unique"])) for ix in db.get("indexes", [])]
+    return V, classes, vclass, rids, edge_sets, props, indexes
 
 
 def ldbc_csr(n_persons=70000, target_edges=2_000_000, seed=10):

@@ -80,6 +80,51 @@ def test_bfs_kernels_reported(rmat10, monkeypatch):
     assert names & {"k_bfs_push", "k_bfs_pull"}
 
 
+@pytest.mark.parametrize("hubs", ["16", "0"], ids=["partial_hubs", "no_hubs"])
+@pytest.mark.parametrize("q", [q for q in VARLEN if q[0] in ("two_batches", "where_target", "in_dir", "both_dir")],
+                         ids=lambda q: q[0])
+def test_varlen_pull_hub_threshold(rmat10, q, hubs, monkeypatch):
+    """Bottom-up levels with only the 16 highest-degree sources annotated as hubs (the degree threshold
+    then picks a strict subset, as at C3's scale), or none (plain col)."""
+    monkeypatch.setenv("OMX_VARLEN", "bfs")
+    monkeypatch.setenv("OMX_BFS_PULL_DIV", "1000000000000")
+    monkeypatch.setenv("OMX_PULL_HUBS", hubs)
+    g, ref = rmat10
+    _parity(g, ref, q[1], _cols(q[1]))
+
+
+@pytest.fixture(scope="module")
+def rmat14():
+    import orientdb_amd as o
+    return o.GraphSnapshot.rmat(14, device=0, keep_csr=True)
+
+
+@pytest.mark.parametrize("pull", ["auto", "pull"])
+def test_varlen_rmat14_hub_root_vs_c_bfs(rmat14, pull, monkeypatch):
+    """RMAT-14 from the highest-degree vertex and 63 others (rows straddle pull tiles; the hub
+    threshold picks a strict subset of the sources) against oracle/bfs_ref.c, all levels bottom-up
+    in the "pull" mode."""
+    import numpy as np
+    import orientdb_amd as o
+    from oracle import dfs
+    monkeypatch.setenv("OMX_VARLEN", "bfs")
+    monkeypatch.setenv("OMX_PULL_HUBS", "512")
+    if pull == "pull":
+        monkeypatch.setenv("OMX_BFS_PULL_DIV", "1000000000000")
+    g = rmat14
+    rp, col = g.csr
+    top = int(np.argmax(np.diff(rp)))
+    roots = np.unique(np.concatenate([[top], np.arange(63)])).astype(np.uint32)
+    q = "MATCH {class:Person,as:s,where:(uid = %d or uid < 63)}-Knows->{as:v, while:($depth < 3)} RETURN s, v" % top
+    rs = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_NO_RID_MAP)
+    ref = dfs.bfs_varlen(rp, col, roots, max_depth=3, nthreads=8)
+    assert rs.info["n_rows"] == ref["n"]
+    assert rs.info["edges_traversed"] == ref["edges"]
+    got = np.sort(rs.rows[:, 0].astype(np.uint64) << np.uint64(32) | rs.rows[:, 1].astype(np.uint64))
+    want = np.sort(roots[ref["pairs"][:, 0]].astype(np.uint64) << np.uint64(32) | ref["pairs"][:, 1].astype(np.uint64))
+    assert np.array_equal(got, want)
+
+
 @pytest.fixture(scope="module")
 def rmat16():
     import orientdb_amd as o
