@@ -23,7 +23,7 @@ namespace omx {
 
 // ---- threads ----------------------------------------------------------------------------------------
 
-ThreadHub::ThreadHub(int w) : world(w), counts(w, std::vector<uint64_t>(w, 0)), sbuf(w), sdispl(w) {}
+ThreadHub::ThreadHub(int w) : world(w), counts(w, std::vector<uint64_t>(w, 0)), sbuf(w), sdispl(w), gathered(w, 0) {}
 
 void ThreadHub::barrier() {
   std::unique_lock<std::mutex> lk(m);
@@ -97,6 +97,21 @@ class ThreadTransport : public Transport {
 
   void abort() override { hub_->abort(); }
 
+  std::vector<uint64_t> allgather(uint64_t x, hipStream_t) override {
+    {
+      std::lock_guard<std::mutex> lk(hub_->m);
+      hub_->gathered[rank_] = x;
+    }
+    hub_->barrier();
+    std::vector<uint64_t> out;
+    {
+      std::lock_guard<std::mutex> lk(hub_->m);
+      out = hub_->gathered;
+    }
+    hub_->barrier();  // the slots may be reused
+    return out;
+  }
+
  private:
   std::shared_ptr<ThreadHub> hub_;
   int rank_;
@@ -113,16 +128,30 @@ class RcclTransport : public Transport {
     HIP_OK(hipSetDevice(device));
     NCCL_OK(ncclCommInitRank(&comm_, world, uid, rank));
     HIP_OK(hipMalloc((void **)&d_recv_, std::max(1, world) * sizeof(uint64_t)));
+    HIP_OK(hipMalloc((void **)&d_one_, sizeof(uint64_t)));
+    HIP_OK(hipMalloc((void **)&d_all_, std::max(1, world) * sizeof(uint64_t)));
   }
   ~RcclTransport() override {
     (void)hipSetDevice(device_);
     if (d_recv_) (void)hipFree(d_recv_);
+    if (d_one_) (void)hipFree(d_one_);
+    if (d_all_) (void)hipFree(d_all_);
     if (comm_) (void)ncclCommDestroy(comm_);
   }
   // peers inside a collective with this rank are released with an error (ncclCommAbort)
   void abort() override {
     if (comm_) (void)ncclCommAbort(comm_);
     comm_ = nullptr;
+  }
+
+  std::vector<uint64_t> allgather(uint64_t x, hipStream_t s) override {
+    if (!comm_) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: the communicator was aborted");
+    HIP_OK(hipMemcpyAsync(d_one_, &x, sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    NCCL_OK(ncclAllGather(d_one_, d_all_, 1, ncclUint64, comm_, s));
+    std::vector<uint64_t> out(world_);
+    HIP_OK(hipMemcpyAsync(out.data(), d_all_, world_ * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return out;
   }
   int rank() const override { return rank_; }
   int world() const override { return world_; }
@@ -154,6 +183,7 @@ class RcclTransport : public Transport {
   int rank_, world_, device_;
   ncclComm_t comm_ = nullptr;
   uint64_t *d_recv_ = nullptr;
+  uint64_t *d_one_ = nullptr, *d_all_ = nullptr;  // allgather staging
 };
 
 }  // namespace

@@ -41,6 +41,8 @@ class Transport {
   // called when this rank's execute fails: peers blocked in (or later entering) an exchange fail too
   // instead of waiting forever. The communicator is unusable afterwards.
   virtual void abort() = 0;
+  // every rank's x (host values), in rank order
+  virtual std::vector<uint64_t> allgather(uint64_t x, hipStream_t s) = 0;
 };
 
 // threads of one process as ranks
@@ -57,6 +59,7 @@ struct ThreadHub {
   std::vector<std::vector<uint64_t>> counts;                // [src][dst]
   std::vector<std::vector<const uint32_t *>> sbuf;          // [src][column]
   std::vector<std::vector<uint64_t>> sdispl;                // [src][dst]
+  std::vector<uint64_t> gathered;                           // [src] (allgather)
 };
 
 std::unique_ptr<Transport> make_thread_transport(std::shared_ptr<ThreadHub> hub, int rank);

@@ -463,12 +463,14 @@ class Executor {
     alg_bytes_ += (uint64_t)g_.V * 4;
   }
 
+  // words of a filter bitmap: padded to whole slices (the sliced kernels stage slices unchecked)
+  uint64_t padded_words() const { return (nwords_ + kBitmapPadWords - 1) / kBitmapPadWords * kBitmapPadWords; }
+
   const uint64_t *bitmap(int id) {
     if (id < 0) return nullptr;
     if (!bms_[id].p) {
-      const uint64_t padded = (nwords_ + kBitmapPadWords - 1) / kBitmapPadWords * kBitmapPadWords;
-      bms_[id] = DBuf<uint64_t>(&pool_, padded);
-      eval_bitmap(p_.bitmaps[id].prog, p_.bitmaps[id].class_id, 0, bms_[id].p, padded);
+      bms_[id] = DBuf<uint64_t>(&pool_, padded_words());
+      eval_bitmap(p_.bitmaps[id].prog, p_.bitmaps[id].class_id, 0, bms_[id].p, padded_words());
     }
     return bms_[id].p;
   }
@@ -550,8 +552,8 @@ class Executor {
       fail(OMX_E_INVALID, "snapshot rows [" + std::to_string(g_.part_lo) + ", " + std::to_string(g_.part_hi) +
                               ") are not rank " + std::to_string(r) + "'s block of " + std::to_string(W));
     for (const Step &st : p_.steps)
-      if (st.kind == S_VARLEN || st.kind == S_MULTI || st.kind == S_NEWROOT || st.kind == S_CARTESIAN)
-        unsupported("variable-length and multi-step items and disconnected patterns are not supported on a partitioned snapshot");
+      if (st.kind == S_NEWROOT || st.kind == S_CARTESIAN)
+        unsupported("disconnected patterns are not supported on a partitioned snapshot");
     for (const PredProgram &pp : p_.progs)
       for (const DPredInstr &in : pp.code)
         if (in.op == P_PUSH_DEG) unsupported("out()/in()/both().size() in WHERE is not supported on a partitioned snapshot");
@@ -563,11 +565,25 @@ class Executor {
     dist_ = true;
   }
 
+  // (row, vertex) pairs of an item's result sets (see traverse)
+  struct PairSet {
+    DBuf<uint32_t> row, v;
+    uint64_t n = 0;
+  };
+
   // rows travel to dest[r]; hist[p] = rows for rank p (both on the device)
   void route_rows(DBuf<uint32_t> &dest, DBuf<uint64_t> &hist) {
+    std::vector<DBuf<uint32_t> *> cs;
+    for (int c : bound_cols()) cs.push_back(&col_[c]);
+    R_ = exchange_cols(cs, R_, dest, hist);
+    segmented_ = false;
+  }
+
+  // columns of R rows travel to dest[r] (hist[p] = rows for rank p): a one-pass radix sort by
+  // destination, an all-to-all of the counts, an all-to-all-v per column; returns the rows received
+  uint64_t exchange_cols(const std::vector<DBuf<uint32_t> *> &cols, uint64_t R, DBuf<uint32_t> &dest,
+                         DBuf<uint64_t> &hist) {
     const int W = tr_->world();
-    const uint64_t R = R_;
-    const std::vector<int> cols = bound_cols();
     DBuf<uint32_t> perm;
     if (R) {
       DBuf<uint32_t> iota(&pool_, R), sdest(&pool_, R);
@@ -591,9 +607,9 @@ class Executor {
     std::vector<const uint32_t *> sp;
     std::vector<uint32_t *> rp;
     tm_.begin("k_route_gather");
-    for (int c : cols) {
+    for (DBuf<uint32_t> *c : cols) {
       sb.emplace_back(&pool_, std::max<uint64_t>(R, 1));
-      if (R) launch_gather_u32(col_[c].p, perm.p, R, sb.back().p, s_);
+      if (R) launch_gather_u32(c->p, perm.p, R, sb.back().p, s_);
       rb.emplace_back(&pool_, std::max<uint64_t>(Rn, 1));
       sp.push_back(sb.back().p);
       rp.push_back(rb.back().p);
@@ -602,9 +618,26 @@ class Executor {
     tm_.begin("exchange");
     tr_->alltoallv(sp, send, sdispl, rp, recv, rdispl, s_);
     tm_.end((R + Rn) * 4ull * cols.size());
-    for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(rb[i]);
-    R_ = Rn;
-    segmented_ = false;
+    for (size_t i = 0; i < cols.size(); ++i) *cols[i] = std::move(rb[i]);
+    return Rn;
+  }
+
+  // Σ over ranks (a partitioned run's loops must end on every rank at the same level)
+  uint64_t global_sum(uint64_t x) {
+    if (!dist_) return x;
+    uint64_t t = 0;
+    for (uint64_t y : tr_->allgather(x, s_)) t += y;
+    return t;
+  }
+  // pairs travel to the owner of their vertex (partitioned: its adjacency is local there)
+  void route_pairs_owner(PairSet &p) {
+    if (!dist_ || (tr_->world() == 1 && !route_self_)) return;
+    const int W = tr_->world();
+    DBuf<uint32_t> dest(&pool_, std::max<uint64_t>(p.n, 1));
+    DBuf<uint64_t> hist(&pool_, W);
+    HIP_CHECK(hipMemsetAsync(hist.p, 0, W * sizeof(uint64_t), s_));
+    if (p.n) launch_route_owner(p.v.p, p.n, block_, (uint32_t)W, dest.p, hist.p, s_);
+    p.n = exchange_cols({&p.row, &p.v}, p.n, dest, hist);
   }
 
   // before a step that reads column c's adjacency: rows go to the rank that owns row[c]
@@ -776,6 +809,9 @@ class Executor {
                         (uint64_t)g_.V <= ((uint64_t)kMaxSlices << slice_shift_);
     const uint32_t P = sliced ? (uint32_t)(((uint64_t)g_.V + (1ull << slice_shift_) - 1) >> slice_shift_) : 1;
     const DCuts cuts = sliced ? slice_cuts_of(adjs, P) : DCuts{};
+    // the sliced kernels stage whole bitmap slices with unchecked loads: the filter must be padded
+    if (sliced && pool_.size_of(filter) < padded_words() * 8)
+      fail(OMX_E_INVALID, "internal: a sliced expansion's filter bitmap is not padded to whole slices");
     // sliced: a heavy row is cut into P pieces, one chunk each; below ~128 edges per piece a chunk issues
     // its 16 loads for a few live slots, so the cut grows with P (RMAT-24, P = 16: 2048 measured best of
     // 256…4096, profiles/r02/hd_sweep; RMAT-22, P = 4: 512 against 256, 1.80 against 1.83 ms per step)
@@ -1334,7 +1370,8 @@ class Executor {
   // terminates on cycles.
   void varlen_step(const Step &st) {
     bool depth_only_while = false;
-    if (varlen_mode_ != "pairs" && bfs_exact(st, depth_only_while)) {
+    // partitioned: (row, vertex) pairs routed to the owner of their vertex every level
+    if (!dist_ && varlen_mode_ != "pairs" && bfs_exact(st, depth_only_while)) {
       const uint64_t nb = (R_ + 63) / 64;
       if (varlen_mode_ == "bfs" || nb <= 64 || nb * (uint64_t)g_.V <= (1ull << 30)) {
         varlen_msbfs(st, depth_only_while);
@@ -1541,10 +1578,6 @@ class Executor {
   // A pair set holds, per binding row, the set of vertices an item's executeTraversal returned so far
   // (P/OMatchPathItem.java:49-107): distinct (row, v) pairs, kept as two u32 columns. Sets of rows with
   // the same start vertex are the same, so per-row sets equal the reference's per-start-vertex HashSets.
-  struct PairSet {
-    DBuf<uint32_t> row, v;
-    uint64_t n = 0;
-  };
 
   int pair_key_bits() const { return 32 + bits_for(g_.V); }
 
@@ -1577,31 +1610,46 @@ class Executor {
   }
   // bitmap of a predicate program at $depth = depth (cached when it does not read $depth)
   std::map<int, DBuf<uint64_t>> prog_bms_;
+  // (padded: a traversal's WHERE bitmap filters expansions, so the sliced kernels may stage it)
   const uint64_t *prog_bitmap(int prog, int64_t depth, DBuf<uint64_t> &scratch) {
     if (prog < 0) return nullptr;
     if (p_.progs[prog].uses_depth) {
-      if (!scratch.p) scratch = DBuf<uint64_t>(&pool_, nwords_);
-      eval_bitmap(prog, -1, depth, scratch.p);
+      if (!scratch.p) scratch = DBuf<uint64_t>(&pool_, padded_words());
+      eval_bitmap(prog, -1, depth, scratch.p, padded_words());
       return scratch.p;
     }
     DBuf<uint64_t> &b = prog_bms_[prog];
     if (!b.p) {
-      b = DBuf<uint64_t>(&pool_, nwords_);
-      eval_bitmap(prog, -1, 0, b.p);
+      b = DBuf<uint64_t>(&pool_, padded_words());
+      eval_bitmap(prog, -1, 0, b.p, padded_words());
     }
     return b.p;
   }
 
   // one hop of a single-method item over a pair set (target bitmap optional), distinct pairs out
-  PairSet hop_pairs(const PairSet &in, const AdjSpec &adj, const uint64_t *filter) {
-    if (in.n == 0) return PairSet{};
-    ExpandOut ex = expand_core(in.v.p, in.n, adj, filter, {in.row.p}, true);
+  PairSet hop_pairs(const PairSet &in_, const AdjSpec &adj, const uint64_t *filter) {
+    const PairSet *in = &in_;
+    PairSet routed;
+    if (dist_) {  // expand where the vertex's rows are; new pairs meet at their vertex's owner for the dedup
+      DBuf<uint64_t> k = pair_keys(in_);
+      routed = pairs_from_keys(k, in_.n, true);
+      route_pairs_owner(routed);
+      in = &routed;
+    }
+    if (in->n == 0 && !dist_) return PairSet{};
+    ExpandOut ex = in->n ? expand_core(in->v.p, in->n, adj, filter, {in->row.p}, true) : ExpandOut{};
     edges_ += ex.E;
     edges_iter_ += ex.E;
-    if (ex.n == 0) return PairSet{};
-    DBuf<uint64_t> keys(&pool_, ex.n);
-    launch_pack_pairs(ex.carry[0].p, ex.dst.p, ex.n, keys.p, s_);
-    return pairs_from_keys(keys, ex.n);
+    PairSet out;
+    if (ex.n) {
+      out.n = ex.n;
+      out.row = std::move(ex.carry[0]);
+      out.v = std::move(ex.dst);
+    }
+    route_pairs_owner(out);
+    if (out.n == 0) return PairSet{};
+    DBuf<uint64_t> keys = pair_keys(out);
+    return pairs_from_keys(keys, out.n);
   }
 
   // traversePatternEdge of an item (P/OMatchPathItem.java:109-126): the neighbour set without the
@@ -1614,7 +1662,7 @@ class Executor {
       cur = pairs_from_keys(k, in.n, true);
     }
     for (const TravSpec &sub : t.subs) {
-      if (cur.n == 0) break;
+      if (global_sum(cur.n) == 0) break;
       cur = traverse(sub, cur);
     }
     return cur;
@@ -1647,7 +1695,7 @@ class Executor {
     }
     std::vector<DBuf<uint64_t>> res_parts;
     std::vector<uint64_t> res_n;
-    for (int64_t d = 0; F.n; ++d) {
+    for (int64_t d = 0; global_sum(F.n); ++d) {
       if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate (the reference recurses without bound)");
       {  // include F_d ∩ where_d
         PairSet inc = filter_pairs(F, prog_bitmap(t.where_prog, d, where_scratch));
@@ -1658,7 +1706,7 @@ class Executor {
       }
       if (t.has_max_depth && d >= t.max_depth) break;
       PairSet G = filter_pairs(F, prog_bitmap(t.while_prog, d, while_scratch));  // F_d ∩ while_d
-      if (G.n == 0) break;
+      if (global_sum(G.n) == 0) break;
       PairSet N = pattern_edge(t, G);
       if (!dep && N.n) {  // drop the pairs seen at an earlier level
         DBuf<uint64_t> keys = pair_keys(N);
@@ -1691,19 +1739,44 @@ class Executor {
   }
 
   // the binding rows' start pairs (row index, source vertex)
+  // (partitioned: row ids are global, rank r's rows from row_bounds_[r]; pairs are routed to the owners
+  // of their vertices by the hops and back to the rows' ranks by bind_pairs)
+  std::vector<uint64_t> row_bounds_;
   PairSet start_pairs(int src) {
     require_u32_rows("a variable-length or multi-step item");
+    uint64_t base = 0;
+    if (dist_) {
+      const std::vector<uint64_t> rs = tr_->allgather(R_, s_);
+      row_bounds_.assign(rs.size() + 1, 0);
+      for (size_t p = 0; p < rs.size(); ++p) row_bounds_[p + 1] = row_bounds_[p] + rs[p];
+      if (row_bounds_.back() >= (1ull << 32)) unsupported("a partitioned variable-length item over 2^32 or more rows");
+      base = row_bounds_[tr_->rank()];
+    }
     PairSet p;
     p.n = R_;
     p.row = DBuf<uint32_t>(&pool_, std::max<uint64_t>(R_, 1));
     p.v = DBuf<uint32_t>(&pool_, std::max<uint64_t>(R_, 1));
     launch_iota(p.row.p, R_, s_);
-    HIP_CHECK(hipMemcpyAsync(p.v.p, col_[src].p, R_ * 4, hipMemcpyDeviceToDevice, s_));
+    launch_add_u32(p.row.p, R_, (int64_t)base, s_);
+    if (R_) HIP_CHECK(hipMemcpyAsync(p.v.p, col_[src].p, R_ * 4, hipMemcpyDeviceToDevice, s_));
     return p;
   }
 
   // processContext's three branches (:468-497) over an item's (row, v) result set
   void bind_pairs(const Step &st, PairSet &res) {
+    if (dist_) {  // the result pairs return to the ranks of their rows (local row ids)
+      const int W = tr_->world();
+      DBuf<uint32_t> dest(&pool_, std::max<uint64_t>(res.n, 1));
+      DBuf<uint64_t> hist(&pool_, W);
+      HIP_CHECK(hipMemsetAsync(hist.p, 0, W * sizeof(uint64_t), s_));
+      if (res.n) launch_route_bounds(res.row.p, res.n, row_bounds_.data(), (uint32_t)W, dest.p, hist.p, s_);
+      res.n = exchange_cols({&res.row, &res.v}, res.n, dest, hist);
+      launch_add_u32(res.row.p, res.n, -(int64_t)row_bounds_[tr_->rank()], s_);
+      DBuf<uint64_t> k = pair_keys(res);
+      res = pairs_from_keys(k, res.n);  // sorted again (bound targets are looked up by binary search)
+      owner_col_ = -1;                  // the rows are back on their own ranks
+      bound_[st.dst] = 1;
+    }
     const uint64_t R = R_;
     if (st.mode == T_BOUND) {  // keep a row iff its bound target is in its set (existence)
       DBuf<uint64_t> rk = pair_keys(res);

@@ -34,6 +34,11 @@ class DevicePool {
   void trim();
   ~DevicePool();
   size_t cached_bytes() const { return cached_; }
+  // bytes of the live allocation starting at p (0 if p is not one)
+  size_t size_of(const void *p) const {
+    auto it = live_.find(const_cast<void *>(p));
+    return it == live_.end() ? 0 : it->second;
+  }
 
  private:
   std::multimap<size_t, void *> free_;

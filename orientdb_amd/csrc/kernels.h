@@ -131,6 +131,10 @@ void launch_route_owner(const uint32_t *v, uint64_t R, uint32_t block, uint32_t 
                         hipStream_t s);
 void launch_route_hash(int ncols, const uint32_t *const *cols, uint64_t R, uint32_t W, uint32_t *dest, uint64_t *hist,
                        hipStream_t s);
+// dest[r] = p with bounds[p] <= id[r] < bounds[p+1] (host bounds[0..W])
+void launch_route_bounds(const uint32_t *id, uint64_t R, const uint64_t *bounds, uint32_t W, uint32_t *dest,
+                         uint64_t *hist, hipStream_t s);
+void launch_add_u32(uint32_t *x, uint64_t n, int64_t delta, hipStream_t s);
 
 void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t *deg, hipStream_t s);
 void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part,

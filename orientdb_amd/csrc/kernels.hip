@@ -1765,6 +1765,43 @@ void launch_route_owner(const uint32_t *v, uint64_t R, uint32_t block, uint32_t 
   KCHECK("k_route_owner");
 }
 
+// a row id's origin: the rank p with bounds[p] <= id < bounds[p+1] (global row ids of a pair set)
+struct RankBounds {
+  uint64_t b[kMaxRanks + 1];
+};
+__global__ void k_route_bounds(const uint32_t *id, uint64_t R, RankBounds rb, uint32_t W, uint32_t *dest,
+                               unsigned long long *hist) {
+  __shared__ unsigned long long s_h[kMaxRanks];
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) s_h[i] = 0;
+  __syncthreads();
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t d = 0;
+  if (r < R) {
+    const uint64_t x = id[r];
+    while (d + 1 < W && rb.b[d + 1] <= x) ++d;
+    dest[r] = d;
+  }
+  route_count(d, r < R, W, s_h, hist);
+}
+void launch_route_bounds(const uint32_t *id, uint64_t R, const uint64_t *bounds, uint32_t W, uint32_t *dest,
+                         uint64_t *hist, hipStream_t s) {
+  if (!R) return;
+  RankBounds rb{};
+  for (uint32_t i = 0; i <= W; ++i) rb.b[i] = bounds[i];
+  hipLaunchKernelGGL(k_route_bounds, dim3(nblocks(R, 256)), dim3(256), 0, s, id, R, rb, W, dest,
+                     reinterpret_cast<unsigned long long *>(hist));
+  KCHECK("k_route_bounds");
+}
+__global__ void k_add_u32(uint32_t *x, uint64_t n, int64_t delta) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = (uint32_t)((int64_t)x[i] + delta);
+}
+void launch_add_u32(uint32_t *x, uint64_t n, int64_t delta, hipStream_t s) {
+  if (!n || !delta) return;
+  hipLaunchKernelGGL(k_add_u32, dim3(nblocks(n, 256)), dim3(256), 0, s, x, n, delta);
+  KCHECK("k_add_u32");
+}
+
 // a hash of the projected tuple: equal rows meet on one rank for the distinct pass
 __global__ void k_route_hash(int ncols, ColPtrs cp, uint64_t R, uint32_t W, uint32_t *dest, unsigned long long *hist) {
   __shared__ unsigned long long s_h[kMaxRanks];

@@ -114,6 +114,47 @@ def test_rccl_one_rank_routes_through_itself(rmat10_full, monkeypatch):
         comm.close()
 
 
+from tests.test_gpu_varlen import VARLEN  # noqa: E402
+
+# variable-length and multi-step items on partitions: (row, vertex) pairs travel to the owner of their
+# vertex every level (its adjacency is local there; all copies of a pair meet for the per-level dedup)
+# and back to the rows' ranks at the end (exec.hip traverse / bind_pairs)
+DIST_VARLEN = [q for q in VARLEN if q[0] in ("depth_only", "two_batches", "shared_sources", "where_target", "maxdepth",
+                                             "maxdepth0", "while_prop", "in_dir", "both_dir", "where_depth",
+                                             "bound_target")] + \
+    [(q[0], q[1]) for q in RMAT_QUERIES if q[0] in ("multi_two_hops", "multi_varlen", "multi_edge_pair")]
+
+
+def _vcols(q):
+    return [c.strip() for c in q.split("RETURN")[1].split(",")]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("q", DIST_VARLEN, ids=[q[0] for q in DIST_VARLEN])
+def test_partitioned_varlen_parity(rmat10_full, world, q):
+    import orientdb_amd as o
+    g, ref = rmat10_full
+    cols = _vcols(q[1])
+    want = ref.expected(q[1], cols)
+    res = run_ranks(_parts(world), q[1])
+    got = [gpu_set(r, cols) for r in res]
+    assert set().union(*got) == want
+    assert sum(len(x) for x in got) == len(want)  # each row's result pairs end on the row's rank
+
+
+@pytest.mark.parametrize("q", [q for q in DIST_VARLEN if q[0] in ("two_batches", "while_prop", "both_dir")],
+                         ids=lambda q: q[0])
+def test_partitioned_varlen_edges_match_replicated(rmat10_full, q, monkeypatch):
+    """The partitioned traversal expands the same (row, vertex) frontiers as the replicated pair path."""
+    import orientdb_amd as o
+    g, _ = rmat10_full
+    monkeypatch.setenv("OMX_VARLEN", "pairs")
+    full = o.OMatchStatement(q[1]).execute(g)
+    res = run_ranks(_parts(2), q[1])
+    assert sum(r.info["edges_traversed"] for r in res) == full.info["edges_traversed"]
+    assert sum(r.info["n_rows"] for r in res) == full.info["n_rows"]
+
+
 def test_failing_rank_releases_its_peers(rmat10_full):
     """A rank whose execute fails (here: a missing query parameter on rank 0 only) aborts the thread
     communicator; its peer fails with an error instead of waiting forever in the exchange."""
@@ -148,8 +189,8 @@ def test_partition_errors(rmat10_full):
     comms = o.Comm.threads(2)
     with pytest.raises(o.OmxError):  # rank 1's communicator with rank 0's rows
         o.OMatchStatement(RMAT_QUERIES[0][1]).execute(parts[0], comm=comms[1])
-    with pytest.raises(o.OmxUnsupported):  # variable-length items stay on replicated snapshots
-        q = [x for x in RMAT_QUERIES if x[0] == "varlen_depth"][0][1]
+    with pytest.raises(o.OmxUnsupported):  # disconnected patterns stay on replicated snapshots
+        q = [x for x in RMAT_QUERIES if x[0] == "cartesian"][0][1]
         o.OMatchStatement(q).execute(parts[0], comm=comms[0])
     for c in comms:
         c.close()
