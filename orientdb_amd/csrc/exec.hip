@@ -608,6 +608,7 @@ class Executor {
     std::vector<uint32_t *> rp;
     tm_.begin("k_route_gather");
     for (DBuf<uint32_t> *c : cols) {
+      if (R && !c->p) fail(OMX_E_INVALID, "internal: an exchanged column is not materialized");
       sb.emplace_back(&pool_, std::max<uint64_t>(R, 1));
       if (R) launch_gather_u32(c->p, perm.p, R, sb.back().p, s_);
       rb.emplace_back(&pool_, std::max<uint64_t>(Rn, 1));
@@ -1264,6 +1265,8 @@ class Executor {
 
   void gather_rows(const uint32_t *idx, uint64_t n) {
     std::vector<int> cols = bound_cols();
+    for (int c : cols)
+      if (!col_[c].p && R_) fail(OMX_E_INVALID, "internal: bound column " + p_.aliases[c] + " is not materialized");
     std::vector<DBuf<uint32_t>> nc;
     std::vector<const uint32_t *> in;
     std::vector<uint32_t *> out;
@@ -1775,7 +1778,6 @@ class Executor {
       DBuf<uint64_t> k = pair_keys(res);
       res = pairs_from_keys(k, res.n);  // sorted again (bound targets are looked up by binary search)
       owner_col_ = -1;                  // the rows are back on their own ranks
-      bound_[st.dst] = 1;
     }
     const uint64_t R = R_;
     if (st.mode == T_BOUND) {  // keep a row iff its bound target is in its set (existence)
@@ -1791,8 +1793,9 @@ class Executor {
       return;
     }
     if (st.mode == T_CAND) res = filter_pairs(res, bitmap(st.cand_bm));
-    gather_rows(res.row.p, res.n);
+    gather_rows(res.row.p, res.n);  // (before dst is marked bound: gather_rows moves the bound columns)
     col_[st.dst] = std::move(res.v);
+    bound_[st.dst] = 1;
   }
 
   // variable-length item over (row, vertex) pairs (any $depth use)
