@@ -153,6 +153,10 @@ class Executor {
     debug_expand_ = std::getenv("OMX_DEBUG_EXPAND") != nullptr;  // one stderr line per expansion
     if (const char *ls = std::getenv("OMX_LIGHT_SLICED")) light_sliced_ = std::strcmp(ls, "0") != 0;
     if (const char *ae = std::getenv("OMX_ARENA_ESTIMATE")) arena_estimate_ = std::strcmp(ae, "0") != 0;
+    if (const char *fz = std::getenv("OMX_FACTOR")) {  // "0": never; "force": every filtered hop (tests)
+      factor_ = std::strcmp(fz, "0") != 0;
+      if (std::strcmp(fz, "force") == 0) factor_min_rows_ = 1, factor_min_ratio_ = 0;
+    }
     if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
     dist_setup();
   }
@@ -347,6 +351,8 @@ class Executor {
   // OMX_ARENA_MARGIN scales the estimate, 0 forces the short-arena re-run in tests)
   bool arena_estimate_ = true;
   double arena_margin_ = 1.25;
+  bool factor_ = true;           // factorized expansion of filtered hops (OMX_FACTOR=0: direct)
+  uint64_t factorized_hops_ = 0;
   uint64_t arena_retries_ = 0;
 
   // ---- helpers -----------------------------------------------------------------------------------
@@ -791,12 +797,13 @@ class Executor {
   // segments (the final step of a plan whose rows are distinct by construction).
   // member_src/member_adj: fused closing check (ExpandArgs::member_src); the edges it stands for are
   // returned in ExpandOut::E_member.
+  // raw_adj: an adjacency that is not a snapshot CSR (the factorized expansion's grouped lists)
   ExpandOut expand_core(const uint32_t *src, uint64_t R, const AdjSpec &adjs, const uint64_t *filter,
                         const std::vector<const uint32_t *> &carry, bool write, bool allow_segmented = false,
                         const uint32_t *member_src = nullptr, const AdjSpec *member_adj = nullptr,
-                        const uint64_t *member_filter = nullptr) {
+                        const uint64_t *member_filter = nullptr, const DAdj *raw_adj = nullptr) {
     ExpandOut o;
-    DAdj adj = make_adj(adjs);
+    DAdj adj = raw_adj ? *raw_adj : make_adj(adjs);
     if (adj.n == 0 || R == 0) return o;
     const bool member = member_src != nullptr;
     DBuf<unsigned long long> medges;
@@ -806,7 +813,7 @@ class Executor {
     }
     // 1. degree binning + scans (light edges: merge path; heavy rows: chunks). A filtered hop over a
     // sorted adjacency cuts the heavy rows' chunks at bitmap-slice boundaries (LDS-sliced kernel).
-    const bool sliced = filter != nullptr && !member && adj.sorted && sliced_ &&
+    const bool sliced = filter != nullptr && !member && !raw_adj && adj.sorted && sliced_ &&
                         (uint64_t)g_.V <= ((uint64_t)kMaxSlices << slice_shift_);
     const uint32_t P = sliced ? (uint32_t)(((uint64_t)g_.V + (1ull << slice_shift_) - 1) >> slice_shift_) : 1;
     const DCuts cuts = sliced ? slice_cuts_of(adjs, P) : DCuts{};
@@ -1144,6 +1151,10 @@ class Executor {
       }
     }
     std::vector<int> cols = bound_cols();  // the carried columns (st.dst is not bound yet)
+    if (!check && !st.optional && st.filter_bm >= 0 && factor_ && R_ >= factor_min_rows_ && expand_factorized(st, write, cols)) {
+      bound_[st.dst] = 1;
+      return;
+    }
     bound_[st.dst] = 1;
     std::vector<const uint32_t *> carry;
     for (int c : cols) carry.push_back(col_[c].p);
@@ -1172,6 +1183,75 @@ class Executor {
     segmented_ = o.segmented;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
     col_[st.dst] = std::move(o.dst);
+  }
+
+  // Factorized expansion of a filtered hop whose rows repeat their source vertices (hubs reached from
+  // many roots: C2's second hop reads each distinct b's adjacency 31× over at RMAT-22, 50× at RMAT-24):
+  //   1. the distinct sources U (radix sort + unique) and each row's index into them;
+  //   2. the filtered neighbour list L(u) of every distinct source: one filtered expansion of U rows;
+  //   3. L grouped by source into a CSR (histogram, scan, scatter);
+  //   4. an unfiltered expansion of the rows over L: dense output of exactly the result rows.
+  // The rows are the direct expansion's (same multiset, processContext :491-497 per row); E_t still
+  // counts Σ_rows deg; edges_read counts what was iterated (Σ_U deg + the L entries).
+  // Returns false (nothing done) when the rows repeat their sources less than kFactorMinRatio-fold.
+  uint64_t factor_min_rows_ = 4096, factor_min_ratio_ = 4;
+  bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
+    const uint64_t R = R_;
+    const uint32_t *src = col_[st.src].p;
+    DBuf<uint32_t> ub(&pool_, R);
+    uint64_t U = 0;
+    {
+      DBuf<uint32_t> sorted(&pool_, R);
+      DBuf<uint64_t> nsel(&pool_, 1);
+      const int vbits = bits_for(g_.V);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceRadixSort::SortKeys(t, b, src, sorted.p, (int64_t)R, 0, vbits, s_); });
+      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Unique(t, b, sorted.p, ub.p, nsel.p, (int64_t)R, s_); });
+      U = read1(nsel.p);
+    }
+    const uint64_t Et = degree_sum(src, R, st.adj), EU = degree_sum(ub.p, U, st.adj);
+    if (Et < factor_min_ratio_ * EU) return false;
+    edges_ += Et;
+    // 1. row → distinct source index
+    DBuf<uint32_t> g(&pool_, R), iu(&pool_, std::max<uint64_t>(U, 1));
+    launch_index_of(ub.p, U, src, R, g.p, s_);
+    launch_iota(iu.p, U, s_);
+    // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
+    ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true);
+    edges_iter_ += l.E;
+    // 3. grouped by source: offsets (U + 1) and the neighbours in group order
+    DBuf<unsigned long long> cnt(&pool_, U + 1);
+    DBuf<uint64_t> loff(&pool_, U + 1);
+    HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));
+    if (l.n) launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
+    cub([&](void *t, size_t &b) {
+      return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
+    });
+    DBuf<uint32_t> lcol(&pool_, std::max<uint64_t>(l.n, 1));
+    if (l.n) {
+      HIP_CHECK(hipMemcpyAsync(cnt.p, loff.p, (U + 1) * 8, hipMemcpyDeviceToDevice, s_));
+      launch_key_scatter(l.carry[0].p, l.dst.p, l.n, cnt.p, lcol.p, s_);
+    }
+    // 4. the rows over their sources' lists
+    DAdj ladj{};
+    ladj.n = 1;
+    ladj.sorted = 0;
+    ladj.p[0].rp = loff.p;
+    ladj.p[0].col = lcol.p;
+    std::vector<const uint32_t *> carry;
+    for (int c : cols) carry.push_back(col_[c].p);
+    ExpandOut o = expand_core(g.p, R, st.adj, nullptr, carry, write, false, nullptr, nullptr, nullptr, &ladj);
+    if (!o.counted_from_degrees) edges_iter_ += o.E;
+    R_ = o.n;
+    factorized_hops_++;
+    if (debug_expand_)
+      std::fprintf(stderr, "[omx factorized] R=%llu U=%llu Et=%llu EU=%llu lists=%llu rows=%llu\n", (unsigned long long)R,
+                   (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU, (unsigned long long)l.n,
+                   (unsigned long long)o.n);
+    if (!write || R_ == 0) return true;
+    segmented_ = false;
+    for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
+    col_[st.dst] = std::move(o.dst);
+    return true;
   }
 
   // WHERE conjunct `$matched.X op $currentMatch` of the alias the previous step bound

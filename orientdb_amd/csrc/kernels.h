@@ -214,6 +214,11 @@ void launch_swap_flags(const uint32_t *xs, const uint32_t *ys, uint64_t R, const
 void launch_flag_colcmp(const uint32_t *a, const uint32_t *b, uint64_t n, bool eq, uint8_t *flags, hipStream_t s);
 void launch_iota(uint32_t *out, uint64_t n, hipStream_t s);
 void launch_fill_u32(uint32_t *out, uint64_t n, uint32_t x, hipStream_t s);
+// factorized expansion: position of each key in a sorted unique list; a key histogram; a scatter by key
+void launch_index_of(const uint32_t *sorted, uint64_t n, const uint32_t *keys, uint64_t m, uint32_t *out, hipStream_t s);
+void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
+void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor, uint32_t *out,
+                        hipStream_t s);
 void launch_pack_pairs(const uint32_t *hi, const uint32_t *lo, uint64_t n, uint64_t *keys, hipStream_t s);
 void launch_unpack_pairs(const uint64_t *keys, uint64_t n, uint32_t *hi, uint32_t *lo, hipStream_t s);
 void launch_flag_not_in(const uint64_t *sorted, uint64_t nsorted, const uint64_t *keys, uint64_t n, uint8_t *flags,

@@ -2074,6 +2074,48 @@ void launch_flag_colcmp(const uint32_t *a, const uint32_t *b, uint64_t n, bool e
   KCHECK("k_flag_colcmp");
 }
 
+// ---- factorized expansion (Executor::expand_factorized) ---------------------------------------------
+// out[i] = index of keys[i] in the sorted, duplicate-free sorted[0..n) (every key is present)
+__global__ void k_index_of(const uint32_t *sorted, uint64_t n, const uint32_t *keys, uint64_t m, uint32_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t k = keys[i];
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (sorted[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  out[i] = (uint32_t)lo;
+}
+void launch_index_of(const uint32_t *sorted, uint64_t n, const uint32_t *keys, uint64_t m, uint32_t *out, hipStream_t s) {
+  if (!m) return;
+  hipLaunchKernelGGL(k_index_of, dim3(nblocks(m, 256)), dim3(256), 0, s, sorted, n, keys, m, out);
+  KCHECK("k_index_of");
+}
+// counts[key[i]] += 1
+__global__ void k_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&counts[key[i]], 1ull);
+}
+void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_key_hist, dim3(nblocks(n, 256)), dim3(256), 0, s, key, n, counts);
+  KCHECK("k_key_hist");
+}
+// out[cursor[key[i]]++] = val[i] (cursor starts at the groups' offsets; order inside a group is free)
+__global__ void k_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor,
+                              uint32_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[atomicAdd(&cursor[key[i]], 1ull)] = val[i];
+}
+void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor, uint32_t *out,
+                        hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_key_scatter, dim3(nblocks(n, 256)), dim3(256), 0, s, key, val, n, cursor, out);
+  KCHECK("k_key_scatter");
+}
+
 __global__ void k_fill_u32(uint32_t *out, uint64_t n, uint32_t x) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = x;

@@ -294,6 +294,24 @@ def test_rmat_parity_l2_probe_heavy(rmat10, q, monkeypatch):
     _parity(g, ref, q[1], q[2])
 
 
+FACTOR_IDS = ("c2_both_ends", "c1_abc", "two_cols_dedup", "in_dir", "both_dir", "three_hop", "triangle_filtered", "matches",
+              "paths", "elements", "fof_not_me", "matched_and_filter", "optional_free", "bound_candidate")
+
+
+@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
+def test_rmat_parity_factorized(rmat10, q, monkeypatch):
+    """Every filtered hop through the factorized expansion (distinct sources → filtered lists → rows
+    over the lists, Executor::expand_factorized): same rows, same E_t."""
+    import orientdb_amd as o
+    g, ref = rmat10
+    monkeypatch.setenv("OMX_FACTOR", "0")
+    direct = o.OMatchStatement(q[1]).execute(g, documents=False)
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    rs = _parity(g, ref, q[1], q[2])
+    assert rs.info["edges_traversed"] == direct.info["edges_traversed"]
+    assert rs.info["bindings"] == direct.info["bindings"]
+
+
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in ("c2_both_ends", "in_dir", "three_hop", "matches")],
                          ids=lambda q: q[0])
 def test_rmat_parity_short_arena_rerun(rmat10, q, monkeypatch):
