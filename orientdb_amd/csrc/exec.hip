@@ -1334,6 +1334,10 @@ class Executor {
 
   // keep the rows whose flag is set (all bound columns)
   void select_rows(const uint8_t *flags, uint64_t R) {
+    if (R == 0) {  // (a partitioned rank without rows: nothing to select)
+      R_ = 0;
+      return;
+    }
     require_u32_rows("a row selection");
     DBuf<uint32_t> idx(&pool_, R);
     DBuf<uint64_t> nsel(&pool_, 1);
@@ -1898,6 +1902,7 @@ class Executor {
   }
 
   void invert_flags(const uint8_t *in, uint8_t *out, uint64_t n) {
+    if (!n) return;
     hipLaunchKernelGGL(k_invert_flags, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s_, in, out, n);
   }
 
