@@ -586,6 +586,20 @@ class Planner {
     }
   }
 
+  // can the value be null for some vertex of the snapshot (a property with absent values, a field no
+  // vertex has, arithmetic over either)
+  bool may_be_null(const ExprP &e) const {
+    if (fold(e)) return false;
+    switch (e->kind) {
+      case Expr::FIELD: {
+        const int p = g_.prop_id(e->name);
+        return p < 0 || g_.props[p].has_nulls;
+      }
+      case Expr::MATH: return may_be_null(e->kids[0]) || may_be_null(e->kids[1]);
+      default: return false;  // $depth, out()/in()/both().size()
+    }
+  }
+
   static std::string flip(const std::string &op) {
     if (op == "<") return ">";
     if (op == ">") return "<";
@@ -657,7 +671,11 @@ class Planner {
         std::string op = e->name;
         int prop;
         auto fl = fold(L), fr = fold(R);
-        if (string_field(L, &prop) && fr && fr->kind == Value::STR) return emit_string_cmp(b, prop, op, fr->s);
+        if (string_field(L, &prop) && fr && fr->kind == Value::STR) {
+          if ((op == ">" || op == ">=" || op == "<=") && g_.props[prop].has_nulls)
+            unsupported("a possibly-null left operand of " + op + " (NullPointerException in the reference): " + expr_text(L));
+          return emit_string_cmp(b, prop, op, fr->s);
+        }
         if (string_field(R, &prop) && fl && fl->kind == Value::STR) return emit_string_cmp(b, prop, flip(op), fl->s);
         if (fr && fr->kind == Value::NUL) {
           b.emit(P_PUSH_BOOL, 0, op == "!=", 0, 1);
@@ -670,6 +688,12 @@ class Planner {
           }
           unsupported("null left operand of " + op);
         }
+        // OGtOperator / OGeOperator / OLeOperator throw NullPointerException on a null left operand
+        // (P/OGtOperator.java:22-33, P/OGeOperator.java:43-54, P/OLeOperator.java:22-33); whether it is
+        // thrown depends on which records the DFS reaches, so a left operand that can be null on this
+        // snapshot is left to the reference engine instead of being compared false
+        if ((op == ">" || op == ">=" || op == "<=") && may_be_null(L))
+          unsupported("a possibly-null left operand of " + op + " (NullPointerException in the reference): " + expr_text(L));
         CT l = compile_value(b, L, allow_depth);
         CT r = compile_value(b, R, allow_depth);
         if ((l == C_BOOL) != (r == C_BOOL) && l != C_NUL && r != C_NUL)

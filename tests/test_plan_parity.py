@@ -37,3 +37,18 @@ def test_rmat_plan_c2():
     assert p["estimates"] == {"a": 128}
     assert p["root"] == "a" and p["edges"] == [["a", "b", True], ["b", "c", True]]
     assert p["supported"]
+
+
+def test_null_left_operand_goes_to_reference(host_graph):
+    """`>`, `>=`, `<=` with a left operand that is null on some vertex throw NullPointerException in the
+    reference (P/OGtOperator.java:22-33, OGeOperator.java:43-54, OLeOperator.java:22-33) depending on
+    which records the DFS reaches: the device declines those (OMX_E_UNSUPPORTED → the reference runs);
+    `<` (null → false), `=`, `!=` and null-free columns stay on the device."""
+    import orientdb_amd as o
+    base = "match {class:TriangleV, as:a, where:(uid = 0)}.out('TriangleE'){as:b, where:(%s)} return a, b"
+    for cond, supported in [("uid > 3", False), ("uid >= 3", False), ("uid <= 3", False), ("uid + 1 > 3", False),
+                            ("uid < 3", True), ("uid = 3", True), ("uid != 3", True), ("3 < uid", True)]:
+        p = o.OMatchStatement(base % cond).explain(host_graph)
+        assert p["supported"] == supported, (cond, p["unsupported_reason"])
+        if not supported:
+            assert "NullPointerException" in p["unsupported_reason"]
