@@ -10,9 +10,11 @@ from ._native import (OmxError, OmxExecutionError, OmxParseError, OmxUnsupported
 from .graph import (GraphSnapshot, pack_rid, unpack_rid, rmat_csr, ldbc_csr, csr_transpose, synthetic_int_column,
                     partition_range, rmat_partition)
 from .dist import Comm
-from .match import GraphDatabase, OCommandSQL, OMatchStatement, OResultSet, ODocument, ORecordId
+from .match import (GraphDatabase, OCommandSQL, OMatchStatement, OCommandExecutorSQLTraverse,
+                    OCommandExecutorSQLSelectExpand, OResultSet, ODocument, ORecordId)
 
-__all__ = ["GraphSnapshot", "GraphDatabase", "OCommandSQL", "OMatchStatement", "OResultSet", "ODocument",
+__all__ = ["GraphSnapshot", "GraphDatabase", "OCommandSQL", "OMatchStatement", "OCommandExecutorSQLTraverse",
+           "OCommandExecutorSQLSelectExpand", "OResultSet", "ODocument",
            "ORecordId", "Comm", "partition_range", "rmat_partition", "OmxError", "OmxExecutionError", "OmxParseError", "OmxUnsupported", "pack_rid",
            "unpack_rid", "rmat_csr", "ldbc_csr", "csr_transpose", "synthetic_int_column", "OMX_MODE_COUNT",
            "OMX_MODE_MATERIALIZE", "OMX_FLAG_KERNEL_TIMING", "OMX_FLAG_NO_RID_MAP", "OMX_FLAG_KEEP_DEVICE", "OMX_FLAG_TIME_HOT",

@@ -178,9 +178,14 @@ class Executor {
     HIP_CHECK(hipEventCreate(&eb));
     HIP_CHECK(hipEventRecord(ea, s_));
     mark("events");
-    bool empty = p_.empty || !check_candidates();
+    const bool chain = p_.kind != Plan::MATCH;
+    bool empty = !chain && (p_.empty || !check_candidates());
     bool counted_only = false;
-    if (!empty) {
+    std::vector<DBuf<uint32_t>> chain_out;
+    if (chain) {
+      if (dist_ || o_.shard_world > 1) unsupported("TRAVERSE / SELECT expand() on a partitioned or sharded execution");
+      chain_out.push_back(p_.kind == Plan::TRAVERSE ? traverse_bfs() : select_expand());
+    } else if (!empty) {
       // a partitioned run keeps stepping with no local rows: every rank takes part in every exchange
       for (size_t i = 0; i < p_.steps.size() && (R_ > 0 || dist_); ++i) {
         const Step &st = p_.steps[i];
@@ -221,14 +226,18 @@ class Executor {
     } else {
       R_ = 0;
     }
-    bindings_ = R_;
+    if (!chain) bindings_ = R_;
     uint64_t n = 0;
     int ncols = 0;
     std::vector<DBuf<uint32_t>> out;
     // partitioned + distinct projection: equal tuples meet on one rank first
     if (dist_ && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
     const bool docs = p_.proj == Plan::PROJ_EXPR || p_.proj == Plan::PROJ_JSON;
-    if (R_ > 0 && !counted_only && docs) {
+    if (chain) {  // the records in emission order (duplicates are the reference's: not de-duplicated)
+      n = R_;
+      ncols = 1;
+      out = std::move(chain_out);
+    } else if (R_ > 0 && !counted_only && docs) {
       // RETURN expressions / JSON: distinct tuples of the aliases they read (device), then one document
       // per tuple, de-duplicated by content (project.cpp: the OResultSet fill of addResult :698-719)
       if (!p_.out_aliases.empty()) project_dedup(out, n);
@@ -801,7 +810,7 @@ class Executor {
   ExpandOut expand_core(const uint32_t *src, uint64_t R, const AdjSpec &adjs, const uint64_t *filter,
                         const std::vector<const uint32_t *> &carry, bool write, bool allow_segmented = false,
                         const uint32_t *member_src = nullptr, const AdjSpec *member_adj = nullptr,
-                        const uint64_t *member_filter = nullptr, const DAdj *raw_adj = nullptr) {
+                        const uint64_t *member_filter = nullptr, const DAdj *raw_adj = nullptr, bool ordered = false) {
     ExpandOut o;
     DAdj adj = raw_adj ? *raw_adj : make_adj(adjs);
     if (adj.n == 0 || R == 0) return o;
@@ -823,7 +832,13 @@ class Executor {
     // sliced: a heavy row is cut into P pieces, one chunk each; below ~128 edges per piece a chunk issues
     // its 16 loads for a few live slots, so the cut grows with P (RMAT-24, P = 16: 2048 measured best of
     // 256…4096, profiles/r02/hd_sweep; RMAT-22, P = 4: 512 against 256, 1.80 against 1.83 ms per step)
-    const uint64_t hd = !sliced ? heavy_deg_ : heavy_deg_fixed_ ? heavy_deg_sliced_ : std::max<uint64_t>(heavy_deg_sliced_, 128ull * P);
+    // ordered (unfiltered, TRAVERSE / SELECT expand): every row through the merge-path kernel, whose dense
+    // output is in row order (the heavy kernel's rows come first)
+    const uint64_t hd = ordered ? UINT64_MAX
+                        : !sliced ? heavy_deg_
+                        : heavy_deg_fixed_ ? heavy_deg_sliced_
+                                           : std::max<uint64_t>(heavy_deg_sliced_, 128ull * P);
+    if (ordered && (filter || member)) fail(OMX_E_INVALID, "internal: an ordered expansion is unfiltered");
     // per-tile sums → one-workgroup scan (posts the totals to the host) → per-tile offsets and chunks
     DBuf<uint64_t> blk(&pool_, (uint64_t)(kBinKeys + P) * bin_tiles(R)), qb(&pool_, P + 1);
     // a sliced hop that writes rows sizes its arenas from the target bitmap's density per slice
@@ -1252,6 +1267,123 @@ class Executor {
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
     col_[st.dst] = std::move(o.dst);
     return true;
+  }
+
+  // ---- TRAVERSE / SELECT expand(): ordered record lists (Plan::chain) ------------------------------
+  // the FROM records in target order: a class's vertices in snapshot order, or the listed RIDs that
+  // name a vertex (an unknown RID is skipped, like a record that does not load); `where` filters them
+  DBuf<uint32_t> chain_roots(uint64_t &n, int where) {
+    const ChainSpec &c = p_.chain;
+    DBuf<uint64_t> wscratch;
+    if (c.root_class >= 0) {
+      DBuf<uint64_t> bm(&pool_, padded_words());
+      eval_bitmap(where, c.root_class, 0, bm.p, padded_words());
+      return bitmap_list(bm.p, 0, 1, n);
+    }
+    n = 0;
+    const uint64_t m = c.root_rids.size();
+    if (!m) return DBuf<uint32_t>(&pool_, 1);
+    DBuf<uint64_t> keys(&pool_, m);
+    DBuf<uint32_t> ids(&pool_, m);
+    HIP_CHECK(hipMemcpyAsync(keys.p, c.root_rids.data(), m * 8, hipMemcpyHostToDevice, s_));
+    launch_fill_u32(ids.p, m, UINT32_MAX, s_);
+    launch_find_rids(g_.d_rids, g_.V, keys.p, (uint32_t)m, ids.p, s_);
+    std::vector<uint32_t> h(m);
+    HIP_CHECK(hipMemcpyAsync(h.data(), ids.p, m * 4, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    std::vector<uint32_t> found;
+    for (uint32_t v : h)
+      if (v != UINT32_MAX) found.push_back(v);
+    DBuf<uint32_t> r(&pool_, std::max<size_t>(found.size(), 1));
+    n = found.size();
+    if (n) HIP_CHECK(hipMemcpyAsync(r.p, found.data(), n * 4, hipMemcpyHostToDevice, s_));
+    const uint64_t *wb = prog_bitmap(where, 0, wscratch);
+    if (!n || !wb) return r;
+    DBuf<uint8_t> flags(&pool_, n);
+    launch_flag_bitmap(r.p, n, wb, flags.p, s_);
+    DBuf<uint32_t> sel(&pool_, n);
+    DBuf<uint64_t> nsel(&pool_, 1);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, r.p, flags.p, sel.p, nsel.p, (int64_t)n, s_); });
+    n = read1(nsel.p);
+    return sel;
+  }
+
+  // one move of an ordered list: every entry's neighbours, entries in order (duplicates kept)
+  DBuf<uint32_t> ordered_hop(const uint32_t *cur, uint64_t n, const AdjSpec &adj, uint64_t &out_n) {
+    out_n = 0;
+    if (!n) return DBuf<uint32_t>(&pool_, 1);
+    ExpandOut o = expand_core(cur, n, adj, nullptr, {}, true, false, nullptr, nullptr, nullptr, nullptr, true);
+    edges_ += o.E;
+    edges_iter_ += o.E;
+    out_n = o.n;
+    if (!o.n) return DBuf<uint32_t>(&pool_, 1);
+    return std::move(o.dst);
+  }
+
+  int64_t chain_limit() const { return p_.limit >= 0 ? p_.limit : o_.limit; }
+
+  // TRAVERSE <fields> FROM <target> [WHILE <cond>] [MAXDEPTH d] [LIMIT n] STRATEGY BREADTH_FIRST.
+  // OTraverse's queue (OTraverseContext.QueueMemory) holds, level by level, the records the previous
+  // level's fields pushed, in push order; a record is emitted when it is processed, is not in the
+  // history and passes WHILE with $depth = its level (OTraverseRecordProcess.process :49-105). A
+  // processed record below MAXDEPTH stays in the history, so it is emitted once, at its first entry;
+  // one at MAXDEPTH is popped with its history entry removed (:66-69, OTraverseContext.pop :58-70), so
+  // every entry of the MAXDEPTH level that is not in the history is emitted, repeats included. LIMIT
+  // stops the work list after n results (OTraverse.hasNext :68-70).
+  DBuf<uint32_t> traverse_bfs() {
+    const ChainSpec &c = p_.chain;
+    uint64_t n = 0;
+    DBuf<uint32_t> cur = chain_roots(n, -1);
+    DBuf<uint64_t> hist(&pool_, std::max<uint64_t>(nwords_, 1)), pscratch;
+    DBuf<uint32_t> first(&pool_, std::max<uint64_t>(g_.V, 1));
+    HIP_CHECK(hipMemsetAsync(hist.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+    launch_fill_u32(first.p, g_.V, UINT32_MAX, s_);
+    const int64_t limit = chain_limit();
+    std::vector<DBuf<uint32_t>> parts;
+    std::vector<uint64_t> pn;
+    uint64_t total = 0;
+    for (int64_t d = 0; n > 0; ++d) {
+      if (n >= UINT32_MAX) unsupported("a TRAVERSE level of 2^32 or more work-list entries");
+      const bool last = c.max_depth >= 0 && d == c.max_depth;
+      const uint64_t *pred = prog_bitmap(c.pred_prog, d, pscratch);
+      DBuf<uint8_t> flags(&pool_, n);
+      tm_.begin("k_trav_filter");
+      launch_trav_filter(cur.p, n, hist.p, pred, first.p, flags.p, !last, s_);
+      tm_.end(n * (4 + 8 + 8 + 1) + (last ? 0 : n * 9));
+      DBuf<uint32_t> acc(&pool_, n);
+      DBuf<uint64_t> nsel(&pool_, 1);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cur.p, flags.p, acc.p, nsel.p, (int64_t)n, s_); });
+      const uint64_t k = read1(nsel.p);
+      if (!last) launch_trav_accept(acc.p, k, hist.p, first.p, s_);
+      if (k) {
+        parts.push_back(std::move(acc));
+        pn.push_back(k);
+        total += k;
+      }
+      if (last || k == 0 || (limit > 0 && total >= (uint64_t)limit)) break;
+      cur = ordered_hop(parts.back().p, k, c.hops[0], n);
+    }
+    R_ = limit > 0 ? std::min<uint64_t>(total, (uint64_t)limit) : total;
+    bindings_ = total;
+    return concat_batches(parts, pn, total);
+  }
+
+  // SELECT expand(m0(...).m1(...)...) FROM <target> [WHERE <cond>] [LIMIT n]: each call moves the whole
+  // list, every record's result concatenated in order (OSQLEngine.foreachRecord, S/OSQLEngine.java:264-290)
+  DBuf<uint32_t> select_expand() {
+    const ChainSpec &c = p_.chain;
+    uint64_t n = 0;
+    DBuf<uint32_t> cur = chain_roots(n, c.pred_prog);
+    for (const AdjSpec &h : c.hops) {
+      if (!n) break;
+      uint64_t m = 0;
+      cur = ordered_hop(cur.p, n, h, m);
+      n = m;
+    }
+    const int64_t limit = chain_limit();
+    bindings_ = n;
+    R_ = limit > 0 ? std::min<uint64_t>(n, (uint64_t)limit) : n;
+    return cur;
   }
 
   // WHERE conjunct `$matched.X op $currentMatch` of the alias the previous step bound

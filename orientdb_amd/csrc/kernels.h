@@ -232,6 +232,12 @@ void launch_check_optional(const uint32_t *src, uint32_t *dst, uint64_t R, const
                            uint32_t V, unsigned int *npe, hipStream_t s);
 void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out, hipStream_t s);
 void launch_flag_row_change(int ncols, const uint32_t *const *cols, uint64_t n, uint8_t *flags, hipStream_t s);
+// TRAVERSE: RID lookup of the target records; a level's history / WHILE filter with first-position
+// claims (dedup); the accepted records into the history
+void launch_find_rids(const uint64_t *rids, uint32_t V, const uint64_t *keys, uint32_t m, uint32_t *out, hipStream_t s);
+void launch_trav_filter(const uint32_t *w, uint64_t n, const uint64_t *hist, const uint64_t *pred, uint32_t *first,
+                        uint8_t *flags, bool dedup, hipStream_t s);
+void launch_trav_accept(const uint32_t *w, uint64_t n, uint64_t *hist, uint32_t *first, hipStream_t s);
 // a null binding (dense id ≥ V: an unmatched optional node) maps to kNullRid
 constexpr uint64_t kNullRid = ~0ull;
 void launch_map_rids(int ncols, const uint32_t *const *cols, uint64_t n, const uint64_t *rids, uint64_t *out,

@@ -2094,26 +2094,111 @@ void launch_index_of(const uint32_t *sorted, uint64_t n, const uint32_t *keys, u
   KCHECK("k_index_of");
 }
 // counts[key[i]] += 1
+// Keys arrive in runs (an expansion writes one source's survivors contiguously), and a hub's run would
+// serialise on one counter: every wave combines its runs of equal keys and issues one atomic per run.
+__device__ __forceinline__ uint64_t key_runs(uint32_t k, bool valid, int lane) {
+  const uint32_t prev = __shfl_up(k, 1, 64);
+  return __ballot(valid && (lane == 0 || prev != k));
+}
 __global__ void k_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) atomicAdd(&counts[key[i]], 1ull);
+  const int lane = threadIdx.x & 63;
+  const bool valid = i < n;
+  const uint32_t k = valid ? key[i] : 0xFFFFFFFFu;
+  const uint64_t heads = key_runs(k, valid, lane);
+  const int nvalid = __popcll(__ballot(valid));  // the valid lanes are a prefix of the wave
+  if (valid && ((heads >> lane) & 1)) {
+    const uint64_t later = lane == 63 ? 0 : heads & (~0ull << (lane + 1));
+    const int nxt = later ? __ffsll((unsigned long long)later) - 1 : 64;
+    atomicAdd(&counts[k], (unsigned long long)(min(nxt, nvalid) - lane));
+  }
 }
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_key_hist, dim3(nblocks(n, 256)), dim3(256), 0, s, key, n, counts);
   KCHECK("k_key_hist");
 }
-// out[cursor[key[i]]++] = val[i] (cursor starts at the groups' offsets; order inside a group is free)
+// out[cursor[key[i]]++] = val[i] (cursor starts at the groups' offsets; order inside a group is free):
+// the head of each run reserves the run's slots, its lanes write at the head's base + their rank
 __global__ void k_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor,
                               uint32_t *out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[atomicAdd(&cursor[key[i]], 1ull)] = val[i];
+  const int lane = threadIdx.x & 63;
+  const bool valid = i < n;
+  const uint32_t k = valid ? key[i] : 0xFFFFFFFFu;
+  const uint64_t heads = key_runs(k, valid, lane);
+  const int nvalid = __popcll(__ballot(valid));
+  unsigned long long base = 0;
+  if (valid && ((heads >> lane) & 1)) {
+    const uint64_t later = lane == 63 ? 0 : heads & (~0ull << (lane + 1));
+    const int nxt = later ? __ffsll((unsigned long long)later) - 1 : 64;
+    base = atomicAdd(&cursor[k], (unsigned long long)(min(nxt, nvalid) - lane));
+  }
+  const uint64_t upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+  const int hl = upto ? 63 - __clzll((long long)upto) : lane;  // this lane's run head
+  base = __shfl(base, hl, 64);
+  if (valid) out[base + (uint64_t)(lane - hl)] = val[i];
 }
 void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor, uint32_t *out,
                         hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_key_scatter, dim3(nblocks(n, 256)), dim3(256), 0, s, key, val, n, cursor, out);
   KCHECK("k_key_scatter");
+}
+
+// ---- TRAVERSE (exec.hip Executor::traverse_bfs) -----------------------------------------------------
+// out[j] = the vertex whose RID is keys[j] (left untouched when no vertex has it; RIDs are unique)
+__global__ void k_find_rids(const uint64_t *rids, uint32_t V, const uint64_t *keys, uint32_t m, uint32_t *out) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = rids[v];
+    for (uint32_t j = 0; j < m; ++j)
+      if (keys[j] == r) out[j] = (uint32_t)v;
+  }
+}
+void launch_find_rids(const uint64_t *rids, uint32_t V, const uint64_t *keys, uint32_t m, uint32_t *out, hipStream_t s) {
+  if (!V || !m) return;
+  hipLaunchKernelGGL(k_find_rids, dim3((unsigned)std::min<uint64_t>(nblocks(V, 256), 4096)), dim3(256), 0, s, rids, V,
+                     keys, m, out);
+  KCHECK("k_find_rids");
+}
+// A level's work-list entries w[e] in queue order: an entry is processed when its record is not in the
+// history H and passes the WHILE bitmap (OTraverseRecordProcess.process :49-63); `dedup` levels claim
+// each record's first position (a later entry of an accepted record meets it in the history)
+__global__ void k_trav_filter(const uint32_t *w, uint64_t n, const uint64_t *hist, const uint64_t *pred,
+                              uint32_t *first, uint8_t *flags, int dedup) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint32_t v = w[e];
+  bool keep = !((hist[v >> 6] >> (v & 63)) & 1);
+  if (keep && pred) keep = (pred[v >> 6] >> (v & 63)) & 1;
+  if (keep && dedup) atomicMin(&first[v], (uint32_t)e);
+  flags[e] = keep;
+}
+__global__ void k_trav_first(const uint32_t *w, uint64_t n, const uint32_t *first, uint8_t *flags) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n && flags[e] && first[w[e]] != (uint32_t)e) flags[e] = 0;
+}
+void launch_trav_filter(const uint32_t *w, uint64_t n, const uint64_t *hist, const uint64_t *pred, uint32_t *first,
+                        uint8_t *flags, bool dedup, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_trav_filter, dim3(nblocks(n, 256)), dim3(256), 0, s, w, n, hist, pred, first, flags, (int)dedup);
+  KCHECK("k_trav_filter");
+  if (!dedup) return;
+  hipLaunchKernelGGL(k_trav_first, dim3(nblocks(n, 256)), dim3(256), 0, s, w, n, first, flags);
+  KCHECK("k_trav_first");
+}
+// accepted records join the history; their first-position claims are released
+__global__ void k_trav_accept(const uint32_t *w, uint64_t n, uint64_t *hist, uint32_t *first) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint32_t v = w[e];
+  atomicOr((unsigned long long *)&hist[v >> 6], 1ull << (v & 63));
+  first[v] = 0xFFFFFFFFu;
+}
+void launch_trav_accept(const uint32_t *w, uint64_t n, uint64_t *hist, uint32_t *first, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_trav_accept, dim3(nblocks(n, 256)), dim3(256), 0, s, w, n, hist, first);
+  KCHECK("k_trav_accept");
 }
 
 __global__ void k_fill_u32(uint32_t *out, uint64_t n, uint32_t x) {
@@ -2178,13 +2263,21 @@ void launch_flag_not_in(const uint64_t *sorted, uint64_t ns, const uint64_t *key
   KCHECK("k_flag_not_in");
 }
 
-__global__ void k_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, uint32_t V) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && v[i] < V) atomicOr((unsigned long long *)&bm[v[i] >> 6], 1ull << (v[i] & 63));
+// grid-stride; a bit already set is only read (a one-column distinct of 4e8 rows over 4e4 vertices
+// would otherwise serialise on a few hundred words' atomics)
+__global__ __launch_bounds__(256) void k_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, uint32_t V) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t x = v[i];
+    if (x >= V) continue;
+    const uint64_t bit = 1ull << (x & 63);
+    if (!(__hip_atomic_load(&bm[x >> 6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
+      atomicOr((unsigned long long *)&bm[x >> 6], (unsigned long long)bit);
+  }
 }
 void launch_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, uint32_t V, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_mark_bitmap, dim3(nblocks(n, 256)), dim3(256), 0, s, v, n, bm, V);
+  hipLaunchKernelGGL(k_mark_bitmap, dim3((unsigned)std::min<uint64_t>(nblocks(n, 256), 256 * 64)), dim3(256), 0, s, v, n,
+                     bm, V);
   KCHECK("k_mark_bitmap");
 }
 

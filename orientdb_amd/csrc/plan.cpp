@@ -78,6 +78,8 @@ class Planner {
     plan_ = std::make_unique<Plan>();
     exprs_ = st_.expressions;  // private copy: default aliases / rebound filters are assigned here
     assign_default_aliases();
+    // the logical plan (explain) keeps the reference's edge nodes; the device plan fuses them
+    if (!logical_only) fuse_edge_items();
     for (auto &e : exprs_) add_expression(e);
     for (auto &e : exprs_) {
       add_aliases(e.origin);
@@ -101,8 +103,99 @@ class Planner {
     return std::move(plan_);
   }
 
+  // TRAVERSE ... STRATEGY BREADTH_FIRST / SELECT expand(<chain>) FROM <target> (ChainSpec)
+  std::unique_ptr<Plan> run_chain(bool logical_only) {
+    plan_ = std::make_unique<Plan>();
+    Plan &p = *plan_;
+    const bool trav = st_.kind == Statement::TRAVERSE;
+    p.kind = trav ? Plan::TRAVERSE : Plan::SELECT;
+    p.out_names = {"@rid"};
+    p.limit = st_.has_limit ? st_.limit : -1;
+    if (logical_only) return std::move(plan_);
+    p.params = params_;
+    if (!st_.unsupported.empty()) unsupported(st_.unsupported);
+    const Target &t = st_.target;
+    if (!t.other.empty()) unsupported("target " + t.other + " (only records and classes on the device)");
+    ChainSpec &c = p.chain;
+    if (!t.class_name.empty()) {
+      c.root_class = g_.class_id(t.class_name);
+      if (c.root_class < 0) fail(OMX_E_EXECUTION, "Class '" + t.class_name + "' was not found in current database");
+      if (g_.classes[c.root_class].is_edge) unsupported("a target of edge records");
+    }
+    for (auto &r : t.rids)
+      if (r.first >= 0 && r.second >= 0) c.root_rids.push_back(((uint64_t)r.first << 48) | (uint64_t)r.second);
+    legacy_ = true;
+    if (trav) {
+      // OTraverse runs the BREADTH_FIRST work list level by level; DEPTH_FIRST is a sequential stack walk
+      if (!st_.breadth_first) unsupported("TRAVERSE with the DEPTH_FIRST strategy (only BREADTH_FIRST on the device)");
+      AdjSpec cat;
+      std::set<std::string> seen;  // traverse.fields(Set): a field given twice is traversed once
+      for (auto &f : st_.fields) {
+        if (!seen.insert(lower(expr_text(f))).second) continue;
+        AdjSpec a = move_call(f, "traverse field");
+        cat.parts.insert(cat.parts.end(), a.parts.begin(), a.parts.end());
+        cat.sorted = cat.sorted && a.sorted;
+      }
+      if (seen.size() > 1)
+        unsupported("TRAVERSE of several fields (the reference keeps them in a HashSet: their order is unspecified)");
+      if ((int)cat.parts.size() > kMaxAdjParts) unsupported("too many edge classes in one traversal");
+      c.hops.push_back(cat);
+      c.pred_prog = add_prog(st_.where, true);
+      c.max_depth = st_.max_depth;
+    } else {
+      // expand(f0(...).f1(...)...): every call moves the whole list (OSQLEngine.foreachRecord keeps the
+      // order and the duplicates); outE('L').inV() / inE('L').outV() pairs are one hop
+      const ExprP &x = st_.fields[0];
+      std::vector<std::pair<std::string, std::vector<ExprP>>> calls;
+      if (x->kind == Expr::CALL) {
+        calls.emplace_back(x->name, x->kids);
+      } else if (x->kind == Expr::CHAIN && x->kids[0]->kind == Expr::CALL) {
+        calls.emplace_back(x->kids[0]->name, x->kids[0]->kids);
+        for (auto &sfx : x->suffixes) {
+          if (sfx.kind != Suffix::METHOD) unsupported("expand() argument " + expr_text(x));
+          calls.emplace_back(sfx.name, sfx.args);
+        }
+      } else {
+        unsupported("expand() argument " + expr_text(x));
+      }
+      for (size_t i = 0; i < calls.size(); ++i) {
+        const std::string m = lower(calls[i].first);
+        const std::vector<std::string> labels = labels_of(calls[i].second);
+        if ((m == "oute" || m == "ine") && i + 1 < calls.size() && calls[i + 1].second.empty() &&
+            lower(calls[i + 1].first) == (m == "oute" ? "inv" : "outv")) {
+          c.hops.push_back(adjacency(m == "oute" ? "out" : "in", labels));
+          ++i;
+          continue;
+        }
+        if (m != "out" && m != "in" && m != "both") unsupported("function " + calls[i].first + "() in expand() on the device");
+        c.hops.push_back(adjacency(m, labels));
+      }
+      c.pred_prog = add_prog(st_.where, false);
+    }
+    return std::move(plan_);
+  }
+
  private:
+  std::vector<std::string> labels_of(const std::vector<ExprP> &args) const {
+    std::vector<std::string> labels;
+    for (auto &a : args) {
+      auto v = fold(a);
+      if (!v || v->kind != Value::STR) unsupported("non-constant edge label");
+      labels.push_back(v->s);
+    }
+    return labels;
+  }
+  // out('L', ...) / in(...) / both(...) as a field of TRAVERSE
+  AdjSpec move_call(const ExprP &f, const char *what) const {
+    if (f->kind != Expr::CALL) unsupported(std::string(what) + " " + expr_text(f) + " (only out()/in()/both() on the device)");
+    const std::string m = lower(f->name);
+    if (m != "out" && m != "in" && m != "both")
+      unsupported(std::string(what) + " " + expr_text(f) + " (only out()/in()/both() on the device)");
+    return adjacency(m, labels_of(f->kids));
+  }
+
   const Statement &st_;
+  bool legacy_ = false;  // compiling a legacy-SQL condition (TRAVERSE WHILE, SELECT WHERE)
   const Graph &g_;
   const Params &params_;
   std::unique_ptr<Plan> plan_;
@@ -124,6 +217,37 @@ class Planner {
       if (e.origin.alias.empty()) e.origin.alias = kDefaultPrefix + std::to_string(counter++);
       for (auto &it : e.items)
         if (it.filter.alias.empty()) it.filter.alias = kDefaultPrefix + std::to_string(counter++);
+    }
+  }
+  // `outE('L').inV()` / `inE('L').outV()` whose edge step has no filter: its node is an anonymous edge
+  // alias that no other item and no $matches/$patterns/explicit RETURN reads, and OSQLFunctionMove's e2v
+  // yields one vertex per edge (GF/OSQLFunctionMove.java:122-143), so the pair is out('L') / in('L') with
+  // the edge multiplicity, which the distinct result rows absorb. $paths / $pathElements would expose
+  // the edge records: compile_projection leaves those to the reference engine.
+  bool fused_edges_ = false;
+  void fuse_edge_items() {
+    for (auto &e : exprs_) {
+      std::vector<PathItem> items;
+      for (size_t i = 0; i < e.items.size(); ++i) {
+        const PathItem &a = e.items[i];
+        const std::string m = lower(a.method);
+        if (!a.is_multi && !a.has_filter && (m == "oute" || m == "ine") && i + 1 < e.items.size()) {
+          const PathItem &b = e.items[i + 1];
+          const std::string v = lower(b.method);
+          if (!b.is_multi && b.labels.empty() && ((m == "oute" && v == "inv") || (m == "ine" && v == "outv")) &&
+              !b.filter.while_ && !b.filter.has_max_depth) {
+            PathItem f = b;
+            f.method = m == "oute" ? "out" : "in";
+            f.labels = a.labels;
+            items.push_back(f);
+            fused_edges_ = true;
+            ++i;
+            continue;
+          }
+        }
+        items.push_back(a);
+      }
+      e.items.swap(items);
     }
   }
   int node(const MatchFilter &f) {
@@ -608,6 +732,11 @@ class Planner {
     return op;
   }
 
+  bool string_may_be_null(const ExprP &e) const {
+    int p;
+    return string_field(e, &p) && g_.props[p].has_nulls;
+  }
+
   bool string_field(const ExprP &e, int *prop) const {
     if (e->kind != Expr::FIELD || shadowed(e->name)) return false;
     int p = g_.prop_id(e->name);
@@ -671,6 +800,27 @@ class Planner {
         std::string op = e->name;
         int prop;
         auto fl = fold(L), fr = fold(R);
+        if (legacy_) {
+          // legacy operators (S/operator/OQueryOperatorEqualityNotNulls.java:50-56): a null operand makes
+          // every comparison false, != included; the right operand is converted to the left one's type
+          // (OQueryOperatorMajor.java:63-69: OType.convert), which truncates a fractional constant
+          if ((fl && fl->kind == Value::NUL) || (fr && fr->kind == Value::NUL)) {
+            b.emit(P_PUSH_BOOL, 0, 0, 0, 1);
+            return;
+          }
+          if (op == "!=" && (may_be_null(L) || may_be_null(R) || string_may_be_null(L) || string_may_be_null(R)))
+            unsupported("!= with a possibly-null operand in a legacy condition (false in the reference, true on the device)");
+          if (string_field(L, &prop) && fr && fr->kind == Value::STR) return emit_string_cmp(b, prop, op, fr->s);
+          if (string_field(R, &prop) && fl && fl->kind == Value::STR) return emit_string_cmp(b, prop, flip(op), fl->s);
+          CT l = compile_value(b, L, allow_depth);
+          CT r = compile_value(b, R, allow_depth);
+          if (l == C_INT && r == C_DBL) unsupported("an integer compared with a fractional value in a legacy condition (converted)");
+          if ((l == C_BOOL) != (r == C_BOOL)) unsupported("comparison of a boolean with a number");
+          if (l == C_BOOL && op != "=" && op != "!=") unsupported("ordering comparison of booleans");
+          int32_t code = op == "=" ? P_EQ : op == "!=" ? P_NE : op == "<" ? P_LT : op == "<=" ? P_LE : op == ">" ? P_GT : P_GE;
+          b.emit(code, 0, 0, 0, -1);
+          return;
+        }
         if (string_field(L, &prop) && fr && fr->kind == Value::STR) {
           if ((op == ">" || op == ">=" || op == "<=") && g_.props[prop].has_nulls)
             unsupported("a possibly-null left operand of " + op + " (NullPointerException in the reference): " + expr_text(L));
@@ -973,6 +1123,8 @@ class Planner {
       return false;
     };
     Plan &p = *plan_;
+    if (fused_edges_ && (has("$paths") || has("$pathElements")))
+      unsupported("$paths / $pathElements of a pattern with edge steps (the edge records are returned)");
     if (has("$elements") || has("$pathElements")) {
       p.proj = Plan::PROJ_ELEMENTS;
       bool all = has("$elements") ? false : true;
@@ -1055,11 +1207,13 @@ std::string jstr(const std::string &s) {
 
 std::unique_ptr<Plan> build_plan(const Statement &st, const Graph &g, const Params &params, bool logical_only,
                                  std::string *reason) {
-  if (!logical_only) return Planner(st, g, params).run(false);
-  auto p = Planner(st, g, params).run(true);
+  const bool chain = st.kind != Statement::MATCH;
+  if (!logical_only) return chain ? Planner(st, g, params).run_chain(false) : Planner(st, g, params).run(false);
+  auto p = chain ? Planner(st, g, params).run_chain(true) : Planner(st, g, params).run(true);
   if (reason) {
     try {
-      Planner(st, g, params).run(false);
+      if (chain) Planner(st, g, params).run_chain(false);
+      else Planner(st, g, params).run(false);
       reason->clear();
     } catch (const OmxError &e) {
       if (e.code != OMX_E_UNSUPPORTED) throw;
@@ -1071,7 +1225,8 @@ std::unique_ptr<Plan> build_plan(const Statement &st, const Graph &g, const Para
 
 std::string plan_json(const Plan &p, const std::string &reason) {
   std::ostringstream o;
-  o << "{\"aliases\":[";
+  o << "{\"kind\":" << jstr(p.kind == Plan::MATCH ? "MATCH" : p.kind == Plan::TRAVERSE ? "TRAVERSE" : "SELECT");
+  o << ",\"aliases\":[";
   for (size_t i = 0; i < p.aliases.size(); ++i) o << (i ? "," : "") << jstr(p.aliases[i]);
   o << "],\"estimates\":{";
   for (size_t i = 0; i < p.estimates.size(); ++i)

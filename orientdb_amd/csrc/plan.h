@@ -81,7 +81,22 @@ struct Step {
   std::string desc;
 };
 
+// TRAVERSE (C/command/traverse/OTraverse.java, STRATEGY BREADTH_FIRST) and SELECT expand(<chain>)
+// (GF/OSQLFunctionMove.java:66-91 via OSQLEngine.foreachRecord, S/OSQLEngine.java:264-290): an ordered
+// list of records, kept in the reference's emission order.
+struct ChainSpec {
+  // TRAVERSE: one entry, the fields' neighbour lists concatenated in field order (the reference pushes one
+  // OTraverseMultiValueProcess per field, OTraverseRecordProcess.java:136-160); SELECT: one per chained call
+  std::vector<AdjSpec> hops;
+  int pred_prog = -1;       // TRAVERSE WHILE (reads $depth; legacy null semantics) / SELECT WHERE
+  int max_depth = -1;       // TRAVERSE MAXDEPTH
+  int root_class = -1;      // FROM <class>: its vertices (polymorphic) in snapshot order
+  std::vector<uint64_t> root_rids;  // FROM #c:p / [#c:p, ...] (packed c << 48 | p), in the order written
+};
+
 struct Plan {
+  enum Kind { MATCH, TRAVERSE, SELECT } kind = MATCH;
+  ChainSpec chain;  // TRAVERSE / SELECT
   // logical plan (what the reference computes; also reported by omx_statement_explain)
   std::vector<std::string> aliases;  // pattern nodes, insertion order (Pattern.aliasToNode)
   std::vector<bool> explicit_alias;

@@ -23,7 +23,7 @@ bool PathItem::bidirectional() const {
 namespace {
 
 struct Tok {
-  enum Kind { ID, NUM, STR, OP, END } kind;
+  enum Kind { ID, NUM, STR, OP, RID, END } kind;  // RID: "#c:p" → v = "c:p"
   std::string v;
 };
 
@@ -62,6 +62,18 @@ std::vector<Tok> tokenize(const std::string &s) {
       size_t j = i + 1;
       while (j < n && (isalnum((unsigned char)s[j]) || s[j] == '_')) ++j;
       out.push_back({Tok::ID, s.substr(i, j - i)});
+      i = j;
+      continue;
+    }
+    if (c == '#' && i + 1 < n && (isdigit((unsigned char)s[i + 1]) || s[i + 1] == '-')) {  // record id #c:p
+      size_t j = i + 1;
+      if (s[j] == '-') ++j;
+      while (j < n && isdigit((unsigned char)s[j])) ++j;
+      if (j >= n || s[j] != ':') fail(OMX_E_PARSE, "malformed record id at offset " + std::to_string(i));
+      ++j;
+      if (j < n && s[j] == '-') ++j;
+      while (j < n && isdigit((unsigned char)s[j])) ++j;
+      out.push_back({Tok::RID, s.substr(i + 1, j - i - 1)});
       i = j;
       continue;
     }
@@ -105,7 +117,9 @@ class Parser {
   explicit Parser(const std::string &text) : t_(tokenize(text)) {}
 
   std::unique_ptr<Statement> statement() {
-    if (!kw("match")) fail(OMX_E_PARSE, "MATCH expected");
+    if (kw("traverse")) return traverse();
+    if (kw("select")) return select();
+    if (!kw("match")) fail(OMX_E_PARSE, "MATCH, TRAVERSE or SELECT expected");
     ++i_;
     auto st = std::make_unique<Statement>();
     st->expressions.push_back(match_expression());
@@ -129,18 +143,134 @@ class Parser {
       if (op(",")) { ++i_; continue; }
       break;
     }
-    if (kw("limit")) {
-      ++i_;
-      bool neg = false;
-      if (op("-")) { ++i_; neg = true; }
-      Tok n = next();
-      if (n.kind != Tok::NUM) fail(OMX_E_PARSE, "LIMIT expects an integer");
-      st->has_limit = true;
-      st->limit = std::strtoll(n.v.c_str(), nullptr, 10) * (neg ? -1 : 1);
-    }
+    if (kw("limit")) limit(*st);
     if (t_[i_].kind != Tok::END) fail(OMX_E_PARSE, "unexpected token '" + t_[i_].v + "'");
     st->n_positional = nparam_;
     return st;
+  }
+
+  // TRAVERSE <field>[, <field>]* FROM <target> [WHILE <cond>] [LIMIT n] [MAXDEPTH n] [STRATEGY s]
+  // (OCommandExecutorSQLTraverse.parse / parseFields, S/OCommandExecutorSQLTraverse.java:64-139,212-247)
+  std::unique_ptr<Statement> traverse() {
+    ++i_;
+    auto st = std::make_unique<Statement>();
+    st->kind = Statement::TRAVERSE;
+    if (kw("from")) fail(OMX_E_PARSE, "Missed field list to cross in TRAVERSE");
+    for (;;) {
+      if (op("*")) {
+        ++i_;
+        auto all = mk(Expr::FIELD);
+        all->name = "*";
+        st->fields.push_back(all);
+      } else {
+        st->fields.push_back(expr());
+      }
+      if (!op(",")) break;
+      ++i_;
+    }
+    if (!kw("from")) fail(OMX_E_PARSE, "Missed FROM in TRAVERSE");
+    ++i_;
+    target(*st);
+    if (kw("while") || kw("where")) {  // WHERE: the deprecated spelling of WHILE (:93-102)
+      ++i_;
+      st->where = or_expr();
+    }
+    while (t_[i_].kind != Tok::END) {
+      if (kw("limit")) {
+        limit(*st);
+        if (st->limit == 0 || st->limit < -1) fail(OMX_E_PARSE, "Limit must be > 0 or = -1 (no limit)");
+      } else if (kw("maxdepth")) {
+        ++i_;
+        Tok n = next();
+        if (n.kind != Tok::NUM && !(n.kind == Tok::OP && n.v == "-")) fail(OMX_E_PARSE, "Invalid MAXDEPTH value");
+        if (n.kind != Tok::NUM) fail(OMX_E_PARSE, "Invalid MAXDEPTH: value set minor than ZERO");
+        st->max_depth = std::atoi(n.v.c_str());
+      } else if (kw("strategy")) {
+        ++i_;
+        const std::string w = lower(next().v);
+        if (w == "breadth_first") st->breadth_first = true;
+        else if (w == "depth_first") st->breadth_first = false;
+        else fail(OMX_E_PARSE, "Invalid STRATEGY. Use one between [DEPTH_FIRST, BREADTH_FIRST]");
+      } else if (kw("skip") || kw("offset") || kw("timeout")) {
+        st->unsupported = lower(next().v) + " in TRAVERSE";
+        next();
+      } else {
+        fail(OMX_E_PARSE, "unexpected token '" + t_[i_].v + "'");
+      }
+    }
+    st->n_positional = nparam_;
+    return st;
+  }
+
+  // SELECT expand(<chain>) FROM <target> [WHERE <cond>] [LIMIT n]: the rows of the expanded chain
+  // (other SELECT forms are the legacy SQL executor's and stay there)
+  std::unique_ptr<Statement> select() {
+    ++i_;
+    auto st = std::make_unique<Statement>();
+    st->kind = Statement::SELECT;
+    if (!kw("expand") || !op("(", 1)) fail(OMX_E_UNSUPPORTED, "SELECT without expand(): the legacy SQL executor's");
+    ++i_;
+    expect("(");
+    st->fields.push_back(expr());
+    expect(")");
+    if (!kw("from")) fail(OMX_E_UNSUPPORTED, "SELECT expand(...) with more projections or no FROM");
+    ++i_;
+    target(*st);
+    if (kw("where")) {
+      ++i_;
+      st->where = or_expr();
+    }
+    if (kw("limit")) limit(*st);
+    if (t_[i_].kind != Tok::END) fail(OMX_E_UNSUPPORTED, "SELECT clause '" + t_[i_].v + "' on the device");
+    st->n_positional = nparam_;
+    return st;
+  }
+
+  void limit(Statement &st) {
+    ++i_;
+    bool neg = false;
+    if (op("-")) { ++i_; neg = true; }
+    Tok n = next();
+    if (n.kind != Tok::NUM) fail(OMX_E_PARSE, "LIMIT expects an integer");
+    st.has_limit = true;
+    st.limit = std::strtoll(n.v.c_str(), nullptr, 10) * (neg ? -1 : 1);
+  }
+
+  static std::pair<int64_t, int64_t> rid_of(const std::string &v) {
+    const size_t c = v.find(':');
+    return {std::strtoll(v.substr(0, c).c_str(), nullptr, 10), std::strtoll(v.substr(c + 1).c_str(), nullptr, 10)};
+  }
+
+  // OSQLTarget (S/filter/OSQLTarget.java): a record id, a list of them, a class; other forms are kept as
+  // text (the planner reports them unsupported)
+  void target(Statement &st) {
+    if (peek().kind == Tok::RID) {
+      st.target.rids.push_back(rid_of(next().v));
+    } else if (op("[")) {
+      ++i_;
+      while (!op("]")) {
+        Tok t = next();
+        if (t.kind != Tok::RID) fail(OMX_E_PARSE, "record id expected in the target list");
+        st.target.rids.push_back(rid_of(t.v));
+        if (op(",")) ++i_;
+      }
+      ++i_;
+    } else if (op("(")) {
+      int depth = 0;
+      do {
+        if (t_[i_].kind == Tok::END) fail(OMX_E_PARSE, "unbalanced parentheses in the target");
+        if (op("(")) ++depth;
+        if (op(")")) --depth;
+        st.target.other += t_[i_++].v + " ";
+      } while (depth > 0);
+    } else if (peek().kind == Tok::ID && op(":", 1)) {  // cluster:x, index:x, metadata:x
+      st.target.other = next().v;
+      st.target.other += ":" + (++i_, next().v);
+    } else if (peek().kind == Tok::ID) {
+      st.target.class_name = next().v;
+    } else {
+      fail(OMX_E_PARSE, "target expected after FROM");
+    }
   }
 
  private:
@@ -538,6 +668,6 @@ std::string expr_text(const ExprP &e) {
   return "";
 }
 
-std::unique_ptr<Statement> parse_match(const std::string &text) { return Parser(text).statement(); }
+std::unique_ptr<Statement> parse_statement(const std::string &text) { return Parser(text).statement(); }
 
 }  // namespace omx

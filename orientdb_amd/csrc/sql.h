@@ -92,16 +92,34 @@ struct ReturnItem {
   std::string raw;    // the item's tokens joined by spaces (string literals unquoted): its default alias
 };
 
+// FROM target of a legacy TRAVERSE / SELECT (S/filter/OSQLTarget.java): records by RID, or a class
+struct Target {
+  std::vector<std::pair<int64_t, int64_t>> rids;  // #c:p or [#c:p, ...], in the order written
+  std::string class_name;                         // FROM <class> (polymorphic)
+  std::string other;                              // anything else (sub-query, cluster:, index:): its text
+};
+
 struct Statement {
+  // MATCH (P/OMatchStatement.java); TRAVERSE (S/OCommandExecutorSQLTraverse.java:64-139);
+  // SELECT expand(<chain>) (S/OCommandExecutorSQLSelect.java, GF/OSQLFunctionMove.java:66-91)
+  enum Kind { MATCH, TRAVERSE, SELECT } kind = MATCH;
   std::vector<MatchExpression> expressions;
   std::vector<ReturnItem> returns;
   bool has_limit = false;
   int64_t limit = -1;
   int n_positional = 0;
+  // TRAVERSE / SELECT
+  Target target;
+  std::vector<ExprP> fields;  // TRAVERSE: the fields to traverse, as written; SELECT: the expand() argument
+  ExprP where;                // TRAVERSE: WHILE (or the deprecated WHERE); SELECT: WHERE
+  int max_depth = -1;         // TRAVERSE MAXDEPTH (-1: none)
+  bool breadth_first = false; // TRAVERSE STRATEGY BREADTH_FIRST (default DEPTH_FIRST, OTraverse.java)
+  std::string unsupported;    // a clause the device engine does not execute (reported by the planner)
 };
 
-// Parses a MATCH statement; throws OmxError(OMX_E_PARSE) on syntax errors.
-std::unique_ptr<Statement> parse_match(const std::string &text);
+// Parses a MATCH, TRAVERSE or SELECT statement; throws OmxError(OMX_E_PARSE) on syntax errors.
+std::unique_ptr<Statement> parse_statement(const std::string &text);
+inline std::unique_ptr<Statement> parse_match(const std::string &text) { return parse_statement(text); }
 
 // Canonical text of an expression (used for default return aliases and diagnostics).
 std::string expr_text(const ExprP &e);

@@ -226,7 +226,7 @@ class OMatchStatement:
         else:
             rs.rows = np.zeros((0, max(ncols, 0)), np.uint64)
         if documents and rs.rows.shape[0]:
-            if cols and cols[0] in ("$elements", "$pathElements"):
+            if cols and cols[0] in ("$elements", "$pathElements", "@rid"):  # records (also TRAVERSE / SELECT expand)
                 rs.extend(ORecordId.from_packed(x) for x in rs.rows[:, 0])
             else:
                 for row in rs.rows:
@@ -243,6 +243,22 @@ class OMatchStatement:
             self.free()
         except Exception:
             pass
+
+
+class OCommandExecutorSQLTraverse(OMatchStatement):
+    """`TRAVERSE <out|in|both>('L') FROM <rid|[rids]|class> [WHILE <cond>] [MAXDEPTH d] [LIMIT n]
+    STRATEGY BREADTH_FIRST` (S/OCommandExecutorSQLTraverse.java:64-139, C/command/traverse/OTraverse.java):
+    the records in the reference's emission order, as ORecordId. DEPTH_FIRST, `*`, several fields and
+    sub-query targets raise OmxUnsupported (the host keeps the reference executor for those)."""
+
+    KEYWORD_TRAVERSE = "TRAVERSE"
+
+
+class OCommandExecutorSQLSelectExpand(OMatchStatement):
+    """`SELECT expand(<out|in|both>('L')[.<out|in|both>('L')]*) FROM <target> [WHERE <cond>] [LIMIT n]`:
+    every call moves the whole list, duplicates and order kept (S/OSQLEngine.java:264-290)."""
+
+    KEYWORD_SELECT = "SELECT"
 
 
 class OCommandSQL:
@@ -264,8 +280,10 @@ class _BoundCommand:
 
     def execute(self, *args, **named):
         text = self.request.text.strip()
-        if not text[:5].upper() == OMatchStatement.KEYWORD_MATCH:
-            raise N.OmxUnsupported(N.OMX_E_UNSUPPORTED, "only MATCH statements run on the device engine")
+        word = text.split(None, 1)[0].upper() if text else ""
+        if word not in (OMatchStatement.KEYWORD_MATCH, OCommandExecutorSQLTraverse.KEYWORD_TRAVERSE,
+                        OCommandExecutorSQLSelectExpand.KEYWORD_SELECT):
+            raise N.OmxUnsupported(N.OMX_E_UNSUPPORTED, "only MATCH, TRAVERSE and SELECT expand() run on the device engine")
         st = OMatchStatement(text).setLimit(self._limit)
         try:
             return st.execute(self.db.snapshot, *args, **named)

@@ -154,7 +154,7 @@ KNOWN = [
      None, None, (1, None), True),
     ("testTriangleWithEdges4", 1028,
      "match {class:TriangleV, as: friend1}.outE('TriangleE').inV(){as: friend2, where: (uid = 1)}.outE('TriangleE').inV(){as: friend3},{class:TriangleV, as: friend1}.outE('TriangleE').inV(){as: friend3}return $matches",
-     None, None, (1, None), False),
+     None, None, (1, None), True),
     ("testCartesianProduct", 1048,
      "match {class:TriangleV, as: friend1, where:(uid = 1)},{class:TriangleV, as: friend2, where:(uid = 2 or uid = 3)}return $matches",
      None, ("uid_of", "friend1"), (2, {1}), True),

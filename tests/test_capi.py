@@ -33,6 +33,8 @@ def test_errors_are_reported():
     with pytest.raises(o.OmxParseError):
         o.OMatchStatement("match {class:Person, as: p return p")
     with pytest.raises(o.OmxParseError):
+        o.OMatchStatement("update V set x = 1")
+    with pytest.raises(o.OmxUnsupported):  # valid SQL the legacy executor keeps (only SELECT expand() is taken)
         o.OMatchStatement("select from V")
 
 

@@ -1,0 +1,188 @@
+"""TRAVERSE ... STRATEGY BREADTH_FIRST and SELECT expand(<chain>) on the device against the oracle
+(oracle/traverse_ref.py: the reference's OTraverse work list restated, pinned by OTraverseTest's golden
+orders in tests/test_traverse_oracle.py). Results are compared as ORDERED lists: emission order,
+repeats (MAXDEPTH level, expand chains) and LIMIT cut-offs included.
+"""
+import numpy as np
+import pytest
+
+from oracle.traverse_ref import BREADTH_FIRST, expand_chain, traverse
+from tests.test_gpu_parity import _parity, rmat10, rmat10_raw, rmat16  # noqa: F401  (fixtures)
+
+pytestmark = pytest.mark.gpu
+
+
+class _Adj:
+    def __init__(self, g):
+        from orientdb_amd.graph import csr_transpose
+        rp, col = g.csr
+        self.V = len(rp) - 1
+        self.rp, self.col = rp, col
+        self.irp, self.icol = csr_transpose(self.V, rp, col)
+        self.age = np.asarray(g.age)
+
+    def out(self, v):
+        return [int(x) for x in self.col[self.rp[v]:self.rp[v + 1]]]
+
+    def inn(self, v):
+        return [int(x) for x in self.icol[self.irp[v]:self.irp[v + 1]]]
+
+    def both(self, v):  # both('Knows'): the out_Knows list, then in_Knows (the edge set's part order)
+        return self.out(v) + self.inn(v)
+
+    def hubs(self, k):
+        deg = np.diff(self.rp)
+        return [int(x) for x in np.argsort(-deg, kind="stable")[:k]]
+
+
+@pytest.fixture(scope="module")
+def adj10(rmat10):
+    return _Adj(rmat10[0])
+
+
+def _rids(rs):
+    return [(int(r[0]), int(r[1])) for r in rs]
+
+
+def _want(vs):
+    return [(11, int(v)) for v in vs]
+
+
+def _run(g, q):
+    import orientdb_amd as o
+    return o.OMatchStatement(q).execute(g)
+
+
+def _check(g, q, want):
+    rs = _run(g, q)
+    got = _rids(rs)
+    assert len(got) == len(want)
+    assert got == _want(want)
+    return rs
+
+
+def test_traverse_depth_while(rmat10, adj10):
+    g, _ = rmat10
+    for r in adj10.hubs(3) + [5, 77]:
+        want = traverse([r], lambda v: [adj10.out(v)], predicate=lambda v, d: d < 3, strategy=BREADTH_FIRST)
+        _check(g, f"TRAVERSE out('Knows') FROM #11:{r} WHILE $depth < 3 STRATEGY BREADTH_FIRST", want)
+
+
+def test_traverse_unbounded_component(rmat10, adj10):
+    g, _ = rmat10
+    r = adj10.hubs(1)[0]
+    want = traverse([r], lambda v: [adj10.out(v)], strategy=BREADTH_FIRST)
+    rs = _check(g, f"TRAVERSE out('Knows') FROM #11:{r} STRATEGY BREADTH_FIRST", want)
+    assert len(want) > 100
+
+
+def test_traverse_maxdepth_repeats(rmat10, adj10):
+    g, _ = rmat10
+    r = adj10.hubs(2)[1]
+    want = traverse([r], lambda v: [adj10.out(v)], max_depth=2, strategy=BREADTH_FIRST)
+    assert len(want) > len(set(want))  # the MAXDEPTH level's repeats are exercised
+    _check(g, f"TRAVERSE out('Knows') FROM #11:{r} MAXDEPTH 2 STRATEGY BREADTH_FIRST", want)
+    want0 = traverse([r, r], lambda v: [adj10.out(v)], max_depth=0, strategy=BREADTH_FIRST)
+    _check(g, f"TRAVERSE out('Knows') FROM [#11:{r}, #11:{r}] MAXDEPTH 0 STRATEGY BREADTH_FIRST", want0)
+
+
+@pytest.mark.parametrize("limit", [1, 7, 50, 400])
+def test_traverse_limit(rmat10, adj10, limit):
+    g, _ = rmat10
+    r = adj10.hubs(1)[0]
+    want = traverse([r], lambda v: [adj10.out(v)], predicate=lambda v, d: d < 4, strategy=BREADTH_FIRST, limit=limit)
+    _check(g, f"TRAVERSE out('Knows') FROM #11:{r} WHILE $depth < 4 LIMIT {limit} STRATEGY BREADTH_FIRST", want)
+
+
+def test_traverse_property_while(rmat10, adj10):
+    g, _ = rmat10
+    age = adj10.age
+    for r in adj10.hubs(4):
+        want = traverse([r], lambda v: [adj10.out(v)], predicate=lambda v, d: bool(age[v] < 50),
+                        strategy=BREADTH_FIRST)
+        _check(g, f"TRAVERSE out('Knows') FROM #11:{r} WHILE age < 50 STRATEGY BREADTH_FIRST", want)
+    r = adj10.hubs(1)[0]
+    pred = lambda v, d: bool(d < 4 and age[v] > 20) or d == 0
+    want = traverse([r], lambda v: [adj10.out(v)], predicate=pred, strategy=BREADTH_FIRST)
+    _check(g, f"TRAVERSE out('Knows') FROM #11:{r} WHILE ($depth < 4 and age > 20) or $depth = 0 "
+              "STRATEGY BREADTH_FIRST", want)
+
+
+def test_traverse_target_list(rmat10, adj10):
+    g, _ = rmat10
+    h = adj10.hubs(2)
+    roots = [h[0], h[0], 9, h[1]]
+    want = traverse(roots, lambda v: [adj10.out(v)], max_depth=1, strategy=BREADTH_FIRST)
+    _check(g, f"TRAVERSE out('Knows') FROM [#11:{h[0]}, #11:{h[0]}, #11:9, #11:999999, #12:0, #11:{h[1]}] "
+              "MAXDEPTH 1 STRATEGY BREADTH_FIRST", want)
+
+
+def test_traverse_directions(rmat10, adj10):
+    g, _ = rmat10
+    r = adj10.hubs(3)[2]
+    want = traverse([r], lambda v: [adj10.inn(v)], predicate=lambda v, d: d < 3, strategy=BREADTH_FIRST)
+    _check(g, f"TRAVERSE in('Knows') FROM #11:{r} WHILE $depth < 3 STRATEGY BREADTH_FIRST", want)
+    want = traverse([r], lambda v: [adj10.both(v)], predicate=lambda v, d: d < 2, strategy=BREADTH_FIRST)
+    _check(g, f"TRAVERSE both('Knows') FROM #11:{r} WHILE $depth < 2 STRATEGY BREADTH_FIRST", want)
+
+
+def test_traverse_class_target(rmat10, adj10):
+    g, _ = rmat10
+    want = traverse(list(range(adj10.V)), lambda v: [adj10.out(v)], max_depth=1, strategy=BREADTH_FIRST)
+    _check(g, "TRAVERSE out('Knows') FROM Person MAXDEPTH 1 STRATEGY BREADTH_FIRST", want)
+    want = traverse(list(range(adj10.V)), lambda v: [adj10.out(v)], strategy=BREADTH_FIRST, limit=300)
+    _check(g, "TRAVERSE out('Knows') FROM Person LIMIT 300 STRATEGY BREADTH_FIRST", want)
+
+
+def test_traverse_multigraph(rmat10_raw):
+    g, _ = rmat10_raw
+    a = _Adj(g)
+    r = a.hubs(1)[0]
+    want = traverse([r], lambda v: [a.out(v)], max_depth=2, strategy=BREADTH_FIRST)
+    _check(g, f"TRAVERSE out('Knows') FROM #11:{r} MAXDEPTH 2 STRATEGY BREADTH_FIRST", want)
+    want = traverse([r], lambda v: [a.both(v)], predicate=lambda v, d: d < 3, strategy=BREADTH_FIRST)
+    _check(g, f"TRAVERSE both('Knows') FROM #11:{r} WHILE $depth < 3 STRATEGY BREADTH_FIRST", want)
+
+
+def test_traverse_rmat16_component(rmat16):
+    g, _ = rmat16
+    a = _Adj(g)
+    r = a.hubs(1)[0]
+    want = traverse([r], lambda v: [a.out(v)], strategy=BREADTH_FIRST)
+    rs = _check(g, f"TRAVERSE out('Knows') FROM #11:{r} STRATEGY BREADTH_FIRST", want)
+    assert len(want) > 10000
+    assert rs.info["edges_traversed"] == sum(len(a.out(v)) for v in want)
+
+
+def test_select_expand_chains(rmat10, adj10):
+    g, _ = rmat10
+    h = adj10.hubs(3)
+    for r in h + [3]:
+        want = expand_chain([r], [adj10.out, adj10.out])
+        _check(g, f"SELECT expand(out('Knows').out('Knows')) FROM #11:{r}", want)
+    want = expand_chain([h[0]], [adj10.out, adj10.inn, adj10.out])
+    _check(g, f"SELECT expand(out('Knows').in('Knows').out('Knows')) FROM #11:{h[0]} LIMIT 100000", want[:100000])
+    want = expand_chain([h[1], h[1]], [adj10.both])
+    _check(g, f"SELECT expand(both('Knows')) FROM [#11:{h[1]}, #11:{h[1]}]", want)
+
+
+def test_select_expand_where_and_edges(rmat10, adj10):
+    g, _ = rmat10
+    roots = [v for v in range(adj10.V) if v < 40 and adj10.age[v] < 60]
+    want = expand_chain(roots, [adj10.out])
+    _check(g, "SELECT expand(outE('Knows').inV()) FROM Person WHERE uid < 40 and age < 60", want)
+    want = expand_chain(roots, [adj10.out, adj10.out])[:77]
+    _check(g, "SELECT expand(out('Knows').outE('Knows').inV()) FROM Person WHERE uid < 40 and age < 60 LIMIT 77", want)
+
+
+def test_match_edge_steps(rmat10):
+    """`outE('L').inV()` MATCH items (testTriangleWithEdges4's form) are out('L') with the edge
+    multiplicity, which the distinct rows absorb: the oracle of the out() form pins them."""
+    g, ref = rmat10
+    q_edges = "MATCH {class:Person,as:a,where:(uid < 30)}.outE('Knows').inV(){as:b}.inE('Knows').outV(){as:c} RETURN a, b, c"
+    q_moves = "MATCH {class:Person,as:a,where:(uid < 30)}.out('Knows'){as:b}.in('Knows'){as:c} RETURN a, b, c"
+    import orientdb_amd as o
+    want = ref.expected(q_moves, ["a", "b", "c"])
+    rs = o.OMatchStatement(q_edges).execute(g)
+    assert rs.info["n_rows"] == len(want)
+    assert {tuple(int(x) for x in row) for row in rs.rows} == want
