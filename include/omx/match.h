@@ -271,6 +271,26 @@ typedef struct omx_index_rec {
 } omx_index_rec;
 int omx_graph_create_blob(const void *blob, uint64_t size, omx_graph **out);
 
+/* ---- ridbag ingest ------------------------------------------------------------------------------
+ * Decodes, on `device`, the vertices' serialized out_<L> (or in_<L>) ridbag fields into one CSR of dense
+ * vertex ids, each bag's entry order kept (the reference's iteration order). Replaces iterating
+ * ORidBag.rawIterator per vertex on the Java side (C/db/record/ridbag/ORidBag.java:160) when a snapshot
+ * is built from the stored records. Stream format (ORidBag.toStream, ORidBag.java:198-276;
+ * OEmbeddedRidBag.serialize, .../ridbag/embedded/OEmbeddedRidBag.java:424-460; big-endian):
+ *   [1 B config: bit 0 embedded, bit 1 UUID][16 B UUID if bit 1][int32 count][count × (int16 cluster,
+ *   int64 position)]
+ * streams: the vertices' streams concatenated; vertex v's is [offsets[v], offsets[v+1]) (empty: no
+ * field). vertex_rids[V]: every vertex's packed RID (dense order). Lightweight edges: the entries are
+ * vertex RIDs (edge_rids = edge_targets = NULL). Edge records: the entries are edge RIDs and
+ * edge_targets[i] is the opposite vertex RID of edge record edge_rids[i] (its `in` field for out_
+ * bags, `out` for in_ bags). Fills row_ptr[V+1] (may be NULL) and *n_entries; col[*n_entries] when
+ * col != NULL (call once with col = NULL to size it). OMX_E_INVALID: malformed stream, an SBTree
+ * (non-embedded) bag, or an entry that resolves to no vertex. */
+int omx_ridbag_decode_csr(int32_t device, const uint8_t *streams, uint64_t stream_bytes, const uint64_t *offsets,
+                          uint32_t n_vertices, const uint64_t *vertex_rids, const uint64_t *edge_rids,
+                          const uint64_t *edge_targets, uint64_t n_edge_records, uint64_t *row_ptr, uint32_t *col,
+                          uint64_t *n_entries);
+
 /* Parameters as one buffer: uint32_t n, uint32_t reserved, omx_param_rec[n], then the strings. */
 typedef struct omx_param_rec {
   int32_t type, index;       /* OMX_VAL_*, positional index (when name_off == 0)                       */

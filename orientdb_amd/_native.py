@@ -116,6 +116,10 @@ SIGNATURES = {
     "omx_comm_rank": (C.c_int32, [C.c_void_p]),
     "omx_comm_world": (C.c_int32, [C.c_void_p]),
     "omx_comm_destroy": (None, [C.c_void_p]),
+    "omx_ridbag_decode_csr": (C.c_int, [C.c_int32, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32,
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                        C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
+                                        C.POINTER(C.c_uint64)]),
 }
 OMX_COMM_ID_BYTES = 128
 

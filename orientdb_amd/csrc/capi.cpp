@@ -407,6 +407,16 @@ int omx_result_cell(const omx_result *r, uint64_t row, int32_t col, omx_cell *ou
   return OMX_OK;
 }
 
+int omx_ridbag_decode_csr(int32_t device, const uint8_t *streams, uint64_t stream_bytes, const uint64_t *offsets,
+                          uint32_t n_vertices, const uint64_t *vertex_rids, const uint64_t *edge_rids,
+                          const uint64_t *edge_targets, uint64_t n_edge_records, uint64_t *row_ptr, uint32_t *col,
+                          uint64_t *n_entries) {
+  return guard([&] {
+    omx::ridbag_decode_csr(device, streams, stream_bytes, offsets, n_vertices, vertex_rids, edge_rids, edge_targets,
+                           n_edge_records, row_ptr, col, n_entries);
+  });
+}
+
 const char *omx_last_error(void) { return g_last_error.c_str(); }
 
 const char *omx_version(void) { return "omx 0.1 (gfx950)"; }

@@ -184,7 +184,9 @@ class Executor {
     std::vector<DBuf<uint32_t>> chain_out;
     if (chain) {
       if (dist_ || o_.shard_world > 1) unsupported("TRAVERSE / SELECT expand() on a partitioned or sharded execution");
-      chain_out.push_back(p_.kind == Plan::TRAVERSE ? traverse_bfs() : select_expand());
+      chain_out.push_back(p_.kind == Plan::TRAVERSE ? traverse_bfs()
+                          : p_.kind == Plan::SELECT ? select_expand()
+                                                    : shortest_path());
     } else if (!empty) {
       // a partitioned run keeps stepping with no local rows: every rank takes part in every exchange
       for (size_t i = 0; i < p_.steps.size() && (R_ > 0 || dist_); ++i) {
@@ -232,8 +234,32 @@ class Executor {
     std::vector<DBuf<uint32_t>> out;
     // partitioned + distinct projection: equal tuples meet on one rank first
     if (dist_ && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
-    const bool docs = p_.proj == Plan::PROJ_EXPR || p_.proj == Plan::PROJ_JSON;
-    if (chain) {  // the records in emission order (duplicates are the reference's: not de-duplicated)
+    const bool sp_doc = p_.kind == Plan::SHORTEST_PATH && !p_.chain.expand_rows;
+    const bool docs = p_.proj == Plan::PROJ_EXPR || p_.proj == Plan::PROJ_JSON || sp_doc;
+    if (sp_doc) {  // SELECT shortestPath(...): one document whose field is the list of the path's RIDs
+      HVal list;
+      list.k = HVal::LIST;
+      std::vector<uint64_t> rids(R_);
+      if (R_) {
+        DBuf<uint64_t> d(&pool_, R_);
+        const uint32_t *cp = chain_out[0].p;
+        launch_map_rids(1, &cp, R_, g_.d_rids, d.p, g_.V, s_);
+        HIP_CHECK(hipMemcpyAsync(rids.data(), d.p, R_ * 8, hipMemcpyDeviceToHost, s_));
+        HIP_CHECK(hipStreamSynchronize(s_));
+      }
+      list.json = "[";
+      for (uint64_t i = 0; i < R_; ++i) {
+        HVal r;
+        r.k = HVal::RID;
+        r.rid = rids[i];
+        list.items.push_back(r);
+        list.json += (i ? ",\"#" : "\"#") + std::to_string(rids[i] >> 48) + ":" + std::to_string(rids[i] & ((1ull << 48) - 1)) + "\"";
+      }
+      list.json += "]";
+      res->docs.push_back(Document{list});
+      n = 1;
+      ncols = 1;
+    } else if (chain) {  // the records in emission order (duplicates are the reference's: not de-duplicated)
       n = R_;
       ncols = 1;
       out = std::move(chain_out);
@@ -1384,6 +1410,133 @@ class Executor {
     bindings_ = n;
     R_ = limit > 0 ? std::min<uint64_t>(n, (uint64_t)limit) : n;
     return cur;
+  }
+
+  // shortestPath(src, dst, direction, edge class, {maxDepth}) — OSQLFunctionShortestPath.execute
+  // (GF/OSQLFunctionShortestPath.java:85-200): a bidirectional BFS from both ends, each round walking the
+  // side with the shorter queue one whole level first (walkLeft / walkRight :232-292). A walk scans its
+  // queue in order and every queue entry's neighbours in order; the first neighbour the other side has
+  // visited ends the search (computePath :294-313: previouses back to the source, nexts on to the
+  // destination); otherwise a neighbour not yet visited on this side is remembered with the entry that
+  // discovered it first and queued, in discovery order.
+  struct SpSide {
+    DBuf<uint32_t> queue, parent;
+    DBuf<uint64_t> visited;
+    uint64_t n = 0;
+    const AdjSpec *adj = nullptr;
+  };
+  bool sp_walk(SpSide &A, SpSide &B, DBuf<uint32_t> &first, uint32_t *meet_w, uint32_t *meet_cur) {
+    if (!A.n) return false;
+    if (A.n >= UINT32_MAX) unsupported("a shortestPath() level of 2^32 or more vertices");
+    DBuf<uint32_t> rows(&pool_, A.n);
+    launch_iota(rows.p, A.n, s_);
+    ExpandOut o = expand_core(A.queue.p, A.n, *A.adj, nullptr, {rows.p}, true, false, nullptr, nullptr, nullptr, nullptr, true);
+    edges_ += o.E;
+    edges_iter_ += o.E;
+    if (!o.n) {
+      A.n = 0;
+      return false;
+    }
+    if (o.n >= UINT32_MAX) unsupported("a shortestPath() level of 2^32 or more neighbours");
+    DBuf<unsigned long long> pos(&pool_, 1);
+    HIP_CHECK(hipMemsetAsync(pos.p, 0xFF, 8, s_));
+    launch_sp_meet(o.dst.p, o.n, B.visited.p, pos.p, s_);
+    const uint64_t e = read1(reinterpret_cast<const uint64_t *>(pos.p));
+    if (e != ~0ull) {
+      *meet_w = read1(o.dst.p + e);
+      *meet_cur = read1(A.queue.p + read1(o.carry[0].p + e));
+      return true;
+    }
+    DBuf<uint8_t> flags(&pool_, o.n);
+    launch_trav_filter(o.dst.p, o.n, A.visited.p, nullptr, first.p, flags.p, true, s_);
+    DBuf<uint64_t> keys(&pool_, o.n), sel(&pool_, o.n), nsel(&pool_, 1);
+    launch_pack_pairs(o.carry[0].p, o.dst.p, o.n, keys.p, s_);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, keys.p, flags.p, sel.p, nsel.p, (int64_t)o.n, s_); });
+    const uint64_t k = read1(nsel.p);
+    DBuf<uint32_t> next(&pool_, std::max<uint64_t>(k, 1));
+    launch_sp_accept(sel.p, k, A.queue.p, A.parent.p, A.visited.p, first.p, next.p, s_);
+    A.queue = std::move(next);
+    A.n = k;
+    return false;
+  }
+
+  DBuf<uint32_t> shortest_path() {
+    const ChainSpec &c = p_.chain;
+    DBuf<uint64_t> keys(&pool_, 2);
+    DBuf<uint32_t> ids(&pool_, 2);
+    const uint64_t hk[2] = {c.sp_src, c.sp_dst};
+    HIP_CHECK(hipMemcpyAsync(keys.p, hk, 16, hipMemcpyHostToDevice, s_));
+    launch_fill_u32(ids.p, 2, UINT32_MAX, s_);
+    launch_find_rids(g_.d_rids, g_.V, keys.p, 2, ids.p, s_);
+    uint32_t h[2];
+    HIP_CHECK(hipMemcpyAsync(h, ids.p, 8, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    for (int i = 0; i < 2; ++i)
+      if (h[i] == UINT32_MAX)  // graph.getVertex(...) is null: the reference fails on it
+        fail(OMX_E_EXECUTION, std::string("shortestPath(): ") + (i ? "destination" : "source") + " vertex #" +
+                                  std::to_string(hk[i] >> 48) + ":" + std::to_string(hk[i] & ((1ull << 48) - 1)) + " not found");
+    std::vector<uint32_t> path;
+    if (h[0] == h[1]) {
+      path.push_back(h[0]);
+    } else {
+      SpSide L, R;
+      const uint64_t W = std::max<uint64_t>(nwords_, 1);
+      for (SpSide *x : {&L, &R}) {
+        x->visited = DBuf<uint64_t>(&pool_, W);
+        x->parent = DBuf<uint32_t>(&pool_, g_.V);
+        x->queue = DBuf<uint32_t>(&pool_, 1);
+        x->n = 1;
+        HIP_CHECK(hipMemsetAsync(x->visited.p, 0, W * 8, s_));
+        launch_fill_u32(x->parent.p, g_.V, UINT32_MAX, s_);
+      }
+      L.adj = &c.sp_left;
+      R.adj = &c.sp_right;
+      launch_fill_u32(L.queue.p, 1, h[0], s_);
+      launch_fill_u32(R.queue.p, 1, h[1], s_);
+      launch_mark_bitmap(L.queue.p, 1, L.visited.p, g_.V, s_);
+      launch_mark_bitmap(R.queue.p, 1, R.visited.p, g_.V, s_);
+      DBuf<uint32_t> first(&pool_, g_.V);
+      launch_fill_u32(first.p, g_.V, UINT32_MAX, s_);
+      const int maxd = c.sp_max_depth;
+      bool met = false, met_left = false;
+      uint32_t mw = 0, mc = 0;
+      for (int depth = 1;;) {
+        if (maxd >= 0 && maxd <= depth) break;
+        if (!L.n || !R.n) break;
+        const bool left_first = L.n <= R.n;
+        SpSide &A = left_first ? L : R, &B = left_first ? R : L;
+        if (sp_walk(A, B, first, &mw, &mc)) {
+          met = true;
+          met_left = left_first;
+          break;
+        }
+        ++depth;
+        if (maxd >= 0 && maxd <= depth) break;
+        if (!A.n) break;
+        if (sp_walk(B, A, first, &mw, &mc)) {
+          met = true;
+          met_left = !left_first;
+          break;
+        }
+        ++depth;
+      }
+      if (met) {  // computePath: previouses back from the meeting vertex, then its nexts
+        path.push_back(mw);
+        for (uint32_t x = met_left ? mc : read1(L.parent.p + mw); x != UINT32_MAX; x = read1(L.parent.p + x))
+          path.insert(path.begin(), x);
+        for (uint32_t x = met_left ? read1(R.parent.p + mw) : mc; x != UINT32_MAX; x = read1(R.parent.p + x))
+          path.push_back(x);
+      }
+    }
+    const int64_t limit = chain_limit();
+    bindings_ = path.size();
+    R_ = limit > 0 && c.expand_rows ? std::min<uint64_t>(path.size(), (uint64_t)limit) : path.size();
+    DBuf<uint32_t> out(&pool_, std::max<size_t>(path.size(), 1));
+    if (!path.empty()) {
+      HIP_CHECK(hipMemcpyAsync(out.p, path.data(), path.size() * 4, hipMemcpyHostToDevice, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));  // the host vector goes out of scope
+    }
+    return out;
   }
 
   // WHERE conjunct `$matched.X op $currentMatch` of the alias the previous step bound

@@ -169,5 +169,9 @@ struct Graph {
 };
 
 Graph *graph_create(const omx_graph_desc *d);
+// ridbag.hip: omx_ridbag_decode_csr
+void ridbag_decode_csr(int device, const uint8_t *streams, uint64_t nbytes, const uint64_t *offsets, uint32_t V,
+                       const uint64_t *vertex_rids, const uint64_t *edge_rids, const uint64_t *edge_targets,
+                       uint64_t nedges, uint64_t *row_ptr, uint32_t *col, uint64_t *n_entries);
 
 }  // namespace omx

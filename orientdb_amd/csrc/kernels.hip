@@ -2201,6 +2201,38 @@ void launch_trav_accept(const uint32_t *w, uint64_t n, uint64_t *hist, uint32_t 
   KCHECK("k_trav_accept");
 }
 
+// ---- shortestPath (exec.hip Executor::shortest_path) -------------------------------------------------
+// *pos = the first work-list position whose vertex the other side has visited
+__global__ void k_sp_meet(const uint32_t *w, uint64_t n, const uint64_t *other, unsigned long long *pos) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool hit = e < n && ((other[w[e] >> 6] >> (w[e] & 63)) & 1);
+  const uint64_t b = __ballot(hit);
+  if (b && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)b) - 1)) atomicMin(pos, (unsigned long long)e);
+}
+void launch_sp_meet(const uint32_t *w, uint64_t n, const uint64_t *other, unsigned long long *pos, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_sp_meet, dim3(nblocks(n, 256)), dim3(256), 0, s, w, n, other, pos);
+  KCHECK("k_sp_meet");
+}
+// the level's first discoveries (row << 32 | vertex, in discovery order): previous / next of the vertex
+// = the queue entry that discovered it, the vertex joins the side's visited set and its next queue
+__global__ void k_sp_accept(const uint64_t *keys, uint64_t n, const uint32_t *queue, uint32_t *parent, uint64_t *visited,
+                            uint32_t *first, uint32_t *next) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint32_t v = (uint32_t)keys[e], row = (uint32_t)(keys[e] >> 32);
+  parent[v] = queue[row];
+  atomicOr((unsigned long long *)&visited[v >> 6], 1ull << (v & 63));
+  first[v] = 0xFFFFFFFFu;
+  next[e] = v;
+}
+void launch_sp_accept(const uint64_t *keys, uint64_t n, const uint32_t *queue, uint32_t *parent, uint64_t *visited,
+                      uint32_t *first, uint32_t *next, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_sp_accept, dim3(nblocks(n, 256)), dim3(256), 0, s, keys, n, queue, parent, visited, first, next);
+  KCHECK("k_sp_accept");
+}
+
 __global__ void k_fill_u32(uint32_t *out, uint64_t n, uint32_t x) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = x;

@@ -109,6 +109,7 @@ class Planner {
     Plan &p = *plan_;
     const bool trav = st_.kind == Statement::TRAVERSE;
     p.kind = trav ? Plan::TRAVERSE : Plan::SELECT;
+    if (!trav && st_.fields[0]->kind == Expr::CALL && ieq(st_.fields[0]->name, "shortestPath")) p.kind = Plan::SHORTEST_PATH;
     p.out_names = {"@rid"};
     p.limit = st_.has_limit ? st_.limit : -1;
     if (logical_only) return std::move(plan_);
@@ -142,9 +143,13 @@ class Planner {
       c.hops.push_back(cat);
       c.pred_prog = add_prog(st_.where, true);
       c.max_depth = st_.max_depth;
+    } else if (st_.fields[0]->kind == Expr::CALL && ieq(st_.fields[0]->name, "shortestPath")) {
+      compile_shortest_path(st_.fields[0]);
     } else {
       // expand(f0(...).f1(...)...): every call moves the whole list (OSQLEngine.foreachRecord keeps the
       // order and the duplicates); outE('L').inV() / inE('L').outV() pairs are one hop
+      if (!st_.expand) unsupported("a SELECT projection other than shortestPath()");
+      if (t.rids.empty() && t.class_name.empty()) unsupported("SELECT expand() without a FROM target");
       const ExprP &x = st_.fields[0];
       std::vector<std::pair<std::string, std::vector<ExprP>>> calls;
       if (x->kind == Expr::CALL) {
@@ -176,6 +181,75 @@ class Planner {
   }
 
  private:
+  // a record argument: a RID literal, or a string / parameter holding "#c:p" (graph.getVertex(Object))
+  uint64_t rid_arg(const ExprP &e, const char *what) const {
+    if (e->kind == Expr::RID) return (uint64_t)e->value.i;
+    auto v = fold(e);
+    if (v && v->kind == Value::STR) {
+      const std::string &x = v->s;
+      const size_t c = x.find(':');
+      if (!x.empty() && x[0] == '#' && c != std::string::npos) {
+        char *e1 = nullptr, *e2 = nullptr;
+        const long long cl = std::strtoll(x.c_str() + 1, &e1, 10), pos = std::strtoll(x.c_str() + c + 1, &e2, 10);
+        if (e1 == x.c_str() + c && e2 && *e2 == 0 && cl >= 0 && pos >= 0) return ((uint64_t)cl << 48) | (uint64_t)pos;
+      }
+    }
+    unsupported(std::string("shortestPath() ") + what + " " + expr_text(e) + " (a record id on the device)");
+  }
+
+  // shortestPath(<source>, <destination>[, <direction>[, <edge class>[, {maxDepth: n}]]]): the
+  // bidirectional BFS of OSQLFunctionShortestPath.execute (GF/OSQLFunctionShortestPath.java:85-200)
+  void compile_shortest_path(const ExprP &f) {
+    Plan &p = *plan_;
+    p.kind = Plan::SHORTEST_PATH;
+    ChainSpec &c = p.chain;
+    c.expand_rows = st_.expand;
+    if (!st_.expand) p.out_names = {st_.alias.empty() ? std::string("shortestPath") : st_.alias};
+    const Target &t = st_.target;
+    if (!t.rids.empty() || !t.class_name.empty() || !t.other.empty())
+      unsupported("shortestPath() evaluated per record of a FROM target");
+    const auto &a = f->kids;
+    if (a.size() < 2 || a.size() > 5) fail(OMX_E_PARSE, "Syntax error: shortestPath(<sourceVertex>, <destinationVertex>, [<direction>, [ <edgeTypeAsString> ]])");
+    c.sp_src = rid_arg(a[0], "source");
+    c.sp_dst = rid_arg(a[1], "destination");
+    std::string left = "both";
+    if (a.size() > 2) {
+      auto v = fold(a[2]);
+      if (!v) unsupported("non-constant shortestPath() direction");
+      if (v->kind != Value::NUL) {  // Direction.valueOf(toUpperCase): OUT / IN / BOTH
+        if (v->kind != Value::STR) fail(OMX_E_EXECUTION, "No enum constant for direction " + expr_text(a[2]));
+        left = lower(v->s);
+        if (left != "out" && left != "in" && left != "both")
+          fail(OMX_E_EXECUTION, "No enum constant com.tinkerpop.blueprints.Direction." + v->s);
+      }
+    }
+    const std::string right = left == "out" ? "in" : left == "in" ? "out" : "both";
+    std::vector<std::string> labels;
+    if (a.size() > 3) {
+      auto v = fold(a[3]);
+      if (!v) unsupported("non-constant shortestPath() edge class");
+      if (v->kind == Value::STR) labels.push_back(v->s);
+      else if (v->kind != Value::NUL) labels.push_back(expr_text(a[3]));
+    }
+    c.sp_left = adjacency(left, labels);
+    c.sp_right = adjacency(right, labels);
+    if (a.size() > 4 && a[4]->kind == Expr::JSON) {  // bindAdditionalParams: {maxDepth: n}
+      for (size_t i = 0; i < a[4]->json_keys.size(); ++i)
+        if (a[4]->json_keys[i] == "maxDepth") {
+          auto v = fold(a[4]->kids[i]);
+          if (v && v->kind == Value::INT) c.sp_max_depth = (int)v->i;
+          else if (v && v->kind == Value::DBL) c.sp_max_depth = (int)v->d;
+          else if (v && v->kind == Value::STR) {
+            char *e = nullptr;
+            const long x = std::strtol(v->s.c_str(), &e, 10);
+            if (e && *e == 0 && !v->s.empty()) c.sp_max_depth = (int)x;
+          }
+        }
+    } else if (a.size() > 4 && !(fold(a[4]) && fold(a[4])->kind == Value::NUL)) {
+      unsupported("shortestPath() additional parameters other than a {maxDepth: n} map");
+    }
+  }
+
   std::vector<std::string> labels_of(const std::vector<ExprP> &args) const {
     std::vector<std::string> labels;
     for (auto &a : args) {
@@ -1225,7 +1299,8 @@ std::unique_ptr<Plan> build_plan(const Statement &st, const Graph &g, const Para
 
 std::string plan_json(const Plan &p, const std::string &reason) {
   std::ostringstream o;
-  o << "{\"kind\":" << jstr(p.kind == Plan::MATCH ? "MATCH" : p.kind == Plan::TRAVERSE ? "TRAVERSE" : "SELECT");
+  o << "{\"kind\":"
+    << jstr(p.kind == Plan::MATCH ? "MATCH" : p.kind == Plan::TRAVERSE ? "TRAVERSE" : p.kind == Plan::SELECT ? "SELECT" : "SHORTEST_PATH");
   o << ",\"aliases\":[";
   for (size_t i = 0; i < p.aliases.size(); ++i) o << (i ? "," : "") << jstr(p.aliases[i]);
   o << "],\"estimates\":{";

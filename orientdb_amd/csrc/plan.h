@@ -92,11 +92,16 @@ struct ChainSpec {
   int max_depth = -1;       // TRAVERSE MAXDEPTH
   int root_class = -1;      // FROM <class>: its vertices (polymorphic) in snapshot order
   std::vector<uint64_t> root_rids;  // FROM #c:p / [#c:p, ...] (packed c << 48 | p), in the order written
+  // shortestPath(src, dst[, direction[, edge class[, {maxDepth: n}]]]) (GF/OSQLFunctionShortestPath.java)
+  uint64_t sp_src = 0, sp_dst = 0;  // packed RIDs
+  AdjSpec sp_left, sp_right;        // the source side's direction and the destination side's opposite
+  int sp_max_depth = -1;            // -1: none
+  bool expand_rows = true;          // expand(shortestPath(...)): one row per vertex; else one document
 };
 
 struct Plan {
-  enum Kind { MATCH, TRAVERSE, SELECT } kind = MATCH;
-  ChainSpec chain;  // TRAVERSE / SELECT
+  enum Kind { MATCH, TRAVERSE, SELECT, SHORTEST_PATH } kind = MATCH;
+  ChainSpec chain;  // TRAVERSE / SELECT / SHORTEST_PATH
   // logical plan (what the reference computes; also reported by omx_statement_explain)
   std::vector<std::string> aliases;  // pattern nodes, insertion order (Pattern.aliasToNode)
   std::vector<bool> explicit_alias;

@@ -202,18 +202,37 @@ class Parser {
     return st;
   }
 
-  // SELECT expand(<chain>) FROM <target> [WHERE <cond>] [LIMIT n]: the rows of the expanded chain
-  // (other SELECT forms are the legacy SQL executor's and stay there)
+  // SELECT expand(<chain>) FROM <target> [WHERE <cond>] [LIMIT n]: the rows of the expanded chain;
+  // SELECT shortestPath(...) [AS a] / SELECT expand(shortestPath(...)) (no FROM). Other SELECT forms are
+  // the legacy SQL executor's and stay there.
   std::unique_ptr<Statement> select() {
     ++i_;
     auto st = std::make_unique<Statement>();
     st->kind = Statement::SELECT;
-    if (!kw("expand") || !op("(", 1)) fail(OMX_E_UNSUPPORTED, "SELECT without expand(): the legacy SQL executor's");
-    ++i_;
-    expect("(");
-    st->fields.push_back(expr());
-    expect(")");
-    if (!kw("from")) fail(OMX_E_UNSUPPORTED, "SELECT expand(...) with more projections or no FROM");
+    if (kw("expand") && op("(", 1)) {
+      ++i_;
+      expect("(");
+      st->fields.push_back(expr());
+      expect(")");
+    } else if (kw("shortestPath") && op("(", 1)) {
+      st->expand = false;
+      st->fields.push_back(expr());
+      if (kw("as")) {
+        ++i_;
+        st->alias = next().v;
+      }
+    } else {
+      fail(OMX_E_UNSUPPORTED, "SELECT without expand() or shortestPath(): the legacy SQL executor's");
+    }
+    if (op(",")) fail(OMX_E_UNSUPPORTED, "SELECT with several projections on the device");
+    if (!kw("from")) {
+      if (t_[i_].kind != Tok::END && !kw("limit")) fail(OMX_E_UNSUPPORTED, "SELECT clause '" + t_[i_].v + "' on the device");
+      st->target.other = "";
+      if (kw("limit")) limit(*st);
+      if (t_[i_].kind != Tok::END) fail(OMX_E_UNSUPPORTED, "SELECT clause '" + t_[i_].v + "' on the device");
+      st->n_positional = nparam_;
+      return st;
+    }
     ++i_;
     target(*st);
     if (kw("where")) {
@@ -440,6 +459,8 @@ class Parser {
       c->kids.push_back(expr());
       return c;
     }
+    // a parenthesised condition is already boolean: `(a and b) or c`
+    if (l->kind == Expr::OR || l->kind == Expr::AND || l->kind == Expr::NOT || l->kind == Expr::CMP) return l;
     auto tr = mk(Expr::TRUTH);
     tr->kids.push_back(l);
     return tr;
@@ -565,6 +586,13 @@ class Parser {
       if (e->kind == Expr::TRUTH) return e->kids[0];  // a parenthesised value
       return e;
     }
+    if (t.kind == Tok::RID) {
+      auto e = mk(Expr::RID);
+      const auto r = rid_of(t.v);
+      e->value = Value::Int((int64_t)(((uint64_t)r.first << 48) | ((uint64_t)r.second & ((1ull << 48) - 1))));
+      e->name = "#" + t.v;
+      return e;
+    }
     if (t.kind == Tok::OP && t.v == "?") {
       auto e = mk(Expr::PARAM);
       e->param_index = nparam_++;
@@ -664,6 +692,7 @@ std::string expr_text(const ExprP &e) {
     case Expr::NOT: return "not " + expr_text(e->kids[0]);
     case Expr::CMP: return expr_text(e->kids[0]) + " " + e->name + " " + expr_text(e->kids[1]);
     case Expr::TRUTH: return expr_text(e->kids[0]);
+    case Expr::RID: return e->name;
   }
   return "";
 }

@@ -51,6 +51,7 @@ struct Expr {
     OR, AND, NOT,
     CMP,    // op = == != <> < <= > >= ; kids[0], kids[1]
     TRUTH,  // boolean value of kids[0]
+    RID,    // record id literal #c:p: value.i = (c << 48) | p
   } kind;
   Value value;
   std::string name;  // FIELD/VAR/CALL name, PARAM name, MATH/CMP operator
@@ -114,6 +115,8 @@ struct Statement {
   ExprP where;                // TRAVERSE: WHILE (or the deprecated WHERE); SELECT: WHERE
   int max_depth = -1;         // TRAVERSE MAXDEPTH (-1: none)
   bool breadth_first = false; // TRAVERSE STRATEGY BREADTH_FIRST (default DEPTH_FIRST, OTraverse.java)
+  bool expand = true;         // SELECT: expand(fields[0]) (rows) or the projection fields[0] [AS alias]
+  std::string alias;          // SELECT projection alias ("" = the default)
   std::string unsupported;    // a clause the device engine does not execute (reported by the planner)
 };
 

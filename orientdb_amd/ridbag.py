@@ -1,0 +1,50 @@
+"""Ridbag ingest: the vertices' serialized out_<L> / in_<L> fields → a CSR, decoded on the device.
+
+Mirrors what building a snapshot from stored records needs instead of iterating every vertex's
+ORidBag (C/db/record/ridbag/ORidBag.java:160 rawIterator) in Java: the record bytes of the bags go to
+the device as they are (ORidBag.toStream, ORidBag.java:198-276; OEmbeddedRidBag.serialize,
+.../ridbag/embedded/OEmbeddedRidBag.java:424-460) and come back as row pointers + dense vertex ids
+(include/omx/match.h omx_ridbag_decode_csr).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+
+
+def _u64p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint64)) if a is not None else None
+
+
+def decode_ridbags(streams, vertex_rids, edge_rids=None, edge_targets=None, device=0):
+    """streams: one bytes object per vertex (b"" = the vertex has no such field), in dense vertex order.
+    vertex_rids: packed RID of every vertex. edge_rids / edge_targets: for regular (non-lightweight)
+    edges, every edge record's RID and the packed RID of its opposite vertex. Returns (row_ptr u64[V+1],
+    col u32[E]) with each bag's order kept."""
+    V = len(streams)
+    offs = np.zeros(V + 1, np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in streams], dtype=np.uint64)
+    blob = b"".join(streams)
+    return decode_ridbag_blob(blob, offs, vertex_rids, edge_rids, edge_targets, device)
+
+
+def decode_ridbag_blob(blob, offsets, vertex_rids, edge_rids=None, edge_targets=None, device=0):
+    """The same over one concatenated byte string and its offsets[V+1]."""
+    offs = np.ascontiguousarray(offsets, np.uint64)
+    V = len(offs) - 1
+    vr = np.ascontiguousarray(vertex_rids, np.uint64)
+    if len(vr) != V:
+        raise ValueError("vertex_rids must have one RID per stream")
+    er = np.ascontiguousarray(edge_rids, np.uint64) if edge_rids is not None else None
+    et = np.ascontiguousarray(edge_targets, np.uint64) if edge_targets is not None else None
+    ne = len(er) if er is not None else 0
+    buf = np.frombuffer(blob, np.uint8) if len(blob) else np.zeros(1, np.uint8)
+    rp = np.zeros(V + 1, np.uint64)
+    n = C.c_uint64()
+    L = N.lib()
+    args = [device, buf.ctypes.data_as(C.c_void_p), len(blob), _u64p(offs), V, _u64p(vr), _u64p(er), _u64p(et), ne]
+    N.check(L.omx_ridbag_decode_csr(*args, _u64p(rp), None, C.byref(n)))
+    col = np.zeros(max(n.value, 1), np.uint32)
+    N.check(L.omx_ridbag_decode_csr(*args, _u64p(rp), col.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(n)))
+    return rp, col[:n.value]

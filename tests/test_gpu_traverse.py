@@ -31,7 +31,7 @@ class _Adj:
         return self.out(v) + self.inn(v)
 
     def hubs(self, k):
-        deg = np.diff(self.rp)
+        deg = np.diff(self.rp.astype(np.int64))
         return [int(x) for x in np.argsort(-deg, kind="stable")[:k]]
 
 
@@ -186,3 +186,63 @@ def test_match_edge_steps(rmat10):
     rs = o.OMatchStatement(q_edges).execute(g)
     assert rs.info["n_rows"] == len(want)
     assert {tuple(int(x) for x in row) for row in rs.rows} == want
+
+
+# ---- shortestPath() (GF/OSQLFunctionShortestPath.java) against oracle/shortest_path_ref.py ---------------
+
+def _sp_pairs(a, n, seed):
+    rnd = np.random.default_rng(seed)
+    hubs = a.hubs(8)
+    pairs = [(hubs[0], hubs[1]), (hubs[2], hubs[2]), (3, 3)]
+    deg0 = [v for v in range(a.V) if a.rp[v + 1] == a.rp[v]][:2]  # no out-edges: unreachable by OUT
+    pairs += [(int(h), int(z)) for h, z in zip(hubs, deg0)] + [(int(z), int(h)) for h, z in zip(hubs, deg0)]
+    pairs += [(int(x), int(y)) for x, y in rnd.integers(0, a.V, size=(n, 2))]
+    return pairs
+
+
+@pytest.mark.parametrize("direction", ["OUT", "IN", "BOTH"])
+def test_shortest_path_parity(rmat10, adj10, direction):
+    from oracle.shortest_path_ref import shortest_path
+    import orientdb_amd as o
+    g, _ = rmat10
+    left = {"OUT": adj10.out, "IN": adj10.inn, "BOTH": adj10.both}[direction]
+    right = {"OUT": adj10.inn, "IN": adj10.out, "BOTH": adj10.both}[direction]
+    found = 0
+    for s, t in _sp_pairs(adj10, 40, 1):
+        want = shortest_path(s, t, left, right)
+        found += len(want) > 1
+        rs = o.OMatchStatement(f"SELECT expand(shortestPath(#11:{s}, #11:{t}, '{direction}', 'Knows'))").execute(g)
+        assert _rids(rs) == _want(want), (s, t)
+        doc = o.OMatchStatement(f"SELECT shortestPath(#11:{s}, #11:{t}, '{direction}')").execute(g)
+        assert len(doc) == 1 and [tuple(x) for x in doc[0]["shortestPath"]] == _want(want), (s, t)
+    assert found > 10
+
+
+def test_shortest_path_max_depth_and_params(rmat10, adj10):
+    from oracle.shortest_path_ref import shortest_path
+    import orientdb_amd as o
+    g, _ = rmat10
+    for s, t in _sp_pairs(adj10, 20, 2):
+        for md in (1, 2, 3, 5):
+            want = shortest_path(s, t, adj10.both, adj10.both, max_depth=md)
+            rs = o.OMatchStatement(f"SELECT expand(shortestPath(?, ?, 'both', null, {{maxDepth: {md}}}))").execute(
+                g, f"#11:{s}", f"#11:{t}")
+            assert _rids(rs) == _want(want), (s, t, md)
+
+
+def test_shortest_path_multigraph_and_rmat16(rmat10_raw, rmat16):
+    from oracle.shortest_path_ref import shortest_path
+    import orientdb_amd as o
+    for g, _ in (rmat10_raw, rmat16):
+        a = _Adj(g)
+        for s, t in _sp_pairs(a, 12, 3):
+            want = shortest_path(s, t, a.out, a.inn)
+            rs = o.OMatchStatement(f"SELECT expand(shortestPath(#11:{s}, #11:{t}, 'OUT'))").execute(g)
+            assert _rids(rs) == _want(want), (s, t)
+
+
+def test_shortest_path_missing_vertex(rmat10):
+    import orientdb_amd as o
+    g, _ = rmat10
+    with pytest.raises(o.OmxExecutionError):
+        o.OMatchStatement("SELECT shortestPath(#11:1, #11:99999999)").execute(g)

@@ -111,3 +111,38 @@ def test_expand_chain_keeps_order_and_repeats():
     adj = {0: [1, 2], 1: [3], 2: [3, 1], 3: []}
     assert expand_chain([0], [lambda v: adj[v]] * 2) == [3, 3, 1]
     assert expand_chain([0, 0], [lambda v: adj[v]]) == [1, 2, 1, 2]
+
+
+def _bfs_dist(adj, s):
+    dist = {s: 0}
+    q = [s]
+    for v in q:
+        for w in adj[v]:
+            if w not in dist:
+                dist[w] = dist[v] + 1
+                q.append(w)
+    return dist
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_shortest_path_oracle_paths_are_paths(seed):
+    """oracle/shortest_path_ref.py: the returned list is a walk from the source to the destination along
+    the direction's edges whose length is the BFS distance (the bidirectional search meets on a shortest
+    path), and empty exactly when the destination is unreachable (no maxDepth)."""
+    from oracle.shortest_path_ref import shortest_path
+    rnd = random.Random(seed)
+    V = rnd.randint(2, 30)
+    out = {v: [rnd.randrange(V) for _ in range(rnd.randint(0, 3))] for v in range(V)}
+    inn = {v: [] for v in range(V)}
+    for v in range(V):
+        for w in out[v]:
+            inn[w].append(v)
+    s, t = rnd.randrange(V), rnd.randrange(V)
+    p = shortest_path(s, t, lambda v: out[v], lambda v: inn[v])
+    d = _bfs_dist(out, s)
+    if t not in d:
+        assert p == []
+        return
+    assert p[0] == s and p[-1] == t
+    assert all(b in out[a] for a, b in zip(p, p[1:]))
+    assert len(p) - 1 == d[t]

@@ -33,12 +33,19 @@ CASES = [
     ("SELECT expand(in()) FROM [#11:1, #11:2]", True, "SELECT"),
     ("SELECT expand(out('Knows').name) FROM #11:0", False, "SELECT"),
     ("SELECT expand(bothE().bothV()) FROM #11:0", False, "SELECT"),
+    ("SELECT expand(out())", False, "SELECT"),  # no FROM
+    ("SELECT shortestPath(#11:1, #11:9)", True, "SHORTEST_PATH"),
+    ("SELECT shortestPath(#11:1, #11:9, 'OUT', 'Knows') AS p", True, "SHORTEST_PATH"),
+    ("SELECT expand(shortestPath(#11:1, #11:9, 'both', null, {'maxDepth': 3}))", True, "SHORTEST_PATH"),
+    ("SELECT expand(shortestPath(?, ?, 'IN'))", True, "SHORTEST_PATH"),
+    ("SELECT shortestPath(#11:1, #11:9) FROM Person", False, "SHORTEST_PATH"),
+    ("SELECT shortestPath(#11:1, out())", False, "SHORTEST_PATH"),
 ]
 
 
 @pytest.mark.parametrize("q,supported,kind", CASES, ids=[c[0][:60] for c in CASES])
 def test_chain_support(g, q, supported, kind):
-    p = o.OMatchStatement(q).explain(g)
+    p = o.OMatchStatement(q).explain(g, *(["#11:1", "#11:9"] if "?" in q else []))
     assert p["kind"] == kind
     assert p["supported"] == supported, p["unsupported_reason"]
 
@@ -73,3 +80,8 @@ def test_match_edge_steps_fuse(g):
     assert not o.OMatchStatement(q2).explain(g)["supported"]
     q3 = "MATCH {class:Person, as:a, where:(uid = 1)}.outE('Knows'){as:e}.inV(){as:b} RETURN a, b"
     assert not o.OMatchStatement(q3).explain(g)["supported"]
+
+
+def test_shortest_path_bad_direction(g):
+    with pytest.raises(o.OmxExecutionError):
+        o.OMatchStatement("SELECT shortestPath(#11:1, #11:9, 'SIDEWAYS')").explain(g)
