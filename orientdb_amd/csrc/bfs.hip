@@ -12,8 +12,10 @@
 // RMAT levels that cover most of the graph). The result is emitted once per batch from the visited
 // masks.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "devutil.h"
@@ -441,6 +443,16 @@ __global__ __launch_bounds__(kB) void k_hub_mark(const uint64_t *rp, uint32_t V,
   }
 }
 
+// hub degrees (sort keys) and, after the sort, every hub's index = its rank by degree (densest first)
+__global__ void k_hub_deg(const uint32_t *hubs, uint32_t n, const uint64_t *rp, uint32_t *deg) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) deg[i] = (uint32_t)min<uint64_t>(rp[hubs[i] + 1] - rp[hubs[i]], 0xFFFFFFFFull);
+}
+__global__ void k_hub_rank(const uint32_t *hubs, uint32_t n, uint32_t *hub_idx) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) hub_idx[hubs[i]] = i;
+}
+
 __global__ void k_pull_annotate(const uint32_t *col, uint64_t E, const uint32_t *hub_idx, uint32_t *out) {
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t c = col[e];
@@ -470,6 +482,34 @@ uint32_t build_pull_col(const uint64_t *rp_other, const uint32_t *col, uint32_t 
   if (cum == 0) t = ~0ull;  // no hubs: the copy is the plain col
   hipLaunchKernelGGL(k_hub_mark, dim3(g), dim3(kB), 0, s, rp_other, V, (uint64_t)t, hub_idx, hubs, count);
   KCHECK("k_hub_mark");
+  // hub index = rank by degree (descending): the masks gathered most often share the first lines of
+  // the packed array (OMX_PULL_HUB_ORDER=vertex keeps discovery order)
+  static const bool by_rank = [] {
+    const char *e = std::getenv("OMX_PULL_HUB_ORDER");
+    return !(e && std::strcmp(e, "vertex") == 0);
+  }();
+  if (by_rank && cum > 1) {
+    const uint32_t n = (uint32_t)cum;
+    uint32_t *deg = nullptr, *deg2 = nullptr, *h2 = nullptr;
+    void *tmp = nullptr;
+    size_t tb = 0;
+    HIP_CHECK(hipMalloc((void **)&deg, (size_t)n * 4));
+    HIP_CHECK(hipMalloc((void **)&deg2, (size_t)n * 4));
+    HIP_CHECK(hipMalloc((void **)&h2, (size_t)n * 4));
+    hipLaunchKernelGGL(k_hub_deg, dim3(nblocks(n, kB)), dim3(kB), 0, s, hubs, n, rp_other, deg);
+    KCHECK("k_hub_deg");
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, deg, deg2, hubs, h2, (int)n, 0, 32, s));
+    HIP_CHECK(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(tmp, tb, deg, deg2, hubs, h2, (int)n, 0, 32, s));
+    HIP_CHECK(hipMemcpyAsync(hubs, h2, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_hub_rank, dim3(nblocks(n, kB)), dim3(kB), 0, s, hubs, n, hub_idx);
+    KCHECK("k_hub_rank");
+    HIP_CHECK(hipStreamSynchronize(s));
+    (void)hipFree(deg);
+    (void)hipFree(deg2);
+    (void)hipFree(h2);
+    (void)hipFree(tmp);
+  }
   if (E) {
     const unsigned ge = (unsigned)std::min<uint64_t>(nblocks(E, kB), (uint64_t)cus * 16);
     hipLaunchKernelGGL(k_pull_annotate, dim3(ge), dim3(kB), 0, s, col, E, hub_idx, out);

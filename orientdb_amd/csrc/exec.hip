@@ -379,7 +379,9 @@ class Executor {
   std::string varlen_mode_ = "auto";
   std::string fuse_mode_ = "1";
   bool swap_ = true;  // fused closing check iterates the shorter of the two lists (OMX_SWAP_CHECK=0: off)
-  uint32_t pull_hubs_ = 1u << 18;  // hub masks packed for the pull kernel (2 MiB); 0 = plain col
+  // hub masks packed for the pull kernel in degree-rank order (8 MiB); 0 = plain col. 2^20 measured best
+  // of 2^17…2^22 at C3 (profiles/r02/c3rank: pull 4.26 → 4.07 ms per step against 2^18 in vertex order)
+  uint32_t pull_hubs_ = 1u << 20;
   uint64_t pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
   // sliced hops size their arenas from the target bitmap's density (OMX_ARENA_ESTIMATE=0: exact bound;
@@ -1851,6 +1853,10 @@ class Executor {
         edges_ += h[0];
         edges_iter_ += h[0];
         HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
+        if (debug_expand_)
+          std::fprintf(stderr, "[omx bfs] batch %llu level %lld: %s active=%llu push_edges=%llu E_t=%llu\n",
+                       (unsigned long long)row0, (long long)d, h[1] * pull_div_ > eadj ? "pull" : "push",
+                       (unsigned long long)h[2], (unsigned long long)h[1], (unsigned long long)h[0]);
         if (h[1] * pull_div_ > eadj) {
           for (int p = 0; p < radj.n; ++p) {
             const uint64_t nt = bfs_pull_tiles(V, pull_E[p]);
