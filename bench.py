@@ -42,7 +42,13 @@ QUERIES = {
            "MATCH {class:Person,as:a}-Knows->{as:b}-Knows->{as:c}-Knows->{as:a} RETURN a,b,c", "ldbc"),
     "c5": ("C5: RMAT 3-hop MATCH (COUNT), 1-D partitioned graph, per-hop all-to-all row exchange (RCCL)",
            "MATCH {class:Person,as:a,where:(uid < 64)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d", 26),
+    # SURVEY §8(f) rows (not the metric): {hub} = the vertex of highest out-degree
+    "t1": ("T1: TRAVERSE out('Knows') STRATEGY BREADTH_FIRST from the highest-degree vertex (its whole reach)",
+           "TRAVERSE out('Knows') FROM #11:{hub} STRATEGY BREADTH_FIRST", 24),
+    "s1": ("S1: SELECT expand(out('Knows').out('Knows')) from the highest-degree vertex (rows with repeats)",
+           "SELECT expand(out('Knows').out('Knows')) FROM #11:{hub}", 22),
 }
+CHAIN = {"t1", "s1"}
 # Weak scaling over roots on the replicated graph (each root's DFS subtree is independent):
 # at N ranks the root window widens N-fold and every rank keeps ≈ the N=1 share (roots v % N == rank),
 # so per-GPU work is fixed as N grows. At N=1 the query is exactly configs[1]'s.
@@ -58,11 +64,11 @@ def scaled_query(name, query, world, partitioned):
     return query, "strong"
 
 
-REPLICATED_ONLY = {"c1", "c3", "c4"}  # per-GPU structures: C3 multi-source BFS lane masks, C4 LDBC replica; C1 all-root fof
+REPLICATED_ONLY = {"c1", "c3", "c4", "t1", "s1"}  # per-GPU structures: C3 multi-source BFS lane masks, C4 LDBC replica; C1 all-root fof
 COUNT_MODE = {"c5"}   # the last hop counts its rows (count mode)
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # ≈7e4 Person, ≈2e6 Knows
 # kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)
-HOT_KERNELS = ("k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light", "k_expand_light_sliced",
+HOT_KERNELS = ("k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light", "k_expand_light_sliced", "k_trav_filter",
                "k_expand_light_check", "k_expand_heavy_check", "k_check", "k_bfs_pull", "k_bfs_push", "k_bfs_prep", "k_bfs_emit",
                "k_gather_cols", "k_compact_segments")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md §Chip-level parameters)
@@ -106,11 +112,46 @@ def host_threads():
     return (min(share, visible) if share > 0 else visible), visible
 
 
+def cpu_baseline_chain(g, query, target_s):
+    """TRAVERSE / SELECT expand: the oracle's restatement (oracle/traverse_ref.py, pure Python, one core)
+    on a bounded sample of the same kind of work, GTEPS = adjacency entries it iterated / its time.
+    TRAVERSE: the work list FROM the first K vertices MAXDEPTH 1 (every root's out-list pushed and
+    processed); SELECT: the two-call chain over the first K vertices. K doubles until ≈ target_s / 4."""
+    from oracle.traverse_ref import BREADTH_FIRST, expand_chain, traverse
+    rp, col = g.csr
+    seen = [0]
+
+    def out(v):
+        row = col[rp[v]:rp[v + 1]].tolist()
+        seen[0] += len(row)
+        return row
+    k = 256
+    while True:
+        seen[0] = 0
+        roots = list(range(min(k, g.V)))
+        t0 = time.perf_counter()
+        if query.startswith("TRAVERSE"):
+            traverse(roots, lambda v: [out(v)], max_depth=1, strategy=BREADTH_FIRST)
+            what = "the work list from vertices 0..%d, MAXDEPTH 1" % (len(roots) - 1)
+        else:
+            expand_chain(roots, [out, out])
+            what = "the chain out().out() from vertices 0..%d" % (len(roots) - 1)
+        secs = time.perf_counter() - t0
+        if secs > target_s / 4 or k >= g.V:
+            break
+        k *= 2
+    return {"value": seen[0] / secs / 1e9, "unit": "GTEPS", "cores": 1, "kind": "port",
+            "sample": "%s (%.1f s, %d adjacency entries; oracle/traverse_ref.py, pure Python, 1 thread)" % (
+                what, secs, seen[0])}
+
+
 def cpu_baseline(g, query, target_s=12.0):
     """The oracle's C DFS restatement (oracle/dfs_ref.c) on the host cores, on a bounded sample of
     the same workload's roots; GTEPS over the sampled roots."""
     import numpy as np
     from oracle import dfs
+    if query.startswith(("TRAVERSE", "SELECT")):
+        return cpu_baseline_chain(g, query, target_s)
     threads, visible = host_threads()
     if "while:($depth < 4)" in query:
         r = cpu_baseline_varlen(g, 64, 4, target_s, threads)
@@ -216,7 +257,7 @@ def main():
     partitioned = world > 1 and not args.replicated and args.query not in REPLICATED_ONLY and args.scale != "ldbc"
     query, scaling = scaled_query(args.query, query, world, partitioned)
     t_build = time.perf_counter()
-    keep = rank == 0 and world == 1 and not args.no_cpu_baseline
+    keep = (rank == 0 and world == 1 and not args.no_cpu_baseline) or "{hub}" in query
     comm = None
     if args.scale == "ldbc":
         g = o.GraphSnapshot.ldbc_like(device=local, keep_csr=keep, **LDBC_SF10)
@@ -236,6 +277,9 @@ def main():
         g = with_heartbeat("graph build", lambda: o.GraphSnapshot.rmat(args.scale, device=local, keep_csr=keep))
         graph_desc = {"graph": "RMAT", "scale": args.scale, "edge_factor": 16}
     t_build = time.perf_counter() - t_build
+    if "{hub}" in query:  # the vertex of highest out-degree (lowest id on ties)
+        import numpy as np
+        query = query.replace("{hub}", str(int(np.argmax(np.diff(g.csr[0].astype(np.int64))))))
     st = o.OMatchStatement(query)
     flags = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_KERNEL_TIMING | o.OMX_FLAG_TIME_HOT
     mode = o.OMX_MODE_COUNT if (args.query in COUNT_MODE or args.count) else o.OMX_MODE_MATERIALIZE

@@ -45,7 +45,7 @@ class Timer {
     static const char *const kHot[] = {"k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light",
                                        "k_expand_light_sliced", "k_expand_light_check", "k_expand_heavy_check",
                                        "k_check", "k_bfs_pull", "k_bfs_push",
-                                       "k_bfs_emit"};
+                                       "k_bfs_emit", "k_trav_filter", "trav_select"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
     return false;
@@ -137,6 +137,7 @@ class Executor {
       heavy_deg_sliced_ = heavy_deg_;
       heavy_deg_fixed_ = true;
     }
+    if (const char *h = std::getenv("OMX_HEAVY_DEG_UNFILTERED")) heavy_deg_unfiltered_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
     // variable-length strategy: "bfs" (multi-source BFS whenever exact), "pairs" ((row, v) levels), auto
     if (const char *v = std::getenv("OMX_VARLEN")) varlen_mode_ = v;
     if (const char *sl = std::getenv("OMX_SLICED")) sliced_ = std::strcmp(sl, "0") != 0;
@@ -372,6 +373,7 @@ class Executor {
   uint64_t heavy_deg_ = kHeavyDeg;
   uint64_t heavy_deg_sliced_ = kHeavyDegSliced;
   bool heavy_deg_fixed_ = false;  // OMX_HEAVY_DEG given
+  uint64_t heavy_deg_unfiltered_ = kHeavyDeg;  // unfiltered hops (OMX_HEAVY_DEG_UNFILTERED)
   bool debug_expand_ = false;
   bool light_sliced_ = true;  // LDS-sliced light kernel for sliced single-part hops (OMX_LIGHT_SLICED=0: merge path)
   bool sliced_ = true;  // LDS-sliced heavy kernel for filtered hops (OMX_SLICED=0 disables)
@@ -863,6 +865,7 @@ class Executor {
     // ordered (unfiltered, TRAVERSE / SELECT expand): every row through the merge-path kernel, whose dense
     // output is in row order (the heavy kernel's rows come first)
     const uint64_t hd = ordered ? UINT64_MAX
+                        : (!filter && !member && !heavy_deg_fixed_) ? heavy_deg_unfiltered_
                         : !sliced ? heavy_deg_
                         : heavy_deg_fixed_ ? heavy_deg_sliced_
                                            : std::max<uint64_t>(heavy_deg_sliced_, 128ull * P);
@@ -1380,7 +1383,9 @@ class Executor {
       tm_.end(n * (4 + 8 + 8 + 1) + (last ? 0 : n * 9));
       DBuf<uint32_t> acc(&pool_, n);
       DBuf<uint64_t> nsel(&pool_, 1);
+      tm_.begin("trav_select");
       cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cur.p, flags.p, acc.p, nsel.p, (int64_t)n, s_); });
+      tm_.end(n * 9);
       const uint64_t k = read1(nsel.p);
       if (!last) launch_trav_accept(acc.p, k, hist.p, first.p, s_);
       if (k) {

@@ -2171,7 +2171,9 @@ __global__ void k_trav_filter(const uint32_t *w, uint64_t n, const uint64_t *his
   const uint32_t v = w[e];
   bool keep = !((hist[v >> 6] >> (v & 63)) & 1);
   if (keep && pred) keep = (pred[v >> 6] >> (v & 63)) & 1;
-  if (keep && dedup) atomicMin(&first[v], (uint32_t)e);
+  // a repeated record (a hub reached from many entries) would serialise on one address: the claim is
+  // skipped once an earlier position holds it (blocks run roughly in position order)
+  if (keep && dedup && first[v] > (uint32_t)e) atomicMin(&first[v], (uint32_t)e);
   flags[e] = keep;
 }
 __global__ void k_trav_first(const uint32_t *w, uint64_t n, const uint32_t *first, uint8_t *flags) {

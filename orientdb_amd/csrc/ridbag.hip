@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -76,13 +77,8 @@ __device__ __forceinline__ uint32_t bag_header(const uint8_t *s, const uint64_t 
   return n;
 }
 
-// payload offset of a stream the count pass accepted
-__device__ __forceinline__ uint64_t bag_payload(const uint8_t *s, const uint64_t *offs, uint32_t v) {
-  const uint64_t b = offs[v];
-  return b + 1 + ((s[b] & 2) ? 16 : 0) + 4;
-}
-
-__global__ void k_bag_count(const uint8_t *s, const uint64_t *offs, uint32_t V, uint64_t *cnt, uint32_t *err) {
+__global__ void k_bag_count(const uint8_t *s, const uint64_t *offs, uint32_t V, uint64_t *cnt, uint64_t *pay,
+                            uint32_t *err) {
   const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v > V) return;
   if (v == V) {
@@ -91,6 +87,7 @@ __global__ void k_bag_count(const uint8_t *s, const uint64_t *offs, uint32_t V, 
   }
   uint64_t p;
   cnt[v] = bag_header(s, offs, (uint32_t)v, &p, err);
+  pay[v] = p;
 }
 
 // index of key in sorted[0..n) (n if absent)
@@ -104,43 +101,105 @@ __device__ __forceinline__ uint64_t find_sorted(const uint64_t *sorted, uint64_t
   return lo < n && sorted[lo] == key ? lo : n;
 }
 
-__global__ void k_bag_decode(const uint8_t *s, const uint64_t *offs, uint32_t V, const uint64_t *rp, uint64_t E,
-                             const uint64_t *vrid, const uint32_t *vdense, const uint64_t *erid, const uint64_t *etarget,
-                             uint64_t nedges, uint32_t *col, uint32_t *err) {
-  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (uint64_t)gridDim.x * blockDim.x) {
-    // the vertex whose row holds entry e: last v with rp[v] <= e
-    uint64_t lo = 0, hi = V;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi + 1) >> 1;
-      if (rp[mid] <= e) lo = mid;
-      else hi = mid - 1;
+// RID → value lookup. Direct: RIDs whose positions are compact per cluster (the usual case: records
+// are appended) index a table, base[cluster] + position; otherwise a binary search over a RID-sorted copy.
+template <class T>
+struct RidIndex {
+  const int64_t *base;   // [32768] table offset of each cluster, -1 if absent (direct mode)
+  const uint64_t *lim;   // [32768] positions of the cluster are < lim
+  const T *table;        // direct mode; sentinel ~0 = no record
+  const uint64_t *keys;  // sorted mode
+  const T *vals;
+  uint64_t n;
+  int direct;
+  __device__ __forceinline__ bool find(uint64_t rid, T *out) const {
+    if (direct) {
+      const uint32_t c = (uint32_t)(rid >> 48);
+      const uint64_t p = rid & ((1ull << 48) - 1);
+      const int64_t b = c < 32768 ? base[c] : -1;
+      if (b < 0 || p >= lim[c]) return false;
+      const T x = table[b + p];
+      if (x == (T)~(T)0) return false;
+      *out = x;
+      return true;
     }
-    const uint32_t v = (uint32_t)lo;
-    const uint8_t *p = s + bag_payload(s, offs, v) + 10ull * (e - rp[v]);
-    const int16_t cl = (int16_t)(((uint32_t)p[0] << 8) | p[1]);
-    const uint64_t pos = be64(p + 2);
-    uint32_t out = 0xFFFFFFFFu;
-    if (cl < 0 || (pos >> 48)) {
-      atomicOr(err, (uint32_t)kBagPosition);
-    } else {
-      uint64_t rid = ((uint64_t)(uint16_t)cl << 48) | pos;
-      bool ok = true;
-      if (erid) {  // an edge record: its opposite vertex
-        const uint64_t i = find_sorted(erid, nedges, rid);
-        if (i == nedges) {
-          atomicOr(err, (uint32_t)kBagUnknownEdge);
-          ok = false;
-        } else {
-          rid = etarget[i];
+    const uint64_t i = find_sorted(keys, n, rid);
+    if (i == n) return false;
+    *out = vals[i];
+    return true;
+  }
+};
+
+template <class T>
+__global__ void k_index_fill(const uint64_t *rids, const T *vals, uint64_t n, const int64_t *base, T *table) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = rids[i];
+    table[base[r >> 48] + (r & ((1ull << 48) - 1))] = vals ? vals[i] : (T)i;
+  }
+}
+
+// One block decodes kDecTile consecutive entries: their rows lie between the rows of the tile's first
+// and last entry (two searches per block), so each entry's row is a short search in that range.
+constexpr int kDecB = 256, kDecIPT = 8, kDecTile = kDecB * kDecIPT;
+__global__ __launch_bounds__(kDecB) void k_bag_decode(const uint8_t *s, const uint64_t *pay, uint32_t V,
+                                                      const uint64_t *rp, uint64_t E, RidIndex<uint32_t> vix,
+                                                      RidIndex<uint64_t> eix, int edges, uint32_t *col, uint32_t *err) {
+  __shared__ uint64_t s_r[2];
+  for (uint64_t t0 = (uint64_t)blockIdx.x * kDecTile; t0 < E; t0 += (uint64_t)gridDim.x * kDecTile) {
+    const uint64_t t1 = min(t0 + (uint64_t)kDecTile, E) - 1;
+    if (threadIdx.x < 2) {  // last v with rp[v] <= e
+      const uint64_t e = threadIdx.x ? t1 : t0;
+      uint64_t lo = 0, hi = V;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) >> 1;
+        if (rp[mid] <= e) lo = mid;
+        else hi = mid - 1;
+      }
+      s_r[threadIdx.x] = lo;
+    }
+    __syncthreads();
+    const uint64_t r0 = s_r[0], r1 = s_r[1];
+    __syncthreads();
+#pragma unroll 2
+    for (int k = 0; k < kDecIPT; ++k) {
+      const uint64_t e = t0 + (uint64_t)k * kDecB + threadIdx.x;
+      if (e > t1) break;
+      uint64_t lo = r0, hi = r1;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) >> 1;
+        if (rp[mid] <= e) lo = mid;
+        else hi = mid - 1;
+      }
+      // the 10-byte entry from the aligned dwords around it (the buffer is padded by 16 bytes)
+      const uint64_t o = pay[lo] + 10ull * (e - rp[lo]);
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(s + (o & ~3ull));
+      const uint32_t sh = (uint32_t)(o & 3) * 8;
+      const uint64_t wl = ((uint64_t)w[1] << 32) | w[0], wh = ((uint64_t)(sh ? w[3] : 0u) << 32) | w[2];
+      const uint64_t b07 = sh ? (wl >> sh) | (wh << (64 - sh)) : wl;  // entry bytes 0..7, little-endian
+      const uint64_t b89 = (wh >> sh) & 0xFFFFull;                     // entry bytes 8..9
+      const int16_t cl = (int16_t)(((b07 & 0xFF) << 8) | ((b07 >> 8) & 0xFF));
+      const uint64_t pos = __builtin_bswap64((b07 >> 16) | (b89 << 48));
+      uint32_t out = 0xFFFFFFFFu;
+      if (cl < 0 || (pos >> 48)) {
+        atomicOr(err, (uint32_t)kBagPosition);
+      } else {
+        uint64_t rid = ((uint64_t)(uint16_t)cl << 48) | pos;
+        bool ok = true;
+        if (edges) {  // an edge record: its opposite vertex
+          uint64_t target;
+          if (eix.find(rid, &target)) rid = target;
+          else {
+            atomicOr(err, (uint32_t)kBagUnknownEdge);
+            ok = false;
+          }
+        }
+        if (ok && !vix.find(rid, &out)) {
+          atomicOr(err, (uint32_t)kBagUnknownRid);
+          out = 0xFFFFFFFFu;
         }
       }
-      if (ok) {
-        const uint64_t i = find_sorted(vrid, V, rid);
-        if (i == V) atomicOr(err, (uint32_t)kBagUnknownRid);
-        else out = vdense[i];
-      }
+      col[e] = out;
     }
-    col[e] = out;
   }
 }
 
@@ -153,6 +212,81 @@ struct DevArr {
     if (p) (void)hipFree(p);
   }
 };
+
+// RID index on the device (RidIndex), built from host arrays: direct when every RID is packable and the
+// per-cluster position ranges total at most 2n + 64 K slots, else RID-sorted (radix sort) for searches
+template <class T>
+struct HostIndex {
+  std::unique_ptr<DevArr<int64_t>> base;
+  std::unique_ptr<DevArr<uint64_t>> lim, keys;
+  std::unique_ptr<DevArr<T>> table, vals;
+  RidIndex<T> dev{};
+};
+template <class T>
+void build_index(HostIndex<T> &ix, const uint64_t *rids, const T *vals, uint64_t n, hipStream_t s) {
+  std::vector<int64_t> hb(32768, -1);
+  std::vector<uint64_t> hl(32768, 0);
+  bool packable = true;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t c = rids[i] >> 48, p = rids[i] & ((1ull << 48) - 1);
+    if (c >= 32768) {
+      packable = false;
+      break;
+    }
+    hl[c] = std::max(hl[c], p + 1);
+  }
+  uint64_t total = 0;
+  if (packable)
+    for (int c = 0; c < 32768; ++c)
+      if (hl[c]) {
+        hb[c] = (int64_t)total;
+        total += hl[c];
+      }
+  DevArr<uint64_t> dr(n);
+  if (n) HIP_CHECK(hipMemcpyAsync(dr.p, rids, n * 8, hipMemcpyHostToDevice, s));
+  std::unique_ptr<DevArr<T>> dv;
+  if (vals && n) {
+    dv.reset(new DevArr<T>(n));
+    HIP_CHECK(hipMemcpyAsync(dv->p, vals, n * sizeof(T), hipMemcpyHostToDevice, s));
+  }
+  if (packable && total <= 2 * n + 65536) {
+    ix.base.reset(new DevArr<int64_t>(32768));
+    ix.lim.reset(new DevArr<uint64_t>(32768));
+    ix.table.reset(new DevArr<T>(total));
+    HIP_CHECK(hipMemcpyAsync(ix.base->p, hb.data(), 32768 * 8, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(ix.lim->p, hl.data(), 32768 * 8, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemsetAsync(ix.table->p, 0xFF, std::max<uint64_t>(total, 1) * sizeof(T), s));
+    if (n) {
+      hipLaunchKernelGGL(k_index_fill<T>, dim3((unsigned)std::min<uint64_t>(nblocks(n, 256), 65536)), dim3(256), 0, s,
+                         dr.p, dv ? dv->p : nullptr, n, ix.base->p, ix.table->p);
+      KCHECK("k_index_fill");
+    }
+    ix.dev.base = ix.base->p;
+    ix.dev.lim = ix.lim->p;
+    ix.dev.table = ix.table->p;
+    ix.dev.direct = 1;
+  } else {
+    ix.keys.reset(new DevArr<uint64_t>(n));
+    ix.vals.reset(new DevArr<T>(n));
+    DevArr<T> iv(n);
+    if (!dv) {  // values = positions
+      std::vector<T> h(n);
+      for (uint64_t i = 0; i < n; ++i) h[i] = (T)i;
+      if (n) HIP_CHECK(hipMemcpyAsync(iv.p, h.data(), n * sizeof(T), hipMemcpyHostToDevice, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+    }
+    size_t sb = 0;
+    const T *vin = dv ? dv->p : iv.p;
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, dr.p, ix.keys->p, vin, ix.vals->p, (int64_t)n, 0, 64, s));
+    DevArr<uint8_t> stmp(sb);
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(stmp.p, sb, dr.p, ix.keys->p, vin, ix.vals->p, (int64_t)n, 0, 64, s));
+    ix.dev.keys = ix.keys->p;
+    ix.dev.vals = ix.vals->p;
+    ix.dev.n = n;
+    ix.dev.direct = 0;
+  }
+  HIP_CHECK(hipStreamSynchronize(s));  // the temporaries above leave scope
+}
 
 std::string bag_error_text(uint32_t e) {
   std::string m;
@@ -182,13 +316,13 @@ void ridbag_decode_csr(int device, const uint8_t *streams, uint64_t nbytes, cons
     hipStream_t s;
     ~StreamGuard() { (void)hipStreamDestroy(s); }
   } sg{s};
-  DevArr<uint8_t> ds(nbytes);
-  DevArr<uint64_t> doffs(V + 1ull), cnt(V + 1ull), rp(V + 1ull);
+  DevArr<uint8_t> ds(nbytes + 16);  // padding: the decoder reads whole dwords around an entry
+  DevArr<uint64_t> doffs(V + 1ull), cnt(V + 1ull), rp(V + 1ull), pay(V + 1ull);
   DevArr<uint32_t> err(1);
   if (nbytes) HIP_CHECK(hipMemcpyAsync(ds.p, streams, nbytes, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(doffs.p, offsets, (V + 1ull) * 8, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
-  hipLaunchKernelGGL(k_bag_count, dim3(nblocks(V + 1ull, 256)), dim3(256), 0, s, ds.p, doffs.p, V, cnt.p, err.p);
+  hipLaunchKernelGGL(k_bag_count, dim3(nblocks(V + 1ull, 256)), dim3(256), 0, s, ds.p, doffs.p, V, cnt.p, pay.p, err.p);
   KCHECK("k_bag_count");
   size_t tb = 0;
   HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.p, rp.p, (int64_t)V + 1, s));
@@ -206,35 +340,16 @@ void ridbag_decode_csr(int device, const uint8_t *streams, uint64_t nbytes, cons
     HIP_CHECK(hipStreamSynchronize(s));
     return;
   }
-  // RID-sorted vertex table (and edge table): the decoder's binary searches
-  DevArr<uint64_t> vr(V), vrs(V);
-  DevArr<uint32_t> vd(V), vds(V);
-  if (V) {
-    HIP_CHECK(hipMemcpyAsync(vr.p, vertex_rids, (uint64_t)V * 8, hipMemcpyHostToDevice, s));
-    std::vector<uint32_t> iota(V);
-    for (uint32_t v = 0; v < V; ++v) iota[v] = v;
-    HIP_CHECK(hipMemcpyAsync(vd.p, iota.data(), (uint64_t)V * 4, hipMemcpyHostToDevice, s));
-    size_t sb = 0;
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, vr.p, vrs.p, vd.p, vds.p, (int64_t)V, 0, 64, s));
-    DevArr<uint8_t> stmp(sb);
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(stmp.p, sb, vr.p, vrs.p, vd.p, vds.p, (int64_t)V, 0, 64, s));
-    HIP_CHECK(hipStreamSynchronize(s));  // iota leaves scope
-  }
-  DevArr<uint64_t> er(nedges), ers(nedges), et(nedges), ets(nedges);
-  if (edge_rids && nedges) {
-    HIP_CHECK(hipMemcpyAsync(er.p, edge_rids, nedges * 8, hipMemcpyHostToDevice, s));
-    HIP_CHECK(hipMemcpyAsync(et.p, edge_targets, nedges * 8, hipMemcpyHostToDevice, s));
-    size_t sb = 0;
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, er.p, ers.p, et.p, ets.p, (int64_t)nedges, 0, 64, s));
-    DevArr<uint8_t> stmp(sb);
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(stmp.p, sb, er.p, ers.p, et.p, ets.p, (int64_t)nedges, 0, 64, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-  }
+  // RID indexes of the vertices (→ dense id) and of the edge records (→ opposite vertex RID)
+  HostIndex<uint32_t> vix;
+  build_index<uint32_t>(vix, vertex_rids, nullptr, V, s);
+  HostIndex<uint64_t> eix;
+  if (edge_rids) build_index<uint64_t>(eix, edge_rids, edge_targets, nedges, s);
   DevArr<uint32_t> dcol(E);
   if (E) {
-    const unsigned grid = (unsigned)std::min<uint64_t>(nblocks(E, 256), 65536);
-    hipLaunchKernelGGL(k_bag_decode, dim3(grid), dim3(256), 0, s, ds.p, doffs.p, V, rp.p, E, vrs.p, vds.p,
-                       edge_rids ? ers.p : nullptr, edge_rids ? ets.p : nullptr, nedges, dcol.p, err.p);
+    const unsigned grid = (unsigned)std::min<uint64_t>((E + kDecTile - 1) / kDecTile, 65536);
+    hipLaunchKernelGGL(k_bag_decode, dim3(grid), dim3(kDecB), 0, s, ds.p, pay.p, V, rp.p, E, vix.dev, eix.dev,
+                       edge_rids ? 1 : 0, dcol.p, err.p);
     KCHECK("k_bag_decode");
     HIP_CHECK(hipMemcpyAsync(col, dcol.p, E * 4, hipMemcpyDeviceToHost, s));
   }
