@@ -852,7 +852,7 @@ class Executor {
     }
     // 1. degree binning + scans (light edges: merge path; heavy rows: chunks). A filtered hop over a
     // sorted adjacency cuts the heavy rows' chunks at bitmap-slice boundaries (LDS-sliced kernel).
-    const bool sliced = filter != nullptr && !member && !raw_adj && adj.sorted && sliced_ &&
+    const bool sliced = filter != nullptr && !member && !raw_adj && !ordered && adj.sorted && sliced_ &&
                         (uint64_t)g_.V <= ((uint64_t)kMaxSlices << slice_shift_);
     const uint32_t P = sliced ? (uint32_t)(((uint64_t)g_.V + (1ull << slice_shift_) - 1) >> slice_shift_) : 1;
     const DCuts cuts = sliced ? slice_cuts_of(adjs, P) : DCuts{};
@@ -862,14 +862,14 @@ class Executor {
     // sliced: a heavy row is cut into P pieces, one chunk each; below ~128 edges per piece a chunk issues
     // its 16 loads for a few live slots, so the cut grows with P (RMAT-24, P = 16: 2048 measured best of
     // 256…4096, profiles/r02/hd_sweep; RMAT-22, P = 4: 512 against 256, 1.80 against 1.83 ms per step)
-    // ordered (unfiltered, TRAVERSE / SELECT expand): every row through the merge-path kernel, whose dense
-    // output is in row order (the heavy kernel's rows come first)
+    // ordered (TRAVERSE / SELECT expand): every row through the merge-path kernel, whose dense output is
+    // in row order (the heavy kernel's rows would come first); filtered, one tile per block (below)
     const uint64_t hd = ordered ? UINT64_MAX
                         : (!filter && !member && !heavy_deg_fixed_) ? heavy_deg_unfiltered_
                         : !sliced ? heavy_deg_
                         : heavy_deg_fixed_ ? heavy_deg_sliced_
                                            : std::max<uint64_t>(heavy_deg_sliced_, 128ull * P);
-    if (ordered && (filter || member)) fail(OMX_E_INVALID, "internal: an ordered expansion is unfiltered");
+    if (ordered && member) fail(OMX_E_INVALID, "internal: an ordered expansion has no fused check");
     // per-tile sums → one-workgroup scan (posts the totals to the host) → per-tile offsets and chunks
     DBuf<uint64_t> blk(&pool_, (uint64_t)(kBinKeys + P) * bin_tiles(R)), qb(&pool_, P + 1);
     // a sliced hop that writes rows sizes its arenas from the target bitmap's density per slice
@@ -980,7 +980,9 @@ class Executor {
       sa.wg0[P] = w;
     }
     const unsigned gh = !nchunks ? 0 : sliced ? sa.wg0[P] : (unsigned)std::min<uint64_t>(hblocks, sh);
-    const unsigned gl = ntiles ? (unsigned)std::min<uint64_t>(ntiles, sl) : 0;
+    // ordered + filtered: one merge-path tile per block, so the per-block segments are in entry order
+    const unsigned gl = ntiles ? (unsigned)std::min<uint64_t>(ntiles, ordered && filt ? ntiles : sl) : 0;
+    if (ordered && filt && ntiles > 0x7FFFFFFFull) unsupported("an ordered filtered expansion of 2^31 or more tiles");
     // sliced light kernel: one workgroup per CU, split evenly over the slices (light edges spread
     // over V like the heavy ones); a wave's arena holds its share of EL plus one 64-row group
     SliceArgs la{};
@@ -1339,11 +1341,13 @@ class Executor {
     return sel;
   }
 
-  // one move of an ordered list: every entry's neighbours, entries in order (duplicates kept)
-  DBuf<uint32_t> ordered_hop(const uint32_t *cur, uint64_t n, const AdjSpec &adj, uint64_t &out_n) {
+  // one move of an ordered list: every entry's neighbours, entries in order (duplicates kept); with a
+  // filter, only the neighbours in it (still in order)
+  DBuf<uint32_t> ordered_hop(const uint32_t *cur, uint64_t n, const AdjSpec &adj, uint64_t &out_n,
+                             const uint64_t *filter = nullptr) {
     out_n = 0;
     if (!n) return DBuf<uint32_t>(&pool_, 1);
-    ExpandOut o = expand_core(cur, n, adj, nullptr, {}, true, false, nullptr, nullptr, nullptr, nullptr, true);
+    ExpandOut o = expand_core(cur, n, adj, filter, {}, true, false, nullptr, nullptr, nullptr, nullptr, true);
     edges_ += o.E;
     edges_iter_ += o.E;
     out_n = o.n;
@@ -1365,7 +1369,7 @@ class Executor {
     const ChainSpec &c = p_.chain;
     uint64_t n = 0;
     DBuf<uint32_t> cur = chain_roots(n, -1);
-    DBuf<uint64_t> hist(&pool_, std::max<uint64_t>(nwords_, 1)), pscratch;
+    DBuf<uint64_t> hist(&pool_, std::max<uint64_t>(nwords_, 1)), pscratch, keep(&pool_, std::max<uint64_t>(nwords_, 1));
     DBuf<uint32_t> first(&pool_, std::max<uint64_t>(g_.V, 1));
     HIP_CHECK(hipMemsetAsync(hist.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
     launch_fill_u32(first.p, g_.V, UINT32_MAX, s_);
@@ -1373,20 +1377,30 @@ class Executor {
     std::vector<DBuf<uint32_t>> parts;
     std::vector<uint64_t> pn;
     uint64_t total = 0;
+    // level 0 is the FROM list itself; the entries of a later level come from the ordered expansion of
+    // the previous level's records filtered by ¬history ∧ WHILE($depth), so only records that will be
+    // processed are written; what is left per level is the first-entry claim of each record
+    bool filtered = false;
     for (int64_t d = 0; n > 0; ++d) {
       if (n >= UINT32_MAX) unsupported("a TRAVERSE level of 2^32 or more work-list entries");
       const bool last = c.max_depth >= 0 && d == c.max_depth;
-      const uint64_t *pred = prog_bitmap(c.pred_prog, d, pscratch);
-      DBuf<uint8_t> flags(&pool_, n);
-      tm_.begin("k_trav_filter");
-      launch_trav_filter(cur.p, n, hist.p, pred, first.p, flags.p, !last, s_);
-      tm_.end(n * (4 + 8 + 8 + 1) + (last ? 0 : n * 9));
-      DBuf<uint32_t> acc(&pool_, n);
-      DBuf<uint64_t> nsel(&pool_, 1);
-      tm_.begin("trav_select");
-      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cur.p, flags.p, acc.p, nsel.p, (int64_t)n, s_); });
-      tm_.end(n * 9);
-      const uint64_t k = read1(nsel.p);
+      const uint64_t *pred = filtered ? nullptr : prog_bitmap(c.pred_prog, d, pscratch);
+      uint64_t k = n;
+      DBuf<uint32_t> acc;
+      if (!last || !filtered) {
+        DBuf<uint8_t> flags(&pool_, n);
+        tm_.begin("k_trav_filter");
+        launch_trav_filter(cur.p, n, filtered ? nullptr : hist.p, pred, first.p, flags.p, !last, s_);
+        tm_.end(n * 6);
+        acc = DBuf<uint32_t>(&pool_, n);
+        DBuf<uint64_t> nsel(&pool_, 1);
+        tm_.begin("trav_select");
+        select_flagged(cur.p, flags.p, acc.p, nsel.p, n);
+        tm_.end(n * 9);
+        k = read1(nsel.p);
+      } else {
+        acc = std::move(cur);  // the MAXDEPTH level keeps every entry the expansion let through
+      }
       if (!last) launch_trav_accept(acc.p, k, hist.p, first.p, s_);
       if (k) {
         parts.push_back(std::move(acc));
@@ -1394,11 +1408,27 @@ class Executor {
         total += k;
       }
       if (last || k == 0 || (limit > 0 && total >= (uint64_t)limit)) break;
-      cur = ordered_hop(parts.back().p, k, c.hops[0], n);
+      // next level's filter: ¬history ∧ WHILE($depth = d + 1)
+      const uint64_t *np = prog_bitmap(c.pred_prog, d + 1, pscratch);
+      launch_andnot_bitmap(np, hist.p, keep.p, nwords_, s_);
+      cur = ordered_hop(parts.back().p, k, c.hops[0], n, keep.p);
+      filtered = true;
     }
     R_ = limit > 0 ? std::min<uint64_t>(total, (uint64_t)limit) : total;
     bindings_ = total;
     return concat_batches(parts, pn, total);
+  }
+
+  // DeviceSelect::Flagged with 32-bit item counts when they fit (the 64-bit path measured ~10× slower)
+  template <class T>
+  void select_flagged(const T *in, const uint8_t *flags, T *out, uint64_t *nsel, uint64_t n) {
+    if (n < 0x7FFFFFFFull) {
+      DBuf<uint32_t> n32(&pool_, 1);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, in, flags, out, n32.p, (int)n, s_); });
+      launch_post_u32_to_u64(n32.p, nsel, s_);
+    } else {
+      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, in, flags, out, nsel, (int64_t)n, s_); });
+    }
   }
 
   // SELECT expand(m0(...).m1(...)...) FROM <target> [WHERE <cond>] [LIMIT n]: each call moves the whole
@@ -1458,7 +1488,7 @@ class Executor {
     launch_trav_filter(o.dst.p, o.n, A.visited.p, nullptr, first.p, flags.p, true, s_);
     DBuf<uint64_t> keys(&pool_, o.n), sel(&pool_, o.n), nsel(&pool_, 1);
     launch_pack_pairs(o.carry[0].p, o.dst.p, o.n, keys.p, s_);
-    cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, keys.p, flags.p, sel.p, nsel.p, (int64_t)o.n, s_); });
+    select_flagged(keys.p, flags.p, sel.p, nsel.p, o.n);
     const uint64_t k = read1(nsel.p);
     DBuf<uint32_t> next(&pool_, std::max<uint64_t>(k, 1));
     launch_sp_accept(sel.p, k, A.queue.p, A.parent.p, A.visited.p, first.p, next.p, s_);

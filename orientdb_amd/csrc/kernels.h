@@ -238,6 +238,8 @@ void launch_find_rids(const uint64_t *rids, uint32_t V, const uint64_t *keys, ui
 void launch_trav_filter(const uint32_t *w, uint64_t n, const uint64_t *hist, const uint64_t *pred, uint32_t *first,
                         uint8_t *flags, bool dedup, hipStream_t s);
 void launch_trav_accept(const uint32_t *w, uint64_t n, uint64_t *hist, uint32_t *first, hipStream_t s);
+void launch_andnot_bitmap(const uint64_t *pred, const uint64_t *hist, uint64_t *out, uint64_t nwords, hipStream_t s);
+void launch_post_u32_to_u64(const uint32_t *a, uint64_t *b, hipStream_t s);
 // shortestPath: first position meeting the other side's visited set; a level's first discoveries
 void launch_sp_meet(const uint32_t *w, uint64_t n, const uint64_t *other, unsigned long long *pos, hipStream_t s);
 void launch_sp_accept(const uint64_t *keys, uint64_t n, const uint32_t *queue, uint32_t *parent, uint64_t *visited,

@@ -2169,7 +2169,7 @@ __global__ void k_trav_filter(const uint32_t *w, uint64_t n, const uint64_t *his
   const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const uint32_t v = w[e];
-  bool keep = !((hist[v >> 6] >> (v & 63)) & 1);
+  bool keep = !hist || !((hist[v >> 6] >> (v & 63)) & 1);
   if (keep && pred) keep = (pred[v >> 6] >> (v & 63)) & 1;
   // a repeated record (a hub reached from many entries) would serialise on one address: the claim is
   // skipped once an earlier position holds it (blocks run roughly in position order)
@@ -2188,6 +2188,21 @@ void launch_trav_filter(const uint32_t *w, uint64_t n, const uint64_t *hist, con
   if (!dedup) return;
   hipLaunchKernelGGL(k_trav_first, dim3(nblocks(n, 256)), dim3(256), 0, s, w, n, first, flags);
   KCHECK("k_trav_first");
+}
+// out = (pred or all ones) ∧ ¬hist: the next TRAVERSE level's expansion filter
+__global__ void k_andnot_bitmap(const uint64_t *pred, const uint64_t *hist, uint64_t *out, uint64_t nwords) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nwords) out[i] = (pred ? pred[i] : ~0ull) & ~hist[i];
+}
+void launch_andnot_bitmap(const uint64_t *pred, const uint64_t *hist, uint64_t *out, uint64_t nwords, hipStream_t s) {
+  if (!nwords) return;
+  hipLaunchKernelGGL(k_andnot_bitmap, dim3(nblocks(nwords, 256)), dim3(256), 0, s, pred, hist, out, nwords);
+  KCHECK("k_andnot_bitmap");
+}
+__global__ void k_u32_to_u64(const uint32_t *a, uint64_t *b) { *b = *a; }
+void launch_post_u32_to_u64(const uint32_t *a, uint64_t *b, hipStream_t s) {
+  hipLaunchKernelGGL(k_u32_to_u64, dim3(1), dim3(1), 0, s, a, b);
+  KCHECK("k_u32_to_u64");
 }
 // accepted records join the history; their first-position claims are released
 __global__ void k_trav_accept(const uint32_t *w, uint64_t n, uint64_t *hist, uint32_t *first) {

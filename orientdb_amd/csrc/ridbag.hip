@@ -138,13 +138,17 @@ __global__ void k_index_fill(const uint64_t *rids, const T *vals, uint64_t n, co
   }
 }
 
-// One block decodes kDecTile consecutive entries: their rows lie between the rows of the tile's first
-// and last entry (two searches per block), so each entry's row is a short search in that range.
-constexpr int kDecB = 256, kDecIPT = 8, kDecTile = kDecB * kDecIPT;
+// One block decodes kDecTile consecutive entries. Their rows lie between the rows of the tile's first
+// and last entry (two searches per block); the tile's row pointers and payload offsets are staged in
+// LDS, so an entry's row is an LDS search. Each thread then issues its entries' window loads together,
+// and their index lookups together (independent chains in flight instead of one dependent chain).
+constexpr int kDecB = 256, kDecIPT = 8, kDecTile = kDecB * kDecIPT, kDecRows = 1024;
 __global__ __launch_bounds__(kDecB) void k_bag_decode(const uint8_t *s, const uint64_t *pay, uint32_t V,
                                                       const uint64_t *rp, uint64_t E, RidIndex<uint32_t> vix,
                                                       RidIndex<uint64_t> eix, int edges, uint32_t *col, uint32_t *err) {
   __shared__ uint64_t s_r[2];
+  __shared__ uint64_t s_rp[kDecRows + 1];
+  __shared__ uint64_t s_pay[kDecRows];
   for (uint64_t t0 = (uint64_t)blockIdx.x * kDecTile; t0 < E; t0 += (uint64_t)gridDim.x * kDecTile) {
     const uint64_t t1 = min(t0 + (uint64_t)kDecTile, E) - 1;
     if (threadIdx.x < 2) {  // last v with rp[v] <= e
@@ -159,19 +163,42 @@ __global__ __launch_bounds__(kDecB) void k_bag_decode(const uint8_t *s, const ui
     }
     __syncthreads();
     const uint64_t r0 = s_r[0], r1 = s_r[1];
+    const uint64_t nr = r1 - r0 + 1;
+    const bool staged = nr <= kDecRows;
+    if (staged) {
+      for (uint32_t i = threadIdx.x; i <= nr; i += kDecB) s_rp[i] = rp[r0 + i];
+      for (uint32_t i = threadIdx.x; i < nr; i += kDecB) s_pay[i] = pay[r0 + i];
+    }
     __syncthreads();
-#pragma unroll 2
+    uint64_t off[kDecIPT];
+#pragma unroll
     for (int k = 0; k < kDecIPT; ++k) {
       const uint64_t e = t0 + (uint64_t)k * kDecB + threadIdx.x;
-      if (e > t1) break;
-      uint64_t lo = r0, hi = r1;
-      while (lo < hi) {
-        const uint64_t mid = (lo + hi + 1) >> 1;
-        if (rp[mid] <= e) lo = mid;
-        else hi = mid - 1;
+      off[k] = ~0ull;
+      if (e > t1) continue;
+      uint64_t lo = 0, hi = nr - 1;  // row index relative to r0
+      if (staged) {
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi + 1) >> 1;
+          if (s_rp[mid] <= e) lo = mid;
+          else hi = mid - 1;
+        }
+        off[k] = s_pay[lo] + 10ull * (e - s_rp[lo]);
+      } else {
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi + 1) >> 1;
+          if (rp[r0 + mid] <= e) lo = mid;
+          else hi = mid - 1;
+        }
+        off[k] = pay[r0 + lo] + 10ull * (e - rp[r0 + lo]);
       }
-      // the 10-byte entry from the aligned dwords around it (the buffer is padded by 16 bytes)
-      const uint64_t o = pay[lo] + 10ull * (e - rp[lo]);
+    }
+    uint64_t rid[kDecIPT];
+#pragma unroll
+    for (int k = 0; k < kDecIPT; ++k) {  // the 10-byte entries from the aligned dwords around them
+      rid[k] = ~0ull;
+      if (off[k] == ~0ull) continue;
+      const uint64_t o = off[k];
       const uint32_t *w = reinterpret_cast<const uint32_t *>(s + (o & ~3ull));
       const uint32_t sh = (uint32_t)(o & 3) * 8;
       const uint64_t wl = ((uint64_t)w[1] << 32) | w[0], wh = ((uint64_t)(sh ? w[3] : 0u) << 32) | w[2];
@@ -179,27 +206,32 @@ __global__ __launch_bounds__(kDecB) void k_bag_decode(const uint8_t *s, const ui
       const uint64_t b89 = (wh >> sh) & 0xFFFFull;                     // entry bytes 8..9
       const int16_t cl = (int16_t)(((b07 & 0xFF) << 8) | ((b07 >> 8) & 0xFF));
       const uint64_t pos = __builtin_bswap64((b07 >> 16) | (b89 << 48));
-      uint32_t out = 0xFFFFFFFFu;
-      if (cl < 0 || (pos >> 48)) {
-        atomicOr(err, (uint32_t)kBagPosition);
-      } else {
-        uint64_t rid = ((uint64_t)(uint16_t)cl << 48) | pos;
-        bool ok = true;
-        if (edges) {  // an edge record: its opposite vertex
-          uint64_t target;
-          if (eix.find(rid, &target)) rid = target;
-          else {
-            atomicOr(err, (uint32_t)kBagUnknownEdge);
-            ok = false;
-          }
-        }
-        if (ok && !vix.find(rid, &out)) {
-          atomicOr(err, (uint32_t)kBagUnknownRid);
-          out = 0xFFFFFFFFu;
+      if (cl < 0 || (pos >> 48)) atomicOr(err, (uint32_t)kBagPosition);
+      else rid[k] = ((uint64_t)(uint16_t)cl << 48) | pos;
+    }
+    if (edges) {  // edge records: their opposite vertices
+#pragma unroll
+      for (int k = 0; k < kDecIPT; ++k) {
+        if (rid[k] == ~0ull) continue;
+        uint64_t target;
+        if (eix.find(rid[k], &target)) rid[k] = target;
+        else {
+          atomicOr(err, (uint32_t)kBagUnknownEdge);
+          rid[k] = ~0ull;
         }
       }
-      col[e] = out;
     }
+#pragma unroll
+    for (int k = 0; k < kDecIPT; ++k) {
+      if (off[k] == ~0ull) continue;
+      uint32_t out = 0xFFFFFFFFu;
+      if (rid[k] != ~0ull && !vix.find(rid[k], &out)) {
+        atomicOr(err, (uint32_t)kBagUnknownRid);
+        out = 0xFFFFFFFFu;
+      }
+      col[t0 + (uint64_t)k * kDecB + threadIdx.x] = out;
+    }
+    __syncthreads();
   }
 }
 

@@ -99,6 +99,18 @@ def test_partitioned_sliced_kernel(rmat10_full, monkeypatch):
     assert set().union(*[gpu_set(r, cols) for r in res]) == ref.expected(query, cols)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_factorized(rmat10_full, world, monkeypatch):
+    """The factorized expansion (distinct sources, grouped lists, rows over the lists) on every filtered
+    hop of every rank: each rank decides on its own rows, which sit with the owner of their source."""
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    _, ref = rmat10_full
+    for qn in ("c2_both_ends", "three_hop", "triangle_filtered"):
+        name, query, cols = [q for q in RMAT_QUERIES if q[0] == qn][0]
+        res = run_ranks(_parts(world), query)
+        assert set().union(*[gpu_set(r, cols) for r in res]) == ref.expected(query, cols), qn
+
+
 def test_rccl_one_rank_routes_through_itself(rmat10_full, monkeypatch):
     import orientdb_amd as o
     monkeypatch.setenv("OMX_ROUTE_SELF", "1")
