@@ -453,6 +453,30 @@ __global__ void k_hub_rank(const uint32_t *hubs, uint32_t n, uint32_t *hub_idx) 
   if (i < n) hub_idx[hubs[i]] = i;
 }
 
+// Rows of the annotated col re-ordered hub-first by rank (the pull ORs a row's masks in any order):
+// the lanes of a wave then read the hottest hub masks, which share cache lines, before the rest.
+// sort key per entry = row << 32 | (hub ? rank : 2^31 + vertex)
+__global__ void k_row_heads(const uint64_t *rp, uint32_t V, uint32_t *head) {
+  const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < V && rp[v + 1] > rp[v]) head[rp[v]] = (uint32_t)v;
+}
+__global__ void k_pull_keys(const uint32_t *row, const uint32_t *ann, uint64_t E, uint64_t *keys) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t x = ann[e];
+    const uint32_t k = (x >> 31) ? (x & 0x7FFFFFFFu) : (0x80000000u | x);
+    keys[e] = ((uint64_t)row[e] << 32) | k;
+  }
+}
+__global__ void k_pull_unkey(const uint64_t *keys, uint64_t E, uint32_t *ann) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = (uint32_t)keys[e];
+    ann[e] = (k >> 31) ? (k & 0x7FFFFFFFu) : (0x80000000u | k);
+  }
+}
+struct MaxU32 {
+  __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
+};
+
 __global__ void k_pull_annotate(const uint32_t *col, uint64_t E, const uint32_t *hub_idx, uint32_t *out) {
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t c = col[e];
@@ -461,8 +485,8 @@ __global__ void k_pull_annotate(const uint32_t *col, uint64_t E, const uint32_t 
   }
 }
 
-uint32_t build_pull_col(const uint64_t *rp_other, const uint32_t *col, uint32_t V, uint64_t E, uint32_t max_hubs,
-                        uint32_t *hub_idx, uint32_t *hist, unsigned long long *count, uint32_t *hubs,
+uint32_t build_pull_col(const uint64_t *rp_self, const uint64_t *rp_other, const uint32_t *col, uint32_t V, uint64_t E,
+                        uint32_t max_hubs, uint32_t *hub_idx, uint32_t *hist, unsigned long long *count, uint32_t *hubs,
                         uint32_t *out, int cus, hipStream_t s) {
   HIP_CHECK(hipMemsetAsync(hist, 0, kHist * sizeof(uint32_t), s));
   HIP_CHECK(hipMemsetAsync(count, 0, sizeof(unsigned long long), s));
@@ -514,6 +538,43 @@ uint32_t build_pull_col(const uint64_t *rp_other, const uint32_t *col, uint32_t 
     const unsigned ge = (unsigned)std::min<uint64_t>(nblocks(E, kB), (uint64_t)cus * 16);
     hipLaunchKernelGGL(k_pull_annotate, dim3(ge), dim3(kB), 0, s, col, E, hub_idx, out);
     KCHECK("k_pull_annotate");
+    static const bool sort_rows = [] {
+      const char *e = std::getenv("OMX_PULL_SORT");
+      return !(e && std::strcmp(e, "0") == 0);
+    }();
+    if (sort_rows && cum > 0 && E < (1ull << 40)) {
+      uint32_t *row = nullptr;
+      uint64_t *k0 = nullptr, *k1 = nullptr;
+      void *tmp = nullptr;
+      size_t tb = 0;
+      int vbits = 1;
+      while (vbits < 32 && (1ull << vbits) < V) ++vbits;
+      HIP_CHECK(hipMalloc((void **)&row, E * 4));
+      HIP_CHECK(hipMalloc((void **)&k0, E * 8));
+      HIP_CHECK(hipMalloc((void **)&k1, E * 8));
+      HIP_CHECK(hipMemsetAsync(row, 0, E * 4, s));
+      hipLaunchKernelGGL(k_row_heads, dim3(nblocks(V, kB)), dim3(kB), 0, s, rp_self, V, row);
+      KCHECK("k_row_heads");
+      HIP_CHECK(hipcub::DeviceScan::InclusiveScan(nullptr, tb, row, row, MaxU32(), (int64_t)E, s));
+      HIP_CHECK(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+      HIP_CHECK(hipcub::DeviceScan::InclusiveScan(tmp, tb, row, row, MaxU32(), (int64_t)E, s));
+      hipLaunchKernelGGL(k_pull_keys, dim3(ge), dim3(kB), 0, s, row, out, E, k0);
+      KCHECK("k_pull_keys");
+      HIP_CHECK(hipStreamSynchronize(s));
+      (void)hipFree(tmp);
+      tmp = nullptr;
+      tb = 0;
+      HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, k0, k1, (int64_t)E, 0, 32 + vbits, s));
+      HIP_CHECK(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+      HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(tmp, tb, k0, k1, (int64_t)E, 0, 32 + vbits, s));
+      hipLaunchKernelGGL(k_pull_unkey, dim3(ge), dim3(kB), 0, s, k1, E, out);
+      KCHECK("k_pull_unkey");
+      HIP_CHECK(hipStreamSynchronize(s));
+      (void)hipFree(tmp);
+      (void)hipFree(row);
+      (void)hipFree(k0);
+      (void)hipFree(k1);
+    }
   }
   return (uint32_t)cum;
 }

@@ -793,8 +793,8 @@ class Executor {
         HIP_CHECK(hipMalloc((void **)&hubs, std::max<size_t>((size_t)pull_hubs_ * 4, 4)));
         DBuf<uint32_t> hub_idx(&pool_, g_.V), hist(&pool_, 4096);
         DBuf<unsigned long long> cnt(&pool_, 1);
-        nh = build_pull_col(g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, pull_hubs_, hub_idx.p, hist.p, cnt.p, hubs,
-                            pcol, cus(), s_);
+        nh = build_pull_col(g_.rp(es, dir), g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, pull_hubs_, hub_idx.p, hist.p,
+                            cnt.p, hubs, pcol, cus(), s_);
         HIP_CHECK(hipStreamSynchronize(s_));
       } catch (...) {
         if (pcol) (void)hipFree(pcol);
@@ -1235,7 +1235,7 @@ class Executor {
 
   // Factorized expansion of a filtered hop whose rows repeat their source vertices (hubs reached from
   // many roots: C2's second hop reads each distinct b's adjacency 31× over at RMAT-22, 50× at RMAT-24):
-  //   1. the distinct sources U (radix sort + unique) and each row's index into them;
+  //   1. the distinct sources U (V-bit bitmap + list) and each row's index into them;
   //   2. the filtered neighbour list L(u) of every distinct source: one filtered expansion of U rows;
   //   3. L grouped by source into a CSR (histogram, scan, scatter);
   //   4. an unfiltered expansion of the rows over L: dense output of exactly the result rows.
@@ -1246,23 +1246,23 @@ class Executor {
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
-    DBuf<uint32_t> ub(&pool_, R);
+    // the distinct sources, ascending: marked in a V-bit bitmap and listed (no sort of the R rows)
     uint64_t U = 0;
+    DBuf<uint32_t> ub;
     {
-      DBuf<uint32_t> sorted(&pool_, R);
-      DBuf<uint64_t> nsel(&pool_, 1);
-      const int vbits = bits_for(g_.V);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceRadixSort::SortKeys(t, b, src, sorted.p, (int64_t)R, 0, vbits, s_); });
-      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Unique(t, b, sorted.p, ub.p, nsel.p, (int64_t)R, s_); });
-      U = read1(nsel.p);
+      DBuf<uint64_t> ubm(&pool_, std::max<uint64_t>(nwords_, 1));
+      HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+      launch_mark_bitmap(src, R, ubm.p, g_.V, s_);
+      ub = bitmap_list(ubm.p, 0, 1, U);
     }
     const uint64_t Et = degree_sum(src, R, st.adj), EU = degree_sum(ub.p, U, st.adj);
     if (Et < factor_min_ratio_ * EU) return false;
     edges_ += Et;
-    // 1. row → distinct source index
-    DBuf<uint32_t> g(&pool_, R), iu(&pool_, std::max<uint64_t>(U, 1));
-    launch_index_of(ub.p, U, src, R, g.p, s_);
+    // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
+    DBuf<uint32_t> g(&pool_, R), iu(&pool_, std::max<uint64_t>(U, 1)), pos(&pool_, std::max<uint64_t>(g_.V, 1));
     launch_iota(iu.p, U, s_);
+    launch_scatter_u32(ub.p, iu.p, U, pos.p, s_);
+    launch_gather_u32(pos.p, src, R, g.p, s_);
     // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
     ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true);
     edges_iter_ += l.E;

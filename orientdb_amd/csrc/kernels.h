@@ -231,6 +231,7 @@ void launch_flag_no_neighbor(const uint32_t *src, uint64_t R, const DAdj &adj, c
 void launch_check_optional(const uint32_t *src, uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
                            uint32_t V, unsigned int *npe, hipStream_t s);
 void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out, hipStream_t s);
+void launch_scatter_u32(const uint32_t *idx, const uint32_t *val, uint64_t n, uint32_t *out, hipStream_t s);
 void launch_flag_row_change(int ncols, const uint32_t *const *cols, uint64_t n, uint8_t *flags, hipStream_t s);
 // TRAVERSE: RID lookup of the target records; a level's history / WHILE filter with first-position
 // claims (dedup); the accepted records into the history
@@ -270,7 +271,9 @@ void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const 
                      uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *visited,
                      uint64_t *next, int cus, hipStream_t s);
 // hub-annotated col of a CSR for k_bfs_pull (returns the hub count; hub_idx u32[V], hist u32[4096] scratch)
-uint32_t build_pull_col(const uint64_t *rp_other, const uint32_t *col, uint32_t V, uint64_t E, uint32_t max_hubs,
+// rp_self: the CSR's own row pointers (its rows are re-ordered hub-first; OMX_PULL_SORT=0 keeps them)
+uint32_t build_pull_col(const uint64_t *rp_self, const uint64_t *rp_other, const uint32_t *col, uint32_t V, uint64_t E,
+                        uint32_t max_hubs,
                         uint32_t *hub_idx, uint32_t *hist, unsigned long long *count, uint32_t *hubs,
                         uint32_t *out, int cus, hipStream_t s);
 void launch_hub_gather(const uint32_t *hubs, uint32_t n, const uint64_t *frontier, uint64_t *hub_fr, hipStream_t s);

@@ -2330,6 +2330,16 @@ void launch_mark_bitmap(const uint32_t *v, uint64_t n, uint64_t *bm, uint32_t V,
   KCHECK("k_mark_bitmap");
 }
 
+// out[idx[i]] = val[i]
+__global__ void k_scatter_u32(const uint32_t *idx, const uint32_t *val, uint64_t n, uint32_t *out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[idx[i]] = val[i];
+}
+void launch_scatter_u32(const uint32_t *idx, const uint32_t *val, uint64_t n, uint32_t *out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_scatter_u32, dim3(nblocks(n, 256)), dim3(256), 0, s, idx, val, n, out);
+  KCHECK("k_scatter_u32");
+}
 __global__ void k_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = src[idx[i]];
