@@ -23,6 +23,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <climits>
+#include <cstdint>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -105,14 +107,23 @@ __device__ __forceinline__ uint64_t find_sorted(const uint64_t *sorted, uint64_t
 // are appended) index a table, base[cluster] + position; otherwise a binary search over a RID-sorted copy.
 template <class T>
 struct RidIndex {
-  const int64_t *base;   // [32768] table offset of each cluster, -1 if absent (direct mode)
+  const int64_t *base;   // [32768] table offset of each cluster, -1 if absent (direct mode); affine: value − position
   const uint64_t *lim;   // [32768] positions of the cluster are < lim
+  const uint64_t *lo;    // [32768] affine mode: positions are ≥ lo
   const T *table;        // direct mode; sentinel ~0 = no record
   const uint64_t *keys;  // sorted mode
   const T *vals;
   uint64_t n;
   int direct;
+  int affine;            // every cluster's records hold contiguous positions at consecutive values
   __device__ __forceinline__ bool find(uint64_t rid, T *out) const {
+    if (affine) {  // dense layout of the clusters (records appended, none deleted): no table read
+      const uint32_t c = (uint32_t)(rid >> 48);
+      const uint64_t p = rid & ((1ull << 48) - 1);
+      if (c >= 32768 || p < lo[c] || p >= lim[c]) return false;
+      *out = (T)(base[c] + (int64_t)p);
+      return true;
+    }
     if (direct) {
       const uint32_t c = (uint32_t)(rid >> 48);
       const uint64_t p = rid & ((1ull << 48) - 1);
@@ -250,7 +261,7 @@ struct DevArr {
 template <class T>
 struct HostIndex {
   std::unique_ptr<DevArr<int64_t>> base;
-  std::unique_ptr<DevArr<uint64_t>> lim, keys;
+  std::unique_ptr<DevArr<uint64_t>> lim, lo, keys;
   std::unique_ptr<DevArr<T>> table, vals;
   RidIndex<T> dev{};
 };
@@ -266,6 +277,43 @@ void build_index(HostIndex<T> &ix, const uint64_t *rids, const T *vals, uint64_t
       break;
     }
     hl[c] = std::max(hl[c], p + 1);
+  }
+  // affine: values are the positions i (vertex table) and every cluster's RIDs are contiguous positions
+  // p0 … p0 + k − 1 held by consecutive i (value = p + delta): the canonical snapshot order
+  if (packable && !vals && n) {
+    std::vector<int64_t> delta(32768, INT64_MIN);
+    std::vector<uint64_t> cnt(32768, 0), mn(32768, UINT64_MAX);
+    bool affine = true;
+    for (uint64_t i = 0; i < n && affine; ++i) {
+      const uint64_t c = rids[i] >> 48, p = rids[i] & ((1ull << 48) - 1);
+      const int64_t d = (int64_t)i - (int64_t)p;
+      if (delta[c] == INT64_MIN) delta[c] = d;
+      else if (delta[c] != d) affine = false;
+      ++cnt[c];
+      mn[c] = std::min(mn[c], p);
+    }
+    for (int c = 0; c < 32768 && affine; ++c)
+      if (cnt[c] && hl[c] - mn[c] != cnt[c]) affine = false;  // no holes, no repeats
+    if (affine) {
+      std::vector<uint64_t> hlo(32768, 0);
+      for (int c = 0; c < 32768; ++c) {
+        hlo[c] = cnt[c] ? mn[c] : 0;
+        hb[c] = cnt[c] ? delta[c] : 0;
+        if (!cnt[c]) hl[c] = 0;
+      }
+      ix.base.reset(new DevArr<int64_t>(32768));
+      ix.lim.reset(new DevArr<uint64_t>(32768));
+      ix.lo.reset(new DevArr<uint64_t>(32768));
+      HIP_CHECK(hipMemcpyAsync(ix.base->p, hb.data(), 32768 * 8, hipMemcpyHostToDevice, s));
+      HIP_CHECK(hipMemcpyAsync(ix.lim->p, hl.data(), 32768 * 8, hipMemcpyHostToDevice, s));
+      HIP_CHECK(hipMemcpyAsync(ix.lo->p, hlo.data(), 32768 * 8, hipMemcpyHostToDevice, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      ix.dev.base = ix.base->p;
+      ix.dev.lim = ix.lim->p;
+      ix.dev.lo = ix.lo->p;
+      ix.dev.affine = 1;
+      return;
+    }
   }
   uint64_t total = 0;
   if (packable)
