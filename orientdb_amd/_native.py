@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libomx.so")
+# OMX_LIB: an alternative build of the same library (A/B experiments under tools/)
+LIB_PATH = os.environ.get("OMX_LIB") or os.path.join(_HERE, "_lib", "libomx.so")
 
 OMX_OK, OMX_E_UNSUPPORTED, OMX_E_INVALID, OMX_E_OOM, OMX_E_DEVICE, OMX_E_PARSE, OMX_E_EXECUTION = range(7)
 OMX_PROP_INT32, OMX_PROP_INT64, OMX_PROP_DOUBLE, OMX_PROP_STRING, OMX_PROP_BOOL = 1, 2, 3, 4, 5
