@@ -47,8 +47,10 @@ QUERIES = {
            "TRAVERSE out('Knows') FROM #11:{hub} STRATEGY BREADTH_FIRST", 24),
     "s1": ("S1: SELECT expand(out('Knows').out('Knows')) from the highest-degree vertex (rows with repeats)",
            "SELECT expand(out('Knows').out('Knows')) FROM #11:{hub}", 22),
+    "p1": ("P1: shortestPath() over out('Knows') from the lowest-id vertex of out-degree 1 to the highest-degree vertex",
+           "SELECT expand(shortestPath(#11:{leaf}, #11:{hub}, 'OUT', 'Knows'))", 24),
 }
-CHAIN = {"t1", "s1"}
+CHAIN = {"t1", "s1", "p1"}
 # Weak scaling over roots on the replicated graph (each root's DFS subtree is independent):
 # at N ranks the root window widens N-fold and every rank keeps ≈ the N=1 share (roots v % N == rank),
 # so per-GPU work is fixed as N grows. At N=1 the query is exactly configs[1]'s.
@@ -64,7 +66,7 @@ def scaled_query(name, query, world, partitioned):
     return query, "strong"
 
 
-REPLICATED_ONLY = {"c1", "c3", "c4", "t1", "s1"}  # per-GPU structures: C3 multi-source BFS lane masks, C4 LDBC replica; C1 all-root fof
+REPLICATED_ONLY = {"c1", "c3", "c4", "t1", "s1", "p1"}  # per-GPU structures: C3 multi-source BFS lane masks, C4 LDBC replica; C1 all-root fof
 COUNT_MODE = {"c5"}   # the last hop counts its rows (count mode)
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # ≈7e4 Person, ≈2e6 Knows
 # kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)
@@ -145,11 +147,41 @@ def cpu_baseline_chain(g, query, target_s):
                 what, secs, seen[0])}
 
 
+def cpu_baseline_shortest(g, query, target_s):
+    """shortestPath: the oracle's restatement (oracle/shortest_path_ref.py, pure Python, one core) on the
+    same pair, repeated to ≈ target_s / 4; GTEPS = adjacency entries its walks iterated / its time."""
+    import re
+    from oracle.shortest_path_ref import shortest_path
+    from orientdb_amd.graph import csr_transpose
+    rp, col = g.csr
+    a, b = (int(x) for x in re.findall(r"#11:(\d+)", query)[:2])
+    irp, icol = csr_transpose(g.V, rp, col)
+    seen = [0]
+
+    def nb(r, c):
+        def f(v):
+            row = c[r[v]:r[v + 1]].tolist()
+            seen[0] += len(row)
+            return row
+        return f
+    secs, reps = 0.0, 0
+    while secs < target_s / 4 and reps < 100:
+        t0 = time.perf_counter()
+        shortest_path(a, b, nb(rp, col), nb(irp, icol))
+        secs += time.perf_counter() - t0
+        reps += 1
+    return {"value": seen[0] / secs / 1e9, "unit": "GTEPS", "cores": 1, "kind": "port",
+            "sample": "the same pair x %d (%.1f s, %d adjacency entries; oracle/shortest_path_ref.py, pure Python, "
+                      "1 thread)" % (reps, secs, seen[0])}
+
+
 def cpu_baseline(g, query, target_s=12.0):
     """The oracle's C DFS restatement (oracle/dfs_ref.c) on the host cores, on a bounded sample of
     the same workload's roots; GTEPS over the sampled roots."""
     import numpy as np
     from oracle import dfs
+    if "shortestPath" in query:
+        return cpu_baseline_shortest(g, query, target_s)
     if query.startswith(("TRAVERSE", "SELECT")):
         return cpu_baseline_chain(g, query, target_s)
     threads, visible = host_threads()
@@ -279,7 +311,9 @@ def main():
     t_build = time.perf_counter() - t_build
     if "{hub}" in query:  # the vertex of highest out-degree (lowest id on ties)
         import numpy as np
-        query = query.replace("{hub}", str(int(np.argmax(np.diff(g.csr[0].astype(np.int64))))))
+        deg = np.diff(g.csr[0].astype(np.int64))
+        query = query.replace("{hub}", str(int(np.argmax(deg))))
+        query = query.replace("{leaf}", str(int(np.argmax(deg == 1))))
     st = o.OMatchStatement(query)
     flags = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_KERNEL_TIMING | o.OMX_FLAG_TIME_HOT
     mode = o.OMX_MODE_COUNT if (args.query in COUNT_MODE or args.count) else o.OMX_MODE_MATERIALIZE

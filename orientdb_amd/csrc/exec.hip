@@ -137,7 +137,10 @@ class Executor {
       heavy_deg_sliced_ = heavy_deg_;
       heavy_deg_fixed_ = true;
     }
-    if (const char *h = std::getenv("OMX_HEAVY_DEG_UNFILTERED")) heavy_deg_unfiltered_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
+    if (const char *h = std::getenv("OMX_HEAVY_DEG_UNFILTERED")) {
+      heavy_deg_unfiltered_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
+      heavy_deg_unfiltered_set_ = true;
+    }
     // variable-length strategy: "bfs" (multi-source BFS whenever exact), "pairs" ((row, v) levels), auto
     if (const char *v = std::getenv("OMX_VARLEN")) varlen_mode_ = v;
     if (const char *sl = std::getenv("OMX_SLICED")) sliced_ = std::strcmp(sl, "0") != 0;
@@ -373,7 +376,8 @@ class Executor {
   uint64_t heavy_deg_ = kHeavyDeg;
   uint64_t heavy_deg_sliced_ = kHeavyDegSliced;
   bool heavy_deg_fixed_ = false;  // OMX_HEAVY_DEG given
-  uint64_t heavy_deg_unfiltered_ = kHeavyDeg;  // unfiltered hops (OMX_HEAVY_DEG_UNFILTERED)
+  uint64_t heavy_deg_unfiltered_ = kHeavyDeg;  // unfiltered hops (OMX_HEAVY_DEG_UNFILTERED, over OMX_HEAVY_DEG)
+  bool heavy_deg_unfiltered_set_ = false;
   bool debug_expand_ = false;
   bool light_sliced_ = true;  // LDS-sliced light kernel for sliced single-part hops (OMX_LIGHT_SLICED=0: merge path)
   bool sliced_ = true;  // LDS-sliced heavy kernel for filtered hops (OMX_SLICED=0 disables)
@@ -865,7 +869,7 @@ class Executor {
     // ordered (TRAVERSE / SELECT expand): every row through the merge-path kernel, whose dense output is
     // in row order (the heavy kernel's rows would come first); filtered, one tile per block (below)
     const uint64_t hd = ordered ? UINT64_MAX
-                        : (!filter && !member && !heavy_deg_fixed_) ? heavy_deg_unfiltered_
+                        : (!filter && !member && (!heavy_deg_fixed_ || heavy_deg_unfiltered_set_)) ? heavy_deg_unfiltered_
                         : !sliced ? heavy_deg_
                         : heavy_deg_fixed_ ? heavy_deg_sliced_
                                            : std::max<uint64_t>(heavy_deg_sliced_, 128ull * P);
