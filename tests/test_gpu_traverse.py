@@ -246,3 +246,108 @@ def test_shortest_path_missing_vertex(rmat10):
     g, _ = rmat10
     with pytest.raises(o.OmxExecutionError):
         o.OMatchStatement("SELECT shortestPath(#11:1, #11:99999999)").execute(g)
+
+
+# ---- the reference's known-answer graph (OMatchStatementExecutionTest's @BeforeClass data) -------------
+
+class _DbAdj:
+    """Adjacency of every edge class of tests/golden/match_test_db.json as the snapshot holds it
+    (out rows in insertion order, in rows = the stable transpose)."""
+
+    def __init__(self, db):
+        from orientdb_amd.graph import csr_transpose, records_arrays
+        V, classes, vclass, rids, edge_sets, props, _ = records_arrays(db)
+        self.V, self.rids = V, rids
+        self.names = [c[0] for c in classes]
+        self.adj = {}
+        for es in edge_sets:
+            rp, col = es["out_rp"], es["out_col"]
+            irp, icol = csr_transpose(V, rp, col)
+            self.adj[self.names[es["cls"]]] = (rp, col, irp, icol)
+        self.name = {p["name"]: p for p in props}.get("name")
+        self.vclass = vclass
+
+    def out(self, label):
+        rp, col, _, _ = self.adj[label]
+        return lambda v: [int(x) for x in col[rp[v]:rp[v + 1]]]
+
+    def inn(self, label):
+        _, _, irp, icol = self.adj[label]
+        return lambda v: [int(x) for x in icol[irp[v]:irp[v + 1]]]
+
+    def both(self, label):
+        o, i = self.out(label), self.inn(label)
+        return lambda v: o(v) + i(v)
+
+    def name_of(self, v):
+        p = self.name
+        return p["dict"][p["values"][v]] if p["present"][v] else None
+
+    def rid(self, v):
+        r = int(self.rids[v])
+        return "#%d:%d" % (r >> 48, r & ((1 << 48) - 1))
+
+    def find(self, name):
+        return next(v for v in range(self.V) if self.name_of(v) == name)
+
+
+@pytest.fixture(scope="module")
+def kdb(match_test_db_json):
+    import orientdb_amd as o
+    return o.GraphSnapshot.from_records(match_test_db_json, device=0), _DbAdj(match_test_db_json)
+
+
+def _rid_list(rs):
+    return [(int(r[0]), int(r[1])) for r in rs]
+
+
+def _as_rids(a, vs):
+    return [(int(a.rids[v]) >> 48, int(a.rids[v]) & ((1 << 48) - 1)) for v in vs]
+
+
+def test_known_db_traverse(kdb):
+    import orientdb_amd as o
+    g, a = kdb
+    n1 = a.find("n1")
+    cases = [
+        (f"TRAVERSE out('Friend') FROM {a.rid(n1)} WHILE $depth < 3 STRATEGY BREADTH_FIRST",
+         dict(fields=lambda v: [a.out("Friend")(v)], predicate=lambda v, d: d < 3)),
+        (f"TRAVERSE both('Friend') FROM {a.rid(n1)} STRATEGY BREADTH_FIRST",
+         dict(fields=lambda v: [a.both("Friend")(v)])),
+        # legacy null semantics: vertices without `name` fail `name > 'n2'` (no NullPointerException)
+        (f"TRAVERSE both('Friend') FROM {a.rid(n1)} WHILE name > 'n2' or $depth = 0 STRATEGY BREADTH_FIRST",
+         dict(fields=lambda v: [a.both("Friend")(v)],
+              predicate=lambda v, d: d == 0 or (a.name_of(v) is not None and a.name_of(v) > "n2"))),
+        (f"TRAVERSE in('Friend') FROM [{a.rid(a.find('n4'))}, {a.rid(a.find('n6'))}] MAXDEPTH 2 STRATEGY BREADTH_FIRST",
+         dict(roots=[a.find("n4"), a.find("n6")], fields=lambda v: [a.inn("Friend")(v)], max_depth=2)),
+    ]
+    for q, kw in cases:
+        roots = kw.pop("roots", [n1])
+        f = kw.pop("fields")
+        want = traverse(roots, f, strategy=BREADTH_FIRST, **kw)
+        assert _rid_list(o.OMatchStatement(q).execute(g)) == _as_rids(a, want), q
+
+
+def test_known_db_class_target_and_chains(kdb):
+    import orientdb_amd as o
+    g, a = kdb
+    dept = [v for v in range(a.V) if a.names[a.vclass[v]] == "Department"]
+    want = traverse(dept, lambda v: [a.out("ParentDepartment")(v)], max_depth=2, strategy=BREADTH_FIRST)
+    q = "TRAVERSE out('ParentDepartment') FROM Department MAXDEPTH 2 STRATEGY BREADTH_FIRST"
+    assert _rid_list(o.OMatchStatement(q).execute(g)) == _as_rids(a, want)
+    persons = [v for v in range(a.V) if a.names[a.vclass[v]] == "Person" and a.name_of(v) in ("n1", "n2")]
+    want = expand_chain(persons, [a.out("Friend"), a.out("Friend")])
+    q = "SELECT expand(out('Friend').out('Friend')) FROM Person WHERE name = 'n1' or name = 'n2'"
+    assert _rid_list(o.OMatchStatement(q).execute(g)) == _as_rids(a, want)
+
+
+def test_known_db_shortest_path(kdb):
+    from oracle.shortest_path_ref import shortest_path
+    import orientdb_amd as o
+    g, a = kdb
+    people = [a.find("n%d" % i) for i in range(1, 7)]
+    for s in people:
+        for t in people:
+            want = shortest_path(s, t, a.both("Friend"), a.both("Friend"))
+            rs = o.OMatchStatement(f"SELECT expand(shortestPath({a.rid(s)}, {a.rid(t)}, 'BOTH', 'Friend'))").execute(g)
+            assert _rid_list(rs) == _as_rids(a, want), (s, t)
