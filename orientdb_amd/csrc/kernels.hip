@@ -1569,59 +1569,12 @@ void launch_expand_light_sliced(const ExpandArgs &a, const SliceArgs &sa, unsign
   KCHECK("k_expand_light_sliced");
 }
 
-// Unfiltered light rows of a single-part adjacency written densely (the rows' outputs are consecutive:
-// row r's entries go to dense_base + [offs[r], offs[r+1])). Each wave owns output segments of kDenseSeg
-// entries and walks them 64 at a time; a lane finds the row of its own output by a short forward scan
-// from the window's first row (rows are consecutive), so loads stay contiguous inside a row and every
-// store is a full contiguous wave store — the merge-path kernel's LDS row bookkeeping is not needed
-// when nothing is filtered.
-constexpr uint64_t kDenseSeg = 1024;
-__global__ __launch_bounds__(256) void k_expand_dense_rows(ExpandArgs a) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t wid = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nw = (uint64_t)gridDim.x * 4;
-  const uint64_t *offs = a.offs;
-  const uint32_t *col = a.adj.p[0].col;
-  const int nc = a.ncarry;
-  for (uint64_t s0 = wid * kDenseSeg; s0 < a.E; s0 += nw * kDenseSeg) {
-    const uint64_t s1 = min(s0 + kDenseSeg, a.E);
-    uint64_t lo = 0, hi = a.R;  // the row holding output s0: last r with offs[r] <= s0
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi + 1) >> 1;
-      if (offs[mid] <= s0) lo = mid;
-      else hi = mid - 1;
-    }
-    uint64_t r = lo;
-    for (uint64_t o = s0; o < s1; o += 64) {
-      while (offs[r + 1] <= o) ++r;  // uniform: the window's first row (zero-length rows skipped)
-      const uint64_t j = o + lane;
-      if (j < s1) {
-        uint64_t rr = r;
-        while (offs[rr + 1] <= j) ++rr;
-        const uint64_t out = a.dense_base + j;
-        a.out_dst[out] = col[a.lbase[rr] + (j - offs[rr])];
-        for (int k = 0; k < nc; ++k) a.carry_out[k][out] = a.carry_in[k][rr];
-      }
-    }
-  }
-}
-static bool dense_rows() {  // OMX_DENSE_ROWS=0: the merge-path kernel for unfiltered light rows (A/B)
-  static const bool on = [] {
-    const char *e = std::getenv("OMX_DENSE_ROWS");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  return on;
-}
-
 void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s) {
   if (!grid) return;
   const bool single = a.adj.n == 1, member = a.member_src != nullptr, filter = a.filter != nullptr || member;
   dim3 g(grid), b(kExpandBlock);
-  if (single && !filter && write && dense_rows()) {
-    hipLaunchKernelGGL(k_expand_dense_rows, g, dim3(256), 0, s, a);
-    KCHECK("k_expand_dense_rows");
-    return;
-  }
+  // (unfiltered rows: a wave-per-output-window kernel without the LDS row bookkeeping measured 1.6×
+  // slower than these merge-path tiles, profiles/r02/dense)
 #define OMX_EXP(S, F, Wr, M) hipLaunchKernelGGL((k_expand<S, F, Wr, M>), g, b, 0, s, a)
 #define OMX_EXP_W(S, F, M) { if (write) OMX_EXP(S, F, true, M); else OMX_EXP(S, F, false, M); }
   if (single) {
