@@ -149,7 +149,7 @@ class Executor {
     if (const char *f = std::getenv("OMX_FUSE_CHECK")) fuse_mode_ = f;  // "0" disables the intersection
     if (const char *sw = std::getenv("OMX_SWAP_CHECK")) swap_ = std::strcmp(sw, "0") != 0;
     if (const char *hb = std::getenv("OMX_PULL_HUBS")) pull_hubs_ = (uint32_t)std::strtoul(hb, nullptr, 10);
-    if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max<uint64_t>(1, std::strtoull(d, nullptr, 10));
+    if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max(1e-9, std::strtod(d, nullptr));
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
     bound_.assign(p.aliases.size(), 0);
@@ -388,7 +388,7 @@ class Executor {
   // hub masks packed for the pull kernel in degree-rank order (8 MiB); 0 = plain col. 2^20 measured best
   // of 2^17…2^22 at C3 (profiles/r02/c3rank: pull 4.26 → 4.07 ms per step against 2^18 in vertex order)
   uint32_t pull_hubs_ = 1u << 20;
-  uint64_t pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
+  double pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
   // sliced hops size their arenas from the target bitmap's density (OMX_ARENA_ESTIMATE=0: exact bound;
   // OMX_ARENA_MARGIN scales the estimate, 0 forces the short-arena re-run in tests)
@@ -1894,9 +1894,9 @@ class Executor {
         HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
         if (debug_expand_)
           std::fprintf(stderr, "[omx bfs] batch %llu level %lld: %s active=%llu push_edges=%llu E_t=%llu\n",
-                       (unsigned long long)row0, (long long)d, h[1] * pull_div_ > eadj ? "pull" : "push",
+                       (unsigned long long)row0, (long long)d, (double)h[1] * pull_div_ > (double)eadj ? "pull" : "push",
                        (unsigned long long)h[2], (unsigned long long)h[1], (unsigned long long)h[0]);
-        if (h[1] * pull_div_ > eadj) {
+        if ((double)h[1] * pull_div_ > (double)eadj) {
           for (int p = 0; p < radj.n; ++p) {
             const uint64_t nt = bfs_pull_tiles(V, pull_E[p]);
             if (!pull_part[p]) {
