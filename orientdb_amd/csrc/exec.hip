@@ -1333,7 +1333,10 @@ class Executor {
       if (v != UINT32_MAX) found.push_back(v);
     DBuf<uint32_t> r(&pool_, std::max<size_t>(found.size(), 1));
     n = found.size();
-    if (n) HIP_CHECK(hipMemcpyAsync(r.p, found.data(), n * 4, hipMemcpyHostToDevice, s_));
+    if (n) {
+      HIP_CHECK(hipMemcpyAsync(r.p, found.data(), n * 4, hipMemcpyHostToDevice, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));  // `found` leaves scope
+    }
     const uint64_t *wb = prog_bitmap(where, 0, wscratch);
     if (!n || !wb) return r;
     DBuf<uint8_t> flags(&pool_, n);
