@@ -48,13 +48,14 @@ void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *front
 // merged into visited; if the level expands, m is cut to the `while` bitmap and the frontier's
 // statistics are accumulated (one atomic per block and counter): stats[0] = Σ popc(m)·deg (the edges
 // the reference traverses, SURVEY §8(d) E_t), stats[1] = Σ deg over active vertices (push work),
-// stats[2] = active vertices.
+// stats[2] = active vertices, stats[3] = OR of m (the live lanes: a lane whose frontier is empty
+// reaches nothing more, so the pull does not wait for it).
 __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V,
                                                  const uint64_t *while_bm, int expand, DAdj adj,
-                                                 unsigned long long *stats) {
-  __shared__ uint64_t s_r[3][kB / 64];
+                                                 unsigned long long *stats, uint64_t *fbm) {
+  __shared__ uint64_t s_r[4][kB / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint64_t te = 0, td = 0, tn = 0;
+  uint64_t te = 0, td = 0, tn = 0, tl = 0;
   for (uint64_t v0 = (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
     const uint64_t v = v0 + threadIdx.x;
     const uint64_t f = v < V ? frontier[v] : 0;
@@ -70,29 +71,40 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
         te += (uint64_t)__popcll(m) * d;
         td += d;
         tn += 1;
+        tl |= m;
       }
     }
+    const uint64_t word = __ballot(m != 0);  // bit v of fbm: v's frontier mask is non-empty
+    if (fbm && lane == 0 && v0 + wave * 64 < V) fbm[(v0 >> 6) + wave] = word;
   }
   if (!expand) return;
   te = wave_sum_u64(te);
   td = wave_sum_u64(td);
   tn = wave_sum_u64(tn);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) tl |= __shfl_xor(tl, off, 64);
   if (lane == 0) {
     s_r[0][wave] = te;
     s_r[1][wave] = td;
     s_r[2][wave] = tn;
+    s_r[3][wave] = tl;
   }
   __syncthreads();
   if (threadIdx.x < 3) {
     uint64_t x = 0;
     for (int w = 0; w < kB / 64; ++w) x += s_r[threadIdx.x][w];
     if (x) atomicAdd(&stats[threadIdx.x], (unsigned long long)x);
+  } else if (threadIdx.x == 3) {
+    uint64_t x = 0;
+    for (int w = 0; w < kB / 64; ++w) x |= s_r[3][w];
+    if (x) atomicOr(&stats[3], (unsigned long long)x);
   }
 }
 void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
-                     const DAdj &adj, unsigned long long *stats, int cus, hipStream_t s) {
+                     const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s) {
   const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 8);
-  hipLaunchKernelGGL(k_bfs_prep, dim3(g), dim3(kB), 0, s, frontier, visited, V, while_bm, (int)expand, adj, stats);
+  hipLaunchKernelGGL(k_bfs_prep, dim3(g), dim3(kB), 0, s, frontier, visited, V, while_bm, (int)expand, adj, stats,
+                     fbm);
   KCHECK("k_bfs_prep");
 }
 
@@ -161,15 +173,21 @@ void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, u
 __global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part);
 
 // Bottom-up over one reversed adjacency part: merge-path tiles of kPullTile items over (vertices +
-// in-edges), partitioned once per traversal from the part's row_ptr (k_pull_partition with offs = rp). Consecutive lanes take consecutive in-edges (coalesced col[] loads); the in-edges of a
-// vertex whose lanes are all visited are skipped; each edge gathers its source's frontier mask. The
-// col array is the hub-annotated copy (k_pull_annotate): in RMAT most in-edges come from a few
-// hundred thousand high-degree sources, whose masks scattered over the V·8-B frontier cost one cache
-// line each; their copies in the dense hub array (k_hub_gather, ≤ 2 MiB) stay in L2 (C3: pull
-// 7.5 → 5.6 ms). A one-bit "frontier non-empty" probe before the gather of a non-hub mask was
-// measured 10-15% slower, with or without the hub array.
-// Masks are OR-reduced per vertex by a segmented wave scan, merged in LDS (ds_or_b64) and written
-// with one atomicOr per vertex and tile (next[] is zeroed first; k_bfs_prep masks out visited lanes).
+// in-edges), partitioned once per traversal from the part's row_ptr (k_pull_partition with offs = rp).
+// Consecutive lanes take consecutive in-edges (coalesced col[] loads); the in-edges of a vertex that
+// misses no live lane are skipped; each edge gathers its source's frontier mask. The col array is the
+// hub-annotated copy (k_pull_annotate): in RMAT most in-edges come from a few hundred thousand
+// high-degree sources, whose masks scattered over the V·8-B frontier cost one cache line each; their
+// copies in the dense hub array (k_hub_gather) mostly hit L2 (C3: pull 7.5 → 5.6 ms).
+// PROBE (levels whose frontier is sparse): a non-hub mask is gathered only if its bit in the frontier
+// bitmap (V bits, L2-resident) is set. On the dense level the probe costs more than it saves, and a
+// probe of the hubs' bitmap before a hub mask was slower on both (profiles/r02/c3probe, c3hbm).
+// Masks are OR-reduced per vertex in LDS (ds_or_b64) and written with one atomicOr per vertex and tile
+// (next[] is zeroed first; k_bfs_prep masks out visited lanes).
+// Measured and rejected (profiles/r02/c3var, c3pipe, c3direct, c3flat): non-temporal loads of the
+// streamed arrays (no change); the next tile's loads issued before this tile's gathers (no change,
+// fewer waves); a flat kernel without tiles (a per-edge owner array, segmented DPP OR, global atomics:
+// 4.0 against 3.3 ms per C3 step).
 #ifndef OMX_PULL_B
 #define OMX_PULL_B 256
 #endif
@@ -179,10 +197,12 @@ __global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, u
 constexpr int kPullB = OMX_PULL_B, kPullIPT = OMX_PULL_IPT, kPullTile = kPullB * kPullIPT;
 static_assert(kPullTile <= 65535, "s_seg holds tile-local row indices in 16 bits");
 
+template <bool PROBE>
 __global__ __launch_bounds__(kPullB) void k_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col,
                                                      const uint64_t *part, uint64_t E, uint64_t ntiles,
                                                      uint64_t lanes, const uint64_t *frontier,
-                                                     const uint64_t *hub_fr, const uint64_t *visited, uint64_t *next) {
+                                                     const uint64_t *hub_fr, const uint64_t *fbm,
+                                                     const uint64_t *visited, uint64_t *next) {
   constexpr int B = kPullB, IPT = kPullIPT, T = kPullTile, W = B / 64;
   // tile item jl is in-edge j0 + jl (merge-path tiles cover consecutive edges), so a row needs only
   // its lane mask and accumulator here: 18 B per row + 2 B per item → 8 workgroups per CU
@@ -200,6 +220,14 @@ __global__ __launch_bounds__(kPullB) void k_bfs_pull(uint32_t V, const uint64_t 
     if (ne == 0) continue;  // uniform: only edge-less vertices in this tile
     const uint64_t rlast = min(i1, (uint64_t)V - 1);
     const uint32_t nr = (uint32_t)(rlast - i0 + 1);
+    // the tile's col words are requested first, so their round trip overlaps the row setup's
+    // (C3 pull 3.69 → 3.48 ms per step, profiles/r02/c3var)
+    uint32_t xk[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const uint32_t jl = k * B + tid;
+      xk[k] = jl < ne ? col[j0 + jl] : 0u;
+    }
     for (uint32_t x = tid; x < ne; x += B) s_seg[x] = 0;
     __syncthreads();
     for (uint32_t lr = tid; lr < nr; lr += B) {
@@ -242,42 +270,30 @@ __global__ __launch_bounds__(kPullB) void k_bfs_pull(uint32_t V, const uint64_t 
       }
     }
     __syncthreads();
-    // all IPT gathers are issued before the first reduction consumes one (IPT independent
-    // col → frontier chains in flight per lane)
+    // all IPT gathers are issued before the first merge consumes one (IPT independent chains in
+    // flight per lane); every non-empty mask is merged by its own LDS atomic (a segmented wave scan
+    // first measured 1-2% slower)
     uint64_t fk[IPT];
     uint32_t lrk[IPT];
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const uint32_t jl = k * B + tid;
-      const bool valid = jl < ne;
-      const uint32_t lr = valid ? s_seg[jl] : 0xFFFFu;
+      const uint32_t lr = jl < ne ? s_seg[jl] : 0u;
       uint64_t f = 0;
-      if (valid) {
+      if (jl < ne) {
         const uint64_t need = s_need[lr];
+        const uint32_t x = xk[k];
         if (need) {
-          const uint32_t x = col[j0 + jl];
-          f = (x >> 31 ? hub_fr[x & 0x7FFFFFFFu] : frontier[x]) & need;
+          if (x >> 31) f = hub_fr[x & 0x7FFFFFFFu] & need;
+          else if (!PROBE || ((fbm[x >> 6] >> (x & 63)) & 1)) f = frontier[x] & need;
         }
       }
       fk[k] = f;
       lrk[k] = lr;
     }
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      const bool valid = k * B + tid < ne;
-      const uint32_t lr = lrk[k];
-      uint64_t f = fk[k];
-      // segmented inclusive OR over the wave (a vertex's edges are consecutive lanes)
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint64_t yf = __shfl_up(f, off, 64);
-        const uint32_t ylr = __shfl_up(lr, off, 64);
-        if (lane >= (uint32_t)off && ylr == lr) f |= yf;
-      }
-      const uint32_t nlr = __shfl_down(lr, 1, 64);
-      const bool tail = valid && (lane == 63 || nlr != lr);
-      if (tail && f) atomicOr(&s_acc[lr], (unsigned long long)f);
-    }
+    for (int k = 0; k < IPT; ++k)
+      if (fk[k]) atomicOr(&s_acc[lrk[k]], (unsigned long long)fk[k]);
     __syncthreads();
     for (uint32_t lr = tid; lr < nr; lr += B) {
       const unsigned long long a = s_acc[lr];
@@ -294,12 +310,13 @@ void launch_bfs_pull_partition(const uint64_t *rp, uint32_t V, uint64_t E, uint6
   KCHECK("k_pull_partition");
 }
 void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const uint64_t *part, uint64_t E,
-                     uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *visited,
-                     uint64_t *next, int cus, hipStream_t s) {
+                     uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *fbm,
+                     const uint64_t *visited, uint64_t *next, int cus, hipStream_t s) {
   const uint64_t ntiles = bfs_pull_tiles(V, E);
-  if (!ntiles) return;
+  if (!ntiles || !lanes) return;
+  const auto kern = fbm ? k_bfs_pull<true> : k_bfs_pull<false>;
   int per = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bfs_pull, kPullB, 0) != hipSuccess || per < 1) per = 2;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kPullB, 0) != hipSuccess || per < 1) per = 2;
   // resident workgroups per CU: 7 of the 8 that fit measured fastest at C3 (4.26 ms against 5.54 ms
   // at 8 and 4.60 at 5: with a full CU the random gathers thrash L2); OMX_PULL_PER overrides
   static const int cap = [] {
@@ -308,7 +325,7 @@ void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const 
   }();
   if (cap > 0 && cap < per) per = cap;
   const unsigned g = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * per);
-  hipLaunchKernelGGL(k_bfs_pull, dim3(g), dim3(kPullB), 0, s, V, rp, col, part, E, ntiles, lanes, frontier, hub_fr,
+  hipLaunchKernelGGL(kern, dim3(g), dim3(kPullB), 0, s, V, rp, col, part, E, ntiles, lanes, frontier, hub_fr, fbm,
                      visited, next);
   KCHECK("k_bfs_pull");
 }

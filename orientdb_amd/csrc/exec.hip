@@ -44,7 +44,7 @@ class Timer {
   static bool hot(const char *name) {
     static const char *const kHot[] = {"k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light",
                                        "k_expand_light_sliced", "k_expand_light_check", "k_expand_heavy_check",
-                                       "k_check", "k_bfs_pull", "k_bfs_push",
+                                       "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_push",
                                        "k_bfs_emit", "k_trav_filter", "trav_select"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
@@ -150,6 +150,8 @@ class Executor {
     if (const char *sw = std::getenv("OMX_SWAP_CHECK")) swap_ = std::strcmp(sw, "0") != 0;
     if (const char *hb = std::getenv("OMX_PULL_HUBS")) pull_hubs_ = (uint32_t)std::strtoul(hb, nullptr, 10);
     if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max(1e-9, std::strtod(d, nullptr));
+    if (const char *lv = std::getenv("OMX_PULL_LIVE")) pull_live_ = std::strcmp(lv, "0") != 0;
+    if (const char *pr = std::getenv("OMX_PULL_PROBE")) pull_probe_ = std::strtod(pr, nullptr);
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
     bound_.assign(p.aliases.size(), 0);
@@ -389,6 +391,9 @@ class Executor {
   // of 2^17…2^22 at C3 (profiles/r02/c3rank: pull 4.26 → 4.07 ms per step against 2^18 in vertex order)
   uint32_t pull_hubs_ = 1u << 20;
   double pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
+  bool pull_live_ = true;  // the pull waits only for lanes whose frontier is non-empty
+  // levels whose frontier holds fewer than this fraction of the vertices pull through the frontier bitmap
+  double pull_probe_ = 0.1;
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
   // sliced hops size their arenas from the target bitmap's density (OMX_ARENA_ESTIMATE=0: exact bound;
   // OMX_ARENA_MARGIN scales the estimate, 0 forces the short-arena re-run in tests)
@@ -1851,9 +1856,9 @@ class Executor {
     }
     const bool while_never = depth_only_while && p_.progs[st.while_prog].const_false;
     if (depth_only_while) wconst = make_pred(st.while_prog, -1);
-    DBuf<uint64_t> fr(&pool_, V), nx(&pool_, V), vis(&pool_, V);
+    DBuf<uint64_t> fr(&pool_, V), nx(&pool_, V), vis(&pool_, V), fbm(&pool_, nwords_);
     DBuf<uint32_t> list;
-    DBuf<unsigned long long> stats(&pool_, 4);
+    DBuf<unsigned long long> stats(&pool_, 5);
     // bottom-up partitions of every reversed part (once per traversal; built on the first pull level)
     std::vector<DBuf<uint64_t>> hub_fr(radj.n);
     std::vector<const uint64_t *> pull_part(radj.n, nullptr);
@@ -1883,15 +1888,17 @@ class Executor {
         if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate");
         bool expand = !(st.has_max_depth && d >= st.max_depth);
         if (expand && depth_only_while) expand = !while_never && eval_pred_const(wconst, d);
-        HIP_CHECK(hipMemsetAsync(stats.p, 0, 4 * sizeof(unsigned long long), s_));
+        HIP_CHECK(hipMemsetAsync(stats.p, 0, 5 * sizeof(unsigned long long), s_));
         tm_.begin("k_bfs_prep");
-        launch_bfs_prep(fr.p, vis.p, V, while_bm, expand, adj, stats.p, cus(), s_);
+        launch_bfs_prep(fr.p, vis.p, V, while_bm, expand, adj, stats.p, fbm.p, cus(), s_);
         tm_.end(8ull * V);
         if (!expand) break;
-        launch_post_words(stats.p, 3, mail(), s_);
+        launch_post_words(stats.p, 4, mail(), s_);
         const uint64_t *h = wait_mail();
         tm_.amend(8ull * V + 24ull * h[2]);  // frontier scan + visited and row_ptr pair of the active vertices
         if (h[2] == 0) break;
+        // lanes with an empty frontier receive nothing at this level (OMX_PULL_LIVE=0: wait for all lanes)
+        const uint64_t live = pull_live_ ? h[3] : ~0ull;
         edges_ += h[0];
         edges_iter_ += h[0];
         HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
@@ -1908,16 +1915,17 @@ class Executor {
               hub_fr[p] = DBuf<uint64_t>(&pool_, std::max<uint32_t>(pull_nh[p], 1));
             }
             launch_hub_gather(pull_hubs[p], pull_nh[p], fr.p, hub_fr[p].p, s_);
-            tm_.begin("k_bfs_pull");
-            launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p], pull_E[p], lanes, fr.p, hub_fr[p].p, vis.p,
-                            nx.p, cus(), s_);
+            const bool probe = (double)h[2] < pull_probe_ * (double)V;
+            tm_.begin(probe ? "k_bfs_pull_sparse" : "k_bfs_pull");
+            launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p], pull_E[p], lanes & live, fr.p, hub_fr[p].p,
+                            probe ? fbm.p : nullptr, vis.p, nx.p, cus(), s_);
             // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask
             tm_.end(16ull * V + 12ull * pull_E[p]);
           }
         } else {
           if (!list.p) list = DBuf<uint32_t>(&pool_, V);
           tm_.begin("k_bfs_list");
-          launch_bfs_list(fr.p, V, list.p, stats.p + 3, cus(), s_);
+          launch_bfs_list(fr.p, V, list.p, stats.p + 4, cus(), s_);
           tm_.end(8ull * V + 4ull * h[2]);
           const uint64_t nl_act = h[2];
           DBuf<uint64_t> deg(&pool_, nl_act + 1), loffs(&pool_, nl_act + 1);

@@ -258,7 +258,7 @@ bool eval_pred_const(const DPred &pred, int64_t depth);
 // multi-source BFS (bfs.hip): u64 lane mask per vertex, 64 binding rows per batch
 void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, hipStream_t s);
 void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
-                     const DAdj &adj, unsigned long long *stats, int cus, hipStream_t s);
+                     const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s);
 void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsigned long long *count, int cus,
                      hipStream_t s);
 void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg, hipStream_t s);
@@ -268,8 +268,8 @@ void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, u
 uint64_t bfs_pull_tiles(uint32_t V, uint64_t E);
 void launch_bfs_pull_partition(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t *part, hipStream_t s);
 void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const uint64_t *part, uint64_t E,
-                     uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *visited,
-                     uint64_t *next, int cus, hipStream_t s);
+                     uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *fbm,
+                     const uint64_t *visited, uint64_t *next, int cus, hipStream_t s);
 // hub-annotated col of a CSR for k_bfs_pull (returns the hub count; hub_idx u32[V], hist u32[4096] scratch)
 // rp_self: the CSR's own row pointers (its rows are re-ordered hub-first; OMX_PULL_SORT=0 keeps them)
 uint32_t build_pull_col(const uint64_t *rp_self, const uint64_t *rp_other, const uint32_t *col, uint32_t V, uint64_t E,

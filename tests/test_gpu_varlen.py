@@ -33,16 +33,24 @@ def _cols(q):
     return [c.strip() for c in ret.split(",")]
 
 
-# (strategy, OMX_BFS_PULL_DIV): auto push/pull, every level top-down, every level bottom-up
-MODES = [("bfs", None), ("bfs", "1"), ("bfs", "1000000000000"), ("pairs", None)]
+# environment per mode: auto push/pull, every level top-down, every level bottom-up gathering every
+# mask, the same through the frontier bitmap, the same waiting for every lane (not only the live ones)
+_PULL = {"OMX_VARLEN": "bfs", "OMX_BFS_PULL_DIV": "1000000000000"}
+MODES = {
+    "bfs_auto": {"OMX_VARLEN": "bfs"},
+    "bfs_push": {"OMX_VARLEN": "bfs", "OMX_BFS_PULL_DIV": "1"},
+    "bfs_pull": dict(_PULL, OMX_PULL_PROBE="0"),
+    "bfs_pull_probe": dict(_PULL, OMX_PULL_PROBE="2"),
+    "bfs_pull_all_lanes": dict(_PULL, OMX_PULL_LIVE="0"),
+    "pairs": {"OMX_VARLEN": "pairs"},
+}
 
 
-@pytest.mark.parametrize("mode", MODES, ids=["bfs_auto", "bfs_push", "bfs_pull", "pairs"])
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("q", VARLEN, ids=[q[0] for q in VARLEN])
 def test_varlen_parity(rmat10, q, mode, monkeypatch):
-    monkeypatch.setenv("OMX_VARLEN", mode[0])
-    if mode[1]:
-        monkeypatch.setenv("OMX_BFS_PULL_DIV", mode[1])
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
     g, ref = rmat10
     _parity(g, ref, q[1], _cols(q[1]))
 
@@ -77,7 +85,7 @@ def test_bfs_kernels_reported(rmat10, monkeypatch):
     rs = o.OMatchStatement(VARLEN[1][1]).execute(g, flags=o.OMX_FLAG_KERNEL_TIMING)
     names = {k["name"] for k in rs.kernel_stats}
     assert "k_bfs_prep" in names and "k_bfs_emit" in names
-    assert names & {"k_bfs_push", "k_bfs_pull"}
+    assert names & {"k_bfs_push", "k_bfs_pull", "k_bfs_pull_sparse"}
 
 
 @pytest.mark.parametrize("hubs", ["16", "0"], ids=["partial_hubs", "no_hubs"])
@@ -99,18 +107,19 @@ def rmat14():
     return o.GraphSnapshot.rmat(14, device=0, keep_csr=True)
 
 
-@pytest.mark.parametrize("pull", ["auto", "pull"])
+@pytest.mark.parametrize("pull", ["auto", "pull", "pull_probe"])
 def test_varlen_rmat14_hub_root_vs_c_bfs(rmat14, pull, monkeypatch):
     """RMAT-14 from the highest-degree vertex and 63 others (rows straddle pull tiles; the hub
     threshold picks a strict subset of the sources) against oracle/bfs_ref.c, all levels bottom-up
-    in the "pull" mode."""
+    in the "pull" modes ("pull_probe": every level through the frontier bitmap)."""
     import numpy as np
     import orientdb_amd as o
     from oracle import dfs
     monkeypatch.setenv("OMX_VARLEN", "bfs")
     monkeypatch.setenv("OMX_PULL_HUBS", "512")
-    if pull == "pull":
+    if pull != "auto":
         monkeypatch.setenv("OMX_BFS_PULL_DIV", "1000000000000")
+    monkeypatch.setenv("OMX_PULL_PROBE", "2" if pull == "pull_probe" else "0")
     g = rmat14
     rp, col = g.csr
     top = int(np.argmax(np.diff(rp)))
