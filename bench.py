@@ -71,7 +71,7 @@ COUNT_MODE = {"c5"}   # the last hop counts its rows (count mo
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # ≈7e4 Person, ≈2e6 Knows
 # kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)
 HOT_KERNELS = ("k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light", "k_expand_light_sliced", "k_trav_filter",
-               "k_expand_light_check", "k_expand_heavy_check", "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_push", "k_bfs_prep", "k_bfs_emit",
+               "k_expand_light_check", "k_expand_heavy_check", "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit", "k_bfs_push", "k_bfs_prep", "k_bfs_emit",
                "k_gather_cols", "k_compact_segments")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md §Chip-level parameters)
 

@@ -330,6 +330,115 @@ void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const 
   KCHECK("k_bfs_pull");
 }
 
+// Dense levels with an early exit: one thread per vertex walks its in-edges in the annotated col's
+// hub-first order (the first alone, then four at a time) and stops as soon as the gathered masks cover the lanes the vertex
+// still needs. Once the frontier holds a large share of V, most vertices are covered by their first
+// in-edge (a hub every live lane has reached): C3's dense level reads 10 M of its 208 M in-edges
+// (tools/c3_exit_stats.c). A vertex still uncovered after kExitScan in-edges is listed for
+// k_bfs_pull_rest (one wave per vertex). next[] may hold an earlier part's lanes: they are not needed
+// again and are kept. scanned accumulates the in-edges read (for the algorithmic bytes).
+constexpr uint32_t kExitScan = 16;
+__global__ __launch_bounds__(kB) void k_bfs_pull_exit(uint32_t V, const uint64_t *rp, const uint32_t *col,
+                                                      uint64_t lanes, const uint64_t *frontier,
+                                                      const uint64_t *hub_fr, const uint64_t *visited,
+                                                      uint64_t *next, uint32_t *rest, unsigned long long *counts) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t scanned = 0;
+  // persistent grid-stride: the in-edge count is added once per wave (one atomic per vertex wave on a
+  // single counter serialised the launch: 3.2 ms)
+  for (uint64_t v0 = (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
+    const uint64_t v = v0 + threadIdx.x;
+    bool more = false;
+    if (v < V) {
+      const uint64_t old = next[v];
+      const uint64_t need = lanes & ~visited[v] & ~old;
+      const uint64_t s = rp[v], e = rp[v + 1];
+      if (need && e > s) {
+        // the first in-edge alone (the top hub covers most vertices), then four at a time
+        const uint32_t x0 = col[s];
+        uint64_t acc = (x0 >> 31) ? hub_fr[x0 & 0x7FFFFFFFu] : frontier[x0];
+        uint64_t i = s + 1;
+        const uint64_t stop = e - s > kExitScan ? s + kExitScan : e;
+        while (i < stop && (acc & need) != need) {
+          uint32_t x[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) x[k] = i + k < stop ? col[i + k] : 0u;
+          uint64_t m[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            m[k] = 0;
+            if (i + k < stop) m[k] = (x[k] >> 31) ? hub_fr[x[k] & 0x7FFFFFFFu] : frontier[x[k]];
+          }
+          acc |= m[0] | m[1] | m[2] | m[3];
+          i = i + 4 < stop ? i + 4 : stop;
+        }
+        scanned += i - s;
+        acc &= need;
+        if (acc) next[v] = old | acc;
+        more = acc != need && i < e;
+      }
+    }
+    // the uncovered vertices with in-edges left: one slot per wave, then one per lane (rare)
+    const uint64_t mm = __ballot(more);
+    if (mm) {
+      unsigned long long base = 0;
+      const uint32_t first = (uint32_t)__builtin_ctzll(mm);
+      if (lane == first) base = atomicAdd(&counts[1], (unsigned long long)__popcll(mm));
+      base = __shfl(base, (int)first, 64);
+      if (more) rest[base + lane_prefix(mm)] = (uint32_t)v;
+    }
+  }
+  scanned = wave_sum_u64(scanned);
+  if (lane == 0 && scanned) atomicAdd(&counts[0], (unsigned long long)scanned);
+}
+
+// the remaining in-edges of the listed vertices: one wave per vertex, 64 in-edges per step, OR-reduced
+// across the wave, until the vertex's needed lanes are covered or its list ends
+__global__ __launch_bounds__(kB) void k_bfs_pull_rest(const uint32_t *rest, const unsigned long long *counts,
+                                                      const uint64_t *rp, const uint32_t *col, uint64_t lanes,
+                                                      const uint64_t *frontier, const uint64_t *hub_fr,
+                                                      const uint64_t *visited, uint64_t *next,
+                                                      unsigned long long *scanned_out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t n = counts[1];
+  const uint64_t nw = (uint64_t)gridDim.x * (kB / 64);
+  uint64_t scanned = 0;
+  for (uint64_t w = (uint64_t)blockIdx.x * (kB / 64) + (threadIdx.x >> 6); w < n; w += nw) {
+    const uint32_t v = rest[w];
+    const uint64_t old = next[v];
+    const uint64_t need = lanes & ~visited[v] & ~old;
+    const uint64_t e = rp[v + 1];
+    uint64_t acc = 0;
+    for (uint64_t i = rp[v] + kExitScan; i < e; i += 64) {
+      uint64_t m = 0;
+      if (i + lane < e) {
+        const uint32_t x = col[i + lane];
+        m = (x >> 31) ? hub_fr[x & 0x7FFFFFFFu] : frontier[x];
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
+      acc |= m;
+      scanned += e - i < 64 ? e - i : 64;
+      if ((acc & need) == need) break;
+    }
+    acc &= need;
+    if (lane == 0 && acc) next[v] = old | acc;
+  }
+  if (lane == 0 && scanned) atomicAdd(scanned_out, (unsigned long long)scanned);
+}
+
+void launch_bfs_pull_exit(uint32_t V, const uint64_t *rp, const uint32_t *col, uint64_t lanes,
+                          const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *visited, uint64_t *next,
+                          uint32_t *rest, unsigned long long *counts, int cus, hipStream_t s) {
+  if (!V || !lanes) return;
+  hipLaunchKernelGGL(k_bfs_pull_exit, dim3((unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 8)), dim3(kB), 0,
+                     s, V, rp, col, lanes, frontier, hub_fr, visited, next, rest, counts);
+  KCHECK("k_bfs_pull_exit");
+  hipLaunchKernelGGL(k_bfs_pull_rest, dim3((unsigned)cus * 8), dim3(kB), 0, s, rest, counts, rp, col, lanes, frontier,
+                     hub_fr, visited, next, counts);
+  KCHECK("k_bfs_pull_rest");
+}
+
 __global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t > ntiles) return;

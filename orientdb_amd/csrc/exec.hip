@@ -44,7 +44,7 @@ class Timer {
   static bool hot(const char *name) {
     static const char *const kHot[] = {"k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light",
                                        "k_expand_light_sliced", "k_expand_light_check", "k_expand_heavy_check",
-                                       "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_push",
+                                       "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit", "k_bfs_push",
                                        "k_bfs_emit", "k_trav_filter", "trav_select"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
@@ -152,6 +152,7 @@ class Executor {
     if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max(1e-9, std::strtod(d, nullptr));
     if (const char *lv = std::getenv("OMX_PULL_LIVE")) pull_live_ = std::strcmp(lv, "0") != 0;
     if (const char *pr = std::getenv("OMX_PULL_PROBE")) pull_probe_ = std::strtod(pr, nullptr);
+    if (const char *px = std::getenv("OMX_PULL_EXIT")) pull_exit_ = std::strcmp(px, "0") != 0;
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
     bound_.assign(p.aliases.size(), 0);
@@ -394,6 +395,7 @@ class Executor {
   bool pull_live_ = true;  // the pull waits only for lanes whose frontier is non-empty
   // levels whose frontier holds fewer than this fraction of the vertices pull through the frontier bitmap
   double pull_probe_ = 0.1;
+  bool pull_exit_ = true;  // denser levels pull per vertex with an early exit (OMX_PULL_EXIT=0: tiles)
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
   // sliced hops size their arenas from the target bitmap's density (OMX_ARENA_ESTIMATE=0: exact bound;
   // OMX_ARENA_MARGIN scales the estimate, 0 forces the short-arena re-run in tests)
@@ -1866,6 +1868,9 @@ class Executor {
     std::vector<uint32_t> pull_nh(radj.n, 0);
     std::vector<uint64_t> pull_E(radj.n);
     for (int p = 0; p < radj.n; ++p) pull_E[p] = g_.esets[rspec.parts[p].first].n_edges;
+    DBuf<uint32_t> rest;  // dense pull levels: vertices left to the per-wave pass
+    DBuf<unsigned long long> exit_counts;
+    std::vector<size_t> exit_recs;  // their timer records
     DBuf<uint8_t> bflags;
     if (st.mode == T_BOUND) bflags = DBuf<uint8_t>(&pool_, R);
     const unsigned nb = bfs_blocks(V);
@@ -1916,6 +1921,23 @@ class Executor {
             }
             launch_hub_gather(pull_hubs[p], pull_nh[p], fr.p, hub_fr[p].p, s_);
             const bool probe = (double)h[2] < pull_probe_ * (double)V;
+            if (!probe && pull_exit_) {
+              // dense level: per-vertex walks that stop once the needed lanes are covered
+              if (!rest.p) {
+                rest = DBuf<uint32_t>(&pool_, V);
+                exit_counts = DBuf<unsigned long long>(&pool_, 2);
+                HIP_CHECK(hipMemsetAsync(exit_counts.p, 0, sizeof(unsigned long long), s_));
+              }
+              HIP_CHECK(hipMemsetAsync(exit_counts.p + 1, 0, sizeof(unsigned long long), s_));
+              tm_.begin("k_bfs_pull_exit");
+              launch_bfs_pull_exit(V, radj.p[p].rp, pull_col[p], lanes & live, fr.p, hub_fr[p].p, vis.p, nx.p, rest.p,
+                                   exit_counts.p, cus(), s_);
+              // per vertex: row_ptr pair + visited + next; per in-edge read: col + the source's frontier mask
+              // (exit_counts[0] sums the in-edges read over the traversal; added once it has ended)
+              tm_.end(32ull * V);
+              if (tm_.last() != SIZE_MAX) exit_recs.push_back(tm_.last());
+              continue;
+            }
             tm_.begin(probe ? "k_bfs_pull_sparse" : "k_bfs_pull");
             launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p], pull_E[p], lanes & live, fr.p, hub_fr[p].p,
                             probe ? fbm.p : nullptr, vis.p, nx.p, cus(), s_);
@@ -1975,6 +1997,7 @@ class Executor {
       // visited + emission bitmap scans (two passes) + 4 B per written column per row
       tm_.end(16ull * V + 4ull * n * (carry ? bcols.size() + 1 : 2));
     }
+    if (!exit_recs.empty()) tm_.amend_at(exit_recs[0], 32ull * V + 12ull * read1(exit_counts.p));
     if (st.mode == T_BOUND) {
       select_rows(bflags.p, R);
       return;

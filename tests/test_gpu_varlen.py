@@ -39,7 +39,8 @@ _PULL = {"OMX_VARLEN": "bfs", "OMX_BFS_PULL_DIV": "1000000000000"}
 MODES = {
     "bfs_auto": {"OMX_VARLEN": "bfs"},
     "bfs_push": {"OMX_VARLEN": "bfs", "OMX_BFS_PULL_DIV": "1"},
-    "bfs_pull": dict(_PULL, OMX_PULL_PROBE="0"),
+    "bfs_pull": dict(_PULL, OMX_PULL_PROBE="0"),  # dense levels: per-vertex early-exit pull
+    "bfs_pull_tiles": dict(_PULL, OMX_PULL_PROBE="0", OMX_PULL_EXIT="0"),  # dense levels: merge-path tiles
     "bfs_pull_probe": dict(_PULL, OMX_PULL_PROBE="2"),
     "bfs_pull_all_lanes": dict(_PULL, OMX_PULL_LIVE="0"),
     "pairs": {"OMX_VARLEN": "pairs"},
@@ -85,17 +86,21 @@ def test_bfs_kernels_reported(rmat10, monkeypatch):
     rs = o.OMatchStatement(VARLEN[1][1]).execute(g, flags=o.OMX_FLAG_KERNEL_TIMING)
     names = {k["name"] for k in rs.kernel_stats}
     assert "k_bfs_prep" in names and "k_bfs_emit" in names
-    assert names & {"k_bfs_push", "k_bfs_pull", "k_bfs_pull_sparse"}
+    assert names & {"k_bfs_push", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit"}
 
 
+@pytest.mark.parametrize("exit_", ["exit", "tiles"])
 @pytest.mark.parametrize("hubs", ["16", "0"], ids=["partial_hubs", "no_hubs"])
 @pytest.mark.parametrize("q", [q for q in VARLEN if q[0] in ("two_batches", "where_target", "in_dir", "both_dir")],
                          ids=lambda q: q[0])
-def test_varlen_pull_hub_threshold(rmat10, q, hubs, monkeypatch):
+def test_varlen_pull_hub_threshold(rmat10, q, hubs, exit_, monkeypatch):
     """Bottom-up levels with only the 16 highest-degree sources annotated as hubs (the degree threshold
-    then picks a strict subset, as at C3's scale), or none (plain col)."""
+    then picks a strict subset, as at C3's scale), or none (plain col), through the per-vertex
+    early-exit pull or the merge-path tiles."""
     monkeypatch.setenv("OMX_VARLEN", "bfs")
     monkeypatch.setenv("OMX_BFS_PULL_DIV", "1000000000000")
+    monkeypatch.setenv("OMX_PULL_PROBE", "0")
+    monkeypatch.setenv("OMX_PULL_EXIT", "1" if exit_ == "exit" else "0")
     monkeypatch.setenv("OMX_PULL_HUBS", hubs)
     g, ref = rmat10
     _parity(g, ref, q[1], _cols(q[1]))
@@ -107,7 +112,7 @@ def rmat14():
     return o.GraphSnapshot.rmat(14, device=0, keep_csr=True)
 
 
-@pytest.mark.parametrize("pull", ["auto", "pull", "pull_probe"])
+@pytest.mark.parametrize("pull", ["auto", "pull", "pull_tiles", "pull_probe"])
 def test_varlen_rmat14_hub_root_vs_c_bfs(rmat14, pull, monkeypatch):
     """RMAT-14 from the highest-degree vertex and 63 others (rows straddle pull tiles; the hub
     threshold picks a strict subset of the sources) against oracle/bfs_ref.c, all levels bottom-up
@@ -120,6 +125,7 @@ def test_varlen_rmat14_hub_root_vs_c_bfs(rmat14, pull, monkeypatch):
     if pull != "auto":
         monkeypatch.setenv("OMX_BFS_PULL_DIV", "1000000000000")
     monkeypatch.setenv("OMX_PULL_PROBE", "2" if pull == "pull_probe" else "0")
+    monkeypatch.setenv("OMX_PULL_EXIT", "0" if pull == "pull_tiles" else "1")
     g = rmat14
     rp, col = g.csr
     top = int(np.argmax(np.diff(rp)))
