@@ -656,12 +656,18 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
       q[i] = (idx >= d.lo && idx < d.hi) ? col[i * 64 + lane] : 0u;
     }
   };
+  // the carried values of a chunk's row are loaded with its descriptor's prefetch (one chunk ahead)
+  auto carry_load = [&](const ChunkDesc &dd, uint32_t (&cv)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cv[k] = WRITE && k < a.ncarry ? a.carry_in[k][dd.row] : 0u;
+  };
   uint64_t c = wid;
   ChunkDesc d{};
-  uint32_t q[NS];
+  uint32_t q[NS], cv[4] = {0, 0, 0, 0};
   if (c < a.nchunks) {
     d = a.chunks[c];
     load(d, q);
+    carry_load(d, cv);
   }
   while (c < a.nchunks) {
     const uint64_t cn = c + nw;
@@ -688,17 +694,15 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
     }
     // prefetch the next chunk
     ChunkDesc dn = d;
-    uint32_t qn[NS];
+    uint32_t qn[NS], cvn[4] = {0, 0, 0, 0};
     if (cn < a.nchunks) {
       dn = a.chunks[cn];
       load(dn, qn);
+      carry_load(dn, cvn);
     }
     const uint32_t r = d.row;
     if (WRITE) {
-      uint32_t cv[4];
       const int nc = a.ncarry;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) cv[k] = k < nc ? a.carry_in[k][r] : 0;
       uint64_t base = FILTER ? arena + acc : 0;
 #pragma unroll
       for (int i = 0; i < NS; ++i) {
@@ -732,6 +736,8 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
     d = dn;
 #pragma unroll
     for (int i = 0; i < NS; ++i) q[i] = qn[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cv[k] = cvn[k];
   }
   if (MEMBER) {
     wave_add_u64(a.member_edges, medges);
