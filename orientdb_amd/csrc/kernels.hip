@@ -554,6 +554,18 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
         if (((act >> k) & 1u) && !(lo[k] < end[k] && mcol[lo[k]] == nb[k])) passmask &= ~(1u << k);
     }
 
+    // the items' carried values (≤ 4 columns) are all requested before the first store: loaded next to
+    // the store that consumes it, each one waited for its own round trip (8 items × columns per thread)
+    uint32_t cv[WRITE ? IPT : 1][4];
+    if (WRITE) {
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        const uint64_t r = i0 + lrs[k];
+        const bool live = k * B + tid < ne && (FILTER ? ((passmask >> k) & 1u) != 0 : true);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cv[k][c] = live && c < a.ncarry ? a.carry_in[c][r] : 0u;
+      }
+    }
     if (!FILTER) {
       if (WRITE) {
 #pragma unroll
@@ -563,7 +575,10 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
             const uint64_t o = a.dense_base + j0 + jl;
             const uint64_t r = i0 + lrs[k];
             a.out_dst[o] = nb[k];
-            for (int c = 0; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              if (c < a.ncarry) a.carry_out[c][o] = cv[k][c];
+            for (int c = 4; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
           }
         }
       }
@@ -596,7 +611,10 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
           const uint64_t o = arena + acc + s_wave[k * W + wave] + lane_prefix(masks[k]);
           const uint64_t r = i0 + lrs[k];
           a.out_dst[o] = nb[k];
-          for (int c = 0; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (c < a.ncarry) a.carry_out[c][o] = cv[k][c];
+          for (int c = 4; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
         }
       }
     }

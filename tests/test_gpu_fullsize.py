@@ -9,6 +9,8 @@ variable-length item, P/OMatchPathItem.java:79-105):
       155 M (a, b, c) RID tuples (OMX_FLAG_DIGEST: Σ splitmix64-chain(row) mod 2^64, kernels.hip k_digest
       = oracle/dfs.py row_digest), rows left in HBM;
 * M1  the metric's own workload, RMAT-24 2-hop (C2's query at scale 24, ≈1.0e9 rows): the same;
+* M1 partitioned: the same over a 4-rank 1-D partition of RMAT-24 (the multi-GPU bench's configuration;
+      thread transport);
 * C3  RMAT-24, 64 roots, `while:($depth < 4)`: row count, E_t (Σ frontier degrees) and digest;
 * C5  the 3-hop COUNT shape on a 4-rank 1-D partition of RMAT-16 (thread transport): the ranks' bindings
       and edges add up to the oracle's, and the ranks' digests of the materialized rows add up to it.
@@ -72,15 +74,37 @@ def rmat24():
     g.close()
 
 
-def test_m1_rmat24_two_hop_digest(rmat24):
-    """The metric's own config (BASELINE.json: RMAT-24 2-hop): C2's query at scale 24, ≈1e9 distinct rows."""
+@pytest.fixture(scope="module")
+def m1_ref(rmat24):
     from oracle import dfs
-    g = rmat24
-    ref = dfs.run(_cg(g), C2_QUERY, nthreads=THREADS, emit=False, digest=["a", "b", "c"])
+    return dfs.run(_cg(rmat24), C2_QUERY, nthreads=THREADS, emit=False, digest=["a", "b", "c"])
+
+
+def test_m1_rmat24_two_hop_digest(rmat24, m1_ref):
+    """The metric's own config (BASELINE.json: RMAT-24 2-hop): C2's query at scale 24, ≈1e9 distinct rows."""
+    g, ref = rmat24, m1_ref
     rs = _digest_run(g, C2_QUERY)
     assert rs.info["n_rows"] == rs.info["bindings"] == ref["bindings"] > 5e8
     assert rs.info["edges_traversed"] == ref["edges"]
     assert rs.info["digest"] == ref["digest"]
+
+
+def test_m1_partitioned_4ranks_rmat24(m1_ref):
+    """The multi-GPU bench's own configuration at full size: M1 on a 1-D partition of RMAT-24 over 4
+    ranks (thread transport on one GPU, the same routing code as RCCL): rows (a, b) routed to owner(b)
+    before the second hop, no final exchange (rows distinct by construction); the ranks' rows and
+    digests add up to the oracle's."""
+    import orientdb_amd as o
+    from tests.test_gpu_dist import run_ranks
+    parts = [o.GraphSnapshot.rmat(24, device=0, partition=(r, 4)) for r in range(4)]
+    try:
+        mat = run_ranks(parts, C2_QUERY, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST, documents=False)
+        assert sum(r.info["n_rows"] for r in mat) == m1_ref["bindings"] > 5e8
+        assert sum(r.info["edges_traversed"] for r in mat) == m1_ref["edges"]
+        assert sum(r.info["digest"] for r in mat) % (1 << 64) == m1_ref["digest"]
+    finally:
+        for g in parts:
+            g.close()
 
 
 def test_c3_rmat24_varlen_digest(rmat24):
