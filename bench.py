@@ -66,7 +66,7 @@ def scaled_query(name, query, world, partitioned):
     return query, "strong"
 
 
-REPLICATED_ONLY = {"c1", "c3", "c4", "t1", "s1", "p1"}  # per-GPU structures: C3 multi-source BFS lane masks, C4 LDBC replica; C1 all-root fof
+REPLICATED_ONLY = {"c1", "c4", "t1", "s1", "p1"}  # C4 LDBC replica; C1 all-root fof; TRAVERSE / SELECT / shortestPath
 COUNT_MODE = {"c5"}   # the last hop counts its rows (count mode)
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # ≈7e4 Person, ≈2e6 Knows
 # kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)

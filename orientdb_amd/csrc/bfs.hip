@@ -50,13 +50,13 @@ void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *front
 // the reference traverses, SURVEY §8(d) E_t), stats[1] = Σ deg over active vertices (push work),
 // stats[2] = active vertices, stats[3] = OR of m (the live lanes: a lane whose frontier is empty
 // reaches nothing more, so the pull does not wait for it).
-__global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V,
+__global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t vlo, uint32_t V,
                                                  const uint64_t *while_bm, int expand, DAdj adj,
                                                  unsigned long long *stats, uint64_t *fbm) {
   __shared__ uint64_t s_r[4][kB / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint64_t te = 0, td = 0, tn = 0, tl = 0;
-  for (uint64_t v0 = (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
+  for (uint64_t v0 = vlo + (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
     const uint64_t v = v0 + threadIdx.x;
     const uint64_t f = v < V ? frontier[v] : 0;
     uint64_t m = 0;
@@ -101,9 +101,11 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
   }
 }
 void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
-                     const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s) {
-  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 8);
-  hipLaunchKernelGGL(k_bfs_prep, dim3(g), dim3(kB), 0, s, frontier, visited, V, while_bm, (int)expand, adj, stats,
+                     const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s, uint32_t vlo) {
+  if (vlo && fbm) fail(OMX_E_INVALID, "internal: the frontier bitmap covers whole words from vertex 0");
+  if (V <= vlo) return;
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V - vlo, kB), (uint64_t)cus * 8);
+  hipLaunchKernelGGL(k_bfs_prep, dim3(g), dim3(kB), 0, s, frontier, visited, vlo, V, while_bm, (int)expand, adj, stats,
                      fbm);
   KCHECK("k_bfs_prep");
 }
@@ -338,7 +340,7 @@ void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const 
 // k_bfs_pull_rest (one wave per vertex). next[] may hold an earlier part's lanes: they are not needed
 // again and are kept. scanned accumulates the in-edges read (for the algorithmic bytes).
 constexpr uint32_t kExitScan = 16;
-__global__ __launch_bounds__(kB) void k_bfs_pull_exit(uint32_t V, const uint64_t *rp, const uint32_t *col,
+__global__ __launch_bounds__(kB) void k_bfs_pull_exit(uint32_t vlo, uint32_t V, const uint64_t *rp, const uint32_t *col,
                                                       uint64_t lanes, const uint64_t *frontier,
                                                       const uint64_t *hub_fr, const uint64_t *visited,
                                                       uint64_t *next, uint32_t *rest, unsigned long long *counts) {
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(kB) void k_bfs_pull_exit(uint32_t V, const uint64_t
   uint64_t scanned = 0;
   // persistent grid-stride: the in-edge count is added once per wave (one atomic per vertex wave on a
   // single counter serialised the launch: 3.2 ms)
-  for (uint64_t v0 = (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
+  for (uint64_t v0 = vlo + (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
     const uint64_t v = v0 + threadIdx.x;
     bool more = false;
     if (v < V) {
@@ -429,10 +431,10 @@ __global__ __launch_bounds__(kB) void k_bfs_pull_rest(const uint32_t *rest, cons
 
 void launch_bfs_pull_exit(uint32_t V, const uint64_t *rp, const uint32_t *col, uint64_t lanes,
                           const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *visited, uint64_t *next,
-                          uint32_t *rest, unsigned long long *counts, int cus, hipStream_t s) {
-  if (!V || !lanes) return;
-  hipLaunchKernelGGL(k_bfs_pull_exit, dim3((unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 8)), dim3(kB), 0,
-                     s, V, rp, col, lanes, frontier, hub_fr, visited, next, rest, counts);
+                          uint32_t *rest, unsigned long long *counts, int cus, hipStream_t s, uint32_t vlo) {
+  if (V <= vlo || !lanes) return;
+  hipLaunchKernelGGL(k_bfs_pull_exit, dim3((unsigned)std::min<uint64_t>(nblocks(V - vlo, kB), (uint64_t)cus * 8)), dim3(kB),
+                     0, s, vlo, V, rp, col, lanes, frontier, hub_fr, visited, next, rest, counts);
   KCHECK("k_bfs_pull_exit");
   hipLaunchKernelGGL(k_bfs_pull_rest, dim3((unsigned)cus * 8), dim3(kB), 0, s, rest, counts, rp, col, lanes, frontier,
                      hub_fr, visited, next, counts);

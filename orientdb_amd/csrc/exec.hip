@@ -1793,7 +1793,17 @@ class Executor {
   // terminates on cycles.
   void varlen_step(const Step &st) {
     bool depth_only_while = false;
-    // partitioned: (row, vertex) pairs routed to the owner of their vertex every level
+    // partitioned: the multi-source BFS with the frontier blocks allgathered every level (a free or
+    // candidate target, ≤ BfsCarry::kMax bound columns, few batches as below), else (row, vertex) pairs
+    // routed to the owner of their vertex every level
+    if (dist_ && varlen_mode_ != "pairs" && bfs_exact(st, depth_only_while) && st.mode != T_BOUND &&
+        bound_cols().size() <= (size_t)BfsCarry::kMax) {
+      const uint64_t nb = (global_sum(R_) + 63) / 64;  // the same choice on every rank
+      if (varlen_mode_ == "bfs" || nb <= 64 || nb * (uint64_t)g_.V <= (1ull << 30)) {
+        varlen_msbfs(st, depth_only_while);
+        return;
+      }
+    }
     if (!dist_ && varlen_mode_ != "pairs" && bfs_exact(st, depth_only_while)) {
       const uint64_t nb = (R_ + 63) / 64;
       if (varlen_mode_ == "bfs" || nb <= 64 || nb * (uint64_t)g_.V <= (1ull << 30)) {
@@ -1827,8 +1837,59 @@ class Executor {
   // Multi-source BFS over 64-row batches (bfs.hip). Rows (row, v) come out distinct per row.
   void varlen_msbfs(const Step &st, bool depth_only_while) {
     require_u32_rows("a variable-length item");
-    const uint64_t R = R_;
+    uint64_t R = R_;
     const uint32_t V = g_.V;
+    // Partitioned (SURVEY §8(e) "Variable-length: ... when the frontier is dense, an allgather"): every
+    // rank runs every 64-row batch of the global rows, whose bound columns are first gathered to every
+    // rank; prep, pull and visited cover the rank's own vertices [vlo, vhi), whose in-CSR rows it
+    // holds, and each level's frontier blocks are allgathered so that the pull reads any in-neighbour's
+    // mask. Every level pulls (per vertex, early exit). A rank emits the rows of its own vertices (the
+    // rows then live at owner(dst)).
+    const std::vector<int> bcols = bound_cols();
+    const uint32_t *srcc = col_[st.src].p;
+    std::vector<const uint32_t *> cin;
+    for (int c : bcols) cin.push_back(col_[c].p);
+    std::vector<DBuf<uint32_t>> grow;
+    std::vector<uint64_t> plo, phi;
+    uint32_t vlo = 0, vhi = V;
+    if (dist_) {
+      const int W = tr_->world(), me = tr_->rank();
+      const std::vector<uint64_t> rs = tr_->allgather(R_, s_);
+      plo = tr_->allgather(g_.part_lo, s_);
+      phi = tr_->allgather(g_.part_hi, s_);
+      vlo = g_.part_lo;
+      vhi = g_.part_hi;
+      std::vector<uint64_t> send(W, R_), sdispl(W, 0), recv(rs), rdispl(W, 0);
+      R = 0;
+      for (int p = 0; p < W; ++p) {
+        rdispl[p] = R;
+        R += rs[p];
+      }
+      if (R >= (1ull << 32)) unsupported("a partitioned variable-length item over 2^32 or more rows");
+      std::vector<const uint32_t *> sb;
+      std::vector<uint32_t *> rb;
+      DBuf<uint32_t> dummy(&pool_, 1);
+      for (size_t k = 0; k < bcols.size(); ++k) {
+        grow.emplace_back(&pool_, std::max<uint64_t>(R, 1));
+        sb.push_back(R_ ? col_[bcols[k]].p : dummy.p);
+        rb.push_back(grow.back().p);
+      }
+      tm_.begin("exchange");
+      tr_->alltoallv(sb, send, sdispl, rb, recv, rdispl, s_);
+      tm_.end(4ull * bcols.size() * (R_ * W + R));
+      (void)me;
+      for (size_t k = 0; k < bcols.size(); ++k) {
+        cin[k] = grow[k].p;
+        if (bcols[k] == st.src) srcc = grow[k].p;
+      }
+      if (!R) {
+        for (int c : bcols) col_[c] = DBuf<uint32_t>(&pool_, 1);
+        col_[st.dst] = DBuf<uint32_t>(&pool_, 1);
+        R_ = 0;
+        owner_col_ = st.dst;
+        return;
+      }
+    }
     const DAdj adj = make_adj(st.adj);
     AdjSpec rspec = st.adj;
     for (auto &p : rspec.parts) p.second ^= 1;
@@ -1879,7 +1940,6 @@ class Executor {
     std::vector<DBuf<uint32_t>> orow, ov;
     std::vector<uint64_t> on;
     // up to BfsCarry::kMax bound columns are written by the emission itself (no row gather after it)
-    const std::vector<int> bcols = bound_cols();
     const bool carry = bcols.size() <= (size_t)BfsCarry::kMax;
     std::vector<std::vector<DBuf<uint32_t>>> oc(carry ? bcols.size() : 0);
     uint64_t ntotal = 0;
@@ -1888,22 +1948,31 @@ class Executor {
       const uint64_t lanes = nl == 64 ? ~0ull : ((1ull << nl) - 1);
       HIP_CHECK(hipMemsetAsync(fr.p, 0, (size_t)V * 8, s_));
       HIP_CHECK(hipMemsetAsync(vis.p, 0, (size_t)V * 8, s_));
-      launch_bfs_seed(col_[st.src].p, row0, nl, fr.p, s_);
+      launch_bfs_seed(srcc, row0, nl, fr.p, s_);
       for (int64_t d = 0;; ++d) {
         if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate");
         bool expand = !(st.has_max_depth && d >= st.max_depth);
         if (expand && depth_only_while) expand = !while_never && eval_pred_const(wconst, d);
         HIP_CHECK(hipMemsetAsync(stats.p, 0, 5 * sizeof(unsigned long long), s_));
         tm_.begin("k_bfs_prep");
-        launch_bfs_prep(fr.p, vis.p, V, while_bm, expand, adj, stats.p, fbm.p, cus(), s_);
-        tm_.end(8ull * V);
+        launch_bfs_prep(fr.p, vis.p, vhi, while_bm, expand, adj, stats.p, dist_ ? nullptr : fbm.p, cus(), s_, vlo);
+        tm_.end(8ull * (vhi - vlo));
         if (!expand) break;
         launch_post_words(stats.p, 4, mail(), s_);
-        const uint64_t *h = wait_mail();
-        tm_.amend(8ull * V + 24ull * h[2]);  // frontier scan + visited and row_ptr pair of the active vertices
-        if (h[2] == 0) break;
+        const uint64_t *hm = wait_mail();
+        uint64_t h[4] = {hm[0], hm[1], hm[2], hm[3]};
+        tm_.amend(8ull * (vhi - vlo) + 24ull * h[2]);  // frontier scan + visited and row_ptr pair of the active vertices
+        uint64_t live_or = h[3];
+        if (dist_) {  // every rank continues while any rank has an active vertex; live lanes over all ranks
+          const uint64_t active = global_sum(h[2]);
+          live_or = 0;
+          for (uint64_t x : tr_->allgather(h[3], s_)) live_or |= x;
+          if (active == 0) break;
+        } else if (h[2] == 0) {
+          break;
+        }
         // lanes with an empty frontier receive nothing at this level (OMX_PULL_LIVE=0: wait for all lanes)
-        const uint64_t live = pull_live_ ? h[3] : ~0ull;
+        const uint64_t live = pull_live_ ? live_or : ~0ull;
         edges_ += h[0];
         edges_iter_ += h[0];
         HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
@@ -1911,7 +1980,34 @@ class Executor {
           std::fprintf(stderr, "[omx bfs] batch %llu level %lld: %s active=%llu push_edges=%llu E_t=%llu\n",
                        (unsigned long long)row0, (long long)d, (double)h[1] * pull_div_ > (double)eadj ? "pull" : "push",
                        (unsigned long long)h[2], (unsigned long long)h[1], (unsigned long long)h[0]);
-        if ((double)h[1] * pull_div_ > (double)eadj) {
+        if (dist_) {
+          // the frontier blocks of every rank (u64 masks sent as u32 word pairs; nothing to itself)
+          const int W = tr_->world(), me = tr_->rank();
+          std::vector<uint64_t> send(W, 2ull * (vhi - vlo)), sdispl(W, 0), recv(W), rdispl(W);
+          for (int p = 0; p < W; ++p) {
+            recv[p] = 2ull * (phi[p] - plo[p]);
+            rdispl[p] = 2ull * plo[p];
+          }
+          send[me] = recv[me] = 0;
+          tm_.begin("exchange");
+          tr_->alltoallv({reinterpret_cast<const uint32_t *>(fr.p + vlo)}, send, sdispl,
+                         {reinterpret_cast<uint32_t *>(fr.p)}, recv, rdispl, s_);
+          tm_.end(8ull * V);
+          for (int p = 0; p < radj.n; ++p) {
+            if (!rest.p) {
+              rest = DBuf<uint32_t>(&pool_, V);
+              exit_counts = DBuf<unsigned long long>(&pool_, 2);
+              HIP_CHECK(hipMemsetAsync(exit_counts.p, 0, sizeof(unsigned long long), s_));
+            }
+            HIP_CHECK(hipMemsetAsync(exit_counts.p + 1, 0, sizeof(unsigned long long), s_));
+            tm_.begin("k_bfs_pull_exit");
+            // a partition's col has no hub tags (pull_col_of): the hub array is never read
+            launch_bfs_pull_exit(vhi, radj.p[p].rp, radj.p[p].col, lanes & live, fr.p, fr.p, vis.p, nx.p, rest.p,
+                                 exit_counts.p, cus(), s_, vlo);
+            tm_.end(32ull * (vhi - vlo));
+            if (tm_.last() != SIZE_MAX) exit_recs.push_back(tm_.last());
+          }
+        } else if ((double)h[1] * pull_div_ > (double)eadj) {
           for (int p = 0; p < radj.n; ++p) {
             const uint64_t nt = bfs_pull_tiles(V, pull_E[p]);
             if (!pull_part[p]) {
@@ -1982,7 +2078,7 @@ class Executor {
           cc.n = (int)bcols.size();
           for (size_t k = 0; k < bcols.size(); ++k) {
             oc[k].emplace_back(&pool_, n);
-            cc.in[k] = col_[bcols[k]].p;
+            cc.in[k] = cin[k];
             cc.out[k] = oc[k].back().p;
           }
         } else {
@@ -1997,7 +2093,8 @@ class Executor {
       // visited + emission bitmap scans (two passes) + 4 B per written column per row
       tm_.end(16ull * V + 4ull * n * (carry ? bcols.size() + 1 : 2));
     }
-    if (!exit_recs.empty()) tm_.amend_at(exit_recs[0], 32ull * V + 12ull * read1(exit_counts.p));
+    if (!exit_recs.empty()) tm_.amend_at(exit_recs[0], 32ull * (vhi - vlo) + 12ull * read1(exit_counts.p));
+    if (dist_) owner_col_ = st.dst;  // the rows were emitted by the owners of their new vertex
     if (st.mode == T_BOUND) {
       select_rows(bflags.p, R);
       return;

@@ -257,8 +257,10 @@ bool eval_pred_const(const DPred &pred, int64_t depth);
 
 // multi-source BFS (bfs.hip): u64 lane mask per vertex, 64 binding rows per batch
 void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, hipStream_t s);
+// vertices [vlo, V) (a partition's own rows: vlo = part_lo, V = part_hi; fbm only from vertex 0)
 void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
-                     const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s);
+                     const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s,
+                     uint32_t vlo = 0);
 void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsigned long long *count, int cus,
                      hipStream_t s);
 void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg, hipStream_t s);
@@ -270,11 +272,12 @@ void launch_bfs_pull_partition(const uint64_t *rp, uint32_t V, uint64_t E, uint6
 void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const uint64_t *part, uint64_t E,
                      uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *fbm,
                      const uint64_t *visited, uint64_t *next, int cus, hipStream_t s);
-// dense levels: per-vertex pull with an early exit (k_bfs_pull_exit + k_bfs_pull_rest); rest u32[V]
+// dense levels: per-vertex pull with an early exit (k_bfs_pull_exit + k_bfs_pull_rest) over vertices
+// [vlo, V); rest u32[V]
 // scratch; counts[0] += in-edges read, counts[1] = vertices handed to the per-wave pass (zeroed by the caller)
 void launch_bfs_pull_exit(uint32_t V, const uint64_t *rp, const uint32_t *col, uint64_t lanes,
                           const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *visited, uint64_t *next,
-                          uint32_t *rest, unsigned long long *counts, int cus, hipStream_t s);
+                          uint32_t *rest, unsigned long long *counts, int cus, hipStream_t s, uint32_t vlo = 0);
 // hub-annotated col of a CSR for k_bfs_pull (returns the hub count; hub_idx u32[V], hist u32[4096] scratch)
 // rp_self: the CSR's own row pointers (its rows are re-ordered hub-first; OMX_PULL_SORT=0 keeps them)
 uint32_t build_pull_col(const uint64_t *rp_self, const uint64_t *rp_other, const uint32_t *col, uint32_t V, uint64_t E,

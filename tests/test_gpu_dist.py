@@ -141,10 +141,15 @@ def _vcols(q):
     return [c.strip() for c in q.split("RETURN")[1].split(",")]
 
 
+@pytest.mark.parametrize("varlen", ["auto", "pairs"])
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("q", DIST_VARLEN, ids=[q[0] for q in DIST_VARLEN])
-def test_partitioned_varlen_parity(rmat10_full, world, q):
+def test_partitioned_varlen_parity(rmat10_full, world, q, varlen, monkeypatch):
+    """auto: the BFS-exact items run the partitioned multi-source BFS (frontier blocks allgathered every
+    level, rows emitted on the owner of their new vertex); pairs: (row, vertex) pairs routed per level."""
     import orientdb_amd as o
+    if varlen == "pairs":
+        monkeypatch.setenv("OMX_VARLEN", "pairs")
     g, ref = rmat10_full
     cols = _vcols(q[1])
     want = ref.expected(q[1], cols)
@@ -165,6 +170,25 @@ def test_partitioned_varlen_edges_match_replicated(rmat10_full, q, monkeypatch):
     res = run_ranks(_parts(2), q[1])
     assert sum(r.info["edges_traversed"] for r in res) == full.info["edges_traversed"]
     assert sum(r.info["n_rows"] for r in res) == full.info["n_rows"]
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("q", [q for q in DIST_VARLEN if q[0] in ("depth_only", "two_batches", "while_prop", "both_dir",
+                                                                  "where_target", "maxdepth")], ids=lambda q: q[0])
+def test_partitioned_msbfs_matches_replicated(rmat10_full, q, world, monkeypatch):
+    """The partitioned multi-source BFS (every level pulled over the rank's own vertices from the
+    allgathered frontier) finds the replicated BFS's rows, level by level the same E_t."""
+    import orientdb_amd as o
+    g, _ = rmat10_full
+    monkeypatch.setenv("OMX_VARLEN", "bfs")
+    full = o.OMatchStatement(q[1]).execute(g, documents=False)
+    res = run_ranks(_parts(world), q[1], documents=False)
+    assert sum(r.info["edges_traversed"] for r in res) == full.info["edges_traversed"]
+    assert sum(r.info["n_rows"] for r in res) == full.info["n_rows"]
+    cols = _vcols(q[1])
+    want = sorted(map(tuple, np.asarray(full.rows).tolist()))
+    got = sorted(t for r in res for t in map(tuple, np.asarray(r.rows).tolist()))
+    assert got == want and len(cols) == np.asarray(full.rows).shape[1]
 
 
 def test_failing_rank_releases_its_peers(rmat10_full):

@@ -12,6 +12,7 @@ variable-length item, P/OMatchPathItem.java:79-105):
 * M1 partitioned: the same over a 4-rank 1-D partition of RMAT-24 (the multi-GPU bench's configuration;
       thread transport);
 * C3  RMAT-24, 64 roots, `while:($depth < 4)`: row count, E_t (Σ frontier degrees) and digest;
+* C3 partitioned: the same over a 4-rank 1-D partition of RMAT-24 (multi-source BFS, frontier allgather);
 * C5  the 3-hop COUNT shape on a 4-rank 1-D partition of RMAT-16 (thread transport): the ranks' bindings
       and edges add up to the oracle's, and the ranks' digests of the materialized rows add up to it.
 
@@ -118,6 +119,27 @@ def test_c3_rmat24_varlen_digest(rmat24):
     assert rs.info["n_rows"] == ref["n"] > 1e8
     assert rs.info["edges_traversed"] == ref["edges"]
     assert rs.info["digest"] == ref["digest"]
+
+
+def test_c3_partitioned_4ranks_rmat24(rmat24):
+    """configs[2] on a 4-rank 1-D partition of RMAT-24 (thread transport): the partitioned multi-source
+    BFS (frontier blocks allgathered every level) — rows, E_t and digest add up to the oracle's."""
+    import orientdb_amd as o
+    from oracle import dfs
+    from tests.test_gpu_dist import run_ranks
+    g = rmat24
+    q = "MATCH {class:Person,as:s,where:(uid < 64)}-Knows->{as:v, while:($depth < 4)} RETURN s, v"
+    ref = dfs.bfs_varlen(g.csr[0], g.csr[1], np.arange(64, dtype=np.uint32), max_depth=4, nthreads=THREADS,
+                         emit=False)
+    parts = [o.GraphSnapshot.rmat(24, device=0, partition=(r, 4)) for r in range(4)]
+    try:
+        res = run_ranks(parts, q, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST, documents=False)
+        assert sum(r.info["n_rows"] for r in res) == ref["n"] > 1e8
+        assert sum(r.info["edges_traversed"] for r in res) == ref["edges"]
+        assert sum(r.info["digest"] for r in res) % (1 << 64) == ref["digest"]
+    finally:
+        for p in parts:
+            p.close()
 
 
 def test_c5_shape_partitioned_rmat16():
