@@ -177,3 +177,86 @@ def test_two_rank_partitioned_exchange():
         if name == "fof":
             assert sum(len(s) for s in shards) == len(want)  # each distinct tuple on one rank
         assert all(len(g[name]) > 0 for g in gathered) or name == "3hop"
+
+
+# ---- two gloo ranks: restatement of the partitioned multi-source BFS -------------------------------
+def _msbfs_rows(rank, world, roots, depth, dist):
+    """exec.hip varlen_msbfs on a partition, restated: every rank runs the batch of all roots (lanes);
+    per level, prep over its own vertices (new = frontier & ~visited), an allgather of the owned frontier
+    blocks, a pull over its own vertices' in-edges (OR of the in-neighbours' masks & ~visited); it emits
+    (root, v) for its own visited vertices."""
+    import orientdb_amd as o
+    V = 1 << SCALE
+    lo, hi = o.partition_range(V, rank, world)
+    _, _, irp, icol = o.rmat_partition(SCALE, lo, hi, 16, SCALE)
+    fr = np.zeros(V, np.uint64)
+    vis = np.zeros(V, np.uint64)
+    for i, r in enumerate(roots):
+        fr[r] |= np.uint64(1) << np.uint64(i)
+    for d in range(depth + 1):
+        own = slice(lo, hi)
+        new = fr[own] & ~vis[own]
+        vis[own] |= new
+        fr[:] = 0
+        fr[own] = new
+        if d == depth:
+            break
+        blocks = [None] * world
+        dist.all_gather_object(blocks, (lo, hi, fr[own].copy()))
+        for blo, bhi, b in blocks:
+            fr[blo:bhi] = b
+        if sum(int(np.count_nonzero(b)) for _, _, b in blocks) == 0:
+            break
+        nx = np.zeros(V, np.uint64)
+        for v in range(lo, hi):
+            acc = np.uint64(0)
+            for u in icol[irp[v - lo]:irp[v - lo + 1]]:
+                acc |= fr[u]
+            nx[v] = acc & ~vis[v]
+        fr = nx
+    return [(int(roots[i]), v) for v in range(lo, hi) for i in range(len(roots))
+            if (int(vis[v]) >> i) & 1]
+
+
+def _msbfs_worker(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = _msbfs_rows(rank, world, np.arange(40, dtype=np.uint32), 3, dist)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, res)
+        if rank == 0:
+            out.put(gathered)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_partitioned_msbfs():
+    """The partitioned BFS's exchange (allgather of the owned frontier blocks) over two gloo ranks finds
+    the oracle's BFS balls (oracle/bfs_ref.c) and emits each (root, v) on v's owner only."""
+    import orientdb_amd as o
+    from oracle import dfs
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_msbfs_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rp, col = o.rmat_csr(SCALE, 16, SCALE)
+    roots = np.arange(40, dtype=np.uint32)
+    ref = dfs.bfs_varlen(rp, col, roots, max_depth=3, nthreads=2)
+    want = {(int(roots[a]), int(b)) for a, b in ref["pairs"]}
+    got = [set(g) for g in gathered]
+    assert set().union(*got) == want
+    assert sum(len(g) for g in gathered) == len(want)  # every (root, v) on one rank
+    V = 1 << SCALE
+    for r, g in enumerate(gathered):
+        lo, hi = o.partition_range(V, r, world)
+        assert all(lo <= v < hi for _, v in g)
