@@ -137,6 +137,10 @@ class Executor {
       heavy_deg_sliced_ = heavy_deg_;
       heavy_deg_fixed_ = true;
     }
+    if (const char *uc = std::getenv("OMX_UNF_CHUNK")) {
+      const unsigned long c = std::strtoul(uc, nullptr, 10);
+      unf_chunk_shift_ = c == 256 ? 8u : c == 512 ? 9u : c == 2048 ? 11u : 10u;
+    }
     if (const char *h = std::getenv("OMX_HEAVY_DEG_UNFILTERED")) {
       heavy_deg_unfiltered_ = std::max<uint64_t>(1, std::strtoull(h, nullptr, 10));
       heavy_deg_unfiltered_set_ = true;
@@ -379,6 +383,7 @@ class Executor {
   uint64_t heavy_deg_ = kHeavyDeg;
   uint64_t heavy_deg_sliced_ = kHeavyDegSliced;
   bool heavy_deg_fixed_ = false;  // OMX_HEAVY_DEG given
+  uint32_t unf_chunk_shift_ = 11;  // heavy chunk windows of unfiltered writes (OMX_UNF_CHUNK; 2048: profiles/r02/chunkwin)
   uint64_t heavy_deg_unfiltered_ = kHeavyDeg;  // unfiltered hops (OMX_HEAVY_DEG_UNFILTERED, over OMX_HEAVY_DEG)
   bool heavy_deg_unfiltered_set_ = false;
   bool debug_expand_ = false;
@@ -891,8 +896,10 @@ class Executor {
       spop = DBuf<unsigned long long>(&pool_, P);
       launch_slice_popc(filter, g_.V, slice_shift_, P, spop.p, s_);
     }
+    // unfiltered writes may cut heavy rows into other aligned windows (OMX_UNF_CHUNK: 256, 512, 1024, 2048)
+    const uint32_t cs = (!filter && !member && write && !sliced) ? unf_chunk_shift_ : 10u;
     tm_.begin("k_bin_rows");
-    launch_bin_count(sliced, src, R, adj, cuts, hd, P, blk.p, s_);
+    launch_bin_count(sliced, src, R, adj, cuts, hd, P, blk.p, s_, cs);
     launch_bin_scan(blk.p, R, P, qb.p, mail(), s_, spop.p, estimate ? P : 0);
     const uint64_t *m = wait_mail();
     const uint64_t EL = m[0], EH = m[1], nchunks = m[2], NL = m[3];
@@ -943,7 +950,7 @@ class Executor {
     } else if (adj.n == 1) {
       lbase = DBuf<uint64_t>(&pool_, R);
     }
-    launch_bin_fill(sliced, src, R, adj, cuts, hd, P, blk.p, qb.p, loffs.p, lbase.p, lr, chunks.p, schunks.p, s_);
+    launch_bin_fill(sliced, src, R, adj, cuts, hd, P, blk.p, qb.p, loffs.p, lbase.p, lr, chunks.p, schunks.p, s_, cs);
     tm_.end(R * (4 + 16ull * adj.n + 8 + (adj.n == 1 ? 8 : 0)) +
             nchunks * (sliced ? sizeof(SliceChunk) : sizeof(ChunkDesc)));
     const uint64_t ntiles = EL && !lsliced ? (R + EL + kExpandTile - 1) / kExpandTile : 0;
@@ -961,7 +968,7 @@ class Executor {
     const uint64_t hblocks = (nchunks + WPB - 1) / WPB;
     // persistent grids: every resident slot. (Running the two kernels side by side on split grids
     // was measured slower: the light kernel is latency-bound per tile and needs the whole chip.)
-    const uint64_t sh = (uint64_t)cus() * expand_blocks_per_cu(true, single, filt, write, member);
+    const uint64_t sh = (uint64_t)cus() * expand_blocks_per_cu(true, single, filt, write, member, cs);
     const uint64_t sl = (uint64_t)cus() * expand_blocks_per_cu(false, single, filt, write, member);
     constexpr unsigned SWPB = kSliceBlock / 64;
     // sliced: one workgroup per CU, split over the slices in proportion to their chunk counts
@@ -1027,7 +1034,7 @@ class Executor {
                    (unsigned long long)nchunks, P, (unsigned long long)ntiles, gl, gls, gh, (int)filt);
     // heavy output: one arena per wave, sized for the most chunks a wave of the launch owns
     const uint64_t wh = (uint64_t)gh * (sliced ? SWPB : WPB);
-    const uint64_t caph_exact = !gh ? 0 : sliced ? caph_sliced : (nchunks + wh - 1) / wh * (uint64_t)kChunk;
+    const uint64_t caph_exact = !gh ? 0 : sliced ? caph_sliced : (nchunks + wh - 1) / wh * (1ull << cs);
     const uint64_t nseg_h = wh;
     const uint64_t capl_exact = lsliced ? capls : gl ? (ntiles + gl - 1) / gl * (uint64_t)kExpandTile : 0;
     double capl_est = 0;
@@ -1055,6 +1062,7 @@ class Executor {
     a.chunks = chunks.p;
     a.schunks = schunks.p;
     a.nchunks = nchunks;
+    a.chunk_shift = cs;
     a.dense_base = EH;
     if (member) {
       a.member_src = member_src;

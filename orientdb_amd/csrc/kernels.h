@@ -102,6 +102,7 @@ struct ExpandArgs {
   const ChunkDesc *chunks;
   const SliceChunk *schunks;  // sliced kernel
   uint64_t nchunks;
+  uint32_t chunk_shift;       // unsliced chunks: (1 << chunk_shift)-aligned col windows (8, 9 or 10)
   // fused closing check of a cyclic pattern (sorted-adjacency intersection): neighbour n of row r is
   // kept only if n ∈ N_member(member_src[r]); member_edges accumulates Σ |N_member(member_src[r])| over
   // the (row, n) pairs that reach the check, i.e. the edges the unfused check step traverses.
@@ -163,8 +164,9 @@ struct LightRows {
 constexpr int kBinBlock = 256;
 constexpr int kBinKeys = 3;  // keys before the per-slice chunk counts
 inline unsigned bin_tiles(uint64_t R) { return (unsigned)((R + 1 + kBinBlock - 1) / kBinBlock); }
+// chunk_shift: unsliced chunks are the (1 << chunk_shift)-aligned windows a heavy row touches
 void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
-                      uint64_t heavy_deg, uint32_t P, uint64_t *blk, hipStream_t s);
+                      uint64_t heavy_deg, uint32_t P, uint64_t *blk, hipStream_t s, uint32_t chunk_shift = 10);
 // extra[0..nextra) (device words) are posted after the totals: mail[5 + P + i]
 void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s,
                      const unsigned long long *extra = nullptr, uint32_t nextra = 0);
@@ -173,7 +175,8 @@ void launch_slice_popc(const uint64_t *bm, uint32_t V, uint32_t shift, uint32_t 
                        hipStream_t s);
 void launch_bin_fill(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
                      uint64_t heavy_deg, uint32_t P, const uint64_t *blk, const uint64_t *qb, uint64_t *loffs,
-                     uint64_t *lbase, const LightRows &lr, ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s);
+                     uint64_t *lbase, const LightRows &lr, ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s,
+                     uint32_t chunk_shift = 10);
 // grid = sa.wg0[P] workgroups (one per CU); wave w appends to arena_base + w·arena_cap and reports
 // seg_count/seg_start[seg_base + w]
 void launch_expand_heavy_sliced(const ExpandArgs &a, const SliceArgs &sa, unsigned grid, bool write, hipStream_t s);
@@ -184,7 +187,7 @@ void launch_expand_light_sliced(const ExpandArgs &a, const SliceArgs &sa, unsign
 // persistent launches: `grid` blocks loop over the tiles / chunks
 void launch_expand(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);
 void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStream_t s);
-int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool member = false);
+int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool member = false, uint32_t chunk_shift = 10);
 void launch_compact_segments(int ncols, uint32_t *const *in, uint32_t *const *out, const uint64_t *seg_start,
                              const uint32_t *seg_count, const uint64_t *seg_offs, uint32_t nseg, hipStream_t s);
 

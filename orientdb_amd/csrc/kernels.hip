@@ -655,9 +655,10 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
 // the current chunk is filtered (software pipeline).
 __device__ __forceinline__ bool bm_test32(const uint32_t *bm, uint32_t v) { return (bm[v >> 5] >> (v & 31)) & 1u; }
 
-template <bool FILTER, bool WRITE, bool MEMBER>
+template <bool FILTER, bool WRITE, bool MEMBER, int NS = kHeavySlots>
 __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
-  constexpr int NS = kHeavySlots, WPB = kHeavyBlock / 64;
+  constexpr int WPB = kHeavyBlock / 64;
+  constexpr uint64_t CH = 64 * NS;  // the chunk window
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wid = (uint64_t)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nw = (uint64_t)gridDim.x * WPB;
@@ -666,7 +667,7 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
   uint64_t acc = 0;
   uint64_t medges = 0, mprobes = 0;
   auto load = [&](const ChunkDesc &d, uint32_t (&q)[NS]) {
-    const uint64_t win = d.lo / kChunk * kChunk;
+    const uint64_t win = d.lo / CH * CH;
     const uint32_t *col = a.adj.p[d.part].col + win;
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
@@ -689,7 +690,7 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
   }
   while (c < a.nchunks) {
     const uint64_t cn = c + nw;
-    const uint64_t win = d.lo / kChunk * kChunk;
+    const uint64_t win = d.lo / CH * CH;
     uint32_t mask = 0;
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
@@ -865,7 +866,7 @@ void launch_build_cuts(const uint64_t *rp, const uint32_t *col, uint32_t vlo, ui
 template <bool SLICED, int MAXP>
 __device__ __forceinline__ void row_bins(const uint32_t *src, uint64_t r, uint64_t R, const DAdj &adj,
                                          const DCuts &cuts, uint64_t heavy_deg, uint32_t P,
-                                         uint64_t (&x)[kBinKeys + MAXP]) {
+                                         uint64_t (&x)[kBinKeys + MAXP], uint32_t cs = 10) {
 #pragma unroll
   for (int k = 0; k < kBinKeys + MAXP; ++k) x[k] = 0;
   if (r >= R) return;
@@ -885,7 +886,7 @@ __device__ __forceinline__ void row_bins(const uint32_t *src, uint64_t r, uint64
 #pragma unroll
       for (int q = 0; q < MAXP; ++q) x[kBinKeys + q] += chunk_pieces(cut[q], cut[q + 1]);
     } else if (e > b) {
-      x[kBinKeys] += (e - 1) / kChunk - b / kChunk + 1;
+      x[kBinKeys] += ((e - 1) >> cs) - (b >> cs) + 1;
     }
   }
 }
@@ -922,12 +923,12 @@ __device__ __forceinline__ void block_excl_scan_k(uint64_t (&x)[K], uint64_t (&t
 
 template <bool SLICED, int MAXP>
 __global__ __launch_bounds__(kBinBlock) void k_bin_count(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
-                                                          uint64_t heavy_deg, uint32_t P, uint64_t *blk) {
+                                                          uint64_t heavy_deg, uint32_t P, uint64_t *blk, uint32_t cs) {
   constexpr int K = kBinKeys + MAXP;
   __shared__ uint64_t s_w[K * (kBinBlock / 64)];
   const uint64_t r = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x;
   uint64_t x[K], tot[K];
-  row_bins<SLICED, MAXP>(src, r, R, adj, cuts, heavy_deg, P, x);
+  row_bins<SLICED, MAXP>(src, r, R, adj, cuts, heavy_deg, P, x, cs);
   block_excl_scan_k<kBinBlock, K>(x, tot, s_w);
   if (threadIdx.x == 0) {
 #pragma unroll
@@ -1033,13 +1034,14 @@ template <bool SLICED, int MAXP>
 __global__ __launch_bounds__(kBinBlock) void k_bin_fill(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
                                                          uint64_t heavy_deg, uint32_t P, const uint64_t *blk,
                                                          const uint64_t *qb, uint64_t *loffs, uint64_t *lbase,
-                                                         LightRows lr, ChunkDesc *chunks, SliceChunk *schunks) {
+                                                         LightRows lr, ChunkDesc *chunks, SliceChunk *schunks,
+                                                         uint32_t cs) {
   constexpr int K = kBinKeys + MAXP;
   __shared__ uint64_t s_w[K * (kBinBlock / 64)];
   const uint64_t r = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x;
   const uint32_t nb = gridDim.x;
   uint64_t x[K], tot[K];
-  row_bins<SLICED, MAXP>(src, r, R, adj, cuts, heavy_deg, P, x);
+  row_bins<SLICED, MAXP>(src, r, R, adj, cuts, heavy_deg, P, x, cs);
   const uint64_t heavy = x[1], light = x[2];
   block_excl_scan_k<kBinBlock, K>(x, tot, s_w);
   if (r > R) return;
@@ -1072,8 +1074,9 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_fill(const uint32_t *src, uin
     uint64_t pos = x[1] + blk[(uint64_t)nb + blockIdx.x];  // dense output index of the row's first edge
     for (int p = 0; p < adj.n; ++p) {
       const uint64_t b = adj.p[p].rp[v], e = adj.p[p].rp[v + 1];
-      for (uint64_t w = b / kChunk * kChunk; e > b && w < e; w += kChunk) {  // an empty part has no chunk
-        const uint64_t clo = w > b ? w : b, chi = w + kChunk < e ? w + kChunk : e;
+      const uint64_t ch = 1ull << cs;
+      for (uint64_t w = b >> cs << cs; e > b && w < e; w += ch) {  // an empty part has no chunk
+        const uint64_t clo = w > b ? w : b, chi = w + ch < e ? w + ch : e;
         chunks[o++] = ChunkDesc{clo, chi, pos + (clo - b), (uint32_t)r, (uint32_t)p};
       }
       pos += e - b;
@@ -1099,13 +1102,14 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_fill(const uint32_t *src, uin
 }
 
 void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
-                      uint64_t heavy_deg, uint32_t P, uint64_t *blk, hipStream_t s) {
+                      uint64_t heavy_deg, uint32_t P, uint64_t *blk, hipStream_t s, uint32_t chunk_shift) {
   const unsigned nb = bin_tiles(R);
   if (!sliced) {
-    hipLaunchKernelGGL((k_bin_count<false, 1>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, heavy_deg, 1u, blk);
+    hipLaunchKernelGGL((k_bin_count<false, 1>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, heavy_deg, 1u, blk,
+                       chunk_shift);
   } else {
 #define OMX_BN(M) hipLaunchKernelGGL((k_bin_count<true, M>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, \
-                                     heavy_deg, P, blk)
+                                     heavy_deg, P, blk, 10u)
     OMX_BY_MAXP(P, OMX_BN);
 #undef OMX_BN
   }
@@ -1130,14 +1134,15 @@ void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const 
 }
 void launch_bin_fill(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
                      uint64_t heavy_deg, uint32_t P, const uint64_t *blk, const uint64_t *qb, uint64_t *loffs,
-                     uint64_t *lbase, const LightRows &lr, ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s) {
+                     uint64_t *lbase, const LightRows &lr, ChunkDesc *chunks, SliceChunk *schunks, hipStream_t s,
+                     uint32_t chunk_shift) {
   const unsigned nb = bin_tiles(R);
   if (!sliced) {
     hipLaunchKernelGGL((k_bin_fill<false, 1>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, heavy_deg, 1u, blk,
-                       qb, loffs, lbase, lr, chunks, schunks);
+                       qb, loffs, lbase, lr, chunks, schunks, chunk_shift);
   } else {
 #define OMX_BF(M) hipLaunchKernelGGL((k_bin_fill<true, M>), dim3(nb), dim3(kBinBlock), 0, s, src, R, adj, cuts, \
-                                     heavy_deg, P, blk, qb, loffs, lbase, lr, chunks, schunks)
+                                     heavy_deg, P, blk, qb, loffs, lbase, lr, chunks, schunks, 10u)
     OMX_BY_MAXP(P, OMX_BF);
 #undef OMX_BF
   }
@@ -1619,20 +1624,28 @@ void launch_expand_heavy(const ExpandArgs &a, unsigned grid, bool write, hipStre
   if (!grid) return;
   const bool member = a.member_src != nullptr, filter = a.filter != nullptr || member;
   dim3 g(grid), b(kHeavyBlock);
+  // smaller chunk windows only for unfiltered writes (the dense emission of medium rows)
+  if ((filter || !write) && a.chunk_shift != 10) fail(OMX_E_INVALID, "internal: heavy chunks below 1024 only for dense writes");
 #define OMX_EXH(F, Wr, M) hipLaunchKernelGGL((k_expand_heavy<F, Wr, M>), g, b, 0, s, a)
   if (member) { if (write) OMX_EXH(true, true, true); else OMX_EXH(true, false, true); }
   else if (filter) { if (write) OMX_EXH(true, true, false); else OMX_EXH(true, false, false); }
-  else { if (write) OMX_EXH(false, true, false); else OMX_EXH(false, false, false); }
+  else if (!write) OMX_EXH(false, false, false);
+  else if (a.chunk_shift == 8) hipLaunchKernelGGL((k_expand_heavy<false, true, false, 4>), g, b, 0, s, a);
+  else if (a.chunk_shift == 9) hipLaunchKernelGGL((k_expand_heavy<false, true, false, 8>), g, b, 0, s, a);
+  else if (a.chunk_shift == 10) OMX_EXH(false, true, false);
+  else if (a.chunk_shift == 11) hipLaunchKernelGGL((k_expand_heavy<false, true, false, 32>), g, b, 0, s, a);
+  else fail(OMX_E_INVALID, "internal: heavy chunk windows of 256, 512, 1024 or 2048 entries");
 #undef OMX_EXH
   KCHECK("k_expand_heavy");
 }
 
-int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool member) {
+int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool member, uint32_t chunk_shift) {
   // the occupancy query costs a host round trip into the runtime: answer each variant once
-  static int cache[32];
+  static int cache[128];
   static std::mutex cache_m;
   filter = filter || member;
-  const int key = (int)heavy | (int)single << 1 | (int)filter << 2 | (int)write << 3 | (int)member << 4;
+  const int cs = heavy && !filter && write ? (int)(chunk_shift - 8) & 3 : 2;  // 0..3: 256..2048 entries
+  const int key = (int)heavy | (int)single << 1 | (int)filter << 2 | (int)write << 3 | (int)member << 4 | cs << 5;
   {
     std::lock_guard<std::mutex> lk(cache_m);
     if (cache[key]) return cache[key];
@@ -1643,7 +1656,11 @@ int expand_blocks_per_cu(bool heavy, bool single, bool filter, bool write, bool 
   if (heavy) {
     if (member) e = write ? OCC((k_expand_heavy<true, true, true>), kHeavyBlock) : OCC((k_expand_heavy<true, false, true>), kHeavyBlock);
     else if (filter) e = write ? OCC((k_expand_heavy<true, true, false>), kHeavyBlock) : OCC((k_expand_heavy<true, false, false>), kHeavyBlock);
-    else e = write ? OCC((k_expand_heavy<false, true, false>), kHeavyBlock) : OCC((k_expand_heavy<false, false, false>), kHeavyBlock);
+    else if (!write) e = OCC((k_expand_heavy<false, false, false>), kHeavyBlock);
+    else if (cs == 0) e = OCC((k_expand_heavy<false, true, false, 4>), kHeavyBlock);
+    else if (cs == 1) e = OCC((k_expand_heavy<false, true, false, 8>), kHeavyBlock);
+    else if (cs == 3) e = OCC((k_expand_heavy<false, true, false, 32>), kHeavyBlock);
+    else e = OCC((k_expand_heavy<false, true, false>), kHeavyBlock);
   } else if (single) {
     e = member ? OCC((k_expand<true, true, true, true>), kExpandBlock)
                : filter ? OCC((k_expand<true, true, true, false>), kExpandBlock) : OCC((k_expand<true, false, true, false>), kExpandBlock);

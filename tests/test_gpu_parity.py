@@ -252,6 +252,19 @@ def test_rmat_parity_all_rows_chunked(rmat10, q, monkeypatch):
     _parity(g, ref, q[1], q[2])
 
 
+@pytest.mark.parametrize("chunk", ["256", "512", "2048"])
+@pytest.mark.parametrize("q", RMAT_QUERIES, ids=[q[0] for q in RMAT_QUERIES])
+def test_rmat_parity_dense_chunk_windows(rmat10, q, chunk, monkeypatch):
+    """Unfiltered written hops with every row of degree ≥ 2 cut into 256-, 512- or 2048-entry aligned
+    chunk windows (k_expand_heavy with 4 / 8 / 32 slots), factorized hops forced so their row emission
+    takes it."""
+    monkeypatch.setenv("OMX_HEAVY_DEG_UNFILTERED", "2")
+    monkeypatch.setenv("OMX_UNF_CHUNK", chunk)
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    g, ref = rmat10
+    _parity(g, ref, q[1], q[2])
+
+
 SLICED_IDS = ("c2_both_ends", "in_dir", "both_dir", "three_hop", "triangle_filtered", "matches", "varlen_maxdepth",
               "two_cols_dedup")
 
