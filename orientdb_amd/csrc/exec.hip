@@ -168,6 +168,7 @@ class Executor {
       factor_ = std::strcmp(fz, "0") != 0;
       if (std::strcmp(fz, "force") == 0) factor_min_rows_ = 1, factor_min_ratio_ = 0;
     }
+    if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
     if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
     dist_setup();
   }
@@ -223,6 +224,10 @@ class Executor {
           continue;
         }
         prune(p_.live_before[i]);
+        if (last && st.kind == S_EXPAND && mark_ok(st)) {
+          expand_mark(st);
+          continue;
+        }
         switch (st.kind) {
           case S_ROOT: root(st); break;
           case S_EXPAND: expand_step(st, !count_only, seg_ok); counted_only = count_only; break;
@@ -239,7 +244,7 @@ class Executor {
     } else {
       R_ = 0;
     }
-    if (!chain) bindings_ = R_;
+    if (!chain) bindings_ = marked_ ? marked_bindings_ : R_;
     uint64_t n = 0;
     int ncols = 0;
     std::vector<DBuf<uint32_t>> out;
@@ -856,8 +861,11 @@ class Executor {
   ExpandOut expand_core(const uint32_t *src, uint64_t R, const AdjSpec &adjs, const uint64_t *filter,
                         const std::vector<const uint32_t *> &carry, bool write, bool allow_segmented = false,
                         const uint32_t *member_src = nullptr, const AdjSpec *member_adj = nullptr,
-                        const uint64_t *member_filter = nullptr, const DAdj *raw_adj = nullptr, bool ordered = false) {
+                        const uint64_t *member_filter = nullptr, const DAdj *raw_adj = nullptr, bool ordered = false,
+                        uint64_t *mark = nullptr) {
     ExpandOut o;
+    if (mark && (write || filter || member_src || ordered))
+      fail(OMX_E_INVALID, "internal: a marking expansion is unfiltered and writes no rows");
     DAdj adj = raw_adj ? *raw_adj : make_adj(adjs);
     if (adj.n == 0 || R == 0) return o;
     const bool member = member_src != nullptr;
@@ -914,7 +922,7 @@ class Executor {
     const uint64_t E = EL + EH;
     o.E = E;
     if (E == 0) return o;
-    if (!write && filter == nullptr && !member) {
+    if (!write && filter == nullptr && !member && !mark) {
       // counting an unfiltered hop: its bindings are Σ degree, known from the scan — no col[] reads
       // (reported apart: omx_result_info.edges_read excludes these edges)
       o.n = E;
@@ -1063,6 +1071,7 @@ class Executor {
     a.schunks = schunks.p;
     a.nchunks = nchunks;
     a.chunk_shift = cs;
+    a.mark = mark;
     a.dense_base = EH;
     if (member) {
       a.member_src = member_src;
@@ -1250,6 +1259,37 @@ class Executor {
     segmented_ = o.segmented;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
     col_[st.dst] = std::move(o.dst);
+  }
+
+  // The last hop of a plan that returns only its new alias, de-duplicated (configs[0]: `RETURN fof`):
+  // every row's neighbours are marked in a V-bit set as the kernels read them, instead of being written
+  // as rows and then marked (addToUniqueResult keeps one row per distinct value, C/command/
+  // OBasicCommandContext.java:347-353). All Σ deg adjacency entries are still read; the bindings are
+  // that sum. Unfiltered hops on one GPU, no LIMIT, no optional target, not a variable-length item.
+  bool marked_ = false;
+  uint64_t marked_bindings_ = 0;
+  bool mark_fuse_ = true;  // OMX_MARK_FUSE=0: write the rows and mark them in the projection
+  bool mark_ok(const Step &st) const {
+    return mark_fuse_ && !dist_ && st.filter_bm < 0 && !st.optional && p_.kind == Plan::MATCH &&
+           p_.proj == Plan::PROJ_ALIASES && !p_.unique_by_construction && p_.out_aliases.size() == 1 &&
+           p_.out_aliases[0] == st.dst && !p_.optional[st.dst] && p_.limit < 0 && o_.limit < 0 &&
+           o_.mode == OMX_MODE_MATERIALIZE;
+  }
+  void expand_mark(const Step &st) {
+    route_owner(st.src);
+    DBuf<uint64_t> bm(&pool_, std::max<uint64_t>(nwords_, 1));
+    HIP_CHECK(hipMemsetAsync(bm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+    ExpandOut o = expand_core(col_[st.src].p, R_, st.adj, nullptr, {}, false, false, nullptr, nullptr, nullptr, nullptr,
+                              false, bm.p);
+    edges_ += o.E;
+    edges_iter_ += o.E;
+    bound_[st.dst] = 1;
+    marked_ = true;
+    marked_bindings_ = o.E;
+    uint64_t m = 0;
+    col_[st.dst] = bitmap_list(bm.p, 0, 1, m);
+    R_ = m;
+    segmented_ = false;
   }
 
   // Factorized expansion of a filtered hop whose rows repeat their source vertices (hubs reached from
@@ -2401,7 +2441,7 @@ class Executor {
         HIP_CHECK(hipMemcpyAsync(out.back().p, out[taken[a]].p, R_ * 4, hipMemcpyDeviceToDevice, s_));
       }
     }
-    if (p_.unique_by_construction) return;
+    if (p_.unique_by_construction || marked_) return;  // (marked_: the rows are already the distinct set)
     if (segmented_) fail(OMX_E_INVALID, "internal: segmented table reached dedup");
     dedup_ran_ = 1;
     tm_.begin("dedup");

@@ -89,6 +89,7 @@ struct ExpandArgs {
   const uint32_t *carry_in[kMaxCols];
   uint32_t *carry_out[kMaxCols];
   uint32_t *out_dst;        // new column (neighbour)
+  uint64_t *mark;           // write = false: V-bit set of the neighbours (a one-column distinct projection)
   // output placement. Dense (no filter): index = dense_base + edge index (light) or
   // ChunkDesc::dense + position in the chunk (heavy). Arena (filter): each worker w of the launch
   // (a block for the light kernel, a wave for the heavy one) appends to [arena_base + w·arena_cap, …)

@@ -393,6 +393,14 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long *dst, uint64_t x
 
 // Light rows: merge-path tiles of kExpandTile (rows + edges) items, persistent blocks.
 // MEMBER (implies FILTER): fused closing check, see ExpandArgs::member_src.
+// set bit v, reading the word first: hub neighbours are marked again and again, and an atomic on a word
+// that already holds the bit is wasted (a stale read only costs a redundant atomic)
+__device__ __forceinline__ void mark_vertex(uint64_t *bm, uint32_t v) {
+  const uint64_t bit = 1ull << (v & 63);
+  if (!(__hip_atomic_load(&bm[v >> 6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
+    atomicOr((unsigned long long *)&bm[v >> 6], (unsigned long long)bit);
+}
+
 template <bool SINGLE, bool FILTER, bool WRITE, bool MEMBER>
 __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
   constexpr int B = kExpandBlock, IPT = kExpandIPT, T = kExpandTile, W = B / 64;
@@ -581,6 +589,10 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
             for (int c = 4; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
           }
         }
+      } else if (a.mark) {
+#pragma unroll
+        for (int k = 0; k < IPT; ++k)
+          if (k * B + tid < ne) mark_vertex(a.mark, nb[k]);
       }
       __syncthreads();  // LDS reuse by the next tile
       continue;
@@ -745,6 +757,10 @@ __global__ __launch_bounds__(kHeavyBlock) void k_expand_heavy(ExpandArgs a) {
         }
       }
       if (FILTER) acc = base - arena;
+    } else if (!FILTER && a.mark) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        if ((mask >> i) & 1u) mark_vertex(a.mark, q[i]);
     } else if (FILTER) {
       uint32_t cnt = __popc(mask);
 #pragma unroll

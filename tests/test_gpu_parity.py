@@ -265,6 +265,34 @@ def test_rmat_parity_dense_chunk_windows(rmat10, q, chunk, monkeypatch):
     _parity(g, ref, q[1], q[2])
 
 
+MARK_QUERIES = [
+    ("fof", "MATCH {class:Person}-Knows->{}-Knows->{as:fof} RETURN fof", ["fof"]),
+    ("fof_window", "MATCH {class:Person,as:a,where:(age < 20)}-Knows->{as:b}-Knows->{as:c} RETURN c", ["c"]),
+    ("both_dir", "MATCH {class:Person,as:a,where:(age < 10)}-Knows-{as:b}-Knows-{as:c} RETURN c", ["c"]),
+    ("in_dir", "MATCH {class:Person,as:a,where:(age < 30)}<-Knows-{as:b}<-Knows-{as:c} RETURN c", ["c"]),
+    ("three_hop", "MATCH {class:Person,as:a,where:(uid < 8)}-Knows->{}-Knows->{}-Knows->{as:d} RETURN d", ["d"]),
+]
+
+
+@pytest.mark.parametrize("heavy", ["default", "all_heavy"])
+@pytest.mark.parametrize("q", MARK_QUERIES, ids=[q[0] for q in MARK_QUERIES])
+def test_rmat_parity_marked_last_hop(rmat10, rmat10_raw, q, heavy, monkeypatch):
+    """A plan returning only its last alias, de-duplicated: the last hop marks the distinct neighbours
+    as it reads them (Executor::expand_mark) — same rows, bindings and E_t as writing the rows and
+    marking them in the projection (OMX_MARK_FUSE=0), on the simple graph and the multigraph."""
+    import orientdb_amd as o
+    if heavy == "all_heavy":
+        monkeypatch.setenv("OMX_HEAVY_DEG", "2")
+    for g, ref in (rmat10, rmat10_raw):
+        monkeypatch.setenv("OMX_MARK_FUSE", "1")
+        rs = _parity(g, ref, q[1], q[2])
+        monkeypatch.setenv("OMX_MARK_FUSE", "0")
+        plain = o.OMatchStatement(q[1]).execute(g, documents=False)
+        assert rs.info["bindings"] == plain.info["bindings"]
+        assert rs.info["edges_traversed"] == plain.info["edges_traversed"]
+        assert rs.info["n_rows"] == plain.info["n_rows"]
+
+
 SLICED_IDS = ("c2_both_ends", "in_dir", "both_dir", "three_hop", "triangle_filtered", "matches", "varlen_maxdepth",
               "two_cols_dedup")
 
