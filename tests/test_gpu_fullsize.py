@@ -9,7 +9,7 @@ variable-length item, P/OMatchPathItem.java:79-105):
       155 M (a, b, c) RID tuples (OMX_FLAG_DIGEST: Σ splitmix64-chain(row) mod 2^64, kernels.hip k_digest
       = oracle/dfs.py row_digest), rows left in HBM;
 * M1  the metric's own workload, RMAT-24 2-hop (C2's query at scale 24, ≈1.0e9 rows): the same;
-* M1 partitioned: the same over a 4- and an 8-rank 1-D partition of RMAT-24 (the multi-GPU bench's configuration;
+* M1 partitioned: the same over a 4-rank 1-D partition of RMAT-24 (the multi-GPU bench's configuration;
       thread transport);
 * C3  RMAT-24, 64 roots, `while:($depth < 4)`: row count, E_t (Σ frontier degrees) and digest;
 * C3 partitioned: the same over a 4-rank 1-D partition of RMAT-24 (multi-source BFS, frontier allgather);
@@ -90,12 +90,13 @@ def test_m1_rmat24_two_hop_digest(rmat24, m1_ref):
     assert rs.info["digest"] == ref["digest"]
 
 
-@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("world", [4])
 def test_m1_partitioned_rmat24(m1_ref, world):
-    """The multi-GPU bench's own configuration at full size: M1 on a 1-D partition of RMAT-24 over 4 or
-    8 ranks (thread transport on one GPU, the same routing code as RCCL): rows (a, b) routed to owner(b)
+    """The multi-GPU bench's own configuration at full size: M1 on a 1-D partition of RMAT-24 over 4
+    ranks (thread transport on one GPU, the same routing code as RCCL): rows (a, b) routed to owner(b)
     before the second hop, no final exchange (rows distinct by construction); the ranks' rows and
-    digests add up to the oracle's."""
+    digests add up to the oracle's. (8 ranks: green once, profiles/r02/dist_m1; left out of the suite
+    for its 80 s.)"""
     import orientdb_amd as o
     from tests.test_gpu_dist import run_ranks
     parts = [o.GraphSnapshot.rmat(24, device=0, partition=(r, world)) for r in range(world)]
