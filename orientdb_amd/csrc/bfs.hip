@@ -476,10 +476,13 @@ constexpr uint32_t kEmitWin = 4096;
 __global__ __launch_bounds__(kB) void k_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V,
                                                        const uint64_t *blk_offs, uint32_t row0, uint32_t *out_row,
                                                        uint32_t *out_v, BfsCarry cc) {
+  // a staged pair is its lane and its thread (the vertex is the block's first + thread): 2 B of LDS,
+  // so more blocks stay resident than with 4-B lane and vertex words
   __shared__ uint32_t s_w[kB / 64];
-  __shared__ uint32_t s_row[kEmitWin];
-  __shared__ uint32_t s_v[kEmitWin];
+  __shared__ uint8_t s_row[kEmitWin];
+  __shared__ uint8_t s_t[kEmitWin];
   __shared__ uint32_t s_cv[BfsCarry::kMax][64];
+  static_assert(kB <= 256, "s_t holds a thread index in 8 bits");
   const uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x;
   for (int c = 0; c < cc.n; ++c)
     if (threadIdx.x < cc.nl) s_cv[c][threadIdx.x] = cc.in[c][row0 + threadIdx.x];
@@ -496,8 +499,8 @@ __global__ __launch_bounds__(kB) void k_bfs_emit_write(const uint64_t *visited, 
       uint32_t o = off;
       for (; o < w0; ++o) mm &= mm - 1;  // entries that belong to an earlier window
       for (; mm && o < w1; ++o) {
-        s_row[o - w0] = (uint32_t)__builtin_ctzll(mm);
-        s_v[o - w0] = (uint32_t)v;
+        s_row[o - w0] = (uint8_t)__builtin_ctzll(mm);
+        s_t[o - w0] = (uint8_t)threadIdx.x;
         mm &= mm - 1;
       }
     }
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(kB) void k_bfs_emit_write(const uint64_t *visited, 
       const uint32_t l = s_row[i];
       if (cc.n == 0) out_row[base + w0 + i] = row0 + l;
       for (int k = 0; k < cc.n; ++k) cc.out[k][base + w0 + i] = s_cv[k][l];
-      out_v[base + w0 + i] = s_v[i];
+      out_v[base + w0 + i] = (uint32_t)((uint64_t)blockIdx.x * kB + s_t[i]);
     }
     __syncthreads();
   }
