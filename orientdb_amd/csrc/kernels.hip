@@ -562,16 +562,18 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
         if (((act >> k) & 1u) && !(lo[k] < end[k] && mcol[lo[k]] == nb[k])) passmask &= ~(1u << k);
     }
 
-    // the items' carried values (≤ 4 columns) are all requested before the first store: loaded next to
-    // the store that consumes it, each one waited for its own round trip (8 items × columns per thread)
-    uint32_t cv[WRITE ? IPT : 1][4];
+    // the items' first kCvRegs carried values are all requested before the first store: loaded next to
+    // the store that consumes it, each one waited for its own round trip (8 items × columns per thread);
+    // two columns in registers (M1's a, b) keep the kernel at 5 waves per SIMD
+    constexpr int kCvRegs = 2;
+    uint32_t cv[WRITE ? IPT : 1][kCvRegs];
     if (WRITE) {
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
         const uint64_t r = i0 + lrs[k];
         const bool live = k * B + tid < ne && (FILTER ? ((passmask >> k) & 1u) != 0 : true);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) cv[k][c] = live && c < a.ncarry ? a.carry_in[c][r] : 0u;
+        for (int c = 0; c < kCvRegs; ++c) cv[k][c] = live && c < a.ncarry ? a.carry_in[c][r] : 0u;
       }
     }
     if (!FILTER) {
@@ -584,9 +586,9 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
             const uint64_t r = i0 + lrs[k];
             a.out_dst[o] = nb[k];
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
+            for (int c = 0; c < kCvRegs; ++c)
               if (c < a.ncarry) a.carry_out[c][o] = cv[k][c];
-            for (int c = 4; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
+            for (int c = kCvRegs; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
           }
         }
       } else if (a.mark) {
@@ -624,9 +626,9 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(ExpandArgs a) {
           const uint64_t r = i0 + lrs[k];
           a.out_dst[o] = nb[k];
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
+          for (int c = 0; c < kCvRegs; ++c)
             if (c < a.ncarry) a.carry_out[c][o] = cv[k][c];
-          for (int c = 4; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
+          for (int c = kCvRegs; c < a.ncarry; ++c) a.carry_out[c][o] = a.carry_in[c][r];
         }
       }
     }
