@@ -666,14 +666,16 @@ def _equals(a, b):
 
 def _compare(op, a, b):
     """OGtOperator/OGeOperator/OLeOperator throw NPE on a null left operand, OLtOperator returns false
-    (P/OGtOperator.java:22-33, P/OLtOperator.java:22-36, P/OGeOperator.java:43-54, P/OLeOperator.java:22-33);
-    a null right operand compares false."""
+    (P/OGtOperator.java:22-33, P/OLtOperator.java:22-36, P/OGeOperator.java:43-54, P/OLeOperator.java:22-33).
+    With a non-null left operand, all four evaluate `iLeft.getClass() != iRight.getClass()` first, so a
+    null right operand is a NullPointerException too (the `iRight == null` test after OType.convert is
+    never reached with a null)."""
     if a is None:
         if op == "<":
             return False
         raise OracleError("NullPointerException: null left operand of %s" % op)
     if b is None:
-        return False
+        raise OracleError("NullPointerException: null right operand of %s" % op)
     if _num(a) and _num(b):
         pass
     elif isinstance(a, str) and _num(b):

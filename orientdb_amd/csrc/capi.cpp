@@ -1,9 +1,12 @@
 // capi.cpp — the extern "C" boundary (include/omx/match.h).
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "dist.h"
 #include "exec.h"
@@ -133,6 +136,35 @@ class Blob {
   uint64_t size_;
 };
 
+// the blob's contents, not only its extents: a stale or malformed snapshot fails here with
+// OMX_E_INVALID instead of sending out-of-range ids to the kernels (a parallel host scan, cheap next to
+// the upload that follows)
+template <class F>
+bool parallel_all(uint64_t n, F ok) {
+  const uint64_t kMin = 1u << 22;
+  const unsigned nt = n < kMin ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<char> good(nt, 1);
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      const uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+      for (uint64_t i = lo; i < hi; ++i)
+        if (!ok(i)) { good[t] = 0; return; }
+    });
+  for (auto &x : th) x.join();
+  for (char c : good)
+    if (!c) return false;
+  return true;
+}
+void check_csr(const uint64_t *rp, const uint32_t *col, uint64_t rows, uint64_t V, const char *what) {
+  if (!rp) return;
+  if (rp[0] != 0) omx::fail(OMX_E_INVALID, std::string("buffer: ") + what + " row_ptr[0] != 0");
+  if (!parallel_all(rows, [&](uint64_t i) { return rp[i] <= rp[i + 1]; }))
+    omx::fail(OMX_E_INVALID, std::string("buffer: ") + what + " row_ptr is not non-decreasing");
+  if (!parallel_all(rp[rows], [&](uint64_t i) { return col[i] < V; }))
+    omx::fail(OMX_E_INVALID, std::string("buffer: ") + what + " col holds a vertex id >= n_vertices");
+}
+
 }  // namespace
 
 extern "C" {
@@ -177,6 +209,8 @@ int omx_graph_create_blob(const void *blob, uint64_t size, omx_graph **out) {
       es[i].n_in_edges = r.n_in_edges;
       if (es[i].out_row_ptr && es[i].out_row_ptr[VL] != r.n_edges) omx::fail(OMX_E_INVALID, "buffer: out_row_ptr[V] != n_edges");
       if (es[i].in_row_ptr && es[i].in_row_ptr[VL] != nin) omx::fail(OMX_E_INVALID, "buffer: in_row_ptr[V] != n_in_edges");
+      check_csr(es[i].out_row_ptr, es[i].out_col, VL, V, "out");
+      check_csr(es[i].in_row_ptr, es[i].in_col, VL, V, "in");
     }
     d.n_edge_sets = h->n_edge_sets;
     d.edge_sets = es.data();
@@ -305,6 +339,8 @@ void omx_exec_options_init(omx_exec_options *o) {
 }
 
 int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, omx_result **out) {
+  omx::Transport *t = opts && opts->comm ? opts->comm->t.get() : nullptr;
+  const uint64_t exchanges0 = t ? t->exchanges : 0;
   const int rc = guard([&] {
     if (!g || !s || !out) omx::fail(OMX_E_INVALID, "null argument");
     omx_exec_options o;
@@ -320,10 +356,14 @@ int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, om
       s->plan_key = key;
     }
     std::lock_guard<std::mutex> lk(g->m);
-    *out = omx::execute_plan(*g->g, *s->plan, o, o.comm ? o.comm->t.get() : nullptr);
+    *out = omx::execute_plan(*g->g, *s->plan, o, t);
   });
-  // a rank that fails (planning included) releases the peers waiting for it in an exchange
-  if (rc != OMX_OK && opts && opts->comm) opts->comm->t->abort();
+  // A rank that fails releases the peers waiting for it in an exchange; the communicator is unusable
+  // afterwards. The exception is OMX_E_UNSUPPORTED raised before this call's first exchange: the
+  // planner and the plan's partition checks see the same statement, parameters and replicated schema
+  // on every rank, so every rank refused alike, nobody waits, the host falls back to the reference
+  // engine and the communicator stays usable for the next query.
+  if (rc != OMX_OK && t && (rc != OMX_E_UNSUPPORTED || t->exchanges != exchanges0)) t->abort();
   return rc;
 }
 

@@ -55,6 +55,7 @@ class ThreadTransport : public Transport {
 
   void counts(const uint64_t *d_send, std::vector<uint64_t> &send, std::vector<uint64_t> &recv,
               hipStream_t s) override {
+    ++exchanges;
     const int W = world();
     send.assign(W, 0);
     HIP_OK(hipMemcpyAsync(send.data(), d_send, W * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -76,6 +77,7 @@ class ThreadTransport : public Transport {
                  const std::vector<uint64_t> &sdispl, const std::vector<uint32_t *> &rbuf,
                  const std::vector<uint64_t> &recv, const std::vector<uint64_t> &rdispl, hipStream_t s) override {
     (void)send;
+    ++exchanges;
     const int W = world();
     HIP_OK(hipStreamSynchronize(s));  // this rank's send buffers are complete before peers read them
     {
@@ -98,6 +100,7 @@ class ThreadTransport : public Transport {
   void abort() override { hub_->abort(); }
 
   std::vector<uint64_t> allgather(uint64_t x, hipStream_t) override {
+    ++exchanges;
     {
       std::lock_guard<std::mutex> lk(hub_->m);
       hub_->gathered[rank_] = x;
@@ -145,6 +148,7 @@ class RcclTransport : public Transport {
   }
 
   std::vector<uint64_t> allgather(uint64_t x, hipStream_t s) override {
+    ++exchanges;
     if (!comm_) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: the communicator was aborted");
     HIP_OK(hipMemcpyAsync(d_one_, &x, sizeof(uint64_t), hipMemcpyHostToDevice, s));
     NCCL_OK(ncclAllGather(d_one_, d_all_, 1, ncclUint64, comm_, s));
@@ -158,6 +162,7 @@ class RcclTransport : public Transport {
 
   void counts(const uint64_t *d_send, std::vector<uint64_t> &send, std::vector<uint64_t> &recv,
               hipStream_t s) override {
+    ++exchanges;
     if (!comm_) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: the communicator was aborted");
     NCCL_OK(ncclAllToAll(d_send, d_recv_, 1, ncclUint64, comm_, s));
     send.assign(world_, 0);
@@ -170,6 +175,7 @@ class RcclTransport : public Transport {
   void alltoallv(const std::vector<const uint32_t *> &sbuf, const std::vector<uint64_t> &send,
                  const std::vector<uint64_t> &sdispl, const std::vector<uint32_t *> &rbuf,
                  const std::vector<uint64_t> &recv, const std::vector<uint64_t> &rdispl, hipStream_t s) override {
+    ++exchanges;
     if (!comm_) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: the communicator was aborted");
     std::vector<size_t> sc(send.begin(), send.end()), sd(sdispl.begin(), sdispl.end()), rc(recv.begin(), recv.end()),
         rd(rdispl.begin(), rdispl.end());

@@ -43,6 +43,10 @@ class Transport {
   virtual void abort() = 0;
   // every rank's x (host values), in rank order
   virtual std::vector<uint64_t> allgather(uint64_t x, hipStream_t s) = 0;
+  // collectives this rank has entered (counts / alltoallv / allgather): an execute that fails before
+  // its first exchange failed the same way on every rank (the plan and its checks are replicated), so
+  // nobody waits for it and the communicator stays usable
+  uint64_t exchanges = 0;
 };
 
 // threads of one process as ranks

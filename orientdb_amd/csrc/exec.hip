@@ -1885,6 +1885,9 @@ class Executor {
   // Multi-source BFS over 64-row batches (bfs.hip). Rows (row, v) come out distinct per row.
   void varlen_msbfs(const Step &st, bool depth_only_while) {
     require_u32_rows("a variable-length item");
+    // the pull kernels read bit 31 of an in-CSR entry as a hub tag (pull_col_of), and the partitioned
+    // pull reads the raw col: ids must stay below 2^31 (checked before any exchange: V is replicated)
+    if (g_.V >= 0x80000000u) unsupported("variable-length traversal over 2^31 or more vertices");
     uint64_t R = R_;
     const uint32_t V = g_.V;
     // Partitioned (SURVEY §8(e) "Variable-length: ... when the frontier is dense, an allgather"): every
@@ -2021,8 +2024,10 @@ class Executor {
         }
         // lanes with an empty frontier receive nothing at this level (OMX_PULL_LIVE=0: wait for all lanes)
         const uint64_t live = pull_live_ ? live_or : ~0ull;
+        // E_t: the frontier's adjacency summed per row (lane); edges_iter_ counts the adjacency entries the
+        // level's kernels actually read (push: the frontier's out-edges once for all lanes; tiled pull:
+        // every in-edge; early-exit pull: the in-edges walked, added when the traversal ends)
         edges_ += h[0];
-        edges_iter_ += h[0];
         HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
         if (debug_expand_)
           std::fprintf(stderr, "[omx bfs] batch %llu level %lld: %s active=%llu push_edges=%llu E_t=%llu\n",
@@ -2087,6 +2092,7 @@ class Executor {
                             probe ? fbm.p : nullptr, vis.p, nx.p, cus(), s_);
             // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask
             tm_.end(16ull * V + 12ull * pull_E[p]);
+            edges_iter_ += pull_E[p];
           }
         } else {
           if (!list.p) list = DBuf<uint32_t>(&pool_, V);
@@ -2105,6 +2111,7 @@ class Executor {
             launch_bfs_push(list.p, loffs.p, nl_act, etot, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, cus(), s_);
             // per frontier edge: col + visited + next (+ row_ptr and frontier mask per listed vertex)
             tm_.end(20ull * etot + 24ull * nl_act);
+            edges_iter_ += etot;
           }
         }
         std::swap(fr, nx);
@@ -2141,7 +2148,11 @@ class Executor {
       // visited + emission bitmap scans (two passes) + 4 B per written column per row
       tm_.end(16ull * V + 4ull * n * (carry ? bcols.size() + 1 : 2));
     }
-    if (!exit_recs.empty()) tm_.amend_at(exit_recs[0], 32ull * (vhi - vlo) + 12ull * read1(exit_counts.p));
+    if (exit_counts.p) {
+      const uint64_t walked = read1(exit_counts.p);
+      edges_iter_ += walked;
+      if (!exit_recs.empty()) tm_.amend_at(exit_recs[0], 32ull * (vhi - vlo) + 12ull * walked);
+    }
     if (dist_) owner_col_ = st.dst;  // the rows were emitted by the owners of their new vertex
     if (st.mode == T_BOUND) {
       select_rows(bflags.p, R);

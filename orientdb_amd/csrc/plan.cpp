@@ -484,7 +484,7 @@ class Planner {
           if (op == "<") return Value::Bool(false);
           unsupported("comparison with a null left operand (NullPointerException in the reference)");
         }
-        if (b->kind == Value::NUL) return Value::Bool(false);
+        if (b->kind == Value::NUL) unsupported("comparison with a null right operand (NullPointerException in the reference)");
         int c;
         if (is_num(*a) && is_num(*b)) {
           if (a->kind == Value::INT && b->kind == Value::INT) c = a->i < b->i ? -1 : a->i > b->i;
@@ -900,10 +900,24 @@ class Planner {
             unsupported("a possibly-null left operand of " + op + " (NullPointerException in the reference): " + expr_text(L));
           return emit_string_cmp(b, prop, op, fr->s);
         }
-        if (string_field(R, &prop) && fl && fl->kind == Value::STR) return emit_string_cmp(b, prop, flip(op), fl->s);
+        const bool ordering = op == "<" || op == "<=" || op == ">" || op == ">=";
+        if (string_field(R, &prop) && fl && fl->kind == Value::STR) {
+          // a constant left operand: a null right one is the reference's NPE for every ordering operator
+          if (ordering && g_.props[prop].has_nulls)
+            unsupported("a possibly-null right operand of " + op + " (NullPointerException in the reference): " + expr_text(R));
+          return emit_string_cmp(b, prop, flip(op), fl->s);
+        }
         if (fr && fr->kind == Value::NUL) {
-          b.emit(P_PUSH_BOOL, 0, op == "!=", 0, 1);
-          return;
+          if (!ordering) {
+            b.emit(P_PUSH_BOOL, 0, op == "!=", 0, 1);
+            return;
+          }
+          // null < null is false (OLtOperator tests the left operand first); anything else throws
+          if (op == "<" && fl && fl->kind == Value::NUL) {
+            b.emit(P_PUSH_BOOL, 0, 0, 0, 1);
+            return;
+          }
+          unsupported("null right operand of " + op + " (NullPointerException in the reference)");
         }
         if (fl && fl->kind == Value::NUL) {
           if (op == "=" || op == "!=" || op == "<") {
@@ -918,6 +932,10 @@ class Planner {
         // snapshot is left to the reference engine instead of being compared false
         if ((op == ">" || op == ">=" || op == "<=") && may_be_null(L))
           unsupported("a possibly-null left operand of " + op + " (NullPointerException in the reference): " + expr_text(L));
+        // all four ordering operators dereference a null right operand once the left one is non-null
+        // (`iLeft.getClass() != iRight.getClass()`): compared false on the device, thrown by the reference
+        if (ordering && (may_be_null(R) || string_may_be_null(R)))
+          unsupported("a possibly-null right operand of " + op + " (NullPointerException in the reference): " + expr_text(R));
         CT l = compile_value(b, L, allow_depth);
         CT r = compile_value(b, R, allow_depth);
         if ((l == C_BOOL) != (r == C_BOOL) && l != C_NUL && r != C_NUL)

@@ -251,7 +251,9 @@ class Evaluator {
       if (op == "<") return false;
       fail(OMX_E_EXECUTION, "NullPointerException: null left operand of " + op);
     }
-    if (b.k == HVal::NUL) return false;
+    // a non-null left operand: iLeft.getClass() != iRight.getClass() dereferences the right one first
+    // (P/OGtOperator.java:22-33, P/OLtOperator.java:22-36, P/OGeOperator.java:43-54, P/OLeOperator.java:22-33)
+    if (b.k == HVal::NUL) fail(OMX_E_EXECUTION, "NullPointerException: null right operand of " + op);
     int c;
     if (is_num(a) && is_num(b)) {
       if (a.k == HVal::INT && b.k == HVal::INT) c = a.i < b.i ? -1 : a.i > b.i;

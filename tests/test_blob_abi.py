@@ -61,6 +61,38 @@ def test_blob_rejects_bad_buffers(blob_graphs):
     assert _create(bad) == o._native.OMX_E_INVALID
 
 
+def _edge_set0(buf):
+    """(n_vertices, out_row_ptr offset, out_col offset, in_col offset) of the first edge-set record."""
+    raw = buf.view(np.uint8)
+    V = int(raw[8:12].view(np.uint32)[0])
+    es_off = int(buf[8])  # header word 8
+    rec = raw[es_off:es_off + 56].view(np.uint64)
+    return V, int(rec[2]), int(rec[3]), int(rec[5]), int(rec[1])
+
+
+def test_blob_rejects_bad_contents(blob_graphs):
+    """Contents, not only extents: a column id >= n_vertices (out or in) or a decreasing row pointer fails
+    with OMX_E_INVALID at create time instead of reaching the kernels (capi.cpp check_csr)."""
+    import orientdb_amd as o
+    _, _, buf = blob_graphs
+    V, o_rp, o_col, i_col, n_e = _edge_set0(buf)
+    assert n_e > 0
+    raw = buf.view(np.uint8)
+    bad = buf.copy()
+    bad.view(np.uint8)[o_col:o_col + 4].view(np.uint32)[0] = V  # out-of-range neighbour
+    assert _create(bad) == o._native.OMX_E_INVALID
+    bad = buf.copy()
+    bad.view(np.uint8)[i_col + 4 * (n_e - 1):i_col + 4 * n_e].view(np.uint32)[0] = 0xFFFFFFF0
+    assert _create(bad) == o._native.OMX_E_INVALID
+    rp = raw[o_rp:o_rp + 8 * (V + 1)].view(np.uint64)
+    i = int(np.nonzero(np.diff(rp.astype(np.int64)) > 0)[0][0])  # rp[i] < rp[i + 1]
+    bad = buf.copy()
+    brp = bad.view(np.uint8)[o_rp:o_rp + 8 * (V + 1)].view(np.uint64)
+    brp[i + 1] = brp[i + 2] + 1 if i + 2 <= V else brp[i + 1]  # rp[i+1] > rp[i+2]
+    brp[i] = brp[i + 1] + 5  # rp[i] > rp[i+1]
+    assert _create(bad) == o._native.OMX_E_INVALID
+
+
 def test_param_blob_layout():
     b = param_blob([7, "n1", 2.5, None, True], {"x": 3})
     raw = b.tobytes()

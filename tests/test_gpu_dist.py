@@ -217,6 +217,41 @@ def test_failing_rank_releases_its_peers(rmat10_full):
         c.close()
 
 
+def test_unsupported_keeps_communicator_usable(rmat10_full):
+    """OMX_E_UNSUPPORTED before the first exchange is the host's 'run the reference engine' signal and
+    is raised alike on every rank: it must not abort the communicator (ADVICE r2 capi.cpp), so the
+    next supported query on the same Comm runs and matches the oracle."""
+    import orientdb_amd as o
+    _, ref = rmat10_full
+    parts = _parts(2)
+    comms = o.Comm.threads(2)
+    name, query, cols = [q for q in RMAT_QUERIES if q[0] == "c2_both_ends"][0]
+    unsup = "TRAVERSE out('Knows') FROM #11:0 STRATEGY BREADTH_FIRST"
+    out, errs = [None, None], [[], []]
+
+    def work(r):
+        try:
+            for _ in range(2):
+                try:
+                    o.OMatchStatement(unsup).execute(parts[r], comm=comms[r])
+                except o.OmxUnsupported as e:
+                    errs[r].append(e)
+            out[r] = o.OMatchStatement(query).execute(parts[r], comm=comms[r])
+        except BaseException as e:  # noqa: BLE001
+            errs[r].append(e)
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th)
+    for c in comms:
+        c.close()
+    assert all(len(e) == 2 and all(isinstance(x, o.OmxUnsupported) for x in e) for e in errs), errs
+    assert set().union(*[gpu_set(r, cols) for r in out]) == ref.expected(query, cols)
+
+
 def test_partition_errors(rmat10_full):
     import orientdb_amd as o
     parts = _parts(2)

@@ -43,12 +43,33 @@ def test_null_left_operand_goes_to_reference(host_graph):
     """`>`, `>=`, `<=` with a left operand that is null on some vertex throw NullPointerException in the
     reference (P/OGtOperator.java:22-33, OGeOperator.java:43-54, OLeOperator.java:22-33) depending on
     which records the DFS reaches: the device declines those (OMX_E_UNSUPPORTED → the reference runs);
-    `<` (null → false), `=`, `!=` and null-free columns stay on the device."""
+    `<` (null → false), `=`, `!=` and null-free columns stay on the device. With a non-null left operand
+    all four ordering operators evaluate `iLeft.getClass() != iRight.getClass()` first, so a right operand
+    that may be null (`3 < uid`, a null literal) is the same NullPointerException (ADVICE r2 plan.cpp)."""
     import orientdb_amd as o
     base = "match {class:TriangleV, as:a, where:(uid = 0)}.out('TriangleE'){as:b, where:(%s)} return a, b"
     for cond, supported in [("uid > 3", False), ("uid >= 3", False), ("uid <= 3", False), ("uid + 1 > 3", False),
-                            ("uid < 3", True), ("uid = 3", True), ("uid != 3", True), ("3 < uid", True)]:
+                            ("uid < 3", True), ("uid = 3", True), ("uid != 3", True), ("3 < uid", False),
+                            ("3 > uid", False), ("3 <= uid + 1", False), ("uid < null", False), ("uid = null", True),
+                            ("null < null", True)]:
         p = o.OMatchStatement(base % cond).explain(host_graph)
         assert p["supported"] == supported, (cond, p["unsupported_reason"])
         if not supported:
             assert "NullPointerException" in p["unsupported_reason"]
+
+
+def test_null_right_operand_raises_in_oracle_and_goes_to_reference(refdb, host_graph):
+    """A traversal target's `3 < uid` / `'a' < surname` reaches Person records without uid / surname:
+    the reference throws NullPointerException (`iRight.getClass()`, P/OLtOperator.java:22-36), the oracle
+    raises, and the planner hands the statement to the reference (OMX_E_UNSUPPORTED). `uid < 3` (a null
+    left operand of `<` is false) stays on the device with the oracle's answer."""
+    import orientdb_amd as o
+    from oracle.match_ref import MatchOracle, OracleError
+    base = "match {class:Person, as:a, where:(name = 'n1')}.out('Friend'){as:b, where:(%s)} return a, b"
+    for cond in ("3 < uid", "'a' < surname", "3 >= uid"):
+        with pytest.raises(OracleError):
+            MatchOracle(refdb, base % cond).execute()
+        p = o.OMatchStatement(base % cond).explain(host_graph)
+        assert not p["supported"] and "NullPointerException" in p["unsupported_reason"], cond
+    assert MatchOracle(refdb, base % "uid < 3").execute() == []
+    assert o.OMatchStatement(base % "uid < 3").explain(host_graph)["supported"]
