@@ -190,7 +190,8 @@ typedef struct omx_result_info {
                              /* 0x9E3779B97F4A7C15, h = mix(h ^ rid)); 0 otherwise                  */
   int32_t documents;         /* 1: rows are documents of RETURN expressions / JSON (omx_result_cell); */
                              /* 0: rows are RID tuples (omx_result_rows)                             */
-  int32_t reserved;
+  int32_t factorized_hops;   /* filtered hops run through the factorized expansion (distinct       */
+                             /* sources → grouped filtered lists → rows over the lists; diagnostic) */
 } omx_result_info;
 
 /* A null binding (an unmatched optional node, P/OMatchStatement.java:448-458) in omx_result_rows. */
@@ -340,6 +341,14 @@ int omx_ldbc_knows_generate(uint32_t n_persons, uint64_t target_edges, uint64_t 
 int omx_rmat_generate_part(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t simple, uint32_t lo, uint32_t hi,
                            uint64_t **out_row_ptr, uint32_t **out_col, uint64_t *n_out, uint64_t **in_row_ptr,
                            uint32_t **in_col, uint64_t *n_in);
+/* The same two generators run on GPU `device` (every edge drawn in parallel, the CSR built by a radix
+ * sort of (row, neighbour) keys): identical output arrays, host-owned (omx_host_free); seconds for
+ * RMAT-26 where the host generators take minutes. */
+int omx_rmat_generate_dev(int32_t device, int32_t scale, int32_t edge_factor, uint64_t seed, int32_t simple,
+                          uint64_t **out_row_ptr, uint32_t **out_col, uint64_t *n_edges);
+int omx_rmat_generate_part_dev(int32_t device, int32_t scale, int32_t edge_factor, uint64_t seed, int32_t simple,
+                               uint32_t lo, uint32_t hi, uint64_t **out_row_ptr, uint32_t **out_col, uint64_t *n_out,
+                               uint64_t **in_row_ptr, uint32_t **in_col, uint64_t *n_in);
 /* CSR transpose (host, multi-threaded); rows of the output are sorted. */
 int omx_csr_transpose(uint32_t n_vertices, const uint64_t *row_ptr, const uint32_t *col, uint64_t **t_row_ptr,
                       uint32_t **t_col);

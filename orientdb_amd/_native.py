@@ -61,7 +61,7 @@ class omx_result_info(C.Structure):
     _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_int32), ("deduplicated", C.c_int32),
                 ("edges_traversed", C.c_uint64), ("bindings", C.c_uint64), ("alg_bytes", C.c_uint64),
                 ("device_ms", C.c_double), ("total_ms", C.c_double), ("edges_read", C.c_uint64),
-                ("digest", C.c_uint64), ("documents", C.c_int32), ("reserved", C.c_int32)]
+                ("digest", C.c_uint64), ("documents", C.c_int32), ("factorized_hops", C.c_int32)]
 
 
 OMX_NULL_RID = (1 << 64) - 1  # a null binding (unmatched optional node)
@@ -111,6 +111,14 @@ SIGNATURES = {
                                          C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)),
                                          C.POINTER(C.c_uint64), C.POINTER(C.POINTER(C.c_uint64)),
                                          C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64)]),
+    "omx_rmat_generate_dev": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_uint64, C.c_int32,
+                                        C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)),
+                                        C.POINTER(C.c_uint64)]),
+    "omx_rmat_generate_part_dev": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_uint64, C.c_int32, C.c_uint32,
+                                             C.c_uint32, C.POINTER(C.POINTER(C.c_uint64)),
+                                             C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_uint64),
+                                             C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.POINTER(C.c_uint32)),
+                                             C.POINTER(C.c_uint64)]),
     "omx_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "omx_comm_create_rccl": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]),
     "omx_comm_create_threads": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),

@@ -341,6 +341,7 @@ class Executor {
     res->info.deduplicated = dedup_ran_;
     res->info.edges_traversed = edges_;
     res->info.edges_read = edges_iter_;
+    res->info.factorized_hops = (int32_t)factorized_hops_;
     res->info.digest = digest_;
     res->info.documents = docs ? 1 : 0;
     res->info.bindings = bindings_;

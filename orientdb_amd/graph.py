@@ -5,6 +5,7 @@ per edge class the out_/in_ ridbags of every vertex as CSR, every vertex's class
 column per property. It is built once and shared read-only by every statement executed on it.
 """
 import ctypes as C
+import os
 import json
 
 import numpy as np
@@ -173,11 +174,11 @@ class GraphSnapshot:
         V = 1 << scale
         part = None
         if partition is None:
-            rp, col = rmat_csr(scale, edge_factor, seed, simple)
+            rp, col = rmat_csr(scale, edge_factor, seed, simple, device=device)
             es = {"cls": 3, "out_rp": rp, "out_col": col}
         else:
             part = partition_range(V, *partition)
-            rp, col, irp, icol = rmat_partition(scale, part[0], part[1], edge_factor, seed, simple)
+            rp, col, irp, icol = rmat_partition(scale, part[0], part[1], edge_factor, seed, simple, device=device)
             es = {"cls": 3, "out_rp": rp, "out_col": col, "in_rp": irp, "in_col": icol}
         classes = [("V", -1, False, 9), ("E", -1, True, 10), ("Person", 0, False, 11), ("Knows", 1, True, 12)]
         vclass = np.full(V, 2, np.uint16)
@@ -273,14 +274,28 @@ def ldbc_csr(n_persons=70000, target_edges=2_000_000, seed=10):
     return rp, col
 
 
-def rmat_csr(scale, edge_factor=16, seed=None, simple=True):
-    """(row_ptr u64[V+1], col u32[E]) of the deterministic RMAT generator in libomx."""
+def _gen_device(device):
+    """Device for the RMAT generator: the snapshot's GPU (gen.hip: draws + radix sort, the same arrays as
+    the host generator gen.cpp), or None for the host generator (CPU snapshots, OMX_GEN_HOST=1)."""
+    if device is None or device < 0 or os.environ.get("OMX_GEN_HOST") == "1":
+        return None
+    return device
+
+
+def rmat_csr(scale, edge_factor=16, seed=None, simple=True, device=None):
+    """(row_ptr u64[V+1], col u32[E]) of the deterministic RMAT generator in libomx (built on `device`
+    when one is given)."""
     L = N.lib()
     seed = scale if seed is None else seed
     prp = C.POINTER(C.c_uint64)()
     pcol = C.POINTER(C.c_uint32)()
     ne = C.c_uint64()
-    N.check(L.omx_rmat_generate(scale, edge_factor, seed, int(simple), C.byref(prp), C.byref(pcol), C.byref(ne)))
+    dev = _gen_device(device)
+    if dev is None:
+        N.check(L.omx_rmat_generate(scale, edge_factor, seed, int(simple), C.byref(prp), C.byref(pcol), C.byref(ne)))
+    else:
+        N.check(L.omx_rmat_generate_dev(dev, scale, edge_factor, seed, int(simple), C.byref(prp), C.byref(pcol),
+                                        C.byref(ne)))
     V = 1 << scale
     rp = np.ctypeslib.as_array(prp, shape=(V + 1,)).copy()
     col = np.ctypeslib.as_array(pcol, shape=(max(1, ne.value),))[:ne.value].copy()
@@ -295,14 +310,19 @@ def partition_range(V, rank, world):
     return min(V, rank * b), min(V, (rank + 1) * b)
 
 
-def rmat_partition(scale, lo, hi, edge_factor=16, seed=None, simple=True):
+def rmat_partition(scale, lo, hi, edge_factor=16, seed=None, simple=True, device=None):
     """(out_rp, out_col, in_rp, in_col) of the RMAT rows [lo, hi) (local row pointers)."""
     L = N.lib()
     seed = scale if seed is None else seed
     orp, ocol, irp, icol = C.POINTER(C.c_uint64)(), C.POINTER(C.c_uint32)(), C.POINTER(C.c_uint64)(), C.POINTER(C.c_uint32)()
     no, ni = C.c_uint64(), C.c_uint64()
-    N.check(L.omx_rmat_generate_part(scale, edge_factor, seed, int(simple), lo, hi, C.byref(orp), C.byref(ocol),
-                                     C.byref(no), C.byref(irp), C.byref(icol), C.byref(ni)))
+    dev = _gen_device(device)
+    if dev is None:
+        N.check(L.omx_rmat_generate_part(scale, edge_factor, seed, int(simple), lo, hi, C.byref(orp), C.byref(ocol),
+                                         C.byref(no), C.byref(irp), C.byref(icol), C.byref(ni)))
+    else:
+        N.check(L.omx_rmat_generate_part_dev(dev, scale, edge_factor, seed, int(simple), lo, hi, C.byref(orp),
+                                             C.byref(ocol), C.byref(no), C.byref(irp), C.byref(icol), C.byref(ni)))
     n = hi - lo
     out = (np.ctypeslib.as_array(orp, shape=(n + 1,)).copy(),
            np.ctypeslib.as_array(ocol, shape=(max(1, no.value),))[:no.value].copy(),

@@ -159,3 +159,59 @@ def test_c5_shape_partitioned_rmat16():
     mat = run_ranks(parts, q, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST)
     assert sum(r.info["n_rows"] for r in mat) == ref["bindings"]
     assert sum(r.info["digest"] for r in mat) % (1 << 64) == ref["digest"]
+
+
+C5_QUERY = "MATCH {class:Person,as:a,where:(uid < 64)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d"
+C5_WINDOW = "MATCH {class:Person,as:a,where:(uid < 4)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d"
+
+
+@pytest.fixture(scope="module")
+def rmat26():
+    """configs[4]'s graph: RMAT-26 (67 M vertices, 1.07 G simple edges), built by the device generator."""
+    import orientdb_amd as o
+    g = o.GraphSnapshot.rmat(26, device=0, keep_csr=True)
+    yield g
+    g.close()
+
+
+@pytest.fixture(scope="module")
+def c5_ref(rmat26):
+    from oracle import dfs
+    return dfs.run(_cg(rmat26), C5_QUERY, nthreads=THREADS, emit=False)
+
+
+def test_c5_rmat26_count(rmat26, c5_ref):
+    """configs[4] verbatim at its own scale on one GPU, COUNT mode: the bindings (≈2e10) and E_t of the
+    3-hop walk from 64 roots equal the DFS oracle's (P/OMatchStatement.java:412-568)."""
+    import orientdb_amd as o
+    rs = o.OMatchStatement(C5_QUERY).execute(rmat26, mode=o.OMX_MODE_COUNT)
+    assert rs.info["bindings"] == c5_ref["bindings"] > 1e9
+    assert rs.info["edges_traversed"] == c5_ref["edges"]
+
+
+def test_c5_rmat26_window_materialized_digest(rmat26):
+    """configs[4]'s 3-hop on a root window that fits HBM when materialized (uid < 4): every row of the
+    last hop is expanded and written (no degree sum), and the digest of all (a, b, c, d) RID tuples
+    equals the oracle's."""
+    from oracle import dfs
+    ref = dfs.run(_cg(rmat26), C5_WINDOW, nthreads=THREADS, emit=False, digest=["a", "b", "c", "d"])
+    rs = _digest_run(rmat26, C5_WINDOW)
+    assert rs.info["n_rows"] == rs.info["bindings"] == ref["bindings"] > 1e7
+    assert rs.info["edges_traversed"] == ref["edges"]
+    assert rs.info["digest"] == ref["digest"]
+
+
+def test_c5_rmat26_partitioned_4ranks_count(c5_ref):
+    """configs[4] on a 4-rank 1-D partition of RMAT-26 (thread transport, the routing code RCCL drives
+    across GPUs): rows go to owner(b), then owner(c) before the last hop; the ranks' bindings and E_t add
+    up to the oracle's."""
+    import orientdb_amd as o
+    from tests.test_gpu_dist import run_ranks
+    parts = [o.GraphSnapshot.rmat(26, device=0, partition=(r, 4)) for r in range(4)]
+    try:
+        cnt = run_ranks(parts, C5_QUERY, mode=o.OMX_MODE_COUNT)
+        assert sum(r.info["bindings"] for r in cnt) == c5_ref["bindings"]
+        assert sum(r.info["edges_traversed"] for r in cnt) == c5_ref["edges"]
+    finally:
+        for p in parts:
+            p.close()

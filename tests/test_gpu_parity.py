@@ -339,18 +339,54 @@ FACTOR_IDS = ("c2_both_ends", "c1_abc", "two_cols_dedup", "in_dir", "both_dir", 
               "paths", "elements", "fof_not_me", "matched_and_filter", "optional_free", "bound_candidate")
 
 
+@pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
-def test_rmat_parity_factorized(rmat10, q, monkeypatch):
+def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, monkeypatch):
     """Every filtered hop through the factorized expansion (distinct sources → filtered lists → rows
-    over the lists, Executor::expand_factorized): same rows, same E_t."""
+    over the lists, Executor::expand_factorized): same rows, same E_t — on the simple graph and on the
+    multigraph, whose parallel edges repeat a neighbour in a source's list (ridbag multiplicity,
+    OSBTreeRidBag.java:292-295) through the distinct-source grouping (k_key_hist / k_key_scatter)."""
     import orientdb_amd as o
-    g, ref = rmat10
+    g, ref = rmat10 if graph == "simple" else rmat10_raw
     monkeypatch.setenv("OMX_FACTOR", "0")
     direct = o.OMatchStatement(q[1]).execute(g, documents=False)
     monkeypatch.setenv("OMX_FACTOR", "force")
     rs = _parity(g, ref, q[1], q[2])
+    assert direct.info["factorized_hops"] == 0
     assert rs.info["edges_traversed"] == direct.info["edges_traversed"]
     assert rs.info["bindings"] == direct.info["bindings"]
+
+
+@pytest.mark.parametrize("simple", [True, False], ids=["simple", "multigraph"])
+def test_factorized_auto_threshold_rmat14(simple):
+    """The factorized expansion as the planner picks it by itself (≥ 4096 rows whose sources repeat ≥ 4×,
+    exec.hip expand_factorized): RMAT-14 2-hop with the WHERE on both ends, on the simple graph and the
+    multigraph (parallel edges: a neighbour repeated in a source's list is one row per edge,
+    OSBTreeRidBag.java:292-295). The device reports the hop as factorized; rows, E_t and bindings equal
+    the DFS oracle's and the direct expansion's."""
+    import orientdb_amd as o
+    from oracle import dfs
+    g = o.GraphSnapshot.rmat(14, device=0, simple=simple, keep_csr=True)
+    q = "MATCH {class:Person,as:a,where:(age < 5)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a,b,c"
+    cg = dfs.CsrGraph(g.csr[0], g.csr[1], {"uid": np.arange(g.V, dtype=np.int64), "age": g.age}, simple=simple)
+    ref = dfs.run(cg, q, nthreads=8)
+    rs = o.OMatchStatement(q).execute(g, documents=False)
+    assert rs.info["factorized_hops"] >= 1
+    got = {tuple(int(x) & ((1 << 48) - 1) for x in row) for row in rs.rows}
+    want = {tuple(int(v) for v in row) for row in ref["rows"]}
+    assert got == want and rs.info["n_rows"] == len(want)
+    assert rs.info["edges_traversed"] == ref["edges"]
+    assert rs.info["bindings"] == ref["bindings"]
+    import os
+    os.environ["OMX_FACTOR"] = "0"
+    try:
+        direct = o.OMatchStatement(q).execute(g, documents=False)
+    finally:
+        del os.environ["OMX_FACTOR"]
+    assert direct.info["factorized_hops"] == 0
+    assert direct.info["edges_traversed"] == rs.info["edges_traversed"]
+    assert direct.info["bindings"] == rs.info["bindings"]
+    g.close()
 
 
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in ("c2_both_ends", "in_dir", "three_hop", "matches")],
