@@ -206,6 +206,9 @@ const uint64_t *omx_result_rows(const omx_result *r);
  * algorithmic bytes the launches of that kernel moved. Returns OMX_E_INVALID past the end. */
 int omx_result_kernel_stat(const omx_result *r, int32_t i, const char **name, int64_t *launches, double *total_ms,
                            uint64_t *alg_bytes);
+/* The same timing launch by launch, in issue order (a kernel launched several times per execution,
+ * e.g. a first hop and a row emission, is reported per launch). Returns OMX_E_INVALID past the end. */
+int omx_result_kernel_launch(const omx_result *r, int32_t i, const char **name, double *ms, uint64_t *alg_bytes);
 void omx_result_free(omx_result *r);
 
 /* One field of a result document (info.documents = 1): the value of RETURN item `col` (or of JSON key

@@ -91,6 +91,8 @@ SIGNATURES = {
     "omx_result_rows": (C.POINTER(C.c_uint64), [C.c_void_p]),
     "omx_result_kernel_stat": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_char_p), C.POINTER(C.c_int64),
                                          C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "omx_result_kernel_launch": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_char_p), C.POINTER(C.c_double),
+                                          C.POINTER(C.c_uint64)]),
     "omx_result_free": (None, [C.c_void_p]),
     "omx_result_cell": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int32, C.POINTER(omx_cell)]),
     "omx_graph_create_blob": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),

@@ -428,6 +428,15 @@ int omx_result_kernel_stat(const omx_result *r, int32_t i, const char **name, in
   return OMX_OK;
 }
 
+int omx_result_kernel_launch(const omx_result *r, int32_t i, const char **name, double *ms, uint64_t *alg_bytes) {
+  if (!r || i < 0 || (size_t)i >= r->klaunches.size()) return OMX_E_INVALID;
+  const auto &k = r->klaunches[i];
+  if (name) *name = k.name.c_str();
+  if (ms) *ms = k.ms;
+  if (alg_bytes) *alg_bytes = k.bytes;
+  return OMX_OK;
+}
+
 void omx_result_free(omx_result *r) { delete r; }
 
 int omx_result_cell(const omx_result *r, uint64_t row, int32_t col, omx_cell *out) {

@@ -19,6 +19,7 @@ struct omx_result {
     uint64_t bytes = 0;
   };
   std::vector<KStat> kstats;
+  std::vector<KStat> klaunches;  // every timed launch in issue order (launches = 1 each)
 };
 
 namespace omx {

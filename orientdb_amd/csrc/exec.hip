@@ -50,9 +50,13 @@ class Timer {
       if (std::strcmp(name, h) == 0) return true;
     return false;
   }
+  // regions nest (a span such as "dedup" may hold a timed kernel): begin pushes, end closes the
+  // innermost open region
   void begin(const char *name, hipStream_t st = nullptr) {
-    skip_ = !on_ || (hot_only_ && !hot(name));
-    if (skip_) return;
+    if (!on_ || (hot_only_ && !hot(name))) {
+      open_.push_back(SIZE_MAX);
+      return;
+    }
     Rec r;
     r.name = name;
     r.s = st ? st : s_;
@@ -60,27 +64,32 @@ class Timer {
     r.b = event();
     HIP_CHECK(hipEventRecord(r.a, r.s));
     recs_.push_back(r);
+    open_.push_back(recs_.size() - 1);
   }
   void end(uint64_t bytes = 0) {
-    if (skip_) return;
-    recs_.back().bytes = bytes;
-    HIP_CHECK(hipEventRecord(recs_.back().b, recs_.back().s));
+    if (open_.empty()) return;
+    last_ = open_.back();
+    open_.pop_back();
+    if (last_ == SIZE_MAX) return;
+    recs_[last_].bytes = bytes;
+    HIP_CHECK(hipEventRecord(recs_[last_].b, recs_[last_].s));
   }
-  // algorithmic bytes of a record when they are only known after the launch
+  // algorithmic bytes of the region just closed, when they are only known after the launch
   void amend(uint64_t bytes) {
-    if (!skip_ && !recs_.empty()) recs_.back().bytes = bytes;
+    if (last_ != SIZE_MAX) recs_[last_].bytes = bytes;
   }
-  // index of the record just closed (SIZE_MAX when it was not recorded)
-  size_t last() const { return skip_ || recs_.empty() ? SIZE_MAX : recs_.size() - 1; }
+  // index of the region just closed (SIZE_MAX when it was not recorded)
+  size_t last() const { return last_; }
   void amend_at(size_t i, uint64_t bytes) {
-    if (on_ && i < recs_.size()) recs_[i].bytes = bytes;
+    if (i < recs_.size()) recs_[i].bytes = bytes;
   }
   // precondition: the stream has completed (Executor::run waits for its end event first)
-  void collect(std::vector<omx_result::KStat> &out) {
+  void collect(std::vector<omx_result::KStat> &out, std::vector<omx_result::KStat> &each) {
     if (!on_) return;
     for (auto &r : recs_) {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
+      each.push_back({r.name, 1, ms, r.bytes});
       auto it = std::find_if(out.begin(), out.end(), [&](const omx_result::KStat &k) { return k.name == r.name; });
       if (it == out.end()) {
         out.push_back({r.name, 0, 0, 0});
@@ -110,7 +119,8 @@ class Timer {
     uint64_t bytes = 0;
   };
   bool on_, hot_only_;
-  bool skip_ = true;
+  std::vector<size_t> open_;
+  size_t last_ = SIZE_MAX;
   hipStream_t s_;
   std::vector<hipEvent_t> *pool_;
   std::vector<Rec> recs_;
@@ -335,7 +345,7 @@ class Executor {
     HIP_CHECK(hipEventElapsedTime(&dms, ea, eb));
     (void)hipEventDestroy(ea);
     (void)hipEventDestroy(eb);
-    tm_.collect(res->kstats);
+    tm_.collect(res->kstats, res->klaunches);
     res->info.n_rows = n;
     res->info.n_cols = n ? ncols : 0;
     res->info.deduplicated = dedup_ran_;
@@ -1312,7 +1322,9 @@ class Executor {
     {
       DBuf<uint64_t> ubm(&pool_, std::max<uint64_t>(nwords_, 1));
       HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+      tm_.begin("k_mark_bitmap");
       launch_mark_bitmap(src, R, ubm.p, g_.V, s_);
+      tm_.end(4ull * R + 8ull * nwords_);
       ub = bitmap_list(ubm.p, 0, 1, U);
     }
     const uint64_t Et = degree_sum(src, R, st.adj), EU = degree_sum(ub.p, U, st.adj);
@@ -1321,8 +1333,12 @@ class Executor {
     // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
     DBuf<uint32_t> g(&pool_, R), iu(&pool_, std::max<uint64_t>(U, 1)), pos(&pool_, std::max<uint64_t>(g_.V, 1));
     launch_iota(iu.p, U, s_);
+    tm_.begin("k_scatter_u32");
     launch_scatter_u32(ub.p, iu.p, U, pos.p, s_);
+    tm_.end(12ull * U);
+    tm_.begin("k_gather_u32");
     launch_gather_u32(pos.p, src, R, g.p, s_);
+    tm_.end(12ull * R);
     // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
     ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true);
     edges_iter_ += l.E;
@@ -1330,14 +1346,20 @@ class Executor {
     DBuf<unsigned long long> cnt(&pool_, U + 1);
     DBuf<uint64_t> loff(&pool_, U + 1);
     HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));
-    if (l.n) launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
+    if (l.n) {
+      tm_.begin("k_key_hist");
+      launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
+      tm_.end(4ull * l.n + 8ull * U);
+    }
     cub([&](void *t, size_t &b) {
       return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
     });
     DBuf<uint32_t> lcol(&pool_, std::max<uint64_t>(l.n, 1));
     if (l.n) {
       HIP_CHECK(hipMemcpyAsync(cnt.p, loff.p, (U + 1) * 8, hipMemcpyDeviceToDevice, s_));
+      tm_.begin("k_key_scatter");
       launch_key_scatter(l.carry[0].p, l.dst.p, l.n, cnt.p, lcol.p, s_);
+      tm_.end(12ull * l.n + 8ull * U);
     }
     // 4. the rows over their sources' lists
     DAdj ladj{};
@@ -1765,7 +1787,9 @@ class Executor {
     DAdj adj = make_adj(adjs);
     if (adj.n == 0 || R == 0) return 0;
     DBuf<uint64_t> deg(&pool_, R + 1), sum(&pool_, 1);
+    tm_.begin("k_row_degree");
     launch_row_degree(src, R, adj, deg.p, s_);
+    tm_.end(R * (4ull + 8ull * adj.n + 8ull));  // source id + row_ptr pair per part, 8-B degree written
     cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, deg.p, sum.p, (int64_t)(R + 1), s_); });
     return read1(sum.p);
   }

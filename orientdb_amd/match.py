@@ -71,6 +71,7 @@ class OResultSet(list):
     """Distinct result rows + execution statistics (edges traversed, bindings, timings)."""
     info = None
     kernel_stats = None
+    kernel_launches = None
     columns = None
     rows = None  # numpy u64 [n, k] of packed RIDs
 
@@ -209,6 +210,15 @@ class OMatchStatement:
             stats.append({"name": name.value.decode(), "launches": launches.value, "ms": ms.value, "alg_bytes": by.value})
             i += 1
         rs.kernel_stats = stats
+        launches = []
+        i = 0
+        while True:
+            name, ms, by = C.c_char_p(), C.c_double(), C.c_uint64()
+            if L.omx_result_kernel_launch(r, i, C.byref(name), C.byref(ms), C.byref(by)) != 0:
+                break
+            launches.append({"name": name.value.decode(), "ms": ms.value, "alg_bytes": by.value})
+            i += 1
+        rs.kernel_launches = launches
         nrows, ncols = info.n_rows, info.n_cols
         if info.documents:  # RETURN expressions / JSON: one document per row (omx_result_cell)
             rs.rows = np.zeros((0, 0), np.uint64)

@@ -15,12 +15,17 @@ import os
 import re
 
 
-def per_dispatch(path, counter, kre):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if r["Counter_Name"] == counter and re.search(kre, r["Kernel_Name"])]
-    if not vals:
+def dispatches(path, counter, kre):
+    """The counter's value per dispatch of the kernel, in dispatch order (summed over rows of one
+    dispatch: a counter may be reported per XCD or per instance)."""
+    by = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter and re.search(kre, r["Kernel_Name"]):
+            k = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or len(by))
+            by[k] = by.get(k, 0.0) + float(r["Counter_Value"])
+    if not by:
         raise SystemExit("no %s rows for %s in %s" % (counter, kre, path))
-    return sum(vals) / len(vals), len(vals)
+    return [by[k] for k in sorted(by)]
 
 
 def main():
@@ -31,11 +36,20 @@ def main():
     ap.add_argument("query")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic.json"))
     a = ap.parse_args()
-    fetch, nf = per_dispatch(os.path.join(a.pmc_dir, "p1", "pmc_counter_collection.csv"), "FETCH_SIZE", a.kernel_regex)
-    write, nw = per_dispatch(os.path.join(a.pmc_dir, "p2", "pmc_counter_collection.csv"), "WRITE_SIZE", a.kernel_regex)
+    f = dispatches(os.path.join(a.pmc_dir, "p1", "pmc_counter_collection.csv"), "FETCH_SIZE", a.kernel_regex)
+    w = dispatches(os.path.join(a.pmc_dir, "p2", "pmc_counter_collection.csv"), "WRITE_SIZE", a.kernel_regex)
+    if len(f) != len(w):
+        raise SystemExit("dispatch counts differ between the passes: %d vs %d" % (len(f), len(w)))
+    # a kernel launched several times per step with very different sizes (M1: the first hop, then the
+    # row emission) is reported on its main launches: those moving at least half the largest one's bytes
+    tot = [2 * x + y for x, y in zip(f, w)]
+    main = [i for i, t in enumerate(tot) if t >= 0.5 * max(tot)]
+    fetch = sum(f[i] for i in main) / len(main)
+    write = sum(w[i] for i in main) / len(main)
     rec = {"kernel": a.timer_name, "fetch_size_kib": fetch, "write_size_kib": write,
            "read_bytes": 2 * fetch * 1024, "write_bytes": write * 1024,
-           "bytes_per_launch": 2 * fetch * 1024 + write * 1024, "dispatches": [nf, nw],
+           "bytes_per_launch": 2 * fetch * 1024 + write * 1024, "dispatches": [len(f), len(main)],
+           "dispatches_note": "[all dispatches of the kernel, main dispatches averaged]",
            "source": os.path.relpath(a.pmc_dir, os.path.join(os.path.dirname(__file__), ".."))}
     db = json.load(open(a.out)) if os.path.exists(a.out) else {}
     db[a.query] = rec
