@@ -295,6 +295,29 @@ int omx_ridbag_decode_csr(int32_t device, const uint8_t *streams, uint64_t strea
                           const uint64_t *edge_targets, uint64_t n_edge_records, uint64_t *row_ptr, uint32_t *col,
                           uint64_t *n_entries);
 
+/* SBTree-bonsai ridbags (config bit 0 clear: every bag of >= 40 entries by default,
+ * C/config/OGlobalConfiguration.java:356-358) keep their entries in a collection file
+ * (collections_<cluster>.sbc). Stream (C/db/record/ridbag/sbtree/OSBTreeRidBag.java:855-880, big-endian):
+ * [config][UUID?][int64 fileId][int64 root pageIndex][int32 root pageOffset][int32 cached size]
+ * [int32 n][n × (int16 cluster, int64 position, int8 change type, int32 value)]. The host passes each
+ * collection file's pages as stored (OSBTreeBonsaiBucket layout, C/index/sbtreebonsai/local/
+ * OSBTreeBonsaiBucket.java:44-60,263-279): the bag's entries are decoded on the device in the order
+ * OSBTreeRidBag's iterator yields them (tree entries in RID order merged with the changes, each RID
+ * `counter` times, :256-425). files = NULL: as omx_ridbag_decode_csr. page_size 0: 64 KiB
+ * (DISK_CACHE_PAGE_SIZE). OMX_E_INVALID also for a bag whose file is missing, a bucket pointer or
+ * entry outside its page, a tree deeper than 64 levels, or changes out of RID order. */
+#define OMX_BONSAI_PAGE_SIZE 65536u
+typedef struct omx_bonsai_file {
+  int64_t file_id;       /* the fileId an SBTree bag's stream names                                   */
+  const uint8_t *pages;  /* n_pages × page_size bytes: page i at i × page_size                         */
+  uint64_t n_pages;
+} omx_bonsai_file;
+int omx_ridbag_decode_csr_ex(int32_t device, const uint8_t *streams, uint64_t stream_bytes, const uint64_t *offsets,
+                             uint32_t n_vertices, const uint64_t *vertex_rids, const uint64_t *edge_rids,
+                             const uint64_t *edge_targets, uint64_t n_edge_records, const omx_bonsai_file *files,
+                             int32_t n_files, uint32_t page_size, uint64_t *row_ptr, uint32_t *col,
+                             uint64_t *n_entries);
+
 /* Parameters as one buffer: uint32_t n, uint32_t reserved, omx_param_rec[n], then the strings. */
 typedef struct omx_param_rec {
   int32_t type, index;       /* OMX_VAL_*, positional index (when name_off == 0)                       */

@@ -131,7 +131,15 @@ SIGNATURES = {
                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                         C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
                                         C.POINTER(C.c_uint64)]),
+    "omx_ridbag_decode_csr_ex": (C.c_int, [C.c_int32, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32,
+                                           C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                           C.c_uint64, C.c_void_p, C.c_int32, C.c_uint32, C.POINTER(C.c_uint64),
+                                           C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
 }
+
+
+class omx_bonsai_file(C.Structure):
+    _fields_ = [("file_id", C.c_int64), ("pages", C.c_void_p), ("n_pages", C.c_uint64)]
 OMX_COMM_ID_BYTES = 128
 
 _lib = None

@@ -462,7 +462,19 @@ int omx_ridbag_decode_csr(int32_t device, const uint8_t *streams, uint64_t strea
                           uint64_t *n_entries) {
   return guard([&] {
     omx::ridbag_decode_csr(device, streams, stream_bytes, offsets, n_vertices, vertex_rids, edge_rids, edge_targets,
-                           n_edge_records, row_ptr, col, n_entries);
+                           n_edge_records, nullptr, 0, 0, row_ptr, col, n_entries);
+  });
+}
+
+int omx_ridbag_decode_csr_ex(int32_t device, const uint8_t *streams, uint64_t stream_bytes, const uint64_t *offsets,
+                             uint32_t n_vertices, const uint64_t *vertex_rids, const uint64_t *edge_rids,
+                             const uint64_t *edge_targets, uint64_t n_edge_records, const omx_bonsai_file *files,
+                             int32_t n_files, uint32_t page_size, uint64_t *row_ptr, uint32_t *col,
+                             uint64_t *n_entries) {
+  return guard([&] {
+    omx::ridbag_decode_csr(device, streams, stream_bytes, offsets, n_vertices, vertex_rids, edge_rids, edge_targets,
+                           n_edge_records, files, files ? n_files : 0,
+                           page_size ? page_size : OMX_BONSAI_PAGE_SIZE, row_ptr, col, n_entries);
   });
 }
 

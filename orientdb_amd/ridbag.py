@@ -17,19 +17,22 @@ def _u64p(a):
     return a.ctypes.data_as(C.POINTER(C.c_uint64)) if a is not None else None
 
 
-def decode_ridbags(streams, vertex_rids, edge_rids=None, edge_targets=None, device=0):
+def decode_ridbags(streams, vertex_rids, edge_rids=None, edge_targets=None, device=0, files=None,
+                   page_size=65536):
     """streams: one bytes object per vertex (b"" = the vertex has no such field), in dense vertex order.
     vertex_rids: packed RID of every vertex. edge_rids / edge_targets: for regular (non-lightweight)
-    edges, every edge record's RID and the packed RID of its opposite vertex. Returns (row_ptr u64[V+1],
-    col u32[E]) with each bag's order kept."""
+    edges, every edge record's RID and the packed RID of its opposite vertex. files: {fileId: pages
+    (bytes-like, n × page_size)} of the SBTree collection files that SBTree-bonsai bags point into
+    (None: embedded bags only). Returns (row_ptr u64[V+1], col u32[E]) with each bag's iteration order."""
     V = len(streams)
     offs = np.zeros(V + 1, np.uint64)
     offs[1:] = np.cumsum([len(b) for b in streams], dtype=np.uint64)
     blob = b"".join(streams)
-    return decode_ridbag_blob(blob, offs, vertex_rids, edge_rids, edge_targets, device)
+    return decode_ridbag_blob(blob, offs, vertex_rids, edge_rids, edge_targets, device, files, page_size)
 
 
-def decode_ridbag_blob(blob, offsets, vertex_rids, edge_rids=None, edge_targets=None, device=0):
+def decode_ridbag_blob(blob, offsets, vertex_rids, edge_rids=None, edge_targets=None, device=0, files=None,
+                       page_size=65536):
     """The same over one concatenated byte string and its offsets[V+1]."""
     offs = np.ascontiguousarray(offsets, np.uint64)
     V = len(offs) - 1
@@ -44,7 +47,19 @@ def decode_ridbag_blob(blob, offsets, vertex_rids, edge_rids=None, edge_targets=
     n = C.c_uint64()
     L = N.lib()
     args = [device, buf.ctypes.data_as(C.c_void_p), len(blob), _u64p(offs), V, _u64p(vr), _u64p(er), _u64p(et), ne]
-    N.check(L.omx_ridbag_decode_csr(*args, _u64p(rp), None, C.byref(n)))
+    if files is None:
+        fn, extra = L.omx_ridbag_decode_csr, []
+    else:
+        keep = [np.frombuffer(bytes(p), np.uint8) if len(p) else np.zeros(1, np.uint8) for p in files.values()]
+        recs = (N.omx_bonsai_file * max(1, len(files)))()
+        for i, (fid, pages) in enumerate(files.items()):
+            if len(pages) % page_size:
+                raise ValueError("collection file %d is not a whole number of pages" % fid)
+            recs[i].file_id = int(fid)
+            recs[i].pages = keep[i].ctypes.data_as(C.c_void_p)
+            recs[i].n_pages = len(pages) // page_size
+        fn, extra = L.omx_ridbag_decode_csr_ex, [C.cast(recs, C.c_void_p), len(files), page_size]
+    N.check(fn(*args, *extra, _u64p(rp), None, C.byref(n)))
     col = np.zeros(max(n.value, 1), np.uint32)
-    N.check(L.omx_ridbag_decode_csr(*args, _u64p(rp), col.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(n)))
+    N.check(fn(*args, *extra, _u64p(rp), col.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(n)))
     return rp, col[:n.value]

@@ -120,3 +120,125 @@ def test_ingested_snapshot_answers_like_the_original():
     r1 = o.OMatchStatement(q).execute(g1, flags=o.OMX_FLAG_DIGEST)
     assert r0.info["n_rows"] == r1.info["n_rows"] > 0
     assert r0.info["digest"] == r1.info["digest"]
+
+
+# ---- SBTree-bonsai bags (omx_ridbag_decode_csr_ex) -----------------------------------------------------
+def _mixed_streams(rp, col, f, rng, threshold=40, cluster=11):
+    """Bags of >= threshold entries as SBTree bags in collection file f (RIDBag.toStream converts at
+    RID_BAG_EMBEDDED_TO_SBTREEBONSAI_THRESHOLD, OGlobalConfiguration.java:356-358; the tree keeps one
+    counter per distinct RID), the others embedded."""
+    out, ntree = [], 0
+    for v in range(len(rp) - 1):
+        row = col[rp[v]:rp[v + 1]]
+        if len(row) >= threshold:
+            u, c = np.unique(row, return_counts=True)
+            root = f.build_tree([((cluster, int(a)), int(b)) for a, b in zip(u, c)], rng=rng,
+                                empty_leaf_every=7 if v % 5 == 0 else 0)
+            out.append(R.encode_sbtree_pointer(f.file_id, *root, uuid=bytes(16) if v % 3 == 0 else None))
+            ntree += 1
+        else:
+            out.append(R.encode_embedded([(cluster, int(w)) for w in row]))
+    return out, ntree
+
+
+@pytest.mark.parametrize("simple", [True, False], ids=["simple", "multigraph"])
+def test_sbtree_and_embedded_rmat16_decode_to_the_csr(simple):
+    """RMAT-16 (1 M entries): the hubs' bags as SBTree-bonsai trees (random leaf fill, buckets scattered
+    over the pages, emptied leaves in the sibling chain; parallel edges as tree counters), the rest
+    embedded: the device decodes the original CSR, every row in the bag's iteration order (RID order for
+    a tree); a 2-hop MATCH on the decoded snapshot answers with the original's rows and digest."""
+    import random
+
+    import orientdb_amd as o
+    from orientdb_amd.graph import rmat_csr
+    from orientdb_amd.ridbag import decode_ridbags
+    rp, col = rmat_csr(16, seed=3, simple=simple)
+    V = len(rp) - 1
+    f = R.BonsaiFile(5, rng=random.Random(1))
+    streams, ntree = _mixed_streams(rp, col, f, random.Random(2))
+    assert ntree > 1000
+    vr = (np.uint64(11) << np.uint64(48)) | np.arange(V, dtype=np.uint64)
+    grp, gcol = decode_ridbags(streams, vr, files={5: f.data()})
+    assert np.array_equal(grp, rp.astype(np.uint64))
+    assert np.array_equal(gcol, col)
+    g0 = o.GraphSnapshot.person_knows(rp, col, seed=7)
+    g1 = o.GraphSnapshot.person_knows(grp, gcol, seed=7)
+    q = "MATCH {class:Person,as:a,where:(uid < 300)}-Knows->{as:b}-Knows->{as:c,where:(age < 20)} RETURN a, b, c"
+    r0 = o.OMatchStatement(q).execute(g0, flags=o.OMX_FLAG_DIGEST)
+    r1 = o.OMatchStatement(q).execute(g1, flags=o.OMX_FLAG_DIGEST)
+    assert r0.info["n_rows"] == r1.info["n_rows"] > 0
+    assert r0.info["digest"] == r1.info["digest"]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_sbtree_bags_with_changes_match_the_oracle(seed):
+    """Random bags against the literal restatement of OSBTreeRidBag's iterator (oracle/ridbag_ref.py):
+    trees of 1 to 3000 entries with counters 1-3, serialized changes (DiffChange / AbsoluteChange, new,
+    removed and re-counted RIDs), bags whose tree was never created (fileId -1), two collection files,
+    RIDs over several clusters at scattered positions, regular edges (the bags hold edge records)."""
+    import random
+
+    from orientdb_amd.ridbag import decode_ridbags
+    rnd = random.Random(seed)
+    V = 400
+    cl = [rnd.choice((11, 12)) for _ in range(V)]
+    pos = rnd.sample(range(1 << 30), V)
+    vrid = [(cl[v], pos[v]) for v in range(V)]
+    vr = np.array([R.pack(*x) for x in vrid], np.uint64)
+    files = {3: R.BonsaiFile(3, rng=random.Random(seed)), 9: R.BonsaiFile(9, rng=random.Random(seed + 1))}
+    streams, want = [], []
+    for v in range(V):
+        kind = rnd.random()
+        if kind < 0.3:
+            row = [vrid[rnd.randrange(V)] for _ in range(rnd.randrange(0, 30))]
+            streams.append(R.encode_embedded(row))
+        else:
+            n = rnd.choice((1, 5, 60, 300, 3000 if v % 50 == 0 else 200))
+            keys = sorted({vrid[rnd.randrange(V)] for _ in range(n)})
+            counts = [(k, rnd.choice((1, 1, 2, 3))) for k in keys]
+            chg = {}
+            for _ in range(rnd.randrange(0, 6) if kind < 0.7 else 0):
+                k = keys[rnd.randrange(len(keys))] if rnd.random() < 0.6 else vrid[rnd.randrange(V)]
+                chg[k] = (rnd.choice((0, 1)), rnd.randrange(-2, 4))
+            changes = [(k, t, x) for k, (t, x) in sorted(chg.items())]
+            if kind > 0.95:
+                streams.append(R.encode_sbtree_pointer(-1, -1, -1, changes=changes))
+            else:
+                fid = rnd.choice((3, 9))
+                root = files[fid].build_tree(counts, rng=rnd, empty_leaf_every=rnd.choice((0, 3)))
+                streams.append(R.encode_sbtree_pointer(fid, *root, changes=changes,
+                                                       uuid=bytes(range(16)) if v % 4 == 0 else None))
+        row = R.decode(streams[-1], files)
+        want.append([vrid.index(r) for r in row])
+    grp, gcol = decode_ridbags(streams, vr, files={k: f.data() for k, f in files.items()})
+    assert [gcol[grp[v]:grp[v + 1]].tolist() for v in range(V)] == want
+
+
+@pytest.mark.parametrize("bad", ["missing_file", "root_past_file", "child_past_file", "changes_unsorted",
+                                 "change_type", "no_files"])
+def test_sbtree_refused(bad):
+    import orientdb_amd as o
+    from orientdb_amd.ridbag import decode_ridbags
+    V = 64
+    vr = np.array([R.pack(11, v) for v in range(V)], np.uint64)
+    f = R.BonsaiFile(4)
+    root = f.build_tree([((11, v), 1) for v in range(0, 64)], leaf_fill=5)
+    stream = R.encode_sbtree_pointer(4, *root)
+    files = {4: f.data()}
+    if bad == "missing_file":
+        files = {5: f.data()}
+    elif bad == "root_past_file":
+        stream = R.encode_sbtree_pointer(4, len(f.pages) + 2, 0)
+    elif bad == "child_past_file":
+        data = bytearray(f.data())
+        b = R._Bucket({4: f}, 4, root)
+        p = root[0] * R.PAGE_SIZE + root[1] + (b._pos(0) - root[1])
+        data[p:p + 8] = (10 ** 6).to_bytes(8, "little")  # entry 0's left child page
+        files = {4: bytes(data)}
+    elif bad == "changes_unsorted":
+        stream = R.encode_sbtree_pointer(4, *root, changes=[((11, 9), 0, 1), ((11, 2), 0, 1)])
+    elif bad == "change_type":
+        stream = R.encode_sbtree_pointer(4, *root, changes=[((11, 9), 7, 1)])
+    streams = [stream] + [b""] * (V - 1)
+    with pytest.raises(o.OmxError):
+        decode_ridbags(streams, vr, files=None if bad == "no_files" else files)
