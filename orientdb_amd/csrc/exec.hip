@@ -2572,13 +2572,10 @@ void Executor::unpack_tuple(const uint64_t *keys, uint64_t n, std::vector<DBuf<u
 omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts, Transport *tr) {
   if (!g.on_device()) fail(OMX_E_DEVICE, "graph snapshot is host-only (device = -1)");
   HIP_CHECK(hipSetDevice(g.device));
-  try {
-    Executor ex(g, p, opts, tr);
-    return ex.run();
-  } catch (...) {
-    if (tr) tr->abort();  // release the peers waiting in an exchange with this rank
-    throw;
-  }
+  // a failure releases the peers waiting in an exchange with this rank: omx_execute (capi.cpp) aborts the
+  // communicator unless the failure is a refusal every rank made alike before exchanging anything
+  Executor ex(g, p, opts, tr);
+  return ex.run();
 }
 
 }  // namespace omx

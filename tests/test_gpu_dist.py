@@ -248,8 +248,8 @@ def test_unsupported_keeps_communicator_usable(rmat10_full):
     assert not any(t.is_alive() for t in th)
     for c in comms:
         c.close()
-    for r, e in enumerate(errs):
-        assert len(e) == 2 and all(isinstance(x, o.OmxUnsupported) for x in e), (r, [str(x) for x in e])
+    msg = [[type(x).__name__ + ": " + str(x) for x in e] for e in errs]
+    assert all(len(e) == 2 and all(isinstance(x, o.OmxUnsupported) for x in e) for e in errs), msg[::-1]
     assert set().union(*[gpu_set(r, cols) for r in out]) == ref.expected(query, cols)
 
 
