@@ -177,7 +177,8 @@ typedef struct omx_result_info {
   int32_t n_cols;            /* RID columns per row (0 for an empty result)                        */
   int32_t deduplicated;      /* 1 if a dedup pass ran, 0 if rows were distinct by construction     */
   uint64_t edges_traversed;  /* Σ_h E_t(h), SURVEY §8(d)                                           */
-  uint64_t bindings;         /* complete matches before dedup                                      */
+  uint64_t bindings;         /* complete matches before dedup (a parallel edge into a filtered     */
+                             /* target binds once per edge; the reference HashSet binds it once)   */
   uint64_t alg_bytes;        /* algorithmic HBM bytes, SURVEY §8(d)                                */
   double device_ms;          /* wall time of the device part (root scan → last kernel)             */
   double total_ms;           /* wall time of omx_execute                                           */
