@@ -178,6 +178,7 @@ class Executor {
       factor_ = std::strcmp(fz, "0") != 0;
       if (std::strcmp(fz, "force") == 0) factor_min_rows_ = 1, factor_min_ratio_ = 0;
     }
+    if (const char *fl = std::getenv("OMX_FLIST")) flist_ = std::strcmp(fl, "0") != 0;
     if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
     if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
     dist_setup();
@@ -1313,6 +1314,7 @@ class Executor {
   // counts Σ_rows deg; edges_read counts what was iterated (Σ_U deg + the L entries).
   // Returns false (nothing done) when the rows repeat their sources less than kFactorMinRatio-fold.
   uint64_t factor_min_rows_ = 4096, factor_min_ratio_ = 4;
+  bool flist_ = true;  // OMX_FLIST=0: the lists through the generic filtered expansion + key grouping
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
@@ -1327,7 +1329,14 @@ class Executor {
       tm_.end(4ull * R + 8ull * nwords_);
       ub = bitmap_list(ubm.p, 0, 1, U);
     }
-    const uint64_t Et = degree_sum(src, R, st.adj), EU = degree_sum(ub.p, U, st.adj);
+    // the distinct sources' degrees, scanned: doff[u] = the first of u's entries in the flat list space
+    const uint64_t Et = degree_sum(src, R, st.adj);
+    DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1);
+    tm_.begin("k_row_degree");
+    launch_row_degree(ub.p, U, make_adj(st.adj), udeg.p, s_);
+    tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(U + 1), s_); });
+    const uint64_t EU = read1(doff.p + U);
     if (Et < factor_min_ratio_ * EU) return false;
     edges_ += Et;
     // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
@@ -1339,13 +1348,41 @@ class Executor {
     tm_.begin("k_gather_u32");
     launch_gather_u32(pos.p, src, R, g.p, s_);
     tm_.end(12ull * R);
-    // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
-    ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true);
-    edges_iter_ += l.E;
-    // 3. grouped by source: offsets (U + 1) and the neighbours in group order
     DBuf<unsigned long long> cnt(&pool_, U + 1);
     DBuf<uint64_t> loff(&pool_, U + 1);
     HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));
+    DBuf<uint32_t> lcol;
+    uint64_t nlist = 0;
+    if (flist_ && st.adj.parts.size() == 1) {
+      // 2+3. the filtered lists, grouped by source in source order (factor.hip): tiles of the flat entry
+      // space compact their survivors in order, per-source counts give the offsets
+      const DAdj a = make_adj(st.adj);
+      const uint64_t nt = flist_tiles(EU);
+      DBuf<uint32_t> tmp(&pool_, std::max<uint64_t>(EU, 1)), tcnt(&pool_, nt + 1);
+      DBuf<uint64_t> toff(&pool_, nt + 1);
+      HIP_CHECK(hipMemsetAsync(tcnt.p + nt, 0, 4, s_));
+      tm_.begin("k_flist_tile");
+      launch_flist_tile(ub.p, U, doff.p, EU, a.p[0], bitmap(st.filter_bm), tmp.p, tcnt.p, cnt.p, cus(), s_);
+      tm_.end(4ull * EU + 24ull * U + 8ull * nt);  // col per entry, row tables per source; amended below
+      const size_t rec = tm_.last();
+      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> tc(tcnt.p, CastU64());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tc, toff.p, (int64_t)(nt + 1), s_); });
+      cub([&](void *t, size_t &b) {
+        return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
+      });
+      nlist = read1(toff.p + nt);
+      tm_.amend_at(rec, 4ull * EU + 24ull * U + 8ull * nt + 4ull * nlist);
+      lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(nlist, 1));
+      tm_.begin("k_flist_gather");
+      launch_flist_gather(tmp.p, tcnt.p, toff.p, nt, lcol.p, cus(), s_);
+      tm_.end(8ull * nlist + 12ull * nt);
+      edges_iter_ += EU;
+    } else {
+    // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
+    ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true);
+    edges_iter_ += l.E;
+    nlist = l.n;
+    // 3. grouped by source: offsets (U + 1) and the neighbours in group order
     if (l.n) {
       tm_.begin("k_key_hist");
       launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
@@ -1354,12 +1391,13 @@ class Executor {
     cub([&](void *t, size_t &b) {
       return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
     });
-    DBuf<uint32_t> lcol(&pool_, std::max<uint64_t>(l.n, 1));
+    lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(l.n, 1));
     if (l.n) {
       HIP_CHECK(hipMemcpyAsync(cnt.p, loff.p, (U + 1) * 8, hipMemcpyDeviceToDevice, s_));
       tm_.begin("k_key_scatter");
       launch_key_scatter(l.carry[0].p, l.dst.p, l.n, cnt.p, lcol.p, s_);
       tm_.end(12ull * l.n + 8ull * U);
+    }
     }
     // 4. the rows over their sources' lists
     DAdj ladj{};
@@ -1375,7 +1413,7 @@ class Executor {
     factorized_hops_++;
     if (debug_expand_)
       std::fprintf(stderr, "[omx factorized] R=%llu U=%llu Et=%llu EU=%llu lists=%llu rows=%llu\n", (unsigned long long)R,
-                   (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU, (unsigned long long)l.n,
+                   (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU, (unsigned long long)nlist,
                    (unsigned long long)o.n);
     if (!write || R_ == 0) return true;
     segmented_ = false;

@@ -1,0 +1,140 @@
+// factor.hip — the filtered neighbour lists of a factorized hop (exec.hip Executor::expand_factorized).
+//
+// A filtered hop whose rows repeat their source vertices is expanded once per distinct source u: L(u) =
+// the neighbours of u passing the target's WHERE bitmap (OMatchPathItem.executeTraversal with the
+// filter, P/OMatchPathItem.java:63-78), grouped by source so that the rows are written over the lists.
+// Here the distinct sources' adjacency entries are one flat range [0, EU) in source order (doff = the
+// exclusive scan of their degrees), cut into tiles of kFlTile entries:
+//   k_flist_tile   one workgroup per tile: each entry's source row from the tile's row range staged in
+//                  LDS, the col word (coalesced: a wave reads 64 consecutive entries per step, so a hub
+//                  row's sorted neighbours probe few bitmap lines), the bitmap probe (L2-resident
+//                  V-bit bitmap), the survivors compacted in entry order into the tile's slot of a
+//                  scratch buffer, and per-source survivor counts (LDS, then one global atomic per
+//                  source and tile);
+//   k_flist_gather the tiles' survivors moved to their final place (a scan of the tile counts).
+// The lists come out grouped by source in source order, so their offsets are the scan of the counts —
+// no key histogram / scatter, no arenas, no degree binning. Reads: 4 B per entry (+ the probe); writes:
+// 4 B per survivor, twice.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "devutil.h"
+
+namespace omx {
+
+namespace {
+
+constexpr int kFlB = 256, kFlSteps = 4, kFlTile = kFlB * kFlSteps, kFlRows = 1024;  // 20.5 KiB of LDS
+
+// last r in [lo, hi] with off[r] <= e (off ascending, off[lo] <= e)
+template <class T>
+__device__ __forceinline__ uint64_t last_le_range(const T *off, uint64_t lo, uint64_t hi, uint64_t e) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= e) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kFlB) void k_flist_tile(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU,
+                                                     DAdjPart a, const uint64_t *filter, uint32_t *tmp,
+                                                     uint32_t *tile_cnt, unsigned long long *cnt) {
+  __shared__ uint64_t s_off[kFlRows + 1];  // doff of the tile's rows
+  __shared__ uint64_t s_adj[kFlRows];      // col position of each row's first neighbour
+  __shared__ uint32_t s_cnt[kFlRows];      // survivors per row in this tile
+  __shared__ uint64_t s_r[2];
+  __shared__ uint32_t s_w[kFlB / 64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t ntiles = (EU + kFlTile - 1) / kFlTile;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t t0 = tile * kFlTile, t1 = min(t0 + (uint64_t)kFlTile, EU) - 1;
+    if (threadIdx.x < 2) s_r[threadIdx.x] = last_le_range(doff, 0, U - 1, threadIdx.x ? t1 : t0);
+    __syncthreads();
+    const uint64_t r0 = s_r[0], nr = s_r[1] - r0 + 1;
+    const bool staged = nr <= kFlRows;
+    if (staged) {
+      for (uint32_t i = threadIdx.x; i <= nr; i += kFlB) s_off[i] = doff[r0 + i];
+      for (uint32_t i = threadIdx.x; i < nr; i += kFlB) {
+        s_adj[i] = a.rp[ub[r0 + i]];
+        s_cnt[i] = 0;
+      }
+    }
+    __syncthreads();
+    uint32_t base = 0;  // survivors of the earlier steps of this tile
+    for (int k = 0; k < kFlSteps; ++k) {
+      const uint64_t e = t0 + (uint64_t)k * kFlB + threadIdx.x;
+      bool keep = false;
+      uint32_t x = 0;
+      uint64_t r = 0;
+      if (e <= t1) {
+        uint64_t pos;
+        if (staged) {
+          r = last_le_range(s_off, 0, nr - 1, e);
+          pos = s_adj[r] + (e - s_off[r]);
+        } else {
+          r = last_le_range(doff, r0, r0 + nr - 1, e);
+          pos = a.rp[ub[r]] + (e - doff[r]);
+        }
+        x = a.col[pos];
+        keep = bm_test(filter, x);
+      }
+      const uint64_t m = __ballot(keep);
+      if (lane == 0) s_w[wave] = (uint32_t)__popcll(m);
+      __syncthreads();
+      uint32_t before = 0, total = 0;
+#pragma unroll
+      for (int w = 0; w < kFlB / 64; ++w) {
+        const uint32_t c = s_w[w];
+        before += (uint32_t)w < wave ? c : 0;
+        total += c;
+      }
+      if (keep) {
+        tmp[t0 + base + before + lane_prefix(m)] = x;
+        if (staged) atomicAdd(&s_cnt[r], 1u);
+        else atomicAdd(&cnt[r], 1ull);
+      }
+      base += total;
+      __syncthreads();  // s_w is rewritten by the next step
+    }
+    if (threadIdx.x == 0) tile_cnt[tile] = base;
+    if (staged)
+      for (uint32_t i = threadIdx.x; i < nr; i += kFlB)
+        if (s_cnt[i]) atomicAdd(&cnt[r0 + i], (unsigned long long)s_cnt[i]);
+    __syncthreads();  // the LDS row tables are restaged by the next tile
+  }
+}
+
+__global__ __launch_bounds__(kFlB) void k_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt,
+                                                       const uint64_t *tile_off, uint64_t ntiles, uint32_t *out) {
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint32_t n = tile_cnt[tile];
+    const uint64_t src = tile * kFlTile, dst = tile_off[tile];
+    for (uint32_t i = threadIdx.x; i < n; i += kFlB) out[dst + i] = tmp[src + i];
+  }
+}
+
+}  // namespace
+
+uint64_t flist_tiles(uint64_t EU) { return (EU + kFlTile - 1) / kFlTile; }
+
+void launch_flist_tile(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const DAdjPart &a,
+                       const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, int cus,
+                       hipStream_t s) {
+  if (!EU || !U) return;
+  const uint64_t nt = flist_tiles(EU);
+  hipLaunchKernelGGL(k_flist_tile, dim3((unsigned)std::min<uint64_t>(nt, (uint64_t)cus * 8)), dim3(kFlB), 0, s, ub, U,
+                     doff, EU, a, filter, tmp, tile_cnt, cnt);
+  KCHECK("k_flist_tile");
+}
+
+void launch_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt, const uint64_t *tile_off, uint64_t ntiles,
+                         uint32_t *out, int cus, hipStream_t s) {
+  if (!ntiles) return;
+  hipLaunchKernelGGL(k_flist_gather, dim3((unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * 8)), dim3(kFlB), 0, s, tmp,
+                     tile_cnt, tile_off, ntiles, out);
+  KCHECK("k_flist_gather");
+}
+
+}  // namespace omx

@@ -220,6 +220,13 @@ void launch_iota(uint32_t *out, uint64_t n, hipStream_t s);
 void launch_fill_u32(uint32_t *out, uint64_t n, uint32_t x, hipStream_t s);
 // factorized expansion: position of each key in a sorted unique list; a key histogram; a scatter by key
 void launch_index_of(const uint32_t *sorted, uint64_t n, const uint32_t *keys, uint64_t m, uint32_t *out, hipStream_t s);
+// factor.hip: the filtered lists of a factorized hop's distinct sources (see there)
+uint64_t flist_tiles(uint64_t EU);
+void launch_flist_tile(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const DAdjPart &a,
+                       const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, int cus,
+                       hipStream_t s);
+void launch_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt, const uint64_t *tile_off, uint64_t ntiles,
+                         uint32_t *out, int cus, hipStream_t s);
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
 void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor, uint32_t *out,
                         hipStream_t s);
