@@ -218,7 +218,7 @@ class Executor {
         bool count_only = last && o_.mode == OMX_MODE_COUNT && p_.unique_by_construction && st.kind == S_EXPAND;
         // the last expansion of a plan whose rows are distinct by construction may stay block-
         // segmented in HBM when the rows are not copied to the host
-        bool seg_ok = last && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES &&
+        bool seg_ok = last && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES && !gather0_ &&
                       (o_.flags & OMX_FLAG_KEEP_DEVICE) && !(o_.flags & OMX_FLAG_DIGEST);
         // expansion + closing check fused into one intersection pass
         const Step *fuse = nullptr;
@@ -227,7 +227,7 @@ class Executor {
           fuse = &p_.steps[i + 1];
           const bool last2 = i + 2 == p_.steps.size();
           count_only = last2 && o_.mode == OMX_MODE_COUNT && p_.unique_by_construction;
-          seg_ok = last2 && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES &&
+          seg_ok = last2 && p_.unique_by_construction && p_.proj == Plan::PROJ_ALIASES && !gather0_ &&
                    (o_.flags & OMX_FLAG_KEEP_DEVICE) && !(o_.flags & OMX_FLAG_DIGEST);
           expand_step(st, !count_only, seg_ok, fuse);
           counted_only = count_only;
@@ -260,7 +260,8 @@ class Executor {
     int ncols = 0;
     std::vector<DBuf<uint32_t>> out;
     // partitioned + distinct projection: equal tuples meet on one rank first
-    if (dist_ && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
+    if (dist_ && !empty && !counted_only && gather0_) route_rank0();
+    else if (dist_ && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
     const bool sp_doc = p_.kind == Plan::SHORTEST_PATH && !p_.chain.expand_rows;
     const bool docs = p_.proj == Plan::PROJ_EXPR || p_.proj == Plan::PROJ_JSON || sp_doc;
     if (sp_doc) {  // SELECT shortestPath(...): one document whose field is the list of the path's RIDs
@@ -635,12 +636,37 @@ class Executor {
     for (const PredProgram &pp : p_.progs)
       for (const DPredInstr &in : pp.code)
         if (in.op == P_PUSH_DEG) unsupported("out()/in()/both().size() in WHERE is not supported on a partitioned snapshot");
-    if (p_.proj != Plan::PROJ_ALIASES)
-      unsupported("$elements, $pathElements and RETURN expressions are not supported on a partitioned snapshot");
-    for (char opt : p_.optional)
-      if (opt) unsupported("optional nodes are not supported on a partitioned snapshot");
-    if (p_.limit >= 0 || o_.limit >= 0) unsupported("LIMIT is not supported on a partitioned snapshot");
+    // RETURN expressions read the replicated property columns, but out()/in()/both() inside them read
+    // adjacency rows a partition may not hold
+    if (!p_.ret_adj.empty())
+      unsupported("out()/in()/both() in a RETURN expression is not supported on a partitioned snapshot");
+    const bool limited = p_.limit >= 0 || o_.limit >= 0;
+    if (limited && o_.mode == OMX_MODE_COUNT) unsupported("LIMIT in COUNT mode on a partitioned snapshot");
+    // optional nodes need nothing more: a row is flagged or checked on the owner of the vertex whose
+    // adjacency it reads (a traversal never starts from an optional alias, plan.cpp); RETURN expressions,
+    // $elements / $pathElements and LIMIT are evaluated over the content-distinct result as a whole, so
+    // the rows of every rank meet on rank 0 first (route_rank0)
+    gather0_ = p_.proj != Plan::PROJ_ALIASES || limited;
     dist_ = true;
+  }
+  bool gather0_ = false;  // partitioned: the final rows go to rank 0 (projection over the whole result)
+
+  // every rank's rows to rank 0 (before a projection that needs the whole result: documents by content,
+  // $elements, LIMIT); the other ranks end with no rows
+  void route_rank0() {
+    owner_col_ = -1;
+    if (tr_->world() == 1 && !route_self_) return;
+    const int W = tr_->world();
+    DBuf<uint32_t> dest(&pool_, std::max<uint64_t>(R_, 1));
+    DBuf<uint64_t> hist(&pool_, W);
+    HIP_CHECK(hipMemsetAsync(hist.p, 0, W * sizeof(uint64_t), s_));
+    if (R_) {
+      const uint64_t h0 = R_;
+      HIP_CHECK(hipMemsetAsync(dest.p, 0, R_ * sizeof(uint32_t), s_));
+      HIP_CHECK(hipMemcpyAsync(hist.p, &h0, sizeof(uint64_t), hipMemcpyHostToDevice, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));  // (h0 is a local)
+    }
+    route_rows(dest, hist);
   }
 
   // (row, vertex) pairs of an item's result sets (see traverse)

@@ -266,3 +266,74 @@ def test_partition_errors(rmat10_full):
         o.OMatchStatement(q).execute(parts[0], comm=comms[0])
     for c in comms:
         c.close()
+
+
+# ---- partitioned coverage: optional nodes, RETURN expressions / JSON / $elements, LIMIT ---------------
+from tests.test_gpu_parity import DOC_QUERIES, doc_set, oracle_rows  # noqa: E402
+
+OPT_IDS = ("optional_free", "optional_bound", "elements", "paths", "matches")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in OPT_IDS], ids=lambda q: q[0])
+def test_partitioned_optional_and_elements(rmat10_full, world, q):
+    """Optional nodes (a row whose traversal finds nothing continues with the alias null, flagged on the
+    owner of the source: P/OMatchStatement.java:448-458) and $elements / $paths / $matches on partitions;
+    $elements is de-duplicated over the whole result, on rank 0 after every rank's rows met there."""
+    _, ref = rmat10_full
+    name, query, cols = q
+    want = ref.expected(query, cols)
+    res = run_ranks(_parts(world), query)
+    cset = cols if cols and res[0].columns and res[0].columns[0] not in ("$elements", "$pathElements") else None
+    got = [gpu_set(r, cset) for r in res]
+    assert set().union(*got) == want
+    assert sum(len(x) for x in got) == len(want)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("q", [q for q in DOC_QUERIES if q[0] != "out_list"], ids=lambda q: q[0])
+def test_partitioned_documents(rmat10_full, world, q):
+    """RETURN expressions / JSON over a partitioned snapshot: every rank's rows meet on rank 0, which
+    builds the documents from the replicated property columns and de-duplicates them by content
+    (addResult :698-719, ODocumentEqualityWrapper); the other ranks return nothing."""
+    g, ref = rmat10_full
+    want = oracle_rows(ref.db, q[1])
+    res = run_ranks(_parts(world), q[1])
+    assert all(len(r) == 0 for r in res[1:])
+    assert res[0].info["documents"] == 1
+    assert doc_set(res[0]) == doc_set(want)
+
+
+def test_partitioned_return_adjacency_is_unsupported():
+    """out()/in() inside a RETURN expression reads adjacency rows a partition does not hold: refused
+    alike on every rank before any exchange (the host runs the reference engine)."""
+    import orientdb_amd as o
+    q = [x for x in DOC_QUERIES if x[0] == "out_list"][0][1]
+    with pytest.raises(o.OmxUnsupported):
+        run_ranks(_parts(2), q)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("limit", [0, 1, 7, 100000])
+def test_partitioned_limit(rmat10_full, world, limit):
+    """LIMIT over the content-distinct result as a whole (OMatchStatement.java:741-746, LIMIT 0 = one row
+    like addSingleResult :737-750): rank 0 returns min(max(limit, 1), total) distinct rows of the oracle's
+    set, the others none."""
+    _, ref = rmat10_full
+    name, query, cols = [q for q in RMAT_QUERIES if q[0] == "c2_both_ends"][0]
+    want = ref.expected(query, cols)
+    res = run_ranks(_parts(world), query + " LIMIT %d" % limit)
+    assert all(r.info["n_rows"] == 0 for r in res[1:])
+    got = gpu_set(res[0], cols)
+    assert len(got) == min(max(limit, 1), len(want))
+    assert got <= want
+
+
+def test_partitioned_optional_null_reached_again_raises(rmat10_full):
+    """The NPE of a null optional alias reached again (P/OMatchStatement.java:468) fails the partitioned
+    execution on every rank (the rank that finds it aborts the exchanges of the others)."""
+    import orientdb_amd as o
+    q = ("MATCH {class:Person,as:a,where:(uid < 40)}-Knows->{as:b}-Knows->{as:c, where:(age < 30), optional:true},"
+         "{as:a}-Knows->{as:c, optional:true} RETURN a, b, c")
+    with pytest.raises(o.OmxError):
+        run_ranks(_parts(2), q)

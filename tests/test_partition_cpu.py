@@ -260,3 +260,72 @@ def test_two_rank_partitioned_msbfs():
     for r, g in enumerate(gathered):
         lo, hi = o.partition_range(V, r, world)
         assert all(lo <= v < hi for _, v in g)
+
+
+# ---- two gloo ranks: restatement of the rank-0 projection (optional node, RETURN expressions, LIMIT) ---
+DOC_Q = ("MATCH {class:Person,as:a,where:(uid < 200)}-Knows->{as:b, where:(age < 3), optional:true} "
+         "RETURN a.uid as au, b.age as ba")
+
+
+def _doc_rows(rank, world, dist):
+    """exec.hip on a partition: the rank's roots; the optional hop on the owner of a (a row with no
+    surviving neighbour continues with b = null, P/OMatchStatement.java:448-458); then every rank's rows
+    go to rank 0 (route_rank0), which builds the documents from the replicated property columns and
+    keeps the content-distinct ones (addResult :698-719)."""
+    import orientdb_amd as o
+    V = 1 << SCALE
+    lo, hi = o.partition_range(V, rank, world)
+    orp, ocol, _, _ = o.rmat_partition(SCALE, lo, hi, 16, SCALE)
+    age = o.synthetic_int_column(V, SCALE ^ 0xA9E, 100)
+    rows = []
+    for a in range(lo, min(hi, 200)):
+        bs = [int(w) for w in ocol[orp[a - lo]:orp[a - lo + 1]] if age[w] < 3]
+        rows += [(a, b) for b in bs] if bs else [(a, None)]
+    gathered = [None] * world
+    dist.all_gather_object(gathered, rows)  # the all-to-all whose only destination is rank 0
+    if rank != 0:
+        return None
+    docs = {(a, None if b is None else int(age[b])) for g in gathered for a, b in g}
+    return sorted(docs, key=lambda d: (d[0], -1 if d[1] is None else d[1]))
+
+
+def _doc_worker(rank, world, port, out):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r = _doc_rows(rank, world, dist)
+        if rank == 0:
+            out.put(r)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_documents_on_rank0():
+    """The partitioned projection of RETURN expressions (documents by content, over the whole result:
+    the rows of both gloo ranks meet on rank 0) equals the oracle's OResultSet on the full graph; LIMIT
+    then cuts that one set (count only: which documents is HashSet-order-dependent, :404)."""
+    import orientdb_amd as o
+    from oracle.match_ref import MatchOracle
+    from tests.rmat_oracle import refdb_from_csr
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_doc_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    docs = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rp, col = o.rmat_csr(SCALE, 16, SCALE)
+    age = o.synthetic_int_column(1 << SCALE, SCALE ^ 0xA9E, 100)
+    want = MatchOracle(refdb_from_csr(rp, col, age), DOC_Q).execute()
+    assert {(d["au"], d["ba"]) for d in want} == set(docs)
+    assert len(want) == len(docs)
+    assert any(d[1] is None for d in docs)  # the optional branch is exercised
+    for limit in (1, 5):
+        lim = MatchOracle(refdb_from_csr(rp, col, age), DOC_Q + " LIMIT %d" % limit).execute()
+        assert len(lim) == min(limit, len(docs))
