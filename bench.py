@@ -42,6 +42,8 @@ QUERIES = {
            "MATCH {class:Person,as:a}-Knows->{as:b}-Knows->{as:c}-Knows->{as:a} RETURN a,b,c", "ldbc"),
     "c5": ("C5: RMAT 3-hop MATCH (COUNT), 1-D partitioned graph, per-hop all-to-all row exchange (RCCL)",
            "MATCH {class:Person,as:a,where:(uid < 64)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d", 26),
+    "r1": ("R1: configs[1]'s 2-hop at RMAT-22 returning RETURN expressions (documents by content, evaluated on the device)",
+           "MATCH {class:Person,as:a,where:(age < 1)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a.uid, b.age", 22),
     # SURVEY §8(f) rows (not the metric): {hub} = the vertex of highest out-degree
     "t1": ("T1: TRAVERSE out('Knows') STRATEGY BREADTH_FIRST from the highest-degree vertex (its whole reach)",
            "TRAVERSE out('Knows') FROM #11:{hub} STRATEGY BREADTH_FIRST", 24),
@@ -193,6 +195,10 @@ def cpu_baseline(g, query, target_s=12.0):
         return r
     rp, col = g.csr
     cg = dfs.CsrGraph(rp, col, {"uid": np.arange(g.V, dtype=np.int64), "age": g.age})
+    head, ret = query.split("RETURN")
+    if "." in ret:  # RETURN expressions: the DFS enumerates the same bindings of the aliases they read
+        import re as _re
+        query = head + "RETURN " + ",".join(sorted(set(_re.findall(r"\b([a-z]+)\.", ret))))
     probe = dfs.run(cg, query, nthreads=threads, emit=False, root_sample=64)
     import re
     m = re.search(r"\((age|uid) < (\d+)\)", query.split("-")[0])
@@ -406,6 +412,8 @@ def main():
                    "mode": "count" if mode == o.OMX_MODE_COUNT else "materialize (rows kept in HBM)",
                    "graph_build_s": round(t_build, 2)},
         "bindings_per_s": bindings_all / dt_max,
+        # distinct result rows (documents for RETURN expressions) per second
+        "rows_per_s": rows_all * args.steps / dt_max,
         # adjacency entries the kernels actually iterated per second (GTEPS counts E_t)
         "read_rate": {"value": edges_read_all / dt_max / 1e9, "unit": "G adjacency entries read/s"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -12,6 +12,7 @@
 #include "exec.h"
 #include "graph.h"
 #include "plan.h"
+#include "projdev.h"
 #include "sql.h"
 
 struct omx_graph {
@@ -440,6 +441,21 @@ int omx_result_kernel_launch(const omx_result *r, int32_t i, const char **name, 
 void omx_result_free(omx_result *r) { delete r; }
 
 int omx_result_cell(const omx_result *r, uint64_t row, int32_t col, omx_cell *out) {
+  if (r && out && !r->pcols.empty()) {  // documents evaluated on the device (projdev.hip): columnar cells
+    if (row >= r->n_pcol_rows || col < 0 || (size_t)col >= r->pcols.size()) return OMX_E_INVALID;
+    const omx_result::PCol &pc = r->pcols[col];
+    const uint64_t x = pc.val[row];
+    std::memset(out, 0, sizeof(*out));
+    switch (pc.kind[row]) {
+      case omx::PJ_K_INT: out->type = OMX_CELL_INT; out->i = (int64_t)x; break;
+      case omx::PJ_K_DBL: out->type = OMX_CELL_DOUBLE; std::memcpy(&out->d, &x, 8); break;
+      case omx::PJ_K_STR: out->type = OMX_CELL_STRING; out->s = pc.strs.at(x).c_str(); break;
+      case omx::PJ_K_BOOL: out->type = OMX_CELL_BOOL; out->i = (int64_t)x; break;
+      case omx::PJ_K_RID: out->type = OMX_CELL_RID; out->rid = x; break;
+      default: out->type = OMX_CELL_NULL; break;
+    }
+    return OMX_OK;
+  }
   if (!r || !out || row >= r->docs.size() || col < 0 || (size_t)col >= r->docs[row].size()) return OMX_E_INVALID;
   const omx::HVal &v = r->docs[row][col];
   std::memset(out, 0, sizeof(*out));

@@ -1,6 +1,7 @@
 // exec.h — runs a compiled Plan on the device and produces the distinct RETURN rows.
 #pragma once
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "graph.h"
@@ -20,6 +21,14 @@ struct omx_result {
   };
   std::vector<KStat> kstats;
   std::vector<KStat> klaunches;  // every timed launch in issue order (launches = 1 each)
+  // documents evaluated on the device (projdev.hip): one column per RETURN item, n_pcol_rows cells each
+  struct PCol {
+    std::vector<uint8_t> kind;                        // omx::PJ_K_*
+    std::vector<uint64_t> val;                        // int64 / double bits / dictionary code / bool / RID
+    std::unordered_map<uint64_t, std::string> strs;  // dictionary code → string (string columns)
+  };
+  std::vector<PCol> pcols;
+  uint64_t n_pcol_rows = 0;
 };
 
 namespace omx {

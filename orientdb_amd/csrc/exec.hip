@@ -8,6 +8,7 @@
 // (C/command/OBasicCommandContext.java:347-353). Scans, radix sorts and flagged selects are hipCUB
 // (rocPRIM) device primitives; the traversal kernels are hand-written (kernels.hip).
 #include "exec.h"
+#include "projdev.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -179,6 +180,7 @@ class Executor {
       if (std::strcmp(fz, "force") == 0) factor_min_rows_ = 1, factor_min_ratio_ = 0;
     }
     if (const char *fl = std::getenv("OMX_FLIST")) flist_ = std::strcmp(fl, "0") != 0;
+    if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
     if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
     if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
     dist_setup();
@@ -299,10 +301,18 @@ class Executor {
       std::vector<const uint32_t *> cp;
       for (auto &c : out) cp.push_back(c.p);
       int64_t lim = p_.limit >= 0 ? p_.limit : o_.limit;
-      tm_.begin("documents");
-      res->docs = build_documents(g_, p_, cp, n, lim, s_);
-      tm_.end();
-      n = res->docs.size();
+      if (devproj_ && !p_.out_aliases.empty() && device_projection_ok(g_, p_, nullptr)) {
+        // scalar items: evaluated and de-duplicated by content on the device (projdev.hip)
+        tm_.begin("k_pj_eval");
+        device_project(g_, p_, cp, n, lim, cus(), s_, *res);
+        tm_.end(n * (4ull * cp.size() + 9ull * p_.returns.size()) * 2);
+        n = res->n_pcol_rows;
+      } else {
+        tm_.begin("documents");
+        res->docs = build_documents(g_, p_, cp, n, lim, s_);
+        tm_.end();
+        n = res->docs.size();
+      }
       ncols = (int)p_.out_names.size();
       dedup_ran_ = 1;
     } else if (R_ > 0 && !counted_only) {
@@ -650,6 +660,7 @@ class Executor {
     dist_ = true;
   }
   bool gather0_ = false;  // partitioned: the final rows go to rank 0 (projection over the whole result)
+  bool devproj_ = true;   // OMX_DEVPROJ=0: every RETURN expression through the host evaluator
 
   // every rank's rows to rank 0 (before a projection that needs the whole result: documents by content,
   // $elements, LIMIT); the other ranks end with no rows

@@ -200,10 +200,21 @@ DOC_QUERIES = [
 ]
 
 
+DOC_QUERIES += [
+    ("math_dbl", "MATCH {class:Person,as:a,where:(uid < 40)}-Knows->{as:b} RETURN b.age / 2.0 as h, b.age % 7 as m"),
+    ("rid_and_const", "MATCH {class:Person,as:a,where:(uid < 25)}-Knows->{as:b} RETURN b.@rid as r, 3 as k, a.nope as z"),
+    ("int_div", "MATCH {class:Person,as:a,where:(uid < 25)}-Knows->{as:b} RETURN (a.uid + 7) / 3 as q, -a.uid as n"),
+]
+
+
+@pytest.mark.parametrize("devproj", ["device", "host"])
 @pytest.mark.parametrize("q", DOC_QUERIES, ids=[q[0] for q in DOC_QUERIES])
-def test_rmat_documents(rmat10, q):
-    """RETURN expressions / JSON (addResult :698-719, jsonToDoc :791-806): documents equal by content."""
+def test_rmat_documents(rmat10, q, devproj, monkeypatch):
+    """RETURN expressions / JSON (addResult :698-719, jsonToDoc :791-806): documents equal by content —
+    scalar items evaluated and de-duplicated on the device (projdev.hip), or every item through the host
+    evaluator (OMX_DEVPROJ=0, and always for JSON, lists and methods)."""
     import orientdb_amd as o
+    monkeypatch.setenv("OMX_DEVPROJ", "1" if devproj == "device" else "0")
     g, ref = rmat10
     want = oracle_rows(ref.db, q[1])
     rs = o.OMatchStatement(q[1]).execute(g)
@@ -213,6 +224,16 @@ def test_rmat_documents(rmat10, q):
         assert sorted((d["d"], len(d["f"])) for d in rs) == sorted((d["d"], len(d["f"])) for d in want)
         return
     assert doc_set(rs) == doc_set(want)
+
+
+@pytest.mark.parametrize("devproj", ["1", "0"])
+def test_return_division_by_zero_fails(rmat10, devproj, monkeypatch):
+    """An integer division by zero in a RETURN item fails the execution on both evaluators."""
+    import orientdb_amd as o
+    monkeypatch.setenv("OMX_DEVPROJ", devproj)
+    g, _ = rmat10
+    with pytest.raises(o.OmxExecutionError):
+        o.OMatchStatement("MATCH {class:Person,as:a,where:(uid < 5)} RETURN a.uid / 0 as x").execute(g)
 
 
 def test_optional_null_reached_again_raises(rmat10):
