@@ -46,7 +46,7 @@ class Timer {
     static const char *const kHot[] = {"k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light",
                                        "k_expand_light_sliced", "k_expand_light_check", "k_expand_heavy_check",
                                        "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit", "k_bfs_push",
-                                       "k_bfs_emit", "k_trav_filter", "trav_select"};
+                                       "k_bfs_emit", "k_trav_filter", "trav_select", "k_flist_tile"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
     return false;
@@ -1396,10 +1396,10 @@ class Executor {
       const DAdj a = make_adj(st.adj);
       const uint64_t nt = flist_tiles(EU);
       DBuf<uint32_t> tmp(&pool_, std::max<uint64_t>(EU, 1)), tcnt(&pool_, nt + 1);
-      DBuf<uint64_t> toff(&pool_, nt + 1);
+      DBuf<uint64_t> toff(&pool_, nt + 1), rb(&pool_, 2 * nt + 2);
       HIP_CHECK(hipMemsetAsync(tcnt.p + nt, 0, 4, s_));
       tm_.begin("k_flist_tile");
-      launch_flist_tile(ub.p, U, doff.p, EU, a.p[0], bitmap(st.filter_bm), tmp.p, tcnt.p, cnt.p, cus(), s_);
+      launch_flist_tile(ub.p, U, doff.p, EU, a.p[0], bitmap(st.filter_bm), tmp.p, tcnt.p, cnt.p, rb.p, cus(), s_);
       tm_.end(4ull * EU + 24ull * U + 8ull * nt);  // col per entry, row tables per source; amended below
       const size_t rec = tm_.last();
       hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> tc(tcnt.p, CastU64());

@@ -38,21 +38,28 @@ __device__ __forceinline__ uint64_t last_le_range(const T *off, uint64_t lo, uin
   return lo;
 }
 
+// the first and last source row of every tile (one thread per tile: the searches run in parallel rather
+// than as a dependent chain at the head of each tile)
+__global__ void k_flist_bounds(const uint64_t *doff, uint64_t U, uint64_t EU, uint64_t ntiles, uint64_t *rb) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  const uint64_t t0 = t * kFlTile, t1 = min(t0 + (uint64_t)kFlTile, EU) - 1;
+  rb[2 * t] = last_le_range(doff, 0, U - 1, t0);
+  rb[2 * t + 1] = last_le_range(doff, rb[2 * t], U - 1, t1);
+}
+
 __global__ __launch_bounds__(kFlB) void k_flist_tile(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU,
-                                                     DAdjPart a, const uint64_t *filter, uint32_t *tmp,
-                                                     uint32_t *tile_cnt, unsigned long long *cnt) {
+                                                     const uint64_t *rb, DAdjPart a, const uint64_t *filter,
+                                                     uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt) {
   __shared__ uint64_t s_off[kFlRows + 1];  // doff of the tile's rows
   __shared__ uint64_t s_adj[kFlRows];      // col position of each row's first neighbour
   __shared__ uint32_t s_cnt[kFlRows];      // survivors per row in this tile
-  __shared__ uint64_t s_r[2];
   __shared__ uint32_t s_w[kFlB / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t ntiles = (EU + kFlTile - 1) / kFlTile;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * kFlTile, t1 = min(t0 + (uint64_t)kFlTile, EU) - 1;
-    if (threadIdx.x < 2) s_r[threadIdx.x] = last_le_range(doff, 0, U - 1, threadIdx.x ? t1 : t0);
-    __syncthreads();
-    const uint64_t r0 = s_r[0], nr = s_r[1] - r0 + 1;
+    const uint64_t r0 = rb[2 * tile], nr = rb[2 * tile + 1] - r0 + 1;
     const bool staged = nr <= kFlRows;
     if (staged) {
       for (uint32_t i = threadIdx.x; i <= nr; i += kFlB) s_off[i] = doff[r0 + i];
@@ -120,12 +127,14 @@ __global__ __launch_bounds__(kFlB) void k_flist_gather(const uint32_t *tmp, cons
 uint64_t flist_tiles(uint64_t EU) { return (EU + kFlTile - 1) / kFlTile; }
 
 void launch_flist_tile(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const DAdjPart &a,
-                       const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, int cus,
-                       hipStream_t s) {
+                       const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, uint64_t *rb,
+                       int cus, hipStream_t s) {
   if (!EU || !U) return;
   const uint64_t nt = flist_tiles(EU);
+  hipLaunchKernelGGL(k_flist_bounds, dim3(nblocks(nt, 256)), dim3(256), 0, s, doff, U, EU, nt, rb);
+  KCHECK("k_flist_bounds");
   hipLaunchKernelGGL(k_flist_tile, dim3((unsigned)std::min<uint64_t>(nt, (uint64_t)cus * 8)), dim3(kFlB), 0, s, ub, U,
-                     doff, EU, a, filter, tmp, tile_cnt, cnt);
+                     doff, EU, rb, a, filter, tmp, tile_cnt, cnt);
   KCHECK("k_flist_tile");
 }
 

@@ -223,8 +223,8 @@ void launch_index_of(const uint32_t *sorted, uint64_t n, const uint32_t *keys, u
 // factor.hip: the filtered lists of a factorized hop's distinct sources (see there)
 uint64_t flist_tiles(uint64_t EU);
 void launch_flist_tile(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const DAdjPart &a,
-                       const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, int cus,
-                       hipStream_t s);
+                       const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, uint64_t *rb,
+                       int cus, hipStream_t s);
 void launch_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt, const uint64_t *tile_off, uint64_t ntiles,
                          uint32_t *out, int cus, hipStream_t s);
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
