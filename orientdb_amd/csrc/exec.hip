@@ -204,6 +204,7 @@ class Executor {
     HIP_CHECK(hipEventRecord(ea, s_));
     mark("events");
     const bool chain = p_.kind != Plan::MATCH;
+    if (dist_ && !chain) gather_global_degrees();
     bool empty = !chain && (p_.empty || !check_candidates());
     bool counted_only = false;
     std::vector<DBuf<uint32_t>> chain_out;
@@ -489,6 +490,54 @@ class Executor {
     return d;
   }
 
+  // partitioned: out()/in()/both().size() of any vertex, through the gathered degree row pointers
+  DAdj global_degree_adj(const AdjSpec &a) const {
+    DAdj d = make_adj(a);
+    for (size_t i = 0; i < a.parts.size(); ++i) {
+      const uint64_t *g = g_.esets[a.parts[i].first].d_global_rp[a.parts[i].second];
+      if (!g) fail(OMX_E_INVALID, "internal: global degrees not gathered");
+      d.p[i].rp = g;
+      d.p[i].col = nullptr;  // a degree term never reads neighbours
+    }
+    return d;
+  }
+  // every rank's degrees of the CSRs a degree predicate reads, gathered once per snapshot: each rank
+  // sends the degrees of its rows to all ranks (all-to-all-v), the scan gives V + 1 row pointers
+  void gather_global_degrees() {
+    std::vector<std::pair<int, int>> need;
+    for (const PredProgram &pp : p_.progs)
+      for (const AdjSpec &a : pp.deg)
+        for (const auto &part : a.parts)
+          if (!g_.esets[part.first].d_global_rp[part.second] &&
+              std::find(need.begin(), need.end(), part) == need.end())
+            need.push_back(part);
+    if (need.empty()) return;
+    const int W = tr_->world();
+    const std::vector<uint64_t> plo = tr_->allgather(g_.part_lo, s_), phi = tr_->allgather(g_.part_hi, s_);
+    const uint32_t V = g_.V, lo = g_.part_lo, hi = g_.part_hi;
+    for (const auto &part : need) {
+      EdgeSet &es = g_.esets[part.first];
+      DBuf<uint32_t> mine(&pool_, std::max<uint32_t>(hi - lo, 1)), all(&pool_, std::max<uint32_t>(V, 1));
+      DBuf<uint64_t> deg(&pool_, (uint64_t)V + 1);
+      if (hi > lo) launch_row_degree_range(g_.rp(es, part.second), lo, hi, mine.p, s_);
+      std::vector<uint64_t> send(W, hi - lo), sdispl(W, 0), recv(W), rdispl(W);
+      for (int p = 0; p < W; ++p) {
+        recv[p] = phi[p] - plo[p];
+        rdispl[p] = plo[p];
+      }
+      tm_.begin("exchange");
+      tr_->alltoallv({mine.p}, send, sdispl, {all.p}, recv, rdispl, s_);
+      tm_.end(8ull * V);
+      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> d64(all.p, CastU64());
+      uint64_t *grp = nullptr;
+      HIP_CHECK(hipMalloc((void **)&grp, ((uint64_t)V + 1) * 8));
+      HIP_CHECK(hipMemsetAsync(grp, 0, 8, s_));
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, d64, grp + 1, (int64_t)V, s_); });
+      HIP_CHECK(hipStreamSynchronize(s_));
+      es.d_global_rp[part.second] = grp;
+    }
+  }
+
   DPred make_pred(int prog, int class_id) const {
     DPred d{};
     d.cols = g_.d_cols;
@@ -501,7 +550,7 @@ class Executor {
       const PredProgram &pp = p_.progs[prog];
       d.n = (int32_t)pp.code.size();
       for (size_t i = 0; i < pp.code.size(); ++i) d.code[i] = pp.code[i];
-      for (size_t i = 0; i < pp.deg.size(); ++i) d.deg[i] = make_adj(pp.deg[i]);
+      for (size_t i = 0; i < pp.deg.size(); ++i) d.deg[i] = dist_ ? global_degree_adj(pp.deg[i]) : make_adj(pp.deg[i]);
       match_atoms(pp, d);
     }
     return d;
@@ -640,12 +689,9 @@ class Executor {
     if (g_.part_lo != lo || g_.part_hi != hi)
       fail(OMX_E_INVALID, "snapshot rows [" + std::to_string(g_.part_lo) + ", " + std::to_string(g_.part_hi) +
                               ") are not rank " + std::to_string(r) + "'s block of " + std::to_string(W));
-    for (const Step &st : p_.steps)
-      if (st.kind == S_NEWROOT || st.kind == S_CARTESIAN)
-        unsupported("disconnected patterns are not supported on a partitioned snapshot");
-    for (const PredProgram &pp : p_.progs)
-      for (const DPredInstr &in : pp.code)
-        if (in.op == P_PUSH_DEG) unsupported("out()/in()/both().size() in WHERE is not supported on a partitioned snapshot");
+    // disconnected patterns: a new root's candidates are every vertex (replicated classes and columns),
+    // crossed with the rank's own rows, so the product stays partitioned by those rows. Degree
+    // predicates read the gathered degrees (gather_global_degrees, at the start of run()).
     // RETURN expressions read the replicated property columns, but out()/in()/both() inside them read
     // adjacency rows a partition may not hold
     if (!p_.ret_adj.empty())

@@ -81,7 +81,7 @@ Graph::~Graph() {
       f(e.d_out_rp); f(e.d_in_rp); f(e.d_out_col); f(e.d_in_col);
       for (auto &m : e.d_cuts)
         for (auto &kv : m) f(kv.second);
-      for (int d = 0; d < 2; ++d) { f(e.d_pull_col[d]); f(e.d_hubs[d]); f(e.d_pull_part[d]); }
+      for (int d = 0; d < 2; ++d) { f(e.d_pull_col[d]); f(e.d_hubs[d]); f(e.d_pull_part[d]); f(e.d_global_rp[d]); }
     }
     for (auto &p : props) { f(p.d_values); f(p.d_present); }
     if (stream) (void)hipStreamDestroy(stream);

@@ -105,6 +105,9 @@ struct EdgeSet {
   uint32_t hubs_requested[2] = {0, 0};  // the hub budget d_pull_col was built with (rebuilt when it changes)
   // merge-path split of the CSR into pull tiles (bfs.hip k_pull_partition), built with d_pull_col
   uint64_t *d_pull_part[2] = {nullptr, nullptr};
+  // partitioned snapshot: row pointers of every vertex's degree (V + 1 entries, the scan of all ranks'
+  // degrees gathered once) — what out()/in()/both().size() in a WHERE reads (no col[] behind them)
+  uint64_t *d_global_rp[2] = {nullptr, nullptr};
 };
 
 struct Property {

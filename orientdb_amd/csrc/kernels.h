@@ -139,6 +139,7 @@ void launch_route_bounds(const uint32_t *id, uint64_t R, const uint64_t *bounds,
 void launch_add_u32(uint32_t *x, uint64_t n, int64_t delta, hipStream_t s);
 
 void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t *deg, hipStream_t s);
+void launch_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint32_t *deg, hipStream_t s);
 void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part,
                          hipStream_t s);
 // rows [vlo, vhi) (the owned rows of a partition; rp indexed by global vertex id)

@@ -347,6 +347,18 @@ void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_
   KCHECK("k_row_degree");
 }
 
+// degrees of the rows [lo, hi) of one CSR (u32: a row of 2^32 or more entries does not occur in a
+// partition's snapshot)
+__global__ void k_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint32_t *deg) {
+  const uint64_t v = (uint64_t)lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < hi) deg[v - lo] = (uint32_t)(rp[v + 1] - rp[v]);
+}
+void launch_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint32_t *deg, hipStream_t s) {
+  if (hi <= lo) return;
+  hipLaunchKernelGGL(k_row_degree_range, dim3(nblocks(hi - lo, 256)), dim3(256), 0, s, rp, lo, hi, deg);
+  KCHECK("k_row_degree_range");
+}
+
 // merge path over A = row ends (offs[r+1]) and B = edge indices 0..E-1; a row end is consumed
 // before edge j when offs[r+1] <= j.
 __global__ void k_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part) {

@@ -261,9 +261,8 @@ def test_partition_errors(rmat10_full):
     comms = o.Comm.threads(2)
     with pytest.raises(o.OmxError):  # rank 1's communicator with rank 0's rows
         o.OMatchStatement(RMAT_QUERIES[0][1]).execute(parts[0], comm=comms[1])
-    with pytest.raises(o.OmxUnsupported):  # disconnected patterns stay on replicated snapshots
-        q = [x for x in RMAT_QUERIES if x[0] == "cartesian"][0][1]
-        o.OMatchStatement(q).execute(parts[0], comm=comms[0])
+    with pytest.raises(o.OmxUnsupported):  # TRAVERSE stays on replicated snapshots
+        o.OMatchStatement("TRAVERSE out('Knows') FROM #11:0 STRATEGY BREADTH_FIRST").execute(parts[0], comm=comms[0])
     for c in comms:
         c.close()
 
@@ -337,3 +336,28 @@ def test_partitioned_optional_null_reached_again_raises(rmat10_full):
          "{as:a}-Knows->{as:c, optional:true} RETURN a, b, c")
     with pytest.raises(o.OmxError):
         run_ranks(_parts(2), q)
+
+
+PART_EXTRA = [
+    ("cartesian", [q for q in RMAT_QUERIES if q[0] == "cartesian"][0][1], ["a", "b"]),
+    ("cartesian_then_hop", "MATCH {class:Person,as:a,where:(uid < 4)},{class:Person,as:b,where:(uid > 1018)}-Knows->{as:c} "
+                           "RETURN a,b,c", ["a", "b", "c"]),
+    ("degree_root", "MATCH {class:Person,as:a,where:(out('Knows').size() > 40)}-Knows->{as:b} RETURN a,b", ["a", "b"]),
+    ("degree_target", "MATCH {class:Person,as:a,where:(uid < 30)}-Knows->{as:b,where:(in('Knows').size() < 3)} "
+                      "RETURN a,b", ["a", "b"]),
+    ("degree_both", "MATCH {class:Person,as:a,where:(both('Knows').size() = 20)}-Knows->{as:b} RETURN b", ["b"]),
+]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("q", PART_EXTRA, ids=lambda q: q[0])
+def test_partitioned_cartesian_and_degrees(rmat10_full, world, q):
+    """Disconnected patterns (a new root crossed with the rank's own rows: every vertex is a candidate,
+    OMatchStatement.expandCartesianProduct :620-650) and out()/in()/both().size() predicates (the degrees
+    of all ranks gathered once into global row pointers) on partitions."""
+    _, ref = rmat10_full
+    name, query, cols = q
+    want = ref.expected(query, cols)
+    res = run_ranks(_parts(world), query)
+    got = [gpu_set(r, cols) for r in res]
+    assert set().union(*got) == want and len(want) > 0
