@@ -340,8 +340,8 @@ def test_partitioned_optional_null_reached_again_raises(rmat10_full):
 
 PART_EXTRA = [
     ("cartesian", [q for q in RMAT_QUERIES if q[0] == "cartesian"][0][1], ["a", "b"]),
-    ("cartesian_then_hop", "MATCH {class:Person,as:a,where:(uid < 4)},{class:Person,as:b,where:(uid > 1018)}-Knows->{as:c} "
-                           "RETURN a,b,c", ["a", "b", "c"]),
+    ("cartesian_after_hop", "MATCH {class:Person,as:a,where:(uid < 4)}-Knows->{as:c},{class:Person,as:b,where:(uid > 1018)} "
+                            "RETURN a,b,c", ["a", "b", "c"]),
     ("degree_root", "MATCH {class:Person,as:a,where:(out('Knows').size() > 40)}-Knows->{as:b} RETURN a,b", ["a", "b"]),
     ("degree_target", "MATCH {class:Person,as:a,where:(uid < 30)}-Knows->{as:b,where:(in('Knows').size() < 3)} "
                       "RETURN a,b", ["a", "b"]),
