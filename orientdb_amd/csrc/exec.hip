@@ -1414,10 +1414,18 @@ class Executor {
     }
     // the distinct sources' degrees, scanned: doff[u] = the first of u's entries in the flat list space
     const uint64_t Et = degree_sum(src, R, st.adj);
-    DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1);
-    tm_.begin("k_row_degree");
-    launch_row_degree(ub.p, U, make_adj(st.adj), udeg.p, s_);
-    tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
+    const bool tiles = flist_ && st.adj.parts.size() == 1;
+    DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1), astart;
+    if (tiles) {  // degrees and first col positions of the distinct sources, for the list tiles
+      astart = DBuf<uint64_t>(&pool_, std::max<uint64_t>(U, 1));
+      tm_.begin("k_flist_prep");
+      launch_flist_prep(ub.p, U, make_adj(st.adj).p[0].rp, udeg.p, astart.p, s_);
+      tm_.end(U * 36ull);
+    } else {
+      tm_.begin("k_row_degree");
+      launch_row_degree(ub.p, U, make_adj(st.adj), udeg.p, s_);
+      tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
+    }
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(U + 1), s_); });
     const uint64_t EU = read1(doff.p + U);
     if (Et < factor_min_ratio_ * EU) return false;
@@ -1436,7 +1444,7 @@ class Executor {
     HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));
     DBuf<uint32_t> lcol;
     uint64_t nlist = 0;
-    if (flist_ && st.adj.parts.size() == 1) {
+    if (tiles) {
       // 2+3. the filtered lists, grouped by source in source order (factor.hip): tiles of the flat entry
       // space compact their survivors in order, per-source counts give the offsets
       const DAdj a = make_adj(st.adj);
@@ -1445,7 +1453,7 @@ class Executor {
       DBuf<uint64_t> toff(&pool_, nt + 1), rb(&pool_, 2 * nt + 2);
       HIP_CHECK(hipMemsetAsync(tcnt.p + nt, 0, 4, s_));
       tm_.begin("k_flist_tile");
-      launch_flist_tile(ub.p, U, doff.p, EU, a.p[0], bitmap(st.filter_bm), tmp.p, tcnt.p, cnt.p, rb.p, cus(), s_);
+      launch_flist_tile(U, doff.p, astart.p, EU, a.p[0].col, bitmap(st.filter_bm), tmp.p, tcnt.p, cnt.p, rb.p, cus(), s_);
       tm_.end(4ull * EU + 24ull * U + 8ull * nt);  // col per entry, row tables per source; amended below
       const size_t rec = tm_.last();
       hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> tc(tcnt.p, CastU64());

@@ -48,13 +48,27 @@ __global__ void k_flist_bounds(const uint64_t *doff, uint64_t U, uint64_t EU, ui
   rb[2 * t + 1] = last_le_range(doff, rb[2 * t], U - 1, t1);
 }
 
-__global__ __launch_bounds__(kFlB) void k_flist_tile(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU,
-                                                     const uint64_t *rb, DAdjPart a, const uint64_t *filter,
+// degree and first col position of every distinct source (the tiles read both with coalesced loads)
+__global__ void k_flist_prep(const uint32_t *ub, uint64_t U, const uint64_t *rp, uint64_t *deg, uint64_t *astart) {
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u > U) return;
+  if (u == U) {
+    deg[U] = 0;
+    return;
+  }
+  const uint32_t v = ub[u];
+  const uint64_t s = rp[v];
+  deg[u] = rp[v + 1] - s;
+  astart[u] = s;
+}
+
+__global__ __launch_bounds__(kFlB) void k_flist_tile(const uint64_t *doff, const uint64_t *astart, uint64_t EU,
+                                                     const uint64_t *rb, const uint32_t *col, const uint64_t *filter,
                                                      uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt) {
   __shared__ uint64_t s_off[kFlRows + 1];  // doff of the tile's rows
   __shared__ uint64_t s_adj[kFlRows];      // col position of each row's first neighbour
   __shared__ uint32_t s_cnt[kFlRows];      // survivors per row in this tile
-  __shared__ uint32_t s_w[kFlB / 64];
+  __shared__ uint32_t s_w[kFlSteps][kFlB / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t ntiles = (EU + kFlTile - 1) / kFlTile;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -64,52 +78,68 @@ __global__ __launch_bounds__(kFlB) void k_flist_tile(const uint32_t *ub, uint64_
     if (staged) {
       for (uint32_t i = threadIdx.x; i <= nr; i += kFlB) s_off[i] = doff[r0 + i];
       for (uint32_t i = threadIdx.x; i < nr; i += kFlB) {
-        s_adj[i] = a.rp[ub[r0 + i]];
+        s_adj[i] = astart[r0 + i];
         s_cnt[i] = 0;
       }
     }
     __syncthreads();
-    uint32_t base = 0;  // survivors of the earlier steps of this tile
+    // every step's row, col word and probe requested before any is consumed (one latency chain per
+    // tile instead of one per step)
+    uint32_t x[kFlSteps];
+    uint64_t r[kFlSteps];
+#pragma unroll
     for (int k = 0; k < kFlSteps; ++k) {
       const uint64_t e = t0 + (uint64_t)k * kFlB + threadIdx.x;
-      bool keep = false;
-      uint32_t x = 0;
-      uint64_t r = 0;
+      x[k] = 0;
+      r[k] = ~0ull;
       if (e <= t1) {
         uint64_t pos;
         if (staged) {
-          r = last_le_range(s_off, 0, nr - 1, e);
-          pos = s_adj[r] + (e - s_off[r]);
+          r[k] = last_le_range(s_off, 0, nr - 1, e);
+          pos = s_adj[r[k]] + (e - s_off[r[k]]);
         } else {
-          r = last_le_range(doff, r0, r0 + nr - 1, e);
-          pos = a.rp[ub[r]] + (e - doff[r]);
+          r[k] = last_le_range(doff, r0, r0 + nr - 1, e);
+          pos = astart[r[k]] + (e - doff[r[k]]);
         }
-        x = a.col[pos];
-        keep = bm_test(filter, x);
+        x[k] = col[pos];
       }
-      const uint64_t m = __ballot(keep);
-      if (lane == 0) s_w[wave] = (uint32_t)__popcll(m);
-      __syncthreads();
-      uint32_t before = 0, total = 0;
+    }
+    uint32_t keep = 0;
+#pragma unroll
+    for (int k = 0; k < kFlSteps; ++k)
+      if (r[k] != ~0ull && bm_test(filter, x[k])) keep |= 1u << k;
+    uint64_t m[kFlSteps];
+#pragma unroll
+    for (int k = 0; k < kFlSteps; ++k) {
+      m[k] = __ballot((keep >> k) & 1u);
+      if (lane == 0) s_w[k][wave] = (uint32_t)__popcll(m[k]);
+    }
+    __syncthreads();
+    // survivors in entry order: step k's survivors follow all earlier steps' (wave totals in LDS)
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < kFlSteps; ++k) {
+      uint32_t kb = 0, kt = 0;
 #pragma unroll
       for (int w = 0; w < kFlB / 64; ++w) {
-        const uint32_t c = s_w[w];
-        before += (uint32_t)w < wave ? c : 0;
-        total += c;
+        const uint32_t c = s_w[k][w];
+        kb += (uint32_t)w < wave ? c : 0;
+        kt += c;
       }
-      if (keep) {
-        tmp[t0 + base + before + lane_prefix(m)] = x;
-        if (staged) atomicAdd(&s_cnt[r], 1u);
-        else atomicAdd(&cnt[r], 1ull);
+      if ((keep >> k) & 1u) {
+        tmp[t0 + total + kb + lane_prefix(m[k])] = x[k];
+        if (staged) atomicAdd(&s_cnt[r[k]], 1u);
+        else atomicAdd(&cnt[r[k]], 1ull);
       }
-      base += total;
-      __syncthreads();  // s_w is rewritten by the next step
+      total += kt;
     }
-    if (threadIdx.x == 0) tile_cnt[tile] = base;
+    (void)before;
+    if (threadIdx.x == 0) tile_cnt[tile] = total;
+    __syncthreads();  // s_cnt complete
     if (staged)
       for (uint32_t i = threadIdx.x; i < nr; i += kFlB)
         if (s_cnt[i]) atomicAdd(&cnt[r0 + i], (unsigned long long)s_cnt[i]);
-    __syncthreads();  // the LDS row tables are restaged by the next tile
+    __syncthreads();  // the LDS tables are restaged by the next tile
   }
 }
 
@@ -126,15 +156,20 @@ __global__ __launch_bounds__(kFlB) void k_flist_gather(const uint32_t *tmp, cons
 
 uint64_t flist_tiles(uint64_t EU) { return (EU + kFlTile - 1) / kFlTile; }
 
-void launch_flist_tile(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const DAdjPart &a,
+void launch_flist_prep(const uint32_t *ub, uint64_t U, const uint64_t *rp, uint64_t *deg, uint64_t *astart, hipStream_t s) {
+  hipLaunchKernelGGL(k_flist_prep, dim3(nblocks(U + 1, 256)), dim3(256), 0, s, ub, U, rp, deg, astart);
+  KCHECK("k_flist_prep");
+}
+
+void launch_flist_tile(uint64_t U, const uint64_t *doff, const uint64_t *astart, uint64_t EU, const uint32_t *col,
                        const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, uint64_t *rb,
                        int cus, hipStream_t s) {
   if (!EU || !U) return;
   const uint64_t nt = flist_tiles(EU);
   hipLaunchKernelGGL(k_flist_bounds, dim3(nblocks(nt, 256)), dim3(256), 0, s, doff, U, EU, nt, rb);
   KCHECK("k_flist_bounds");
-  hipLaunchKernelGGL(k_flist_tile, dim3((unsigned)std::min<uint64_t>(nt, (uint64_t)cus * 8)), dim3(kFlB), 0, s, ub, U,
-                     doff, EU, rb, a, filter, tmp, tile_cnt, cnt);
+  hipLaunchKernelGGL(k_flist_tile, dim3((unsigned)std::min<uint64_t>(nt, (uint64_t)cus * 8)), dim3(kFlB), 0, s, doff,
+                     astart, EU, rb, col, filter, tmp, tile_cnt, cnt);
   KCHECK("k_flist_tile");
 }
 

@@ -223,7 +223,8 @@ void launch_fill_u32(uint32_t *out, uint64_t n, uint32_t x, hipStream_t s);
 void launch_index_of(const uint32_t *sorted, uint64_t n, const uint32_t *keys, uint64_t m, uint32_t *out, hipStream_t s);
 // factor.hip: the filtered lists of a factorized hop's distinct sources (see there)
 uint64_t flist_tiles(uint64_t EU);
-void launch_flist_tile(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const DAdjPart &a,
+void launch_flist_prep(const uint32_t *ub, uint64_t U, const uint64_t *rp, uint64_t *deg, uint64_t *astart, hipStream_t s);
+void launch_flist_tile(uint64_t U, const uint64_t *doff, const uint64_t *astart, uint64_t EU, const uint32_t *col,
                        const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, uint64_t *rb,
                        int cus, hipStream_t s);
 void launch_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt, const uint64_t *tile_off, uint64_t ntiles,
