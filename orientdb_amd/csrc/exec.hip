@@ -1374,6 +1374,37 @@ class Executor {
     route_owner(st.src);
     DBuf<uint64_t> bm(&pool_, std::max<uint64_t>(nwords_, 1));
     HIP_CHECK(hipMemsetAsync(bm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+    // rows whose sources repeat (C1: every Person a root, each b reached from all its in-neighbours) mark
+    // each distinct source's neighbours once: the marked set is a union, so it is the same; E_t and the
+    // bindings stay Σ over the rows of deg(src); edges_read counts what was iterated
+    if (factor_ && R_ >= factor_min_rows_) {
+      uint64_t U = 0;
+      DBuf<uint32_t> ub;
+      {
+        DBuf<uint64_t> ubm(&pool_, std::max<uint64_t>(nwords_, 1));
+        HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+        tm_.begin("k_mark_bitmap");
+        launch_mark_bitmap(col_[st.src].p, R_, ubm.p, g_.V, s_);
+        tm_.end(4ull * R_ + 8ull * nwords_);
+        ub = bitmap_list(ubm.p, 0, 1, U);
+      }
+      const uint64_t Et = degree_sum(col_[st.src].p, R_, st.adj), EU = degree_sum(ub.p, U, st.adj);
+      if (Et >= factor_min_ratio_ * EU) {
+        ExpandOut o = expand_core(ub.p, U, st.adj, nullptr, {}, false, false, nullptr, nullptr, nullptr, nullptr, false,
+                                  bm.p);
+        edges_ += Et;
+        edges_iter_ += o.E;
+        marked_bindings_ = Et;
+        factorized_hops_++;
+        bound_[st.dst] = 1;
+        marked_ = true;
+        uint64_t m = 0;
+        col_[st.dst] = bitmap_list(bm.p, 0, 1, m);
+        R_ = m;
+        segmented_ = false;
+        return;
+      }
+    }
     ExpandOut o = expand_core(col_[st.src].p, R_, st.adj, nullptr, {}, false, false, nullptr, nullptr, nullptr, nullptr,
                               false, bm.p);
     edges_ += o.E;

@@ -295,15 +295,18 @@ MARK_QUERIES = [
 ]
 
 
+@pytest.mark.parametrize("factor", ["force", "0"])
 @pytest.mark.parametrize("heavy", ["default", "all_heavy"])
 @pytest.mark.parametrize("q", MARK_QUERIES, ids=[q[0] for q in MARK_QUERIES])
-def test_rmat_parity_marked_last_hop(rmat10, rmat10_raw, q, heavy, monkeypatch):
+def test_rmat_parity_marked_last_hop(rmat10, rmat10_raw, q, heavy, factor, monkeypatch):
     """A plan returning only its last alias, de-duplicated: the last hop marks the distinct neighbours
     as it reads them (Executor::expand_mark) — same rows, bindings and E_t as writing the rows and
     marking them in the projection (OMX_MARK_FUSE=0), on the simple graph and the multigraph."""
     import orientdb_amd as o
     if heavy == "all_heavy":
         monkeypatch.setenv("OMX_HEAVY_DEG", "2")
+    # force: each distinct source's neighbours marked once (the rows repeat their sources); 0: every row's
+    monkeypatch.setenv("OMX_FACTOR", factor)
     for g, ref in (rmat10, rmat10_raw):
         monkeypatch.setenv("OMX_MARK_FUSE", "1")
         rs = _parity(g, ref, q[1], q[2])
