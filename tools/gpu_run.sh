@@ -5,7 +5,7 @@
 #
 # Steps run in order; the first failure ends the run (no further GPU work after a fault, a time limit or
 # a crash). Every GPU step has its own time limit.
-#   tests:<pytest args, comma-separated>       e.g. tests:tests/test_gpu_gen.py  or  tests:tests,-k,c5
+#   tests:<pytest args, comma-separated>       e.g. tests:tests/test_gpu_gen.py  or  tests:tests,-k,c5+or+m1
 #   bench:<name>:<query>[:<bench args, comma-separated>][:ENV=V,ENV=V]
 #   prof:<name>:<query>[:<bench args>][:ENV=V]  rocprofv3 --kernel-trace --stats of a short bench run
 #   pmc:<name>:<query>:<timer name>:<kernel regex>[:<bench args>]  FETCH_SIZE / WRITE_SIZE / SQ passes
@@ -23,7 +23,9 @@ for step in "$@"; do
   case "$kind" in
     tests)
       log=$O/tests_$(echo "$a" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40).log
-      timeout -k 10 1100 python -u -m pytest $(commas "$a") -m gpu -x -q --timeout 300 --timeout-method thread \
+      IFS=',' read -ra targs <<< "$a"
+      targs=("${targs[@]//+/ }")  # '+' inside an argument stands for a space (-k,a+or+b)
+      timeout -k 10 1100 python -u -m pytest "${targs[@]}" -m gpu -x -q --timeout 300 --timeout-method thread \
         -p no:cacheprovider > "$log" 2>&1
       rc=$?
       tail -4 "$log"
