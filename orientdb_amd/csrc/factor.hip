@@ -25,7 +25,7 @@ namespace omx {
 
 namespace {
 
-constexpr int kFlB = 256, kFlSteps = 4, kFlTile = kFlB * kFlSteps, kFlRows = 1024;  // 20.5 KiB of LDS
+constexpr int kFlB = 256, kFlSteps = 16, kFlTile = kFlB * kFlSteps, kFlRows = 1024;  // 20.5 KiB of LDS
 
 // last r in [lo, hi] with off[r] <= e (off ascending, off[lo] <= e)
 template <class T>
@@ -62,9 +62,11 @@ __global__ void k_flist_prep(const uint32_t *ub, uint64_t U, const uint64_t *rp,
   astart[u] = s;
 }
 
+// rowv (optional): the rows' vertices; with it every survivor's row vertex is written to tmp_row too
 __global__ __launch_bounds__(kFlB) void k_flist_tile(const uint64_t *doff, const uint64_t *astart, uint64_t EU,
                                                      const uint64_t *rb, const uint32_t *col, const uint64_t *filter,
-                                                     uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt) {
+                                                     uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt,
+                                                     const uint32_t *rowv, uint32_t *tmp_row) {
   __shared__ uint64_t s_off[kFlRows + 1];  // doff of the tile's rows
   __shared__ uint64_t s_adj[kFlRows];      // col position of each row's first neighbour
   __shared__ uint32_t s_cnt[kFlRows];      // survivors per row in this tile
@@ -127,16 +129,22 @@ __global__ __launch_bounds__(kFlB) void k_flist_tile(const uint64_t *doff, const
         kt += c;
       }
       if ((keep >> k) & 1u) {
-        tmp[t0 + total + kb + lane_prefix(m[k])] = x[k];
-        if (staged) atomicAdd(&s_cnt[r[k]], 1u);
-        else atomicAdd(&cnt[r[k]], 1ull);
+        const uint64_t o = t0 + total + kb + lane_prefix(m[k]);
+        tmp[o] = x[k];
+        if (rowv) {
+          tmp_row[o] = rowv[staged ? r0 + r[k] : r[k]];
+        } else if (staged) {
+          atomicAdd(&s_cnt[r[k]], 1u);
+        } else {
+          atomicAdd(&cnt[r[k]], 1ull);
+        }
       }
       total += kt;
     }
     (void)before;
     if (threadIdx.x == 0) tile_cnt[tile] = total;
     __syncthreads();  // s_cnt complete
-    if (staged)
+    if (staged && !rowv)
       for (uint32_t i = threadIdx.x; i < nr; i += kFlB)
         if (s_cnt[i]) atomicAdd(&cnt[r0 + i], (unsigned long long)s_cnt[i]);
     __syncthreads();  // the LDS tables are restaged by the next tile
@@ -144,12 +152,33 @@ __global__ __launch_bounds__(kFlB) void k_flist_tile(const uint64_t *doff, const
 }
 
 __global__ __launch_bounds__(kFlB) void k_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt,
-                                                       const uint64_t *tile_off, uint64_t ntiles, uint32_t *out) {
+                                                       const uint64_t *tile_off, uint64_t ntiles, uint32_t *out,
+                                                       const uint32_t *tmp_row, uint32_t *out_row) {
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint32_t n = tile_cnt[tile];
     const uint64_t src = tile * kFlTile, dst = tile_off[tile];
     for (uint32_t i = threadIdx.x; i < n; i += kFlB) out[dst + i] = tmp[src + i];
+    if (tmp_row)
+      for (uint32_t i = threadIdx.x; i < n; i += kFlB) out_row[dst + i] = tmp_row[src + i];
   }
+}
+
+// reverse lists: offsets of every distinct source's group among the keys sorted ascending
+__global__ void k_flist_group_offsets(const uint32_t *keys, uint64_t n, const uint32_t *ub, uint64_t U, uint64_t *loff) {
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u > U) return;
+  if (u == U) {
+    loff[U] = n;
+    return;
+  }
+  const uint32_t b = ub[u];
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < b) lo = mid + 1;
+    else hi = mid;
+  }
+  loff[u] = lo;
 }
 
 }  // namespace
@@ -163,22 +192,28 @@ void launch_flist_prep(const uint32_t *ub, uint64_t U, const uint64_t *rp, uint6
 
 void launch_flist_tile(uint64_t U, const uint64_t *doff, const uint64_t *astart, uint64_t EU, const uint32_t *col,
                        const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, uint64_t *rb,
-                       int cus, hipStream_t s) {
+                       int cus, hipStream_t s, const uint32_t *rowv, uint32_t *tmp_row) {
   if (!EU || !U) return;
   const uint64_t nt = flist_tiles(EU);
   hipLaunchKernelGGL(k_flist_bounds, dim3(nblocks(nt, 256)), dim3(256), 0, s, doff, U, EU, nt, rb);
   KCHECK("k_flist_bounds");
   hipLaunchKernelGGL(k_flist_tile, dim3((unsigned)std::min<uint64_t>(nt, (uint64_t)cus * 8)), dim3(kFlB), 0, s, doff,
-                     astart, EU, rb, col, filter, tmp, tile_cnt, cnt);
+                     astart, EU, rb, col, filter, tmp, tile_cnt, cnt, rowv, tmp_row);
   KCHECK("k_flist_tile");
 }
 
 void launch_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt, const uint64_t *tile_off, uint64_t ntiles,
-                         uint32_t *out, int cus, hipStream_t s) {
+                         uint32_t *out, int cus, hipStream_t s, const uint32_t *tmp_row, uint32_t *out_row) {
   if (!ntiles) return;
   hipLaunchKernelGGL(k_flist_gather, dim3((unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * 8)), dim3(kFlB), 0, s, tmp,
-                     tile_cnt, tile_off, ntiles, out);
+                     tile_cnt, tile_off, ntiles, out, tmp_row, out_row);
   KCHECK("k_flist_gather");
+}
+
+void launch_flist_group_offsets(const uint32_t *keys, uint64_t n, const uint32_t *ub, uint64_t U, uint64_t *loff,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(k_flist_group_offsets, dim3(nblocks(U + 1, 256)), dim3(256), 0, s, keys, n, ub, U, loff);
+  KCHECK("k_flist_group_offsets");
 }
 
 }  // namespace omx

@@ -226,9 +226,12 @@ uint64_t flist_tiles(uint64_t EU);
 void launch_flist_prep(const uint32_t *ub, uint64_t U, const uint64_t *rp, uint64_t *deg, uint64_t *astart, hipStream_t s);
 void launch_flist_tile(uint64_t U, const uint64_t *doff, const uint64_t *astart, uint64_t EU, const uint32_t *col,
                        const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, uint64_t *rb,
-                       int cus, hipStream_t s);
+                       int cus, hipStream_t s, const uint32_t *rowv = nullptr, uint32_t *tmp_row = nullptr);
 void launch_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt, const uint64_t *tile_off, uint64_t ntiles,
-                         uint32_t *out, int cus, hipStream_t s);
+                         uint32_t *out, int cus, hipStream_t s, const uint32_t *tmp_row = nullptr,
+                         uint32_t *out_row = nullptr);
+void launch_flist_group_offsets(const uint32_t *keys, uint64_t n, const uint32_t *ub, uint64_t U, uint64_t *loff,
+                                hipStream_t s);
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
 void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor, uint32_t *out,
                         hipStream_t s);
