@@ -1513,6 +1513,43 @@ class Executor {
         tm_.begin("k_flist_gather");
         launch_flist_gather(tmp.p, tcnt.p, toff.p, nt, keys.p, cus(), s_, trow.p, vals.p);
         tm_.end(16ull * nlist + 12ull * nt);
+        edges_iter_ += ER;
+        // rows of two columns, the source and one other X (M1 / C2: (a, b)): no grouping of the pairs —
+        // the rows are grouped by source instead (R, not Σ|L|, entries sorted), and every (b, c) pair
+        // is expanded over its source's X values: the same (X, b, c) rows
+        const int other = cols.size() == 2 ? (cols[0] == st.src ? cols[1] : cols[1] == st.src ? cols[0] : -1) : -1;
+        if (other >= 0) {
+          DBuf<uint32_t> sg(&pool_, R), sx(&pool_, R), gp(&pool_, std::max<uint64_t>(nlist, 1));
+          DBuf<uint64_t> aoff(&pool_, U + 1);
+          tm_.begin("flist_row_sort");
+          cub([&](void *t, size_t &b) {
+            return hipcub::DeviceRadixSort::SortPairs(t, b, g.p, sg.p, col_[other].p, sx.p, (int64_t)R, 0,
+                                                      std::max(1, bits_for(U)), s_);
+          });
+          tm_.end(16ull * R * ((bits_for(U) + 7) / 8));
+          launch_flist_group_offsets(sg.p, R, iu.p, U, aoff.p, s_);
+          if (nlist) launch_gather_u32(pos.p, keys.p, nlist, gp.p, s_);
+          DAdj aadj{};
+          aadj.n = 1;
+          aadj.sorted = 0;
+          aadj.p[0].rp = aoff.p;
+          aadj.p[0].col = sx.p;
+          ExpandOut o = expand_core(gp.p, nlist, st.adj, nullptr, {keys.p, vals.p}, write, false, nullptr, nullptr,
+                                    nullptr, &aadj);
+          if (!o.counted_from_degrees) edges_iter_ += o.E;
+          R_ = o.n;
+          factorized_hops_++;
+          if (debug_expand_)
+            std::fprintf(stderr, "[omx factorized] pairs R=%llu U=%llu Et=%llu EU=%llu ER=%llu pairs=%llu rows=%llu\n",
+                         (unsigned long long)R, (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU,
+                         (unsigned long long)ER, (unsigned long long)nlist, (unsigned long long)o.n);
+          if (!write || R_ == 0) return true;
+          segmented_ = false;
+          col_[other] = std::move(o.dst);
+          col_[st.src] = std::move(o.carry[0]);
+          col_[st.dst] = std::move(o.carry[1]);
+          return true;
+        }
         if (nlist) {
           const int vbits = bits_for(g_.V);
           tm_.begin("flist_sort");
@@ -1522,7 +1559,6 @@ class Executor {
           tm_.end(16ull * nlist * ((vbits + 7) / 8));
         }
         launch_flist_group_offsets(skeys.p, nlist, ub.p, U, loff.p, s_);
-        edges_iter_ += ER;
       }
     }
     if (reverse) {

@@ -62,43 +62,82 @@ __global__ void k_flist_prep(const uint32_t *ub, uint64_t U, const uint64_t *rp,
   astart[u] = s;
 }
 
-// rowv (optional): the rows' vertices; with it every survivor's row vertex is written to tmp_row too
+// rowv (optional): the rows' vertices; with it every survivor's row vertex is written to tmp_row too.
+// A tile's rows are staged in LDS (col position of entry e = s_base[row] + e) and every entry finds its
+// row through s_seg: the rows mark their first entry in the tile, an inclusive max-scan spreads the mark
+// (the merge-path trick of kernels.hip k_expand; no per-entry search). A tile over more than kFlRows rows
+// (a run of short rows) searches the global offsets instead.
 __global__ __launch_bounds__(kFlB) void k_flist_tile(const uint64_t *doff, const uint64_t *astart, uint64_t EU,
                                                      const uint64_t *rb, const uint32_t *col, const uint64_t *filter,
                                                      uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt,
                                                      const uint32_t *rowv, uint32_t *tmp_row) {
-  __shared__ uint64_t s_off[kFlRows + 1];  // doff of the tile's rows
-  __shared__ uint64_t s_adj[kFlRows];      // col position of each row's first neighbour
-  __shared__ uint32_t s_cnt[kFlRows];      // survivors per row in this tile
-  __shared__ uint32_t s_w[kFlSteps][kFlB / 64];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int W = kFlB / 64, IPT = kFlSteps;
+  __shared__ uint64_t s_base[kFlRows];  // col position of a row's entry e, minus e
+  __shared__ uint32_t s_cnt[kFlRows];   // survivors per row in this tile
+  __shared__ uint16_t s_seg[kFlTile];   // tile-local row of every entry
+  __shared__ uint32_t s_w[kFlSteps][W];
+  __shared__ uint32_t s_wmax[W];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t ntiles = (EU + kFlTile - 1) / kFlTile;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * kFlTile, t1 = min(t0 + (uint64_t)kFlTile, EU) - 1;
+    const uint32_t ne = (uint32_t)(t1 - t0 + 1);
     const uint64_t r0 = rb[2 * tile], nr = rb[2 * tile + 1] - r0 + 1;
     const bool staged = nr <= kFlRows;
     if (staged) {
-      for (uint32_t i = threadIdx.x; i <= nr; i += kFlB) s_off[i] = doff[r0 + i];
-      for (uint32_t i = threadIdx.x; i < nr; i += kFlB) {
-        s_adj[i] = astart[r0 + i];
-        s_cnt[i] = 0;
+      for (uint32_t x = tid; x < ne; x += kFlB) s_seg[x] = 0;
+      __syncthreads();
+      for (uint32_t lr = tid; lr < nr; lr += kFlB) {
+        const uint64_t rs = doff[r0 + lr], re = doff[r0 + lr + 1];
+        const uint64_t st = rs > t0 ? rs - t0 : 0;
+        if (re > rs && st < ne) s_seg[st] = (uint16_t)lr;
+        s_base[lr] = astart[r0 + lr] - rs;
+        s_cnt[lr] = 0;
+      }
+      __syncthreads();
+      uint32_t vals[IPT];
+      uint32_t mx = 0;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const uint32_t idx = tid * IPT + i;
+        const uint32_t v = idx < ne ? s_seg[idx] : 0;
+        mx = mx > v ? mx : v;
+        vals[i] = mx;
+      }
+      uint32_t incl = mx;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl = incl > y ? incl : y;
+      }
+      if (lane == 63) s_wmax[wave] = incl;
+      uint32_t excl = __shfl_up(incl, 1, 64);
+      if (lane == 0) excl = 0;
+      __syncthreads();
+      uint32_t wp = 0;
+      for (uint32_t w = 0; w < wave; ++w) wp = wp > s_wmax[w] ? wp : s_wmax[w];
+      const uint32_t pre = excl > wp ? excl : wp;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const uint32_t idx = tid * IPT + i;
+        if (idx < ne) s_seg[idx] = (uint16_t)(pre > vals[i] ? pre : vals[i]);
       }
     }
     __syncthreads();
-    // every step's row, col word and probe requested before any is consumed (one latency chain per
-    // tile instead of one per step)
+    // every step's col word and probe requested before any is consumed
     uint32_t x[kFlSteps];
     uint64_t r[kFlSteps];
 #pragma unroll
     for (int k = 0; k < kFlSteps; ++k) {
-      const uint64_t e = t0 + (uint64_t)k * kFlB + threadIdx.x;
+      const uint32_t jl = (uint32_t)k * kFlB + tid;
       x[k] = 0;
       r[k] = ~0ull;
-      if (e <= t1) {
+      if (jl < ne) {
+        const uint64_t e = t0 + jl;
         uint64_t pos;
         if (staged) {
-          r[k] = last_le_range(s_off, 0, nr - 1, e);
-          pos = s_adj[r[k]] + (e - s_off[r[k]]);
+          r[k] = s_seg[jl];
+          pos = s_base[r[k]] + e;
         } else {
           r[k] = last_le_range(doff, r0, r0 + nr - 1, e);
           pos = astart[r[k]] + (e - doff[r[k]]);
