@@ -181,6 +181,7 @@ class Executor {
     }
     if (const char *fl = std::getenv("OMX_FLIST")) flist_ = std::strcmp(fl, "0") != 0;
     if (const char *fr = std::getenv("OMX_FLIST_REVERSE")) flist_reverse_ = std::strcmp(fr, "0") != 0;
+    if (const char *fp = std::getenv("OMX_FLIST_PAIRS")) flist_pairs_ = std::strcmp(fp, "0") != 0;
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
     if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
     if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
@@ -1429,8 +1430,14 @@ class Executor {
   // counts Σ_rows deg; edges_read counts what was iterated (Σ_U deg + the L entries).
   // Returns false (nothing done) when the rows repeat their sources less than kFactorMinRatio-fold.
   uint64_t factor_min_rows_ = 4096, factor_min_ratio_ = 4;
-  bool flist_ = true;  // OMX_FLIST=0: the lists through the generic filtered expansion + key grouping
+  // OMX_FLIST=1: the lists by ordered tiles (factor.hip) instead of the filtered expansion + key grouping
+  // (measured at M1: forward tiles 1.6 ms for 200 M entries, from the targets' side 0.25 ms + a 0.6 ms
+  // pair sort — no faster than the grouped path's 1.3 ms, profiles/r03/flist; kept as an option)
+  bool flist_ = false;
   bool flist_reverse_ = true;  // OMX_FLIST_REVERSE=0: never build the lists from the targets' in-rows
+  // OMX_FLIST_PAIRS=1: with the targets' side, expand the (source, target) pairs over the rows grouped by
+  // source instead of sorting the pairs (measured slower at M1: 21 M short expansions, 6.5 ms a step)
+  bool flist_pairs_ = false;
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
@@ -1517,7 +1524,7 @@ class Executor {
         // rows of two columns, the source and one other X (M1 / C2: (a, b)): no grouping of the pairs —
         // the rows are grouped by source instead (R, not Σ|L|, entries sorted), and every (b, c) pair
         // is expanded over its source's X values: the same (X, b, c) rows
-        const int other = cols.size() == 2 ? (cols[0] == st.src ? cols[1] : cols[1] == st.src ? cols[0] : -1) : -1;
+        const int other = !flist_pairs_ || cols.size() != 2 ? -1 : cols[0] == st.src ? cols[1] : cols[1] == st.src ? cols[0] : -1;
         if (other >= 0) {
           DBuf<uint32_t> sg(&pool_, R), sx(&pool_, R), gp(&pool_, std::max<uint64_t>(nlist, 1));
           DBuf<uint64_t> aoff(&pool_, U + 1);

@@ -363,7 +363,7 @@ FACTOR_IDS = ("c2_both_ends", "c1_abc", "two_cols_dedup", "in_dir", "both_dir", 
               "paths", "elements", "fof_not_me", "matched_and_filter", "optional_free", "bound_candidate")
 
 
-@pytest.mark.parametrize("flist", ["tiles", "tiles_forward", "grouped"])
+@pytest.mark.parametrize("flist", ["tiles", "tiles_forward", "tiles_pairs", "grouped"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
 def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, flist, monkeypatch):
@@ -372,11 +372,13 @@ def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, flist, monkeypatch
     multigraph, whose parallel edges repeat a neighbour in a source's list (ridbag multiplicity,
     OSBTreeRidBag.java:292-295) through the distinct-source grouping. tiles: the lists compacted in
     order by tiles of the flat entry space (factor.hip), from the targets' in-rows when that reads fewer
-    entries (then sorted by source); tiles_forward: from the sources' rows; grouped: the generic filtered
-    expansion + key histogram / scatter (OMX_FLIST=0, and every multi-part adjacency such as both())."""
+    entries (then sorted by source); tiles_forward: from the sources' rows; tiles_pairs: the (source,
+    target) pairs expanded over the rows grouped by source; grouped (the default): the generic filtered
+    expansion + key histogram / scatter (and every multi-part adjacency such as both())."""
     import orientdb_amd as o
     g, ref = rmat10 if graph == "simple" else rmat10_raw
     monkeypatch.setenv("OMX_FLIST", "0" if flist == "grouped" else "1")
+    monkeypatch.setenv("OMX_FLIST_PAIRS", "1" if flist == "tiles_pairs" else "0")
     # tiles: the lists from the targets' in-rows whenever that reads fewer entries; tiles_forward: always
     # from the sources' rows
     monkeypatch.setenv("OMX_FLIST_REVERSE", "0" if flist == "tiles_forward" else "1")
