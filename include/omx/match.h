@@ -232,6 +232,11 @@ typedef struct omx_cell {
   const char *s;  /* STRING (UTF-8), LIST / MAP (JSON)                                              */
 } omx_cell;
 int omx_result_cell(const omx_result *r, uint64_t row, int32_t col, omx_cell *out);
+/* Column `col` of a document result in bulk: types[row] = OMX_CELL_* and bits[row] = the INT / BOOL
+ * value, the DOUBLE's IEEE-754 bits or the packed RID (0 for NULL; STRING / LIST / MAP cells are read
+ * with omx_result_cell). Both arrays hold info.n_rows entries. One call per column replaces n_rows
+ * omx_result_cell calls when a host binding converts the rows (JNI: one long[] per column). */
+int omx_result_column(const omx_result *r, int32_t col, int32_t *types, uint64_t *bits);
 
 const char *omx_last_error(void);
 const char *omx_version(void);

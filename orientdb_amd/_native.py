@@ -95,6 +95,7 @@ SIGNATURES = {
                                           C.POINTER(C.c_uint64)]),
     "omx_result_free": (None, [C.c_void_p]),
     "omx_result_cell": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int32, C.POINTER(omx_cell)]),
+    "omx_result_column": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "omx_graph_create_blob": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "omx_execute_packed": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                      C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),

@@ -472,6 +472,42 @@ int omx_result_cell(const omx_result *r, uint64_t row, int32_t col, omx_cell *ou
   return OMX_OK;
 }
 
+int omx_result_column(const omx_result *r, int32_t col, int32_t *types, uint64_t *bits) {
+  if (!r || !types || !bits || col < 0) return OMX_E_INVALID;
+  if (!r->pcols.empty()) {
+    if ((size_t)col >= r->pcols.size()) return OMX_E_INVALID;
+    const omx_result::PCol &pc = r->pcols[col];
+    for (uint64_t i = 0; i < r->n_pcol_rows; ++i) {
+      switch (pc.kind[i]) {
+        case omx::PJ_K_INT: types[i] = OMX_CELL_INT; bits[i] = pc.val[i]; break;
+        case omx::PJ_K_DBL: types[i] = OMX_CELL_DOUBLE; bits[i] = pc.val[i]; break;
+        case omx::PJ_K_STR: types[i] = OMX_CELL_STRING; bits[i] = 0; break;
+        case omx::PJ_K_BOOL: types[i] = OMX_CELL_BOOL; bits[i] = pc.val[i]; break;
+        case omx::PJ_K_RID: types[i] = OMX_CELL_RID; bits[i] = pc.val[i]; break;
+        default: types[i] = OMX_CELL_NULL; bits[i] = 0; break;
+      }
+    }
+    return OMX_OK;
+  }
+  if (!r->docs.empty() && (size_t)col >= r->docs[0].size()) return OMX_E_INVALID;
+  for (size_t i = 0; i < r->docs.size(); ++i) {
+    if ((size_t)col >= r->docs[i].size()) return OMX_E_INVALID;
+    const omx::HVal &v = r->docs[i][col];
+    bits[i] = 0;
+    switch (v.k) {
+      case omx::HVal::NUL: types[i] = OMX_CELL_NULL; break;
+      case omx::HVal::INT: types[i] = OMX_CELL_INT; bits[i] = (uint64_t)v.i; break;
+      case omx::HVal::DBL: types[i] = OMX_CELL_DOUBLE; std::memcpy(&bits[i], &v.d, 8); break;
+      case omx::HVal::STR: types[i] = OMX_CELL_STRING; break;
+      case omx::HVal::BOOL: types[i] = OMX_CELL_BOOL; bits[i] = (uint64_t)v.i; break;
+      case omx::HVal::RID: types[i] = OMX_CELL_RID; bits[i] = v.rid; break;
+      case omx::HVal::LIST: types[i] = OMX_CELL_LIST; break;
+      case omx::HVal::MAP: types[i] = OMX_CELL_MAP; break;
+    }
+  }
+  return OMX_OK;
+}
+
 int omx_ridbag_decode_csr(int32_t device, const uint8_t *streams, uint64_t stream_bytes, const uint64_t *offsets,
                           uint32_t n_vertices, const uint64_t *vertex_rids, const uint64_t *edge_rids,
                           const uint64_t *edge_targets, uint64_t n_edge_records, uint64_t *row_ptr, uint32_t *col,

@@ -74,6 +74,7 @@ class OResultSet(list):
     kernel_launches = None
     columns = None
     rows = None  # numpy u64 [n, k] of packed RIDs
+    cells = None  # document results: {column: (OMX_CELL_* int32 [n], value bits u64 [n])}
 
 
 def _values(args, named):
@@ -130,6 +131,33 @@ def _cell_value(cell):
     if t == N.OMX_CELL_RID:
         return ORecordId.from_packed(cell.rid)
     return _json_value(json.loads(cell.s.decode("utf-8")))
+
+
+def _column_values(r, c, types, bits):
+    """One result column (omx_result_column's types / bits) as ODocument field values; strings, lists
+    and maps come through omx_result_cell."""
+    out = [None] * len(types)
+    ints, dbls = bits.view(np.int64), bits.view(np.float64)
+    for t in np.unique(types).tolist():
+        idx = np.flatnonzero(types == t)
+        if t == N.OMX_CELL_NULL:
+            continue
+        if t == N.OMX_CELL_INT:
+            vs = ints[idx].tolist()
+        elif t == N.OMX_CELL_DOUBLE:
+            vs = dbls[idx].tolist()
+        elif t == N.OMX_CELL_BOOL:
+            vs = [bool(x) for x in ints[idx].tolist()]
+        elif t == N.OMX_CELL_RID:
+            vs = [ORecordId.from_packed(x) for x in bits[idx].tolist()]
+        else:
+            cell, vs = N.omx_cell(), []
+            for i in idx.tolist():
+                N.check(N.lib().omx_result_cell(r, i, c, C.byref(cell)))
+                vs.append(_cell_value(cell))
+        for i, v in zip(idx.tolist(), vs):
+            out[i] = v
+    return out
 
 
 class OMatchStatement:
@@ -220,15 +248,16 @@ class OMatchStatement:
             i += 1
         rs.kernel_launches = launches
         nrows, ncols = info.n_rows, info.n_cols
-        if info.documents:  # RETURN expressions / JSON: one document per row (omx_result_cell)
+        if info.documents:  # RETURN expressions / JSON: one document per row, read column by column
             rs.rows = np.zeros((0, 0), np.uint64)
-            cell = N.omx_cell()
-            for i in range(nrows):
-                doc = ODocument()
-                for c, name in enumerate(cols):
-                    N.check(L.omx_result_cell(r, i, c, C.byref(cell)))
-                    doc[name] = _cell_value(cell)
-                rs.append(doc)
+            rs.cells = {}
+            for c, name in enumerate(cols):
+                types, bits = np.empty(nrows, np.int32), np.empty(nrows, np.uint64)
+                N.check(L.omx_result_column(r, c, types.ctypes.data_as(C.c_void_p), bits.ctypes.data_as(C.c_void_p)))
+                rs.cells[name] = (types, bits)
+            if documents and nrows:
+                vals = [_column_values(r, c, *rs.cells[name]) for c, name in enumerate(cols)]
+                rs.extend(ODocument(zip(cols, row)) for row in zip(*vals))
             return rs
         p = L.omx_result_rows(r)
         if p and nrows and ncols:

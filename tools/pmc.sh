@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 i=0
 for pmc in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU" \
-           "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum"; do
+           "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -s KILL 300 rocprofv3 --pmc $pmc --kernel-include-regex "$K" -d "$OUT/p$i" -o pmc --output-format csv \
     -- python3 bench.py --no-cpu-baseline "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
