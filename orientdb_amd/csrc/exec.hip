@@ -30,6 +30,9 @@ namespace {
 struct CastU64 {
   __host__ __device__ uint64_t operator()(const uint32_t &x) const { return x; }
 };
+struct NonZeroU64 {
+  __host__ __device__ uint8_t operator()(const uint64_t &x) const { return x != 0; }
+};
 
 class Timer {
  public:
@@ -46,7 +49,7 @@ class Timer {
     static const char *const kHot[] = {"k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light",
                                        "k_expand_light_sliced", "k_expand_light_check", "k_expand_heavy_check",
                                        "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit", "k_bfs_push",
-                                       "k_bfs_emit", "k_trav_filter", "trav_select", "k_flist_tile"};
+                                       "k_bfs_emit", "k_trav_filter", "trav_select", "k_flist_tile", "k_femit"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
     return false;
@@ -182,6 +185,9 @@ class Executor {
     if (const char *fl = std::getenv("OMX_FLIST")) flist_ = std::strcmp(fl, "0") != 0;
     if (const char *fr = std::getenv("OMX_FLIST_REVERSE")) flist_reverse_ = std::strcmp(fr, "0") != 0;
     if (const char *fp = std::getenv("OMX_FLIST_PAIRS")) flist_pairs_ = std::strcmp(fp, "0") != 0;
+    if (const char *fe = std::getenv("OMX_FEMIT")) femit_ = std::strcmp(fe, "0") != 0;
+    if (const char *fs = std::getenv("OMX_FEMIT_SORT")) femit_sort_ = std::strcmp(fs, "0") != 0;
+    if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
     if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
     if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
@@ -1438,6 +1444,103 @@ class Executor {
   // OMX_FLIST_PAIRS=1: with the targets' side, expand the (source, target) pairs over the rows grouped by
   // source instead of sorting the pairs (measured slower at M1: 21 M short expansions, 6.5 ms a step)
   bool flist_pairs_ = false;
+  // OMX_FEMIT=0: write the rows with the generic unfiltered expansion (binned heavy / merge-path rows)
+  // instead of k_femit's output tiles; OMX_FEMIT_SORT=0: keep the rows in their order (the lists are then
+  // re-read from HBM / MALL rather than L2)
+  bool femit_ = true, femit_sort_ = true;
+  bool femit_slow_ = false;  // OMX_FEMIT_SLOW=1: every output tile through k_femit_slow (tests)
+
+  // step 4 of expand_factorized when the rows are written: the output space Σ_rows |L(g[r])| is laid out
+  // row by row and written by tiles of output rows (factor.hip k_femit)
+  void emit_factorized(DBuf<uint32_t> &g, uint64_t R, uint64_t U, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol,
+                       const std::vector<int> &cols, const Step &st) {
+    // 1. the rows whose list is not empty (the others write nothing), in row order or grouped by source
+    DBuf<uint64_t> len(&pool_, R + 1);
+    launch_femit_len(g.p, R, loff.p, len.p, s_);
+    DBuf<uint32_t> idx(&pool_, R);
+    DBuf<uint64_t> nsel(&pool_, 1);
+    {
+      hipcub::CountingInputIterator<uint32_t> cnt(0);
+      hipcub::TransformInputIterator<uint8_t, NonZeroU64, const uint64_t *> fl(len.p, NonZeroU64());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cnt, fl, idx.p, nsel.p, (int64_t)R, s_); });
+    }
+    const uint64_t Rn = read1(nsel.p);
+    DBuf<uint32_t> gs(&pool_, std::max<uint64_t>(Rn, 1)), perm;
+    if (femit_sort_ && Rn > 1) {  // grouped by source: a list is re-read from L2 by its rows
+      DBuf<uint32_t> gk(&pool_, Rn);
+      perm = DBuf<uint32_t>(&pool_, Rn);
+      launch_gather_u32(g.p, idx.p, Rn, gk.p, s_);
+      tm_.begin("femit_row_sort");
+      cub([&](void *t, size_t &b) {
+        return hipcub::DeviceRadixSort::SortPairs(t, b, gk.p, gs.p, idx.p, perm.p, (int64_t)Rn, 0,
+                                                  std::max(1, bits_for(U)), s_);
+      });
+      tm_.end(16ull * Rn * ((bits_for(U) + 7) / 8));
+    } else {
+      if (Rn) launch_gather_u32(g.p, idx.p, Rn, gs.p, s_);
+      perm = std::move(idx);
+    }
+    std::vector<DBuf<uint32_t>> sc;
+    for (int c : cols) {
+      sc.emplace_back(&pool_, std::max<uint64_t>(Rn, 1));
+      if (Rn) launch_gather_u32(col_[c].p, perm.p, Rn, sc.back().p, s_);
+    }
+    // 2. output rows of every binding row: the scan of its list length; list position of output o
+    DBuf<uint64_t> roff(&pool_, Rn + 1), rbase(&pool_, std::max<uint64_t>(Rn, 1));
+    launch_femit_len(gs.p, Rn, loff.p, len.p, s_);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, len.p, roff.p, (int64_t)(Rn + 1), s_); });
+    if (Rn) launch_femit_base(gs.p, Rn, loff.p, roff.p, rbase.p, s_);
+    const uint64_t N = read1(roff.p + Rn);
+    edges_iter_ += N;
+    alg_bytes_ += 8ull * R + 4ull * N * (cols.size() + 2);  // as expand_core's unfiltered written hop
+    R_ = N;
+    factorized_hops_++;
+    if (debug_expand_)
+      std::fprintf(stderr, "[omx factorized] emission R=%llu (non-empty %llu) U=%llu rows=%llu sorted=%d\n",
+                   (unsigned long long)R, (unsigned long long)Rn, (unsigned long long)U, (unsigned long long)N,
+                   (int)femit_sort_);
+    if (N == 0) return;
+    // 3. the output tiles (factor.hip k_femit_w)
+    FemitArgs a{};
+    a.g = gs.p;
+    a.roff = roff.p;
+    a.rbase = rbase.p;
+    a.loff = loff.p;
+    a.lcol = lcol.p;
+    a.R = Rn;
+    a.N = N;
+    a.nc = (int32_t)cols.size();
+    std::vector<DBuf<uint32_t>> outc;
+    for (size_t c = 0; c < cols.size(); ++c) {
+      outc.emplace_back(&pool_, N);
+      a.cin[c] = sc[c].p;
+      a.cout[c] = outc.back().p;
+    }
+    DBuf<uint32_t> dst(&pool_, N);
+    a.dst = dst.p;
+    const uint64_t nt = femit_tiles(N);
+    if (nt > 0xFFFFFFFFull) unsupported("a factorized emission of 2^42 or more rows");
+    // regular tiles (full, ≤ 64 binding rows) → k_femit_w; the others → k_femit_slow
+    DBuf<uint64_t> rb(&pool_, 2 * nt), nreg(&pool_, 1);
+    DBuf<uint8_t> reg(&pool_, nt);
+    DBuf<uint32_t> lists(&pool_, nt);
+    a.rb = rb.p;
+    launch_femit_bounds(a, rb.p, reg.p, femit_slow_, s_);
+    hipcub::CountingInputIterator<uint32_t> it(0);
+    cub([&](void *t, size_t &b) { return hipcub::DevicePartition::Flagged(t, b, it, reg.p, lists.p, nreg.p, (int64_t)nt, s_); });
+    const uint64_t nr = read1(nreg.p);
+    if (debug_expand_)
+      std::fprintf(stderr, "[omx factorized] emission tiles %llu: regular %llu, other %llu\n", (unsigned long long)nt,
+                   (unsigned long long)nr, (unsigned long long)(nt - nr));
+    tm_.begin("k_femit");
+    launch_femit(a, lists.p, nr, lists.p + nr, nt - nr, cus(), s_);
+    // list entry read + every column written per output row; per binding row its offsets and carries
+    tm_.end(N * (4ull + 4ull * (cols.size() + 1)) + Rn * (24ull + 4ull * cols.size()));
+    segmented_ = false;
+    for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(outc[i]);
+    col_[st.dst] = std::move(dst);
+  }
+
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
@@ -1617,6 +1720,10 @@ class Executor {
     }
     }
     // 4. the rows over their sources' lists
+    if (write && femit_ && cols.size() <= (size_t)kFemitCols) {
+      emit_factorized(g, R, U, loff, lcol, cols, st);
+      return true;
+    }
     DAdj ladj{};
     ladj.n = 1;
     ladj.sorted = 0;

@@ -232,6 +232,32 @@ void launch_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt, const ui
                          uint32_t *out_row = nullptr);
 void launch_flist_group_offsets(const uint32_t *keys, uint64_t n, const uint32_t *ub, uint64_t U, uint64_t *loff,
                                 hipStream_t s);
+// factor.hip: the factorized hop's rows written over their sources' lists, by tiles of the output space
+constexpr int kFemitCols = 4;  // carried columns of k_femit_w (more: the generic expansion writes the rows)
+struct FemitArgs {
+  const uint32_t *g;     // [R] binding row → distinct source index
+  const uint64_t *roff;  // [R+1] first output row of every binding row (scan of its list length)
+  const uint64_t *loff;  // [U+1] list offsets
+  const uint32_t *lcol;  // list entries (the new column's values)
+  const uint64_t *rbase; // [R] loff[g[r]] − roff[r]: list position of output row o of row r is rbase[r] + o
+  const uint64_t *rb;    // [2·tiles] first / last binding row of every output tile (launch_femit_bounds)
+  uint64_t R, N;         // binding rows (every list non-empty), output rows
+  int32_t nc;
+  const uint32_t *cin[kFemitCols];
+  uint32_t *cout[kFemitCols];
+  uint32_t *dst;
+};
+uint64_t femit_tiles(uint64_t N);
+// len[r] = |L(g[r])| for r < R, len[R] = 0
+void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s);
+void launch_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, const uint64_t *roff, uint64_t *rbase,
+                       hipStream_t s);
+// rb[2·femit_tiles(N)]: first / last binding row of every output tile; regular[t] = the tile is full and
+// spans at most 64 binding rows (slow_all: none is)
+void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, bool slow_all, hipStream_t s);
+// a.rb set: the regular tiles through k_femit_w, the others through k_femit_slow
+void launch_femit(const FemitArgs &a, const uint32_t *regular_tiles, uint64_t nreg, const uint32_t *other_tiles,
+                  uint64_t nother, int cus, hipStream_t s);
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
 void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor, uint32_t *out,
                         hipStream_t s);

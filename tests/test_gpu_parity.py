@@ -391,6 +391,50 @@ def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, flist, monkeypatch
     assert rs.info["bindings"] == direct.info["bindings"]
 
 
+@pytest.mark.parametrize("emit", ["binned", "unsorted", "slow"])
+@pytest.mark.parametrize("graph", ["simple", "multigraph"])
+@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
+def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, monkeypatch):
+    """The factorized hop's rows written every way (the default — rows grouped by source, output tiles of
+    k_femit_w — is covered by test_rmat_parity_factorized): binned = the generic unfiltered expansion over
+    the lists (OMX_FEMIT=0); unsorted = the rows in their order; slow = every output tile through
+    k_femit_slow (a search of the row offsets per output row). Same rows, E_t and bindings as the direct
+    expansion (P/OMatchStatement.java:491-497 per row)."""
+    import orientdb_amd as o
+    g, ref = rmat10 if graph == "simple" else rmat10_raw
+    monkeypatch.setenv("OMX_FACTOR", "0")
+    direct = o.OMatchStatement(q[1]).execute(g, documents=False)
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    monkeypatch.setenv("OMX_FEMIT", "0" if emit == "binned" else "1")
+    monkeypatch.setenv("OMX_FEMIT_SORT", "0" if emit == "unsorted" else "1")
+    monkeypatch.setenv("OMX_FEMIT_SLOW", "1" if emit == "slow" else "0")
+    rs = _parity(g, ref, q[1], q[2])
+    assert rs.info["edges_traversed"] == direct.info["edges_traversed"]
+    assert rs.info["bindings"] == direct.info["bindings"]
+
+
+@pytest.mark.parametrize("slow", ["0", "1"])
+@pytest.mark.parametrize("sort", ["0", "1"])
+def test_factorized_emission_many_tiles_rmat16(rmat16, slow, sort, monkeypatch):
+    """Output tiles of the factorized emission across many tiles (RMAT-16 2-hop with WHERE on both ends:
+    rows spanning tile boundaries, runs of short lists in one tile, a partial last tile): rows and digest
+    equal with the emission through the generic expansion."""
+    import orientdb_amd as o
+    g = rmat16[0]
+    q = "MATCH {class:Person,as:a,where:(age < 20)}-Knows->{as:b}-Knows->{as:c,where:(age >= 60)} RETURN a,b,c"
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    monkeypatch.setenv("OMX_FEMIT", "0")
+    fl = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST
+    base = o.OMatchStatement(q).execute(g, documents=False, flags=fl)
+    monkeypatch.setenv("OMX_FEMIT", "1")
+    monkeypatch.setenv("OMX_FEMIT_SORT", sort)
+    monkeypatch.setenv("OMX_FEMIT_SLOW", slow)
+    rs = o.OMatchStatement(q).execute(g, documents=False, flags=fl)
+    assert rs.info["factorized_hops"] >= 1 and rs.info["n_rows"] > 100000
+    assert rs.info["n_rows"] == base.info["n_rows"] and rs.info["digest"] == base.info["digest"]
+    assert rs.info["edges_traversed"] == base.info["edges_traversed"]
+
+
 @pytest.mark.parametrize("simple", [True, False], ids=["simple", "multigraph"])
 def test_factorized_auto_threshold_rmat14(simple):
     """The factorized expansion as the planner picks it by itself (≥ 4096 rows whose sources repeat ≥ 4×,
