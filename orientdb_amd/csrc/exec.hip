@@ -188,6 +188,8 @@ class Executor {
     if (const char *fe = std::getenv("OMX_FEMIT")) femit_ = std::strcmp(fe, "0") != 0;
     if (const char *fs = std::getenv("OMX_FEMIT_SORT")) femit_sort_ = std::strcmp(fs, "0") != 0;
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
+    if (const char *fv = std::getenv("OMX_FEMIT_REVERSE"))
+      femit_reverse_ = std::strcmp(fv, "force") == 0 ? 2 : std::strcmp(fv, "0") != 0 ? 1 : 0;
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
     if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
     if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
@@ -1500,15 +1502,19 @@ class Executor {
                    (unsigned long long)R, (unsigned long long)Rn, (unsigned long long)U, (unsigned long long)N,
                    (int)femit_sort_);
     if (N == 0) return;
-    // 3. the output tiles (factor.hip k_femit_w)
+    // 3. the output tiles (factor.hip k_femit_w): the rows' list entries → the new column, their
+    // carried values → their columns
     FemitArgs a{};
     a.g = gs.p;
     a.roff = roff.p;
     a.rbase = rbase.p;
     a.loff = loff.p;
-    a.lcol = lcol.p;
     a.R = Rn;
     a.N = N;
+    a.nl = 1;
+    a.lcol[0] = lcol.p;
+    DBuf<uint32_t> dst(&pool_, N);
+    a.lout[0] = dst.p;
     a.nc = (int32_t)cols.size();
     std::vector<DBuf<uint32_t>> outc;
     for (size_t c = 0; c < cols.size(); ++c) {
@@ -1516,11 +1522,17 @@ class Executor {
       a.cin[c] = sc[c].p;
       a.cout[c] = outc.back().p;
     }
-    DBuf<uint32_t> dst(&pool_, N);
-    a.dst = dst.p;
-    const uint64_t nt = femit_tiles(N);
+    femit_run(a);
+    segmented_ = false;
+    for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(outc[i]);
+    col_[st.dst] = std::move(dst);
+  }
+
+  // the output tiles of a factorized emission (a's rows, offsets, lists and columns set): regular tiles
+  // (full, ≤ 64 binding rows) through k_femit_w, the others through k_femit_slow
+  void femit_run(FemitArgs &a) {
+    const uint64_t nt = femit_tiles(a.N);
     if (nt > 0xFFFFFFFFull) unsupported("a factorized emission of 2^42 or more rows");
-    // regular tiles (full, ≤ 64 binding rows) → k_femit_w; the others → k_femit_slow
     DBuf<uint64_t> rb(&pool_, 2 * nt), nreg(&pool_, 1);
     DBuf<uint8_t> reg(&pool_, nt);
     DBuf<uint32_t> lists(&pool_, nt);
@@ -1534,11 +1546,118 @@ class Executor {
                    (unsigned long long)nr, (unsigned long long)(nt - nr));
     tm_.begin("k_femit");
     launch_femit(a, lists.p, nr, lists.p + nr, nt - nr, cus(), s_);
-    // list entry read + every column written per output row; per binding row its offsets and carries
-    tm_.end(N * (4ull + 4ull * (cols.size() + 1)) + Rn * (24ull + 4ull * cols.size()));
+    // every list column read and every column written per output row; per binding row its offsets and
+    // constants
+    tm_.end(a.N * 4ull * (2ull * a.nl + a.nc) + a.R * (24ull + 4ull * a.nc));
+  }
+
+  // The factorized hop from the targets' side, written without building the lists: for every target c
+  // passing the hop's filter, its in-neighbours b that are distinct sources give the (b, c) pairs (Σ
+  // indeg(C) entries read instead of Σ deg(U): M1's 10 % target window, 26 M against 200 M); the rows are
+  // grouped by source, and each pair writes the rows of its source's group with b and c — the same
+  // multiset of (…, b, c) rows as the rows over L(b) (a parallel edge b → c is one pair per edge, as it is
+  // one list entry). One GPU, a single-part adjacency, 2…4 carried columns. Returns false (nothing done)
+  // when the targets' side reads more than half the sources' entries.
+  // OMX_FEMIT_REVERSE=1: the targets' side when it reads fewer than half the sources' entries; =force:
+  // whenever it applies (tests). Off by default: at M1 it reads 26 M entries instead of 200 M and skips
+  // the lists (1.1 ms), but its pairs come in target order, so each re-reads its source's rows from MALL
+  // rather than L2, and the emission takes 2.93 instead of 2.15 ms: 5.22 against 4.35 ms per step
+  // (profiles/r03/femit/reverse.txt)
+  int femit_reverse_ = 0;
+  bool emit_factorized_reverse(const Step &st, const std::vector<int> &cols, DBuf<uint32_t> &g, uint64_t R,
+                               uint64_t U, const DBuf<uint64_t> &ubm, const DBuf<uint32_t> &iu,
+                               const DBuf<uint32_t> &pos, uint64_t EU) {
+    AdjSpec rs = st.adj;
+    rs.parts[0].second ^= 1;
+    const DAdj ra = make_adj(rs);
+    uint64_t nc = 0;
+    DBuf<uint32_t> cl = bitmap_list(bitmap(st.filter_bm), 0, 1, nc);
+    DBuf<uint64_t> cdeg(&pool_, nc + 1), cdoff(&pool_, nc + 1), castart(&pool_, std::max<uint64_t>(nc, 1));
+    launch_flist_prep(cl.p, nc, ra.p[0].rp, cdeg.p, castart.p, s_);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, cdeg.p, cdoff.p, (int64_t)(nc + 1), s_); });
+    const uint64_t ER = read1(cdoff.p + nc);
+    if (ER * 2 >= EU && femit_reverse_ < 2) return false;
+    // 1. the (b, c) pairs: the targets' in-entries whose neighbour is a distinct source
+    const uint64_t nt = flist_tiles(ER);
+    DBuf<uint32_t> tmp(&pool_, std::max<uint64_t>(ER, 1)), trow(&pool_, std::max<uint64_t>(ER, 1)), tcnt(&pool_, nt + 1);
+    DBuf<uint64_t> toff(&pool_, nt + 1), rb(&pool_, 2 * nt + 2);
+    DBuf<unsigned long long> unused(&pool_, 1);
+    HIP_CHECK(hipMemsetAsync(tcnt.p + nt, 0, 4, s_));
+    tm_.begin("k_flist_tile");
+    launch_flist_tile(nc, cdoff.p, castart.p, ER, ra.p[0].col, ubm.p, tmp.p, tcnt.p, unused.p, rb.p, cus(), s_, cl.p, trow.p);
+    tm_.end(4ull * ER + 24ull * nc + 8ull * nt);
+    const size_t rec = tm_.last();
+    hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> tc(tcnt.p, CastU64());
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tc, toff.p, (int64_t)(nt + 1), s_); });
+    const uint64_t np = read1(toff.p + nt);
+    tm_.amend_at(rec, 4ull * ER + 24ull * nc + 8ull * nt + 8ull * np);
+    edges_iter_ += ER;
+    DBuf<uint32_t> pb(&pool_, std::max<uint64_t>(np, 1)), pc(&pool_, std::max<uint64_t>(np, 1));
+    tm_.begin("k_flist_gather");
+    launch_flist_gather(tmp.p, tcnt.p, toff.p, nt, pb.p, cus(), s_, trow.p, pc.p);
+    tm_.end(16ull * np + 12ull * nt);
+    // 2. the rows grouped by source: aoff[u] = first row of u's group; the other carried columns sorted
+    DBuf<uint32_t> sg(&pool_, R), perm(&pool_, R), idx(&pool_, R);
+    launch_iota(idx.p, R, s_);
+    tm_.begin("femit_row_sort");
+    cub([&](void *t, size_t &b) {
+      return hipcub::DeviceRadixSort::SortPairs(t, b, g.p, sg.p, idx.p, perm.p, (int64_t)R, 0, std::max(1, bits_for(U)), s_);
+    });
+    tm_.end(16ull * R * ((bits_for(U) + 7) / 8));
+    DBuf<uint64_t> aoff(&pool_, U + 1);
+    launch_flist_group_offsets(sg.p, R, iu.p, U, aoff.p, s_);
+    std::vector<int> other;
+    for (int c : cols)
+      if (c != st.src) other.push_back(c);
+    std::vector<DBuf<uint32_t>> sc;
+    for (int c : other) {
+      sc.emplace_back(&pool_, R);
+      launch_gather_u32(col_[c].p, perm.p, R, sc.back().p, s_);
+    }
+    // 3. every pair's group, its output rows (the scan of the group sizes) and list base
+    DBuf<uint32_t> pu(&pool_, std::max<uint64_t>(np, 1));
+    if (np) launch_gather_u32(pos.p, pb.p, np, pu.p, s_);
+    DBuf<uint64_t> len(&pool_, np + 1), roff(&pool_, np + 1), rbase(&pool_, std::max<uint64_t>(np, 1));
+    launch_femit_len(pu.p, np, aoff.p, len.p, s_);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, len.p, roff.p, (int64_t)(np + 1), s_); });
+    if (np) launch_femit_base(pu.p, np, aoff.p, roff.p, rbase.p, s_);
+    const uint64_t N = read1(roff.p + np);
+    edges_iter_ += N;
+    alg_bytes_ += 8ull * R + 4ull * N * (cols.size() + 2);  // as expand_core's unfiltered written hop
+    R_ = N;
+    factorized_hops_++;
+    if (debug_expand_)
+      std::fprintf(stderr, "[omx factorized] targets' side: R=%llu U=%llu targets=%llu ER=%llu pairs=%llu rows=%llu\n",
+                   (unsigned long long)R, (unsigned long long)U, (unsigned long long)nc, (unsigned long long)ER,
+                   (unsigned long long)np, (unsigned long long)N);
+    if (N == 0) return true;
+    // 4. the output tiles: the group rows' other columns, the pair's b and c
+    FemitArgs a{};
+    a.g = pu.p;
+    a.roff = roff.p;
+    a.rbase = rbase.p;
+    a.loff = aoff.p;
+    a.R = np;
+    a.N = N;
+    a.nl = (int32_t)other.size();
+    std::vector<DBuf<uint32_t>> lo;
+    for (size_t m = 0; m < other.size(); ++m) {
+      lo.emplace_back(&pool_, N);
+      a.lcol[m] = sc[m].p;
+      a.lout[m] = lo.back().p;
+    }
+    a.nc = 2;
+    DBuf<uint32_t> ob(&pool_, N), oc(&pool_, N);
+    a.cin[0] = pb.p;
+    a.cout[0] = ob.p;
+    a.cin[1] = pc.p;
+    a.cout[1] = oc.p;
+    femit_run(a);
     segmented_ = false;
-    for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(outc[i]);
-    col_[st.dst] = std::move(dst);
+    for (size_t m = 0; m < other.size(); ++m) col_[other[m]] = std::move(lo[m]);
+    col_[st.src] = std::move(ob);
+    col_[st.dst] = std::move(oc);
+    return true;
   }
 
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
@@ -1580,6 +1699,9 @@ class Executor {
     tm_.begin("k_gather_u32");
     launch_gather_u32(pos.p, src, R, g.p, s_);
     tm_.end(12ull * R);
+    if (write && femit_ && femit_reverse_ && !dist_ && st.adj.parts.size() == 1 && cols.size() >= 2 &&
+        femit_supported((int)cols.size() - 1, 2) && emit_factorized_reverse(st, cols, g, R, U, ubm, iu, pos, EU))
+      return true;
     DBuf<unsigned long long> cnt(&pool_, U + 1);
     DBuf<uint64_t> loff(&pool_, U + 1);
     HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));

@@ -281,7 +281,7 @@ struct EwRows {  // lane k: binding row r0 + k of the tile, as loaded (put into 
 };
 
 // tiles and rb are read with scalar loads: __restrict__ lets the compiler prove nothing here writes them
-template <int NC>
+template <int NL, int NC>
 __device__ __forceinline__ EwRows ew_rows(const FemitArgs &a, const uint32_t *__restrict__ tiles,
                                           const uint64_t *__restrict__ rb, uint64_t i, uint32_t lane) {
   EwRows w;
@@ -296,15 +296,15 @@ __device__ __forceinline__ EwRows ew_rows(const FemitArgs &a, const uint32_t *__
   return w;
 }
 
-template <int NC>
+template <int NL, int NC>
 struct EwTable {
   uint32_t mk[kEwTile / 4];  // kEwTile u8: the table entry of every output row of the tile
   uint64_t base[64];
   uint32_t car[NC > 0 ? NC : 1][64];
 };
 
-template <int NC>
-__device__ __forceinline__ void ew_put(EwTable<NC> &tb, const EwRows &w, uint32_t lane) {
+template <int NL, int NC>
+__device__ __forceinline__ void ew_put(EwTable<NL, NC> &tb, const EwRows &w, uint32_t lane) {
   constexpr int BPL = kEwTile / 64;  // mark bytes per lane
   const uint64_t t0 = w.t * kEwTile;
   uint32_t *mk = tb.mk + lane * (BPL / 4);
@@ -347,49 +347,52 @@ __device__ __forceinline__ void ew_put(EwTable<NC> &tb, const EwRows &w, uint32_
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int NC>
-__device__ __forceinline__ void ew_resolve(const FemitArgs &a, const EwTable<NC> &tb, uint64_t t, uint32_t lane,
-                                           uint32_t (&x)[kEwJ]) {
+template <int NL, int NC>
+__device__ __forceinline__ void ew_resolve(const FemitArgs &a, const EwTable<NL, NC> &tb, uint64_t t, uint32_t lane,
+                                           uint32_t (&x)[NL][kEwJ]) {
   const uint64_t t0 = t * kEwTile;
   const uint8_t *mk = reinterpret_cast<const uint8_t *>(tb.mk);
 #pragma unroll
   for (int j = 0; j < kEwJ; ++j) {
     const uint32_t o = 64 * j + lane;
-    x[j] = a.lcol[tb.base[mk[o]] + t0 + o];
+    const uint64_t p = tb.base[mk[o]] + t0 + o;
+#pragma unroll
+    for (int m = 0; m < NL; ++m) x[m][j] = a.lcol[m][p];
   }
 }
 
-template <int NC>
-__device__ __forceinline__ void ew_store(const FemitArgs &a, const EwTable<NC> &tb, uint64_t t, uint32_t lane,
-                                         const uint32_t (&x)[kEwJ]) {
+template <int NL, int NC>
+__device__ __forceinline__ void ew_store(const FemitArgs &a, const EwTable<NL, NC> &tb, uint64_t t, uint32_t lane,
+                                         const uint32_t (&x)[NL][kEwJ]) {
   const uint64_t t0 = t * kEwTile;
   const uint8_t *mk = reinterpret_cast<const uint8_t *>(tb.mk);
 #pragma unroll
   for (int j = 0; j < kEwJ; ++j) {
     const uint32_t o = 64 * j + lane, k = mk[o];
-    a.dst[t0 + o] = x[j];
+#pragma unroll
+    for (int m = 0; m < NL; ++m) a.lout[m][t0 + o] = x[m][j];
 #pragma unroll
     for (int c = 0; c < NC; ++c) a.cout[c][t0 + o] = tb.car[c][k];
   }
 }
 
 // tiles: the regular tiles, n of them
-template <int NC>
+template <int NL, int NC>
 __global__ __launch_bounds__(64 * kEwWaves) void k_femit_w(FemitArgs a, const uint32_t *__restrict__ tiles,
                                                           const uint64_t *__restrict__ rb, uint64_t n) {
-  __shared__ EwTable<NC> s_tb[kEwWaves][2];
+  __shared__ EwTable<NL, NC> s_tb[kEwWaves][2];
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t W = (uint64_t)gridDim.x * kEwWaves;
   uint64_t i = (uint64_t)blockIdx.x * kEwWaves + wv;
   if (i >= n) return;
   // prologue: tile i's table and list entries, tile i + W's rows (indices past the end are clamped:
   // loaded, never stored)
-  EwRows r0 = ew_rows<NC>(a, tiles, rb, i, lane), r1;
-  ew_put<NC>(s_tb[wv][0], r0, lane);
-  uint32_t x0[kEwJ], x1[kEwJ];
-  ew_resolve<NC>(a, s_tb[wv][0], r0.t, lane, x0);
+  EwRows r0 = ew_rows<NL, NC>(a, tiles, rb, i, lane), r1;
+  ew_put<NL, NC>(s_tb[wv][0], r0, lane);
+  uint32_t x0[NL][kEwJ], x1[NL][kEwJ];
+  ew_resolve<NL, NC>(a, s_tb[wv][0], r0.t, lane, x0);
   uint64_t t_cur = r0.t;
-  r0 = ew_rows<NC>(a, tiles, rb, min(i + W, n - 1), lane);
+  r0 = ew_rows<NL, NC>(a, tiles, rb, min(i + W, n - 1), lane);
   // drain the prologue: the loop's entry then has nothing outstanding, so the waits the compiler places
   // at its head are those of the back edge, not vmcnt(0)
   __builtin_amdgcn_s_waitcnt(0);
@@ -398,10 +401,10 @@ __global__ __launch_bounds__(64 * kEwWaves) void k_femit_w(FemitArgs a, const ui
   // copied (a copy would wait for its loads)
 #define OMX_EW_STEP(rp, rn, xs, xl, bs)                                  \
   {                                                                     \
-    rn = ew_rows<NC>(a, tiles, rb, min(i + 2 * W, n - 1), lane);        \
-    ew_put<NC>(s_tb[wv][(bs) ^ 1], rp, lane);                           \
-    ew_resolve<NC>(a, s_tb[wv][(bs) ^ 1], rp.t, lane, xl);              \
-    ew_store<NC>(a, s_tb[wv][bs], t_cur, lane, xs);                     \
+    rn = ew_rows<NL, NC>(a, tiles, rb, min(i + 2 * W, n - 1), lane);    \
+    ew_put<NL, NC>(s_tb[wv][(bs) ^ 1], rp, lane);                       \
+    ew_resolve<NL, NC>(a, s_tb[wv][(bs) ^ 1], rp.t, lane, xl);          \
+    ew_store<NL, NC>(a, s_tb[wv][bs], t_cur, lane, xs);                 \
     __builtin_amdgcn_wave_barrier(); /* rewritten two tiles on */       \
     t_cur = rp.t;                                                       \
     i += W;                                                             \
@@ -420,10 +423,15 @@ __global__ __launch_bounds__(256) void k_femit_slow(FemitArgs a, const uint32_t 
   for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint64_t t = tiles[i], t0 = t * kEwTile, r0 = a.rb[2 * t], r1 = a.rb[2 * t + 1];
     const uint32_t ne = (uint32_t)min((uint64_t)kEwTile, a.N - t0);
-    for (uint32_t e = threadIdx.x; e < ne; e += blockDim.x) {
-      const uint64_t o = t0 + e, r = last_le_range(a.roff, r0, r1, o);
-      a.dst[o] = a.lcol[a.rbase[r] + o];
-      for (int c = 0; c < a.nc; ++c) a.cout[c][o] = a.cin[c][r];
+    // 4 consecutive output rows per thread: one search, then the rows walked forward
+    for (uint32_t e = 4 * threadIdx.x; e < ne; e += 4 * blockDim.x) {
+      uint64_t r = last_le_range(a.roff, r0, r1, t0 + e);
+      for (uint32_t k = e; k < min(e + 4, ne); ++k) {
+        const uint64_t o = t0 + k;
+        while (a.roff[r + 1] <= o) ++r;
+        for (int m = 0; m < a.nl; ++m) a.lout[m][o] = a.lcol[m][a.rbase[r] + o];
+        for (int c = 0; c < a.nc; ++c) a.cout[c][o] = a.cin[c][r];
+      }
     }
   }
 }
@@ -431,6 +439,10 @@ __global__ __launch_bounds__(256) void k_femit_slow(FemitArgs a, const uint32_t 
 }  // namespace
 
 uint64_t femit_tiles(uint64_t N) { return (N + kEwTile - 1) / kEwTile; }
+
+// the (list columns, constants) instances of k_femit_w: (1, 0…4) the rows over their sources' lists,
+// (1…3, 2) the (source, target) pairs over the rows grouped by source
+bool femit_supported(int nl, int nc) { return (nl == 1 && nc <= 4) || (nc == 2 && nl >= 1 && nl <= 3); }
 
 void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s) {
   hipLaunchKernelGGL(k_femit_len, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, g, R, loff, len);
@@ -452,17 +464,19 @@ void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, boo
 
 void launch_femit(const FemitArgs &a, const uint32_t *regular_tiles, uint64_t nreg, const uint32_t *other_tiles,
                   uint64_t nother, int cus, hipStream_t s) {
-  if (a.nc > kFemitCols) fail(OMX_E_INVALID, "internal: k_femit_w carries at most 4 columns");
+  if (a.nc > kFemitCols || a.nl < 1 || a.nl > kFemitLists || !femit_supported(a.nl, a.nc))
+    fail(OMX_E_INVALID, "internal: no k_femit_w instance for these columns");
   if (nreg) {
     // one workgroup per CU, all resident at once: the tiles are assigned statically
     const dim3 grid((unsigned)std::min<uint64_t>((nreg + kEwWaves - 1) / kEwWaves, (uint64_t)cus)), blk(64 * kEwWaves);
-    switch (a.nc) {
-      case 0: hipLaunchKernelGGL(k_femit_w<0>, grid, blk, 0, s, a, regular_tiles, a.rb, nreg); break;
-      case 1: hipLaunchKernelGGL(k_femit_w<1>, grid, blk, 0, s, a, regular_tiles, a.rb, nreg); break;
-      case 2: hipLaunchKernelGGL(k_femit_w<2>, grid, blk, 0, s, a, regular_tiles, a.rb, nreg); break;
-      case 3: hipLaunchKernelGGL(k_femit_w<3>, grid, blk, 0, s, a, regular_tiles, a.rb, nreg); break;
-      default: hipLaunchKernelGGL(k_femit_w<4>, grid, blk, 0, s, a, regular_tiles, a.rb, nreg); break;
+#define OMX_FEMIT_CASE(L, C) \
+  case L * 8 + C: hipLaunchKernelGGL((k_femit_w<L, C>), grid, blk, 0, s, a, regular_tiles, a.rb, nreg); break;
+    switch (a.nl * 8 + a.nc) {
+      OMX_FEMIT_CASE(1, 0) OMX_FEMIT_CASE(1, 1) OMX_FEMIT_CASE(1, 2) OMX_FEMIT_CASE(1, 3) OMX_FEMIT_CASE(1, 4)
+      OMX_FEMIT_CASE(2, 2) OMX_FEMIT_CASE(3, 2)
+      default: break;
     }
+#undef OMX_FEMIT_CASE
     KCHECK("k_femit_w");
   }
   if (nother) {

@@ -233,20 +233,24 @@ void launch_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt, const ui
 void launch_flist_group_offsets(const uint32_t *keys, uint64_t n, const uint32_t *ub, uint64_t U, uint64_t *loff,
                                 hipStream_t s);
 // factor.hip: the factorized hop's rows written over their sources' lists, by tiles of the output space
-constexpr int kFemitCols = 4;  // carried columns of k_femit_w (more: the generic expansion writes the rows)
+// Binding row r owns the list entries [loff[g[r]], loff[g[r]+1]) of the list columns: output row o of it
+// takes every list column's entry at rbase[r] + o and every constant's value of row r.
+constexpr int kFemitCols = 4;   // constants per binding row
+constexpr int kFemitLists = 3;  // list columns
 struct FemitArgs {
-  const uint32_t *g;     // [R] binding row → distinct source index
+  const uint32_t *g;     // [R] binding row → its list (group) index
   const uint64_t *roff;  // [R+1] first output row of every binding row (scan of its list length)
-  const uint64_t *loff;  // [U+1] list offsets
-  const uint32_t *lcol;  // list entries (the new column's values)
+  const uint64_t *loff;  // [groups+1] list offsets
   const uint64_t *rbase; // [R] loff[g[r]] − roff[r]: list position of output row o of row r is rbase[r] + o
   const uint64_t *rb;    // [2·tiles] first / last binding row of every output tile (launch_femit_bounds)
   uint64_t R, N;         // binding rows (every list non-empty), output rows
-  int32_t nc;
-  const uint32_t *cin[kFemitCols];
-  uint32_t *cout[kFemitCols];
-  uint32_t *dst;
+  int32_t nl, nc;
+  const uint32_t *lcol[kFemitLists];  // list columns …
+  uint32_t *lout[kFemitLists];        // … and where each is written
+  const uint32_t *cin[kFemitCols];    // constants of every binding row …
+  uint32_t *cout[kFemitCols];         // … and where each is written
 };
+bool femit_supported(int nl, int nc);
 uint64_t femit_tiles(uint64_t N);
 // len[r] = |L(g[r])| for r < R, len[R] = 0
 void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s);

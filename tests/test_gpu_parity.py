@@ -391,15 +391,17 @@ def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, flist, monkeypatch
     assert rs.info["bindings"] == direct.info["bindings"]
 
 
-@pytest.mark.parametrize("emit", ["binned", "unsorted", "slow"])
+@pytest.mark.parametrize("emit", ["binned", "unsorted", "slow", "sources", "targets", "targets_slow"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
 def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, monkeypatch):
     """The factorized hop's rows written every way (the default — rows grouped by source, output tiles of
     k_femit_w — is covered by test_rmat_parity_factorized): binned = the generic unfiltered expansion over
     the lists (OMX_FEMIT=0); unsorted = the rows in their order; slow = every output tile through
-    k_femit_slow (a search of the row offsets per output row). Same rows, E_t and bindings as the direct
-    expansion (P/OMatchStatement.java:491-497 per row)."""
+    k_femit_slow (a search of the row offsets per output row); sources = the lists always built from the
+    sources' side; targets = always from the targets' side (the (b, c) pairs of the targets' in-rows
+    written over the rows grouped by source, no lists), also through the slow tiles. Same rows, E_t and
+    bindings as the direct expansion (P/OMatchStatement.java:491-497 per row)."""
     import orientdb_amd as o
     g, ref = rmat10 if graph == "simple" else rmat10_raw
     monkeypatch.setenv("OMX_FACTOR", "0")
@@ -407,15 +409,17 @@ def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, mon
     monkeypatch.setenv("OMX_FACTOR", "force")
     monkeypatch.setenv("OMX_FEMIT", "0" if emit == "binned" else "1")
     monkeypatch.setenv("OMX_FEMIT_SORT", "0" if emit == "unsorted" else "1")
-    monkeypatch.setenv("OMX_FEMIT_SLOW", "1" if emit == "slow" else "0")
+    monkeypatch.setenv("OMX_FEMIT_SLOW", "1" if emit in ("slow", "targets_slow") else "0")
+    monkeypatch.setenv("OMX_FEMIT_REVERSE", "force" if emit.startswith("targets") else "0" if emit == "sources" else "1")
     rs = _parity(g, ref, q[1], q[2])
     assert rs.info["edges_traversed"] == direct.info["edges_traversed"]
     assert rs.info["bindings"] == direct.info["bindings"]
 
 
+@pytest.mark.parametrize("side", ["sources", "targets"])
 @pytest.mark.parametrize("slow", ["0", "1"])
 @pytest.mark.parametrize("sort", ["0", "1"])
-def test_factorized_emission_many_tiles_rmat16(rmat16, slow, sort, monkeypatch):
+def test_factorized_emission_many_tiles_rmat16(rmat16, side, slow, sort, monkeypatch):
     """Output tiles of the factorized emission across many tiles (RMAT-16 2-hop with WHERE on both ends:
     rows spanning tile boundaries, runs of short lists in one tile, a partial last tile): rows and digest
     equal with the emission through the generic expansion."""
@@ -429,6 +433,7 @@ def test_factorized_emission_many_tiles_rmat16(rmat16, slow, sort, monkeypatch):
     monkeypatch.setenv("OMX_FEMIT", "1")
     monkeypatch.setenv("OMX_FEMIT_SORT", sort)
     monkeypatch.setenv("OMX_FEMIT_SLOW", slow)
+    monkeypatch.setenv("OMX_FEMIT_REVERSE", "force" if side == "targets" else "0")
     rs = o.OMatchStatement(q).execute(g, documents=False, flags=fl)
     assert rs.info["factorized_hops"] >= 1 and rs.info["n_rows"] > 100000
     assert rs.info["n_rows"] == base.info["n_rows"] and rs.info["digest"] == base.info["digest"]
