@@ -332,6 +332,223 @@ void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const 
   KCHECK("k_bfs_pull");
 }
 
+// ---- wave-tiled bottom-up level (k_bfs_pull_w) ----------------------------------------------------
+// The same level as k_bfs_pull over the same hub-annotated reversed CSR, tiled by waves over the in-edge
+// space: every wave owns tiles of kPwTile consecutive in-edges (tile i → wave i mod W; no workgroup
+// barriers). A tile's vertices (≤ kPwRows; a tile over more, or the partial last one, goes to
+// k_bfs_pull_w_slow) sit in the wave's own LDS table — lane mask still needed and accumulator — and mark
+// their first in-edge in a byte array spread by a max-scan, so an in-edge's vertex is one LDS byte. Lane l
+// takes in-edges l + 64j: coalesced col[] words; each mask gathered (LDS copy of the first hubs' masks,
+// the hub array, or the frontier after the bitmap probe) is merged into its vertex's accumulator by an
+// LDS atomic, and every non-zero accumulator goes to next[] with one atomicOr.
+// One 16-wave workgroup per CU, so the hub masks staged in LDS (the ≈10 K highest-degree sources, staged
+// once per launch) serve every wave of the CU. Measured at C3's sparse level (profiles/r03/pullw): the
+// level is bound by its L2 traffic (248 M TCP→TCC requests, 36 % missing, per launch; profiles/r03/
+// pmc_c3), not by the tiles' latency — wave tiles alone 1.70-1.99 ms against k_bfs_pull's 1.72-1.74; the
+// LDS hubs take 8 % of the requests' worth off: 1.59 ms.
+#ifndef OMX_PW_WAVES
+#define OMX_PW_WAVES 16
+#endif
+#ifndef OMX_PW_ROWS
+#define OMX_PW_ROWS 256
+#endif
+constexpr int kPwTile = 1024, kPwJ = kPwTile / 64, kPwRows = OMX_PW_ROWS, kPwWaves = OMX_PW_WAVES;
+// the first hub masks (highest degree) staged in LDS once per launch: one workgroup per CU, the rest of
+// its LDS after the waves' tables
+constexpr int kPwLdsHubs = (160 * 1024 - kPwWaves * (kPwTile + 16 * kPwRows) - 64) / 8;
+
+struct PwTable {
+  uint32_t mk[kPwTile / 4];  // kPwTile u8: table entry of every in-edge of the tile
+  uint64_t need[kPwRows];
+  unsigned long long acc[kPwRows];
+};
+
+template <bool PROBE>
+__global__ __launch_bounds__(64 * kPwWaves) void k_bfs_pull_w(const uint64_t *rp, const uint32_t *col,
+                                                             const uint32_t *__restrict__ tiles,
+                                                             const uint64_t *__restrict__ rb, uint64_t n,
+                                                             uint64_t lanes, const uint64_t *frontier,
+                                                             const uint64_t *hub_fr, const uint64_t *fbm,
+                                                             const uint64_t *visited, uint64_t *next, uint32_t nlds) {
+  __shared__ PwTable s_tb[kPwWaves];
+  __shared__ uint64_t s_hub[kPwLdsHubs];
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  PwTable &tb = s_tb[wv];
+  for (uint32_t h = threadIdx.x; h < nlds; h += blockDim.x) s_hub[h] = hub_fr[h];
+  __syncthreads();
+  const uint64_t W = (uint64_t)gridDim.x * kPwWaves;
+  for (uint64_t i = (uint64_t)blockIdx.x * kPwWaves + wv; i < n; i += W) {
+    const uint64_t t = tiles[i], t0 = t * kPwTile, r0 = rb[2 * t];
+    const uint32_t nr = (uint32_t)(rb[2 * t + 1] - r0 + 1);  // ≤ kPwRows (a regular tile)
+    uint32_t x[kPwJ];
+#pragma unroll
+    for (int j = 0; j < kPwJ; ++j) x[j] = col[t0 + 64 * j + lane];
+    uint32_t *mk = tb.mk + lane * (kPwJ / 4);
+#pragma unroll
+    for (int q = 0; q < kPwJ / 4; ++q) mk[q] = 0;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < kPwRows / 64; ++q) {
+      const uint32_t k = lane + 64 * q;
+      if (k < nr) {
+        const uint64_t rs = rp[r0 + k], re = rp[r0 + k + 1];
+        if (re > rs && rs > t0 && rs < t0 + kPwTile) reinterpret_cast<uint8_t *>(tb.mk)[rs - t0] = (uint8_t)k;
+        tb.need[k] = re > rs ? lanes & ~visited[r0 + k] : 0ull;
+        tb.acc[k] = 0;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    {  // max-scan of the marks: lane l holds bytes 16l … 16l + 15
+      uint32_t wd[kPwJ / 4];
+      uint32_t m = 0;
+#pragma unroll
+      for (int q = 0; q < kPwJ / 4; ++q) {
+        wd[q] = mk[q];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) m = max(m, (wd[q] >> (8 * b)) & 0xFFu);
+      }
+      uint32_t incl = m;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl = max(incl, y);
+      }
+      uint32_t run = __shfl_up(incl, 1, 64);
+      if (lane == 0) run = 0;
+#pragma unroll
+      for (int q = 0; q < kPwJ / 4; ++q) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          run = max(run, (wd[q] >> (8 * b)) & 0xFFu);
+          o |= run << (8 * b);
+        }
+        mk[q] = o;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t *mb = reinterpret_cast<const uint8_t *>(tb.mk);
+    uint64_t f[kPwJ];
+    uint32_t kk[kPwJ];
+#pragma unroll
+    for (int j = 0; j < kPwJ; ++j) {  // every gather requested before the first merge
+      const uint32_t k = mb[64 * j + lane];
+      const uint64_t nd = tb.need[k];
+      const uint32_t xv = x[j];
+      uint64_t g = 0;
+      if (nd) {
+        const uint32_t hx = xv & 0x7FFFFFFFu;
+        if ((xv >> 31) && hx < nlds) g = s_hub[hx] & nd;
+        else if (xv >> 31) g = hub_fr[hx] & nd;
+        else if (!PROBE || ((fbm[xv >> 6] >> (xv & 63)) & 1)) g = frontier[xv] & nd;
+      }
+      f[j] = g;
+      kk[j] = k;
+    }
+#pragma unroll
+    for (int j = 0; j < kPwJ; ++j)
+      if (f[j]) atomicOr(&tb.acc[kk[j]], (unsigned long long)f[j]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < kPwRows / 64; ++q) {
+      const uint32_t k = lane + 64 * q;
+      if (k < nr) {
+        const unsigned long long a = tb.acc[k];
+        if (a) atomicOr((unsigned long long *)&next[r0 + k], a);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the table is rebuilt for the next tile
+  }
+}
+
+// the other tiles: one thread per in-edge, its vertex by a search of the row pointers
+template <bool PROBE>
+__global__ __launch_bounds__(256) void k_bfs_pull_w_slow(const uint64_t *rp, const uint32_t *col, uint64_t E,
+                                                        const uint32_t *tiles, const uint64_t *rb, uint64_t n,
+                                                        uint64_t lanes, const uint64_t *frontier,
+                                                        const uint64_t *hub_fr, const uint64_t *fbm,
+                                                        const uint64_t *visited, uint64_t *next) {
+  for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint64_t t = tiles[i], t0 = t * kPwTile, t1 = min(t0 + (uint64_t)kPwTile, E);
+    for (uint64_t e = t0 + threadIdx.x; e < t1; e += blockDim.x) {
+      uint64_t lo = rb[2 * t], hi = rb[2 * t + 1];  // last row with rp[r] <= e
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) >> 1;
+        if (rp[mid] <= e) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint64_t nd = lanes & ~visited[lo];
+      if (!nd) continue;
+      const uint32_t xv = col[e];
+      uint64_t g = 0;
+      if (xv >> 31) g = hub_fr[xv & 0x7FFFFFFFu] & nd;
+      else if (!PROBE || ((fbm[xv >> 6] >> (xv & 63)) & 1)) g = frontier[xv] & nd;
+      if (g) atomicOr((unsigned long long *)&next[lo], (unsigned long long)g);
+    }
+  }
+}
+
+// first / last vertex of every in-edge tile and whether the tile is regular (full, ≤ kPwRows vertices)
+__global__ void k_pull_w_bounds(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t ntiles, uint64_t *rb,
+                                uint8_t *regular) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  const uint64_t e0 = t * kPwTile, e1 = min(e0 + (uint64_t)kPwTile, E) - 1;
+  auto last_le = [&](uint64_t lo, uint64_t hi, uint64_t e) {
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi + 1) >> 1;
+      if (rp[mid] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
+  const uint64_t r0 = last_le(0, V - 1, e0), r1 = last_le(r0, V - 1, e1);
+  rb[2 * t] = r0;
+  rb[2 * t + 1] = r1;
+  regular[t] = r1 - r0 < (uint64_t)kPwRows && e0 + kPwTile <= E;
+}
+
+uint64_t bfs_pull_w_tiles(uint64_t E) { return (E + kPwTile - 1) / kPwTile; }
+void launch_pull_w_bounds(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t *rb, uint8_t *regular, hipStream_t s) {
+  const uint64_t nt = bfs_pull_w_tiles(E);
+  if (!nt) return;
+  hipLaunchKernelGGL(k_pull_w_bounds, dim3(nblocks(nt, kB)), dim3(kB), 0, s, rp, V, E, nt, rb, regular);
+  KCHECK("k_pull_w_bounds");
+}
+void launch_bfs_pull_w(const uint64_t *rp, const uint32_t *col, uint64_t E, const uint32_t *tiles, uint64_t nreg,
+                       const uint64_t *rb, uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr,
+                       uint32_t nhubs, const uint64_t *fbm, const uint64_t *visited, uint64_t *next, int cus,
+                       hipStream_t s) {
+  const uint64_t nt = bfs_pull_w_tiles(E);
+  if (!nt || !lanes) return;
+  static const int per = [] {  // workgroups per CU (4 waves each)
+    const char *e = std::getenv("OMX_PULLW_PER");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  static const uint32_t lds_cap = [] {  // OMX_PULLW_LDS_HUBS=n: at most n hub masks in LDS
+    const char *e = std::getenv("OMX_PULLW_LDS_HUBS");
+    return e ? (uint32_t)std::min<long>(kPwLdsHubs, std::max(0l, std::atol(e))) : (uint32_t)kPwLdsHubs;
+  }();
+  const uint32_t nlds = std::min(nhubs, lds_cap);
+  static const bool slow_all = [] {  // OMX_PULLW_SLOW=1: every tile through k_bfs_pull_w_slow (tests)
+    const char *e = std::getenv("OMX_PULLW_SLOW");
+    return e && std::strcmp(e, "0") != 0;
+  }();
+  if (slow_all) nreg = 0;
+  if (nreg) {
+    const dim3 g((unsigned)std::min<uint64_t>((nreg + kPwWaves - 1) / kPwWaves, (uint64_t)cus * per));
+    if (fbm) hipLaunchKernelGGL(k_bfs_pull_w<true>, g, dim3(64 * kPwWaves), 0, s, rp, col, tiles, rb, nreg, lanes, frontier, hub_fr, fbm, visited, next, nlds);
+    else hipLaunchKernelGGL(k_bfs_pull_w<false>, g, dim3(64 * kPwWaves), 0, s, rp, col, tiles, rb, nreg, lanes, frontier, hub_fr, fbm, visited, next, nlds);
+    KCHECK("k_bfs_pull_w");
+  }
+  if (nt > nreg) {
+    const dim3 g((unsigned)std::min<uint64_t>(nt - nreg, (uint64_t)cus * 8));
+    if (fbm) hipLaunchKernelGGL(k_bfs_pull_w_slow<true>, g, dim3(256), 0, s, rp, col, E, tiles + nreg, rb, nt - nreg, lanes, frontier, hub_fr, fbm, visited, next);
+    else hipLaunchKernelGGL(k_bfs_pull_w_slow<false>, g, dim3(256), 0, s, rp, col, E, tiles + nreg, rb, nt - nreg, lanes, frontier, hub_fr, fbm, visited, next);
+    KCHECK("k_bfs_pull_w_slow");
+  }
+}
+
 // Dense levels with an early exit: one thread per vertex walks its in-edges in the annotated col's
 // hub-first order (the first alone, then four at a time) and stops as soon as the gathered masks cover the lanes the vertex
 // still needs. Once the frontier holds a large share of V, most vertices are covered by their first

@@ -171,6 +171,7 @@ class Executor {
     if (const char *lv = std::getenv("OMX_PULL_LIVE")) pull_live_ = std::strcmp(lv, "0") != 0;
     if (const char *pr = std::getenv("OMX_PULL_PROBE")) pull_probe_ = std::strtod(pr, nullptr);
     if (const char *px = std::getenv("OMX_PULL_EXIT")) pull_exit_ = std::strcmp(px, "0") != 0;
+    if (const char *pw = std::getenv("OMX_PULL_WAVE")) pull_wave_ = std::strcmp(pw, "0") != 0;
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
     bound_.assign(p.aliases.size(), 0);
@@ -439,6 +440,7 @@ class Executor {
   bool pull_live_ = true;  // the pull waits only for lanes whose frontier is non-empty
   // levels whose frontier holds fewer than this fraction of the vertices pull through the frontier bitmap
   double pull_probe_ = 0.1;
+  bool pull_wave_ = true;  // OMX_PULL_WAVE=0: the workgroup-tiled k_bfs_pull for the tiled bottom-up levels
   bool pull_exit_ = true;  // denser levels pull per vertex with an early exit (OMX_PULL_EXIT=0: tiles)
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
   // sliced hops size their arenas from the target bitmap's density (OMX_ARENA_ESTIMATE=0: exact bound;
@@ -894,6 +896,43 @@ class Executor {
       g_.device_bytes += (ntiles + 1) * sizeof(uint64_t);
     }
     return es.d_pull_part[dir];
+  }
+
+  // the in-edge wave tiles of one CSR for k_bfs_pull_w (built once per CSR): tile bounds and the tile
+  // indices, regular tiles first (*nreg of them)
+  const uint32_t *pullw_of(int eset, int dir, const uint64_t *rp, uint64_t E, const uint64_t **rb, uint64_t *nreg) {
+    EdgeSet &es = g_.esets[eset];
+    if (!es.d_pullw_tiles[dir]) {  // built into local buffers, published once complete
+      const uint64_t nt = bfs_pull_w_tiles(E);
+      if (nt > 0xFFFFFFFFull) unsupported("a bottom-up level over 2^42 or more in-edges");
+      uint64_t *b = nullptr;
+      uint32_t *tl = nullptr;
+      HIP_CHECK(hipMalloc((void **)&b, std::max<uint64_t>(2 * nt, 1) * sizeof(uint64_t)));
+      if (hipMalloc((void **)&tl, std::max<uint64_t>(nt, 1) * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipFree(b);
+        fail(OMX_E_OOM, "pull tiles");
+      }
+      uint64_t nr = 0;
+      try {
+        DBuf<uint8_t> reg(&pool_, std::max<uint64_t>(nt, 1));
+        DBuf<uint64_t> cnt(&pool_, 1);
+        launch_pull_w_bounds(rp, g_.V, E, b, reg.p, s_);
+        hipcub::CountingInputIterator<uint32_t> it(0);
+        cub([&](void *t, size_t &bytes) { return hipcub::DevicePartition::Flagged(t, bytes, it, reg.p, tl, cnt.p, (int64_t)nt, s_); });
+        nr = read1(cnt.p);
+      } catch (...) {
+        (void)hipFree(b);
+        (void)hipFree(tl);
+        throw;
+      }
+      es.d_pullw_rb[dir] = b;
+      es.pullw_nreg[dir] = nr;
+      es.d_pullw_tiles[dir] = tl;
+      g_.device_bytes += nt * 20;
+    }
+    *rb = es.d_pullw_rb[dir];
+    *nreg = es.pullw_nreg[dir];
+    return es.d_pullw_tiles[dir];
   }
 
   // the hub-annotated col of one CSR for the bottom-up BFS (built once per CSR, bfs.hip)
@@ -2597,8 +2636,16 @@ class Executor {
               continue;
             }
             tm_.begin(probe ? "k_bfs_pull_sparse" : "k_bfs_pull");
-            launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p], pull_E[p], lanes & live, fr.p, hub_fr[p].p,
-                            probe ? fbm.p : nullptr, vis.p, nx.p, cus(), s_);
+            if (pull_wave_) {  // wave tiles over the in-edges
+              const uint64_t *wrb = nullptr;
+              uint64_t nreg = 0;
+              const uint32_t *wt = pullw_of(rspec.parts[p].first, rspec.parts[p].second, radj.p[p].rp, pull_E[p], &wrb, &nreg);
+              launch_bfs_pull_w(radj.p[p].rp, pull_col[p], pull_E[p], wt, nreg, wrb, lanes & live, fr.p, hub_fr[p].p,
+                                pull_nh[p], probe ? fbm.p : nullptr, vis.p, nx.p, cus(), s_);
+            } else {
+              launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p], pull_E[p], lanes & live, fr.p, hub_fr[p].p,
+                              probe ? fbm.p : nullptr, vis.p, nx.p, cus(), s_);
+            }
             // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask
             tm_.end(16ull * V + 12ull * pull_E[p]);
             edges_iter_ += pull_E[p];

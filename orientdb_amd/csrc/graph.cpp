@@ -81,7 +81,10 @@ Graph::~Graph() {
       f(e.d_out_rp); f(e.d_in_rp); f(e.d_out_col); f(e.d_in_col);
       for (auto &m : e.d_cuts)
         for (auto &kv : m) f(kv.second);
-      for (int d = 0; d < 2; ++d) { f(e.d_pull_col[d]); f(e.d_hubs[d]); f(e.d_pull_part[d]); f(e.d_global_rp[d]); }
+      for (int d = 0; d < 2; ++d) {
+        f(e.d_pull_col[d]); f(e.d_hubs[d]); f(e.d_pull_part[d]); f(e.d_global_rp[d]);
+        f(e.d_pullw_rb[d]); f(e.d_pullw_tiles[d]);
+      }
     }
     for (auto &p : props) { f(p.d_values); f(p.d_present); }
     if (stream) (void)hipStreamDestroy(stream);

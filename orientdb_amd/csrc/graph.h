@@ -105,6 +105,11 @@ struct EdgeSet {
   uint32_t hubs_requested[2] = {0, 0};  // the hub budget d_pull_col was built with (rebuilt when it changes)
   // merge-path split of the CSR into pull tiles (bfs.hip k_pull_partition), built with d_pull_col
   uint64_t *d_pull_part[2] = {nullptr, nullptr};
+  // in-edge wave tiles of the CSR (bfs.hip k_bfs_pull_w): first / last vertex of every tile, and the tile
+  // indices with the regular tiles (full, ≤ 256 vertices) first
+  uint64_t *d_pullw_rb[2] = {nullptr, nullptr};
+  uint32_t *d_pullw_tiles[2] = {nullptr, nullptr};
+  uint64_t pullw_nreg[2] = {0, 0};
   // partitioned snapshot: row pointers of every vertex's degree (V + 1 entries, the scan of all ranks'
   // degrees gathered once) — what out()/in()/both().size() in a WHERE reads (no col[] behind them)
   uint64_t *d_global_rp[2] = {nullptr, nullptr};

@@ -318,6 +318,14 @@ void launch_bfs_pull_partition(const uint64_t *rp, uint32_t V, uint64_t E, uint6
 void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const uint64_t *part, uint64_t E,
                      uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *fbm,
                      const uint64_t *visited, uint64_t *next, int cus, hipStream_t s);
+// the same level tiled by waves over the in-edge space (k_bfs_pull_w): rb[2·tiles] first / last vertex of
+// every tile, regular[tile] (≤ 256 vertices, full); tiles = the tile indices, the nreg regular ones first
+uint64_t bfs_pull_w_tiles(uint64_t E);
+void launch_pull_w_bounds(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t *rb, uint8_t *regular, hipStream_t s);
+void launch_bfs_pull_w(const uint64_t *rp, const uint32_t *col, uint64_t E, const uint32_t *tiles, uint64_t nreg,
+                       const uint64_t *rb, uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr,
+                       uint32_t nhubs, const uint64_t *fbm, const uint64_t *visited, uint64_t *next, int cus,
+                       hipStream_t s);
 // dense levels: per-vertex pull with an early exit (k_bfs_pull_exit + k_bfs_pull_rest) over vertices
 // [vlo, V); rest u32[V]
 // scratch; counts[0] += in-edges read, counts[1] = vertices handed to the per-wave pass (zeroed by the caller)
