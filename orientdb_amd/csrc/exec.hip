@@ -1860,13 +1860,15 @@ class Executor {
       edges_iter_ += EU;
     } else {
     // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
-    ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true);
+    // (the filtered lists stay in the expansion's per-worker segments: grouping reads them in place)
+    ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, true);
     edges_iter_ += l.E;
     nlist = l.n;
     // 3. grouped by source: offsets (U + 1) and the neighbours in group order
     if (l.n) {
       tm_.begin("k_key_hist");
-      launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
+      if (l.segmented) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, s_);
+      else launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
       tm_.end(4ull * l.n + 8ull * U);
     }
     cub([&](void *t, size_t &b) {
@@ -1876,7 +1878,9 @@ class Executor {
     if (l.n) {
       HIP_CHECK(hipMemcpyAsync(cnt.p, loff.p, (U + 1) * 8, hipMemcpyDeviceToDevice, s_));
       tm_.begin("k_key_scatter");
-      launch_key_scatter(l.carry[0].p, l.dst.p, l.n, cnt.p, lcol.p, s_);
+      if (l.segmented)
+        launch_key_scatter_seg(l.carry[0].p, l.dst.p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, lcol.p, s_);
+      else launch_key_scatter(l.carry[0].p, l.dst.p, l.n, cnt.p, lcol.p, s_);
       tm_.end(12ull * l.n + 8ull * U);
     }
     }

@@ -241,7 +241,14 @@ __global__ void k_flist_group_offsets(const uint32_t *keys, uint64_t n, const ui
 // Occupancy: 8 waves per CU (one 512-thread workgroup). Measured at M1 (profiles/r03/femit): 6 or 10
 // waves per CU 2.8 ms, 8 waves 2.2-2.3 ms; 16-byte stores of 4 consecutive rows per lane 2.6-2.9 ms; a
 // contiguous run of tiles per wave 2.7 ms; the binned heavy/merge-path kernels 3.2 ms.
-constexpr int kEwTile = 1024, kEwWaves = 8, kEwJ = kEwTile / 64;
+#ifndef OMX_EW_TILE
+#define OMX_EW_TILE 1024
+#endif
+#ifndef OMX_EW_WAVES
+#define OMX_EW_WAVES 8
+#endif
+constexpr int kEwTile = OMX_EW_TILE, kEwWaves = OMX_EW_WAVES, kEwJ = kEwTile / 64;
+static_assert(kEwTile <= 256 * 64, "a lane's mark bytes are read as u32 words");
 
 __global__ void k_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

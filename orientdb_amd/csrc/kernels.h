@@ -263,6 +263,11 @@ void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, boo
 void launch_femit(const FemitArgs &a, const uint32_t *regular_tiles, uint64_t nreg, const uint32_t *other_tiles,
                   uint64_t nother, int cus, hipStream_t s);
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
+// the same over a block-segmented table (segment s: entries [seg_start[s], + seg_count[s]))
+void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
+                         unsigned long long *counts, hipStream_t s);
+void launch_key_scatter_seg(const uint32_t *key, const uint32_t *val, const uint64_t *seg_start, const uint32_t *seg_count,
+                            uint32_t nseg, unsigned long long *cursor, uint32_t *out, hipStream_t s);
 void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor, uint32_t *out,
                         hipStream_t s);
 void launch_pack_pairs(const uint32_t *hi, const uint32_t *lo, uint64_t n, uint64_t *keys, hipStream_t s);

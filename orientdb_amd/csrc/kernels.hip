@@ -2222,6 +2222,67 @@ void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, un
   KCHECK("k_key_scatter");
 }
 
+// the same over a block-segmented table (an expansion's per-worker arenas, ExpandArgs::seg_start /
+// seg_count) without compacting it first: one wave per segment, 64 entries at a time
+__global__ __launch_bounds__(256) void k_key_hist_seg(const uint32_t *key, const uint64_t *seg_start,
+                                                      const uint32_t *seg_count, uint32_t nseg,
+                                                      unsigned long long *counts) {
+  const uint32_t sg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sg >= nseg) return;
+  const int lane = threadIdx.x & 63;
+  const uint64_t b = seg_start[sg];
+  const uint32_t n = seg_count[sg];
+  for (uint32_t j = 0; j < n; j += 64) {
+    const bool valid = j + lane < n;
+    const uint32_t k = valid ? key[b + j + lane] : 0xFFFFFFFFu;
+    const uint64_t heads = key_runs(k, valid, lane);
+    const int nvalid = (int)min(64u, n - j);
+    if (valid && ((heads >> lane) & 1)) {
+      const uint64_t later = lane == 63 ? 0 : heads & (~0ull << (lane + 1));
+      const int nxt = later ? __ffsll((unsigned long long)later) - 1 : 64;
+      atomicAdd(&counts[k], (unsigned long long)(min(nxt, nvalid) - lane));
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_key_scatter_seg(const uint32_t *key, const uint32_t *val, const uint64_t *seg_start,
+                                                         const uint32_t *seg_count, uint32_t nseg,
+                                                         unsigned long long *cursor, uint32_t *out) {
+  const uint32_t sg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sg >= nseg) return;
+  const int lane = threadIdx.x & 63;
+  const uint64_t b = seg_start[sg];
+  const uint32_t n = seg_count[sg];
+  for (uint32_t j = 0; j < n; j += 64) {
+    const bool valid = j + lane < n;
+    const uint32_t k = valid ? key[b + j + lane] : 0xFFFFFFFFu;
+    const uint64_t heads = key_runs(k, valid, lane);
+    const int nvalid = (int)min(64u, n - j);
+    unsigned long long base = 0;
+    if (valid && ((heads >> lane) & 1)) {
+      const uint64_t later = lane == 63 ? 0 : heads & (~0ull << (lane + 1));
+      const int nxt = later ? __ffsll((unsigned long long)later) - 1 : 64;
+      base = atomicAdd(&cursor[k], (unsigned long long)(min(nxt, nvalid) - lane));
+    }
+    const uint64_t upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+    const int hl = upto ? 63 - __clzll((long long)upto) : lane;
+    base = __shfl(base, hl, 64);
+    if (valid) out[base + (uint64_t)(lane - hl)] = val[b + j + lane];
+  }
+}
+void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
+                         unsigned long long *counts, hipStream_t s) {
+  if (!nseg) return;
+  hipLaunchKernelGGL(k_key_hist_seg, dim3(nblocks(nseg, 4)), dim3(256), 0, s, key, seg_start, seg_count, nseg, counts);
+  KCHECK("k_key_hist_seg");
+}
+void launch_key_scatter_seg(const uint32_t *key, const uint32_t *val, const uint64_t *seg_start, const uint32_t *seg_count,
+                            uint32_t nseg, unsigned long long *cursor, uint32_t *out, hipStream_t s) {
+  if (!nseg) return;
+  hipLaunchKernelGGL(k_key_scatter_seg, dim3(nblocks(nseg, 4)), dim3(256), 0, s, key, val, seg_start, seg_count, nseg,
+                     cursor, out);
+  KCHECK("k_key_scatter_seg");
+}
+
 // ---- TRAVERSE (exec.hip Executor::traverse_bfs) -----------------------------------------------------
 // out[j] = the vertex whose RID is keys[j] (left untouched when no vertex has it; RIDs are unique)
 __global__ void k_find_rids(const uint64_t *rids, uint32_t V, const uint64_t *keys, uint32_t m, uint32_t *out) {
