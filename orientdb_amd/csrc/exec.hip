@@ -33,6 +33,9 @@ struct CastU64 {
 struct NonZeroU64 {
   __host__ __device__ uint8_t operator()(const uint64_t &x) const { return x != 0; }
 };
+struct CastU8U32 {
+  __host__ __device__ uint32_t operator()(const uint8_t &x) const { return x; }
+};
 
 class Timer {
  public:
@@ -1493,8 +1496,10 @@ class Executor {
 
   // step 4 of expand_factorized when the rows are written: the output space Σ_rows |L(g[r])| is laid out
   // row by row and written by tiles of output rows (factor.hip k_femit)
+  // perm_sorted: the rows are already sorted by source (g in that order); perm_sorted[i] = the row at
+  // sorted position i
   void emit_factorized(DBuf<uint32_t> &g, uint64_t R, uint64_t U, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol,
-                       const std::vector<int> &cols, const Step &st) {
+                       const std::vector<int> &cols, const Step &st, const uint32_t *perm_sorted = nullptr) {
     // 1. the rows whose list is not empty (the others write nothing), in row order or grouped by source
     DBuf<uint64_t> len(&pool_, R + 1);
     launch_femit_len(g.p, R, loff.p, len.p, s_);
@@ -1507,7 +1512,13 @@ class Executor {
     }
     const uint64_t Rn = read1(nsel.p);
     DBuf<uint32_t> gs(&pool_, std::max<uint64_t>(Rn, 1)), perm;
-    if (femit_sort_ && Rn > 1) {  // grouped by source: a list is re-read from L2 by its rows
+    if (perm_sorted) {  // grouped already: the non-empty rows keep their sorted order
+      perm = DBuf<uint32_t>(&pool_, std::max<uint64_t>(Rn, 1));
+      if (Rn) {
+        launch_gather_u32(g.p, idx.p, Rn, gs.p, s_);
+        launch_gather_u32(perm_sorted, idx.p, Rn, perm.p, s_);
+      }
+    } else if (femit_sort_ && Rn > 1) {  // grouped by source: a list is re-read from L2 by its rows
       DBuf<uint32_t> gk(&pool_, Rn);
       perm = DBuf<uint32_t>(&pool_, Rn);
       launch_gather_u32(g.p, idx.p, Rn, gk.p, s_);
@@ -1704,13 +1715,41 @@ class Executor {
     const uint32_t *src = col_[st.src].p;
     // the distinct sources, ascending: marked in a V-bit bitmap and listed (no sort of the R rows)
     uint64_t U = 0;
-    DBuf<uint32_t> ub;
-    DBuf<uint64_t> ubm(&pool_, std::max<uint64_t>(nwords_, 1));
-    HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
-    tm_.begin("k_mark_bitmap");
-    launch_mark_bitmap(src, R, ubm.p, g_.V, s_);
-    tm_.end(4ull * R + 8ull * nwords_);
-    ub = bitmap_list(ubm.p, 0, 1, U);
+    DBuf<uint32_t> ub, g, perm_s;
+    DBuf<uint64_t> ubm;
+    // rows emitted by k_femit_w from the sources' lists: the rows are sorted by source here (the emission
+    // wants them grouped), so the distinct sources are the sorted runs' heads and a row's source index
+    // is its run — no bitmap, position map or second sort
+    const bool presort = write && femit_ && femit_sort_ && !flist_ && femit_reverse_ == 0 &&
+                         cols.size() <= (size_t)kFemitCols && R > 0;
+    if (presort) {
+      DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
+      DBuf<uint8_t> head(&pool_, R);
+      DBuf<uint64_t> nsel(&pool_, 1);
+      perm_s = DBuf<uint32_t>(&pool_, R);
+      ub = DBuf<uint32_t>(&pool_, R);
+      g = DBuf<uint32_t>(&pool_, R);
+      launch_iota(iota.p, R, s_);
+      tm_.begin("femit_row_sort");
+      cub([&](void *t, size_t &b) {
+        return hipcub::DeviceRadixSort::SortPairs(t, b, src, ss.p, iota.p, perm_s.p, (int64_t)R, 0,
+                                                  std::max(1, bits_for(g_.V)), s_);
+      });
+      tm_.end(16ull * R * ((bits_for(g_.V) + 7) / 8));
+      launch_run_heads(ss.p, R, head.p, s_);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, ss.p, head.p, ub.p, nsel.p, (int64_t)R, s_); });
+      hipcub::TransformInputIterator<uint32_t, CastU8U32, const uint8_t *> hc(head.p, CastU8U32());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, hc, g.p, (int64_t)R, s_); });
+      launch_add_u32(g.p, R, -1, s_);
+      U = read1(nsel.p);
+    } else {
+      ubm = DBuf<uint64_t>(&pool_, std::max<uint64_t>(nwords_, 1));
+      HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+      tm_.begin("k_mark_bitmap");
+      launch_mark_bitmap(src, R, ubm.p, g_.V, s_);
+      tm_.end(4ull * R + 8ull * nwords_);
+      ub = bitmap_list(ubm.p, 0, 1, U);
+    }
     // the distinct sources' degrees, scanned: doff[u] = the first of u's entries in the flat list space
     const uint64_t Et = degree_sum(src, R, st.adj);
     const bool tiles = flist_ && st.adj.parts.size() == 1;
@@ -1730,15 +1769,20 @@ class Executor {
     if (Et < factor_min_ratio_ * EU) return false;
     edges_ += Et;
     // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
-    DBuf<uint32_t> g(&pool_, R), iu(&pool_, std::max<uint64_t>(U, 1)), pos(&pool_, std::max<uint64_t>(g_.V, 1));
+    // (presorted rows have theirs from the runs)
+    DBuf<uint32_t> iu(&pool_, std::max<uint64_t>(U, 1)), pos;
     launch_iota(iu.p, U, s_);
-    tm_.begin("k_scatter_u32");
-    launch_scatter_u32(ub.p, iu.p, U, pos.p, s_);
-    tm_.end(12ull * U);
-    tm_.begin("k_gather_u32");
-    launch_gather_u32(pos.p, src, R, g.p, s_);
-    tm_.end(12ull * R);
-    if (write && femit_ && femit_reverse_ && !dist_ && st.adj.parts.size() == 1 && cols.size() >= 2 &&
+    if (!presort) {
+      g = DBuf<uint32_t>(&pool_, R);
+      pos = DBuf<uint32_t>(&pool_, std::max<uint64_t>(g_.V, 1));
+      tm_.begin("k_scatter_u32");
+      launch_scatter_u32(ub.p, iu.p, U, pos.p, s_);
+      tm_.end(12ull * U);
+      tm_.begin("k_gather_u32");
+      launch_gather_u32(pos.p, src, R, g.p, s_);
+      tm_.end(12ull * R);
+    }
+    if (!presort && write && femit_ && femit_reverse_ && !dist_ && st.adj.parts.size() == 1 && cols.size() >= 2 &&
         femit_supported((int)cols.size() - 1, 2) && emit_factorized_reverse(st, cols, g, R, U, ubm, iu, pos, EU))
       return true;
     DBuf<unsigned long long> cnt(&pool_, U + 1);
@@ -1886,7 +1930,7 @@ class Executor {
     }
     // 4. the rows over their sources' lists
     if (write && femit_ && cols.size() <= (size_t)kFemitCols) {
-      emit_factorized(g, R, U, loff, lcol, cols, st);
+      emit_factorized(g, R, U, loff, lcol, cols, st, presort ? perm_s.p : nullptr);
       return true;
     }
     DAdj ladj{};

@@ -263,6 +263,8 @@ void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, boo
 void launch_femit(const FemitArgs &a, const uint32_t *regular_tiles, uint64_t nreg, const uint32_t *other_tiles,
                   uint64_t nother, int cus, hipStream_t s);
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
+// head[i] = 1 where a run of equal sorted keys starts
+void launch_run_heads(const uint32_t *sorted, uint64_t n, uint8_t *head, hipStream_t s);
 // the same over a block-segmented table (segment s: entries [seg_start[s], + seg_count[s]))
 void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
                          unsigned long long *counts, hipStream_t s);

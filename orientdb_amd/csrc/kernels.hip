@@ -2222,6 +2222,17 @@ void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, un
   KCHECK("k_key_scatter");
 }
 
+// head[i] = 1 where a sorted key run starts
+__global__ void k_run_heads(const uint32_t *s, uint64_t n, uint8_t *head) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) head[i] = i == 0 || s[i] != s[i - 1];
+}
+void launch_run_heads(const uint32_t *sorted, uint64_t n, uint8_t *head, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_run_heads, dim3(nblocks(n, 256)), dim3(256), 0, s, sorted, n, head);
+  KCHECK("k_run_heads");
+}
+
 // the same over a block-segmented table (an expansion's per-worker arenas, ExpandArgs::seg_start /
 // seg_count) without compacting it first: one wave per segment, 64 entries at a time
 __global__ __launch_bounds__(256) void k_key_hist_seg(const uint32_t *key, const uint64_t *seg_start,
