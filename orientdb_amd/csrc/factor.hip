@@ -266,17 +266,26 @@ __global__ void k_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff
   if (r < R) rbase[r] = loff[g[r]] - roff[r];
 }
 
-// first and last binding row of every output tile (the rows holding its first and last output), and
-// whether the tile is regular (full, ≤ 64 rows); slow_all: every tile through k_femit_slow (tests)
-__global__ void k_femit_bounds(const uint64_t *roff, uint64_t R, uint64_t N, uint64_t ntiles, uint64_t *rb,
-                               uint8_t *regular, int slow_all) {
+// first and last binding row of every output tile (the rows holding its first and last output): one
+// thread per binding row writes the tiles whose first / last output row falls in it (rows are non-empty,
+// so every tile gets exactly one of each); then whether the tile is regular (full, ≤ 64 rows; slow_all:
+// every tile through k_femit_slow, tests). One pass over the rows instead of two binary searches per tile.
+__global__ void k_femit_bounds(const uint64_t *roff, uint64_t R, uint64_t N, uint64_t *rb) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint64_t rs = roff[r], re = roff[r + 1];
+  for (uint64_t t = (rs + kEwTile - 1) / kEwTile; t * kEwTile < re; ++t) rb[2 * t] = r;  // tiles starting here
+  const uint64_t last = (N - 1) / kEwTile;
+  for (uint64_t t = rs / kEwTile; t <= last; ++t) {  // tiles ending here
+    const uint64_t te = min((t + 1) * (uint64_t)kEwTile, N) - 1;
+    if (te >= re) break;
+    if (te >= rs) rb[2 * t + 1] = r;
+  }
+}
+__global__ void k_femit_classify(const uint64_t *rb, uint64_t N, uint64_t ntiles, uint8_t *regular, int slow_all) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntiles) return;
-  const uint64_t t0 = t * kEwTile, t1 = min(t0 + (uint64_t)kEwTile, N) - 1;
-  const uint64_t r0 = last_le_range(roff, 0, R - 1, t0), r1 = last_le_range(roff, r0, R - 1, t1);
-  rb[2 * t] = r0;
-  rb[2 * t + 1] = r1;
-  regular[t] = !slow_all && r1 - r0 < 64 && t0 + kEwTile <= N;
+  regular[t] = !slow_all && rb[2 * t + 1] - rb[2 * t] < 64 && (t + 1) * kEwTile <= N;
 }
 
 struct EwRows {  // lane k: binding row r0 + k of the tile, as loaded (put into the table one step later)
@@ -464,9 +473,11 @@ void launch_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, cons
 
 void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, bool slow_all, hipStream_t s) {
   const uint64_t nt = femit_tiles(a.N);
-  hipLaunchKernelGGL(k_femit_bounds, dim3(nblocks(nt, 256)), dim3(256), 0, s, a.roff, a.R, a.N, nt, rb, regular,
-                     (int)slow_all);
+  if (!nt || !a.R) return;
+  hipLaunchKernelGGL(k_femit_bounds, dim3(nblocks(a.R, 256)), dim3(256), 0, s, a.roff, a.R, a.N, rb);
   KCHECK("k_femit_bounds");
+  hipLaunchKernelGGL(k_femit_classify, dim3(nblocks(nt, 256)), dim3(256), 0, s, rb, a.N, nt, regular, (int)slow_all);
+  KCHECK("k_femit_classify");
 }
 
 void launch_femit(const FemitArgs &a, const uint32_t *regular_tiles, uint64_t nreg, const uint32_t *other_tiles,
