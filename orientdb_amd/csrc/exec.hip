@@ -189,7 +189,8 @@ class Executor {
     if (const char *fl = std::getenv("OMX_FLIST")) flist_ = std::strcmp(fl, "0") != 0;
     if (const char *fr = std::getenv("OMX_FLIST_REVERSE")) flist_reverse_ = std::strcmp(fr, "0") != 0;
     if (const char *fp = std::getenv("OMX_FLIST_PAIRS")) flist_pairs_ = std::strcmp(fp, "0") != 0;
-    if (const char *fe = std::getenv("OMX_FEMIT")) femit_ = std::strcmp(fe, "0") != 0;
+    if (const char *fe = std::getenv("OMX_FEMIT")) femit_ = std::strcmp(fe, "force") == 0 ? 2 : std::strcmp(fe, "0") != 0 ? 1 : 0;
+    if (const char *fm = std::getenv("OMX_FEMIT_MIN_ET")) femit_min_et_ = std::strtoull(fm, nullptr, 10);
     if (const char *fs = std::getenv("OMX_FEMIT_SORT")) femit_sort_ = std::strcmp(fs, "0") != 0;
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
     if (const char *fv = std::getenv("OMX_FEMIT_REVERSE"))
@@ -1491,7 +1492,13 @@ class Executor {
   // OMX_FEMIT=0: write the rows with the generic unfiltered expansion (binned heavy / merge-path rows)
   // instead of k_femit's output tiles; OMX_FEMIT_SORT=0: keep the rows in their order (the lists are then
   // re-read from HBM / MALL rather than L2)
-  bool femit_ = true, femit_sort_ = true;
+  // OMX_FEMIT: 0 = never, 1 = when the hop traverses at least femit_min_et_ edges (E_t), force = always
+  // (tests). Below that its fixed costs (the row sort, selections, tile lists: ≈ 0.2 ms) outweigh the
+  // faster writes: C2 (RMAT-22, E_t 1.5e9) 1.21 ms against 1.15 binned; M1 (E_t 1.03e10) 4.2 against 5.2
+  // (profiles/r03/femit/c2ab.txt)
+  int femit_ = 1;
+  uint64_t femit_min_et_ = 4000000000ull;
+  bool femit_sort_ = true;
   bool femit_slow_ = false;  // OMX_FEMIT_SLOW=1: every output tile through k_femit_slow (tests)
 
   // step 4 of expand_factorized when the rows are written: the output space Σ_rows |L(g[r])| is laid out
@@ -1717,11 +1724,12 @@ class Executor {
     uint64_t U = 0;
     DBuf<uint32_t> ub, g, perm_s;
     DBuf<uint64_t> ubm;
+    const uint64_t Et = degree_sum(src, R, st.adj);
+    const bool femit = write && femit_ && (femit_ == 2 || Et >= femit_min_et_) && cols.size() <= (size_t)kFemitCols;
     // rows emitted by k_femit_w from the sources' lists: the rows are sorted by source here (the emission
     // wants them grouped), so the distinct sources are the sorted runs' heads and a row's source index
     // is its run — no bitmap, position map or second sort
-    const bool presort = write && femit_ && femit_sort_ && !flist_ && femit_reverse_ == 0 &&
-                         cols.size() <= (size_t)kFemitCols && R > 0;
+    const bool presort = femit && femit_sort_ && !flist_ && femit_reverse_ == 0 && R > 0;
     if (presort) {
       DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
       DBuf<uint8_t> head(&pool_, R);
@@ -1751,7 +1759,6 @@ class Executor {
       ub = bitmap_list(ubm.p, 0, 1, U);
     }
     // the distinct sources' degrees, scanned: doff[u] = the first of u's entries in the flat list space
-    const uint64_t Et = degree_sum(src, R, st.adj);
     const bool tiles = flist_ && st.adj.parts.size() == 1;
     DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1), astart;
     if (tiles) {  // degrees and first col positions of the distinct sources, for the list tiles
@@ -1782,7 +1789,7 @@ class Executor {
       launch_gather_u32(pos.p, src, R, g.p, s_);
       tm_.end(12ull * R);
     }
-    if (!presort && write && femit_ && femit_reverse_ && !dist_ && st.adj.parts.size() == 1 && cols.size() >= 2 &&
+    if (!presort && femit && femit_reverse_ && !dist_ && st.adj.parts.size() == 1 && cols.size() >= 2 &&
         femit_supported((int)cols.size() - 1, 2) && emit_factorized_reverse(st, cols, g, R, U, ubm, iu, pos, EU))
       return true;
     DBuf<unsigned long long> cnt(&pool_, U + 1);
@@ -1929,7 +1936,7 @@ class Executor {
     }
     }
     // 4. the rows over their sources' lists
-    if (write && femit_ && cols.size() <= (size_t)kFemitCols) {
+    if (femit) {
       emit_factorized(g, R, U, loff, lcol, cols, st, presort ? perm_s.p : nullptr);
       return true;
     }

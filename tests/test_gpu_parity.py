@@ -382,6 +382,7 @@ def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, flist, monkeypatch
     # tiles: the lists from the targets' in-rows whenever that reads fewer entries; tiles_forward: always
     # from the sources' rows
     monkeypatch.setenv("OMX_FLIST_REVERSE", "0" if flist == "tiles_forward" else "1")
+    monkeypatch.setenv("OMX_FEMIT", "force")  # the rows written by the output-tiled emission at any size
     monkeypatch.setenv("OMX_FACTOR", "0")
     direct = o.OMatchStatement(q[1]).execute(g, documents=False)
     monkeypatch.setenv("OMX_FACTOR", "force")
@@ -407,7 +408,7 @@ def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, mon
     monkeypatch.setenv("OMX_FACTOR", "0")
     direct = o.OMatchStatement(q[1]).execute(g, documents=False)
     monkeypatch.setenv("OMX_FACTOR", "force")
-    monkeypatch.setenv("OMX_FEMIT", "0" if emit == "binned" else "1")
+    monkeypatch.setenv("OMX_FEMIT", "0" if emit == "binned" else "force")
     monkeypatch.setenv("OMX_FEMIT_SORT", "0" if emit == "unsorted" else "1")
     monkeypatch.setenv("OMX_FEMIT_SLOW", "1" if emit in ("slow", "targets_slow") else "0")
     monkeypatch.setenv("OMX_FEMIT_REVERSE", "force" if emit.startswith("targets") else "0" if emit == "sources" else "1")
@@ -430,7 +431,7 @@ def test_factorized_emission_many_tiles_rmat16(rmat16, side, slow, sort, monkeyp
     monkeypatch.setenv("OMX_FEMIT", "0")
     fl = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST
     base = o.OMatchStatement(q).execute(g, documents=False, flags=fl)
-    monkeypatch.setenv("OMX_FEMIT", "1")
+    monkeypatch.setenv("OMX_FEMIT", "force")
     monkeypatch.setenv("OMX_FEMIT_SORT", sort)
     monkeypatch.setenv("OMX_FEMIT_SLOW", slow)
     monkeypatch.setenv("OMX_FEMIT_REVERSE", "force" if side == "targets" else "0")
