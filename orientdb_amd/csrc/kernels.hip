@@ -1507,14 +1507,21 @@ void launch_expand_heavy_sliced(const ExpandArgs &a, const SliceArgs &sa, unsign
 // group's row data (with the carried values, compacted by k_bin_fill for ≤ 4 columns, so a survivor's
 // columns come from a cross-lane read, not a gather) is loaded while the current one is filtered. Survivors go to the wave's arena (cap
 // ⌈EL/W_q⌉ + 64·heavy_deg rows), compacted by ballot.
-constexpr int kLightStage = 320;  // staged survivors per wave (16 waves × 1.6 KiB beside the slice)
+// Round 3: a slot's owners come from a per-wave byte table instead of a 6-step cross-lane search per
+// slot: per round of 64·U entries the pieces mark their first entry (the round's first entry's owner from
+// one search), a max-scan spreads the marks, and each entry reads its owner's lane as one LDS byte
+// (the search cost 40 of the ≈ 67 VALU operations per entry, PMC profiles/r03/pmc_light).
+constexpr int kLightStage = 256;  // staged survivors per wave (16 waves × 1.25 KiB beside the slice)
 template <bool WRITE, int U, int NC>
 __global__ __launch_bounds__(kSliceBlock) void k_expand_light_sliced(ExpandArgs a, SliceArgs sa) {
   constexpr int NCV = NC > 0 ? NC : 1;
   constexpr int WPB = kSliceBlock / 64;
+  constexpr int RB = U;  // mark bytes per lane and round
+  static_assert(RB % 4 == 0, "a lane's marks are whole words");
   __shared__ uint32_t s_bm[kSliceBits / 32];
   __shared__ uint32_t s_stv[WRITE ? WPB * kLightStage : 1];
   __shared__ uint8_t s_stj[WRITE ? WPB * kLightStage : 1];
+  __shared__ uint32_t s_mk[WPB * 64 * U / 4];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t gw = blockIdx.x * WPB + wave;
@@ -1615,16 +1622,55 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_light_sliced(ExpandArgs 
     }
     const uint32_t pre = incl - len;
     const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    uint32_t *const mkt = s_mk + wave * (64 * U / 4);
+    uint8_t *const mb = reinterpret_cast<uint8_t *>(mkt);
     for (uint32_t base = 0; base < T; base += 64 * U) {
+      // owner of entry base: the last lane j with pre_j ≤ base (zero-length pieces share their
+      // successor's offset); the pieces starting inside the round mark their first entry
+      uint32_t j0 = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if ((uint32_t)__shfl(pre, (int)(j0 + st), 64) <= base) j0 += st;
+#pragma unroll
+      for (int i = 0; i < RB / 4; ++i) mkt[lane * (RB / 4) + i] = 0;
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) mb[0] = (uint8_t)j0;
+      if (len && pre > base && pre < base + 64 * U) mb[pre - base] = (uint8_t)lane;
+      __builtin_amdgcn_wave_barrier();
+      {  // max-scan of the marks: lane l holds bytes RB·l … RB·l + RB − 1
+        uint32_t wd[RB / 4];
+        uint32_t mx = 0;
+#pragma unroll
+        for (int i = 0; i < RB / 4; ++i) {
+          wd[i] = mkt[lane * (RB / 4) + i];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) mx = max(mx, (wd[i] >> (8 * b)) & 0xFFu);
+        }
+        uint32_t sc = mx;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t y = __shfl_up(sc, off, 64);
+          if (lane >= (uint32_t)off) sc = max(sc, y);
+        }
+        uint32_t run = __shfl_up(sc, 1, 64);
+        if (lane == 0) run = 0;
+#pragma unroll
+        for (int i = 0; i < RB / 4; ++i) {
+          uint32_t o = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            run = max(run, (wd[i] >> (8 * b)) & 0xFFu);
+            o |= run << (8 * b);
+          }
+          mkt[lane * (RB / 4) + i] = o;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
       uint32_t nb[U], jj[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t e = base + u * 64 + lane;
-        // owner: the last lane j with pre_j ≤ e (zero-length pieces share their successor's offset)
-        uint32_t j = 0;
-#pragma unroll
-        for (int st = 32; st > 0; st >>= 1)
-          if ((uint32_t)__shfl(pre, (int)(j + st), 64) <= e) j += st;
+        const uint32_t j = mb[u * 64 + lane];
         const uint64_t sj = ((uint64_t)(uint32_t)__shfl((uint32_t)(start >> 32), (int)j, 64) << 32) |
                             (uint32_t)__shfl((uint32_t)start, (int)j, 64);
         const uint32_t pj = (uint32_t)__shfl(pre, (int)j, 64);
@@ -1650,6 +1696,7 @@ __global__ __launch_bounds__(kSliceBlock) void k_expand_light_sliced(ExpandArgs 
           acc += (uint64_t)__popcll(mk);
         }
       }
+      __builtin_amdgcn_wave_barrier();  // the round's marks are rewritten by the next round
     }
     if (WRITE && st) flush(m);
   };
@@ -1675,15 +1722,15 @@ void launch_expand_light_sliced(const ExpandArgs &a, const SliceArgs &sa, unsign
   if (!grid) return;
   const dim3 g(grid), b(kSliceBlock);
   if (!write) {
-    hipLaunchKernelGGL((k_expand_light_sliced<false, 16, 0>), g, b, 0, s, a, sa);
+    hipLaunchKernelGGL((k_expand_light_sliced<false, 8, 0>), g, b, 0, s, a, sa);
   } else {
     switch (a.ncarry) {
-      case 0: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 0>), g, b, 0, s, a, sa); break;
-      case 1: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 1>), g, b, 0, s, a, sa); break;
-      case 2: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 2>), g, b, 0, s, a, sa); break;
-      case 3: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 3>), g, b, 0, s, a, sa); break;
-      case 4: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, 4>), g, b, 0, s, a, sa); break;
-      default: hipLaunchKernelGGL((k_expand_light_sliced<true, 16, -1>), g, b, 0, s, a, sa); break;
+      case 0: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 0>), g, b, 0, s, a, sa); break;
+      case 1: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 1>), g, b, 0, s, a, sa); break;
+      case 2: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 2>), g, b, 0, s, a, sa); break;
+      case 3: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 3>), g, b, 0, s, a, sa); break;
+      case 4: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, 4>), g, b, 0, s, a, sa); break;
+      default: hipLaunchKernelGGL((k_expand_light_sliced<true, 8, -1>), g, b, 0, s, a, sa); break;
     }
   }
   KCHECK("k_expand_light_sliced");
