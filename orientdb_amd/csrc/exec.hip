@@ -193,6 +193,7 @@ class Executor {
     if (const char *fm = std::getenv("OMX_FEMIT_MIN_ET")) femit_min_et_ = std::strtoull(fm, nullptr, 10);
     if (const char *fs = std::getenv("OMX_FEMIT_SORT")) femit_sort_ = std::strcmp(fs, "0") != 0;
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
+    if (const char *sj = std::getenv("OMX_SEMI")) semi_ok_ = std::strcmp(sj, "0") != 0;
     if (const char *fv = std::getenv("OMX_FEMIT_REVERSE"))
       femit_reverse_ = std::strcmp(fv, "force") == 0 ? 2 : std::strcmp(fv, "0") != 0 ? 1 : 0;
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
@@ -257,6 +258,7 @@ class Executor {
           expand_mark(st);
           continue;
         }
+        semi_ = last && !count_only && semi_for(st);
         switch (st.kind) {
           case S_ROOT: root(st); break;
           case S_EXPAND: expand_step(st, !count_only, seg_ok); counted_only = count_only; break;
@@ -273,7 +275,7 @@ class Executor {
     } else {
       R_ = 0;
     }
-    if (!chain) bindings_ = marked_ ? marked_bindings_ : R_;
+    if (!chain) bindings_ = marked_ ? marked_bindings_ : semi_hops_ ? semi_bindings_ : R_;
     uint64_t n = 0;
     int ncols = 0;
     std::vector<DBuf<uint32_t>> out;
@@ -453,6 +455,7 @@ class Executor {
   double arena_margin_ = 1.25;
   bool factor_ = true;           // factorized expansion of filtered hops (OMX_FACTOR=0: direct)
   uint64_t factorized_hops_ = 0;
+  uint64_t semi_hops_ = 0;  // last hops written as a semi-join (Executor::semi_join)
   uint64_t arena_retries_ = 0;
 
   // ---- helpers -----------------------------------------------------------------------------------
@@ -1503,6 +1506,45 @@ class Executor {
 
   // step 4 of expand_factorized when the rows are written: the output space Σ_rows |L(g[r])| is laid out
   // row by row and written by tiles of output rows (factor.hip k_femit)
+  // The last hop of a plan whose projection never reads its new alias (RETURN a.uid, b.age over
+  // a-->b-->c): every document of a row (…, b, c) is the document of (…, b), so the result is that of
+  // the rows whose source has a non-empty filtered list — a semi-join, no (…, b, c) row is written. The
+  // bindings (complete matches before de-duplication) are still Σ_rows |L(b)|; E_t is the hop's.
+  // OMX_SEMI=0: write the rows as any other hop.
+  bool semi_ = false, semi_ok_ = true;
+  uint64_t semi_bindings_ = 0;
+  bool semi_for(const Step &st) const {
+    if (!semi_ok_ || p_.kind != Plan::MATCH || st.kind != S_EXPAND || st.optional || p_.optional[st.dst] ||
+        o_.mode != OMX_MODE_MATERIALIZE)
+      return false;
+    if (p_.proj != Plan::PROJ_ALIASES && p_.proj != Plan::PROJ_EXPR && p_.proj != Plan::PROJ_JSON) return false;
+    return std::find(p_.out_aliases.begin(), p_.out_aliases.end(), st.dst) == p_.out_aliases.end();
+  }
+  void semi_join(const DBuf<uint32_t> &g, uint64_t R, const DBuf<uint64_t> &loff, const std::vector<int> &cols) {
+    DBuf<uint64_t> len(&pool_, R + 1), tot(&pool_, 1);
+    launch_femit_len(g.p, R, loff.p, len.p, s_);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, len.p, tot.p, (int64_t)(R + 1), s_); });
+    DBuf<uint32_t> idx(&pool_, std::max<uint64_t>(R, 1));
+    DBuf<uint64_t> nsel(&pool_, 1);
+    hipcub::CountingInputIterator<uint32_t> cnt(0);
+    hipcub::TransformInputIterator<uint8_t, NonZeroU64, const uint64_t *> fl(len.p, NonZeroU64());
+    cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cnt, fl, idx.p, nsel.p, (int64_t)R, s_); });
+    const uint64_t Rn = read1(nsel.p);
+    semi_bindings_ = read1(tot.p);
+    for (int c : cols) {
+      DBuf<uint32_t> o(&pool_, std::max<uint64_t>(Rn, 1));
+      if (Rn) launch_gather_u32(col_[c].p, idx.p, Rn, o.p, s_);
+      col_[c] = std::move(o);
+    }
+    R_ = Rn;
+    segmented_ = false;
+    factorized_hops_++;
+    semi_hops_++;
+    if (debug_expand_)
+      std::fprintf(stderr, "[omx factorized] semi-join R=%llu kept=%llu bindings=%llu\n", (unsigned long long)R,
+                   (unsigned long long)Rn, (unsigned long long)semi_bindings_);
+  }
+
   // perm_sorted: the rows are already sorted by source (g in that order); perm_sorted[i] = the row at
   // sorted position i
   void emit_factorized(DBuf<uint32_t> &g, uint64_t R, uint64_t U, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol,
@@ -1725,7 +1767,7 @@ class Executor {
     DBuf<uint32_t> ub, g, perm_s;
     DBuf<uint64_t> ubm;
     const uint64_t Et = degree_sum(src, R, st.adj);
-    const bool femit = write && femit_ && (femit_ == 2 || Et >= femit_min_et_) && cols.size() <= (size_t)kFemitCols;
+    const bool femit = write && !semi_ && femit_ && (femit_ == 2 || Et >= femit_min_et_) && cols.size() <= (size_t)kFemitCols;
     // rows emitted by k_femit_w from the sources' lists: the rows are sorted by source here (the emission
     // wants them grouped), so the distinct sources are the sorted runs' heads and a row's source index
     // is its run — no bitmap, position map or second sort
@@ -1925,6 +1967,10 @@ class Executor {
     cub([&](void *t, size_t &b) {
       return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
     });
+    if (write && semi_) {  // the new alias is never read again: the rows whose source has a list
+      semi_join(g, R, loff, cols);
+      return true;
+    }
     lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(l.n, 1));
     if (l.n) {
       HIP_CHECK(hipMemcpyAsync(cnt.p, loff.p, (U + 1) * 8, hipMemcpyDeviceToDevice, s_));

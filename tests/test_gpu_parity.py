@@ -441,6 +441,41 @@ def test_factorized_emission_many_tiles_rmat16(rmat16, side, slow, sort, monkeyp
     assert rs.info["edges_traversed"] == base.info["edges_traversed"]
 
 
+SEMI_QUERIES = [
+    ("ab_of_abc", "MATCH {class:Person,as:a,where:(age < 5)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a, b",
+     ["a", "b"]),
+    ("expr_of_abc", "MATCH {class:Person,as:a,where:(age < 5)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a.uid, b.age",
+     None),
+    ("a_of_abc", "MATCH {class:Person,as:a,where:(age < 20)}-Knows->{as:b}-Knows->{as:c,where:(age > 50)} RETURN a", ["a"]),
+    ("three_hop_abc", "MATCH {class:Person,as:a,where:(uid < 8)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d,where:(age<10)} RETURN a, b, c",
+     ["a", "b", "c"]),
+]
+
+
+@pytest.mark.parametrize("graph", ["simple", "multigraph"])
+@pytest.mark.parametrize("q", SEMI_QUERIES, ids=[q[0] for q in SEMI_QUERIES])
+def test_semi_join_last_hop(rmat10, rmat10_raw, q, graph, monkeypatch):
+    """A factorized last hop whose new alias the projection never reads is a semi-join (the rows whose
+    source has a non-empty filtered list; no row per target is written): the same documents / rows as
+    the oracle and as writing every row (OMX_SEMI=0), the same E_t and bindings (Σ |L(b)|, parallel edges
+    included)."""
+    import orientdb_amd as o
+    g, ref = rmat10 if graph == "simple" else rmat10_raw
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    monkeypatch.setenv("OMX_SEMI", "0")
+    full = o.OMatchStatement(q[1]).execute(g, documents=q[2] is None)
+    monkeypatch.setenv("OMX_SEMI", "1")
+    if q[2] is not None:
+        rs = _parity(g, ref, q[1], q[2])
+    else:
+        rs = o.OMatchStatement(q[1]).execute(g)
+        assert doc_set(rs) == doc_set(oracle_rows(ref.db, q[1]))
+        assert doc_set(rs) == doc_set(full)
+    assert rs.info["n_rows"] == full.info["n_rows"]
+    assert rs.info["edges_traversed"] == full.info["edges_traversed"]
+    assert rs.info["bindings"] == full.info["bindings"]
+
+
 @pytest.mark.parametrize("simple", [True, False], ids=["simple", "multigraph"])
 def test_factorized_auto_threshold_rmat14(simple):
     """The factorized expansion as the planner picks it by itself (≥ 4096 rows whose sources repeat ≥ 4×,
