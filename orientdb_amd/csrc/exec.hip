@@ -194,6 +194,7 @@ class Executor {
     if (const char *fs = std::getenv("OMX_FEMIT_SORT")) femit_sort_ = std::strcmp(fs, "0") != 0;
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
     if (const char *sj = std::getenv("OMX_SEMI")) semi_ok_ = std::strcmp(sj, "0") != 0;
+    if (const char *gq = std::getenv("OMX_GRP32")) grp32_ = std::strcmp(gq, "0") != 0;
     if (const char *fv = std::getenv("OMX_FEMIT_REVERSE"))
       femit_reverse_ = std::strcmp(fv, "force") == 0 ? 2 : std::strcmp(fv, "0") != 0 ? 1 : 0;
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
@@ -1512,6 +1513,7 @@ class Executor {
   // bindings (complete matches before de-duplication) are still Σ_rows |L(b)|; E_t is the hop's.
   // OMX_SEMI=0: write the rows as any other hop.
   bool semi_ = false, semi_ok_ = true;
+  bool grp32_ = true;  // OMX_GRP32=0: 64-bit counters in the factorized grouping
   uint64_t semi_bindings_ = 0;
   bool semi_for(const Step &st) const {
     if (!semi_ok_ || p_.kind != Plan::MATCH || st.kind != S_EXPAND || st.optional || p_.optional[st.dst] ||
@@ -1957,22 +1959,43 @@ class Executor {
     ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, true);
     edges_iter_ += l.E;
     nlist = l.n;
-    // 3. grouped by source: offsets (U + 1) and the neighbours in group order
+    // 3. grouped by source: offsets (U + 1) and the neighbours in group order (segmented lists under
+    // 2^32 entries: 32-bit counters and cursors, half the atomics' footprint)
+    const bool c32 = l.segmented && l.n < (1ull << 32) && grp32_;
+    DBuf<uint32_t> h32;
+    if (c32) {
+      h32 = DBuf<uint32_t>(&pool_, U + 1);
+      HIP_CHECK(hipMemsetAsync(h32.p, 0, (U + 1) * 4, s_));
+    }
     if (l.n) {
       tm_.begin("k_key_hist");
-      if (l.segmented) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, s_);
+      if (c32) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, h32.p, s_);
+      else if (l.segmented) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, s_);
       else launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
-      tm_.end(4ull * l.n + 8ull * U);
+      tm_.end(4ull * l.n + (c32 ? 4ull : 8ull) * U);
     }
-    cub([&](void *t, size_t &b) {
-      return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
-    });
+    if (c32) {
+      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> hc(h32.p, CastU64());
+      cub([&](void *t, size_t &b) {
+        return hipcub::DeviceScan::ExclusiveSum(t, b, hc, loff.p, (int64_t)(U + 1), s_);
+      });
+    } else {
+      cub([&](void *t, size_t &b) {
+        return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
+      });
+    }
     if (write && semi_) {  // the new alias is never read again: the rows whose source has a list
       semi_join(g, R, loff, cols);
       return true;
     }
     lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(l.n, 1));
-    if (l.n) {
+    if (l.n && c32) {
+      DBuf<uint32_t> cur(&pool_, U + 1);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, h32.p, cur.p, (int64_t)(U + 1), s_); });
+      tm_.begin("k_key_scatter");
+      launch_key_scatter_seg(l.carry[0].p, l.dst.p, l.seg_start.p, l.seg_count.p, l.nseg, cur.p, lcol.p, s_);
+      tm_.end(12ull * l.n + 4ull * U);
+    } else if (l.n) {
       HIP_CHECK(hipMemcpyAsync(cnt.p, loff.p, (U + 1) * 8, hipMemcpyDeviceToDevice, s_));
       tm_.begin("k_key_scatter");
       if (l.segmented)

@@ -270,6 +270,11 @@ void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const u
                          unsigned long long *counts, hipStream_t s);
 void launch_key_scatter_seg(const uint32_t *key, const uint32_t *val, const uint64_t *seg_start, const uint32_t *seg_count,
                             uint32_t nseg, unsigned long long *cursor, uint32_t *out, hipStream_t s);
+// 32-bit counters and cursors (fewer than 2^32 entries)
+void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
+                         unsigned int *counts, hipStream_t s);
+void launch_key_scatter_seg(const uint32_t *key, const uint32_t *val, const uint64_t *seg_start, const uint32_t *seg_count,
+                            uint32_t nseg, unsigned int *cursor, uint32_t *out, hipStream_t s);
 void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, unsigned long long *cursor, uint32_t *out,
                         hipStream_t s);
 void launch_pack_pairs(const uint32_t *hi, const uint32_t *lo, uint64_t n, uint64_t *keys, hipStream_t s);
