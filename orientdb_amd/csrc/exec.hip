@@ -487,6 +487,12 @@ class Executor {
     std::atomic_thread_fence(std::memory_order_acquire);
     return g_.h_mail;
   }
+  // two u64 words in one host round trip (dptr[0], dptr[1])
+  std::pair<uint64_t, uint64_t> read2(const uint64_t *dptr) {
+    launch_post_words(dptr, 2, mail(), s_, 8);
+    const uint64_t *w = wait_mail();
+    return {w[0], w[1]};
+  }
   template <class T>
   T read1(const T *dptr) {
     static_assert(sizeof(T) == 4 || sizeof(T) == 8, "read1 reads one 4- or 8-byte word");
@@ -1523,16 +1529,16 @@ class Executor {
     return std::find(p_.out_aliases.begin(), p_.out_aliases.end(), st.dst) == p_.out_aliases.end();
   }
   void semi_join(const DBuf<uint32_t> &g, uint64_t R, const DBuf<uint64_t> &loff, const std::vector<int> &cols) {
-    DBuf<uint64_t> len(&pool_, R + 1), tot(&pool_, 1);
+    DBuf<uint64_t> len(&pool_, R + 1), nsel(&pool_, 2);  // nsel: {kept rows, bindings}
     launch_femit_len(g.p, R, loff.p, len.p, s_);
-    cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, len.p, tot.p, (int64_t)(R + 1), s_); });
+    cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, len.p, nsel.p + 1, (int64_t)(R + 1), s_); });
     DBuf<uint32_t> idx(&pool_, std::max<uint64_t>(R, 1));
-    DBuf<uint64_t> nsel(&pool_, 1);
     hipcub::CountingInputIterator<uint32_t> cnt(0);
     hipcub::TransformInputIterator<uint8_t, NonZeroU64, const uint64_t *> fl(len.p, NonZeroU64());
     cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cnt, fl, idx.p, nsel.p, (int64_t)R, s_); });
-    const uint64_t Rn = read1(nsel.p);
-    semi_bindings_ = read1(tot.p);
+    const auto kb = read2(nsel.p);
+    const uint64_t Rn = kb.first;
+    semi_bindings_ = kb.second;
     for (int c : cols) {
       DBuf<uint32_t> o(&pool_, std::max<uint64_t>(Rn, 1));
       if (Rn) launch_gather_u32(col_[c].p, idx.p, Rn, o.p, s_);
@@ -1551,28 +1557,29 @@ class Executor {
   // sorted position i
   void emit_factorized(DBuf<uint32_t> &g, uint64_t R, uint64_t U, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol,
                        const std::vector<int> &cols, const Step &st, const uint32_t *perm_sorted = nullptr) {
-    // 1. the rows whose list is not empty (the others write nothing), in row order or grouped by source
+    // 1. the rows whose list is not empty (the others write nothing), in row order or grouped by source.
+    // Their count Rn stays on the device until the output size N is known: the kernels in between run
+    // over R rows and read Rn, so one host round trip returns both
     DBuf<uint64_t> len(&pool_, R + 1);
     launch_femit_len(g.p, R, loff.p, len.p, s_);
     DBuf<uint32_t> idx(&pool_, R);
-    DBuf<uint64_t> nsel(&pool_, 1);
+    DBuf<uint64_t> nsel(&pool_, 2);
     {
       hipcub::CountingInputIterator<uint32_t> cnt(0);
       hipcub::TransformInputIterator<uint8_t, NonZeroU64, const uint64_t *> fl(len.p, NonZeroU64());
       cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cnt, fl, idx.p, nsel.p, (int64_t)R, s_); });
     }
-    const uint64_t Rn = read1(nsel.p);
-    DBuf<uint32_t> gs(&pool_, std::max<uint64_t>(Rn, 1)), perm;
+    const uint64_t *rn = nsel.p;
+    DBuf<uint32_t> gs(&pool_, std::max<uint64_t>(R, 1)), perm;
     if (perm_sorted) {  // grouped already: the non-empty rows keep their sorted order
+      perm = DBuf<uint32_t>(&pool_, std::max<uint64_t>(R, 1));
+      launch_gather_u32_dev(g.p, idx.p, rn, R, gs.p, s_);
+      launch_gather_u32_dev(perm_sorted, idx.p, rn, R, perm.p, s_);
+    } else if (femit_sort_ && R > 1) {  // grouped by source: a list is re-read from L2 by its rows
+      const uint64_t Rn = read1(nsel.p);
+      DBuf<uint32_t> gk(&pool_, std::max<uint64_t>(Rn, 1));
       perm = DBuf<uint32_t>(&pool_, std::max<uint64_t>(Rn, 1));
-      if (Rn) {
-        launch_gather_u32(g.p, idx.p, Rn, gs.p, s_);
-        launch_gather_u32(perm_sorted, idx.p, Rn, perm.p, s_);
-      }
-    } else if (femit_sort_ && Rn > 1) {  // grouped by source: a list is re-read from L2 by its rows
-      DBuf<uint32_t> gk(&pool_, Rn);
-      perm = DBuf<uint32_t>(&pool_, Rn);
-      launch_gather_u32(g.p, idx.p, Rn, gk.p, s_);
+      if (Rn) launch_gather_u32(g.p, idx.p, Rn, gk.p, s_);
       tm_.begin("femit_row_sort");
       cub([&](void *t, size_t &b) {
         return hipcub::DeviceRadixSort::SortPairs(t, b, gk.p, gs.p, idx.p, perm.p, (int64_t)Rn, 0,
@@ -1580,20 +1587,23 @@ class Executor {
       });
       tm_.end(16ull * Rn * ((bits_for(U) + 7) / 8));
     } else {
-      if (Rn) launch_gather_u32(g.p, idx.p, Rn, gs.p, s_);
+      launch_gather_u32_dev(g.p, idx.p, rn, R, gs.p, s_);
       perm = std::move(idx);
     }
     std::vector<DBuf<uint32_t>> sc;
     for (int c : cols) {
-      sc.emplace_back(&pool_, std::max<uint64_t>(Rn, 1));
-      if (Rn) launch_gather_u32(col_[c].p, perm.p, Rn, sc.back().p, s_);
+      sc.emplace_back(&pool_, std::max<uint64_t>(R, 1));
+      launch_gather_u32_dev(col_[c].p, perm.p, rn, R, sc.back().p, s_);
     }
-    // 2. output rows of every binding row: the scan of its list length; list position of output o
-    DBuf<uint64_t> roff(&pool_, Rn + 1), rbase(&pool_, std::max<uint64_t>(Rn, 1));
-    launch_femit_len(gs.p, Rn, loff.p, len.p, s_);
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, len.p, roff.p, (int64_t)(Rn + 1), s_); });
-    if (Rn) launch_femit_base(gs.p, Rn, loff.p, roff.p, rbase.p, s_);
-    const uint64_t N = read1(roff.p + Rn);
+    // 2. output rows of every binding row: the scan of its list length (rows ≥ Rn: 0, so roff[R] = N);
+    // list position of output o
+    DBuf<uint64_t> roff(&pool_, R + 1), rbase(&pool_, std::max<uint64_t>(R, 1));
+    launch_femit_len(gs.p, R, loff.p, len.p, s_, rn);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, len.p, roff.p, (int64_t)(R + 1), s_); });
+    launch_femit_base(gs.p, R, loff.p, roff.p, rbase.p, s_, rn);
+    HIP_CHECK(hipMemcpyAsync(nsel.p + 1, roff.p + R, 8, hipMemcpyDeviceToDevice, s_));
+    const auto rn_n = read2(nsel.p);
+    const uint64_t Rn = rn_n.first, N = rn_n.second;
     edges_iter_ += N;
     alg_bytes_ += 8ull * R + 4ull * N * (cols.size() + 2);  // as expand_core's unfiltered written hop
     R_ = N;
@@ -1641,12 +1651,13 @@ class Executor {
     launch_femit_bounds(a, rb.p, reg.p, femit_slow_, s_);
     hipcub::CountingInputIterator<uint32_t> it(0);
     cub([&](void *t, size_t &b) { return hipcub::DevicePartition::Flagged(t, b, it, reg.p, lists.p, nreg.p, (int64_t)nt, s_); });
-    const uint64_t nr = read1(nreg.p);
-    if (debug_expand_)
+    if (debug_expand_) {
+      const uint64_t nr = read1(nreg.p);
       std::fprintf(stderr, "[omx factorized] emission tiles %llu: regular %llu, other %llu\n", (unsigned long long)nt,
                    (unsigned long long)nr, (unsigned long long)(nt - nr));
+    }
     tm_.begin("k_femit");
-    launch_femit(a, lists.p, nr, lists.p + nr, nt - nr, cus(), s_);
+    launch_femit(a, lists.p, nreg.p, nt, cus(), s_);  // the kernels read the partition's count (no host wait)
     // every list column read and every column written per output row; per binding row its offsets and
     // constants
     tm_.end(a.N * 4ull * (2ull * a.nl + a.nc) + a.R * (24ull + 4ull * a.nc));

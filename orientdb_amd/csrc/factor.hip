@@ -250,20 +250,23 @@ __global__ void k_flist_group_offsets(const uint32_t *keys, uint64_t n, const ui
 constexpr int kEwTile = OMX_EW_TILE, kEwWaves = OMX_EW_WAVES, kEwJ = kEwTile / 64;
 static_assert(kEwTile <= 256 * 64, "a lane's mark bytes are read as u32 words");
 
-__global__ void k_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len) {
+// len[r] = |L(g[r])| for r < n, 0 for n ≤ r ≤ R; n = *nd when nd is given (a device count ≤ R), else R
+__global__ void k_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, const uint64_t *nd) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r > R) return;
-  if (r == R) {
-    len[R] = 0;
+  const uint64_t n = nd ? *nd : R;
+  if (r >= n) {
+    len[r] = 0;
     return;
   }
   const uint32_t u = g[r];
   len[r] = loff[u + 1] - loff[u];
 }
 
-__global__ void k_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, const uint64_t *roff, uint64_t *rbase) {
+__global__ void k_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, const uint64_t *roff, uint64_t *rbase,
+                             const uint64_t *nd) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < R) rbase[r] = loff[g[r]] - roff[r];
+  if (r < (nd ? *nd : R)) rbase[r] = loff[g[r]] - roff[r];
 }
 
 // first and last binding row of every output tile (the rows holding its first and last output): one
@@ -392,12 +395,15 @@ __device__ __forceinline__ void ew_store(const FemitArgs &a, const EwTable<NL, N
   }
 }
 
-// tiles: the regular tiles, n of them
+// tiles: the regular tiles, *nreg of them (a device count: the partition's, read by the kernel, so the
+// host does not wait for it between the partition and the launch)
 template <int NL, int NC>
 __global__ __launch_bounds__(64 * kEwWaves) void k_femit_w(FemitArgs a, const uint32_t *__restrict__ tiles,
-                                                          const uint64_t *__restrict__ rb, uint64_t n) {
+                                                          const uint64_t *__restrict__ rb,
+                                                          const uint64_t *__restrict__ nreg) {
   __shared__ EwTable<NL, NC> s_tb[kEwWaves][2];
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t n = *nreg;
   const uint64_t W = (uint64_t)gridDim.x * kEwWaves;
   uint64_t i = (uint64_t)blockIdx.x * kEwWaves + wv;
   if (i >= n) return;
@@ -434,8 +440,13 @@ __global__ __launch_bounds__(64 * kEwWaves) void k_femit_w(FemitArgs a, const ui
 #undef OMX_EW_STEP
 }
 
-// the other tiles: one workgroup each, every output row's binding row by a search of the row offsets
-__global__ __launch_bounds__(256) void k_femit_slow(FemitArgs a, const uint32_t *tiles, uint64_t n) {
+// the other tiles (tiles[*nreg, nt)): one workgroup each, every output row's binding row by a search of
+// the row offsets
+__global__ __launch_bounds__(256) void k_femit_slow(FemitArgs a, const uint32_t *all_tiles, const uint64_t *nreg,
+                                                    uint64_t nt) {
+  const uint64_t nr = *nreg;
+  const uint32_t *tiles = all_tiles + nr;
+  const uint64_t n = nt - nr;
   for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint64_t t = tiles[i], t0 = t * kEwTile, r0 = a.rb[2 * t], r1 = a.rb[2 * t + 1];
     const uint32_t ne = (uint32_t)min((uint64_t)kEwTile, a.N - t0);
@@ -460,14 +471,16 @@ uint64_t femit_tiles(uint64_t N) { return (N + kEwTile - 1) / kEwTile; }
 // (1…3, 2) the (source, target) pairs over the rows grouped by source
 bool femit_supported(int nl, int nc) { return (nl == 1 && nc <= 4) || (nc == 2 && nl >= 1 && nl <= 3); }
 
-void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s) {
-  hipLaunchKernelGGL(k_femit_len, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, g, R, loff, len);
+void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s,
+                      const uint64_t *nd) {
+  hipLaunchKernelGGL(k_femit_len, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, g, R, loff, len, nd);
   KCHECK("k_femit_len");
 }
 
 void launch_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, const uint64_t *roff, uint64_t *rbase,
-                       hipStream_t s) {
-  hipLaunchKernelGGL(k_femit_base, dim3(nblocks(R, 256)), dim3(256), 0, s, g, R, loff, roff, rbase);
+                       hipStream_t s, const uint64_t *nd) {
+  if (!R) return;
+  hipLaunchKernelGGL(k_femit_base, dim3(nblocks(R, 256)), dim3(256), 0, s, g, R, loff, roff, rbase, nd);
   KCHECK("k_femit_base");
 }
 
@@ -480,28 +493,26 @@ void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, boo
   KCHECK("k_femit_classify");
 }
 
-void launch_femit(const FemitArgs &a, const uint32_t *regular_tiles, uint64_t nreg, const uint32_t *other_tiles,
-                  uint64_t nother, int cus, hipStream_t s) {
+void launch_femit(const FemitArgs &a, const uint32_t *tiles, const uint64_t *nreg, uint64_t nt, int cus,
+                  hipStream_t s) {
   if (a.nc > kFemitCols || a.nl < 1 || a.nl > kFemitLists || !femit_supported(a.nl, a.nc))
     fail(OMX_E_INVALID, "internal: no k_femit_w instance for these columns");
-  if (nreg) {
-    // one workgroup per CU, all resident at once: the tiles are assigned statically
-    const dim3 grid((unsigned)std::min<uint64_t>((nreg + kEwWaves - 1) / kEwWaves, (uint64_t)cus)), blk(64 * kEwWaves);
+  if (!nt) return;
+  // one workgroup per CU, all resident at once: the tiles are assigned statically (sized for all nt tiles;
+  // waves past the regular count exit at once)
+  const dim3 grid((unsigned)std::min<uint64_t>((nt + kEwWaves - 1) / kEwWaves, (uint64_t)cus)), blk(64 * kEwWaves);
 #define OMX_FEMIT_CASE(L, C) \
-  case L * 8 + C: hipLaunchKernelGGL((k_femit_w<L, C>), grid, blk, 0, s, a, regular_tiles, a.rb, nreg); break;
-    switch (a.nl * 8 + a.nc) {
-      OMX_FEMIT_CASE(1, 0) OMX_FEMIT_CASE(1, 1) OMX_FEMIT_CASE(1, 2) OMX_FEMIT_CASE(1, 3) OMX_FEMIT_CASE(1, 4)
-      OMX_FEMIT_CASE(2, 2) OMX_FEMIT_CASE(3, 2)
-      default: break;
-    }
+  case L * 8 + C: hipLaunchKernelGGL((k_femit_w<L, C>), grid, blk, 0, s, a, tiles, a.rb, nreg); break;
+  switch (a.nl * 8 + a.nc) {
+    OMX_FEMIT_CASE(1, 0) OMX_FEMIT_CASE(1, 1) OMX_FEMIT_CASE(1, 2) OMX_FEMIT_CASE(1, 3) OMX_FEMIT_CASE(1, 4)
+    OMX_FEMIT_CASE(2, 2) OMX_FEMIT_CASE(3, 2)
+    default: break;
+  }
 #undef OMX_FEMIT_CASE
-    KCHECK("k_femit_w");
-  }
-  if (nother) {
-    hipLaunchKernelGGL(k_femit_slow, dim3((unsigned)std::min<uint64_t>(nother, (uint64_t)cus * 8)), dim3(256), 0, s, a,
-                       other_tiles, nother);
-    KCHECK("k_femit_slow");
-  }
+  KCHECK("k_femit_w");
+  hipLaunchKernelGGL(k_femit_slow, dim3((unsigned)std::min<uint64_t>(nt, (uint64_t)cus * 4)), dim3(256), 0, s, a, tiles,
+                     nreg, nt);
+  KCHECK("k_femit_slow");
 }
 
 uint64_t flist_tiles(uint64_t EU) { return (EU + kFlTile - 1) / kFlTile; }

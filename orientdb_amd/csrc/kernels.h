@@ -253,15 +253,18 @@ struct FemitArgs {
 bool femit_supported(int nl, int nc);
 uint64_t femit_tiles(uint64_t N);
 // len[r] = |L(g[r])| for r < R, len[R] = 0
-void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s);
+// nd: a device row count ≤ R (rows past it: length 0, no base); nullptr: all R rows
+void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s,
+                      const uint64_t *nd = nullptr);
 void launch_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, const uint64_t *roff, uint64_t *rbase,
-                       hipStream_t s);
+                       hipStream_t s, const uint64_t *nd = nullptr);
 // rb[2·femit_tiles(N)]: first / last binding row of every output tile; regular[t] = the tile is full and
 // spans at most 64 binding rows (slow_all: none is)
 void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, bool slow_all, hipStream_t s);
-// a.rb set: the regular tiles through k_femit_w, the others through k_femit_slow
-void launch_femit(const FemitArgs &a, const uint32_t *regular_tiles, uint64_t nreg, const uint32_t *other_tiles,
-                  uint64_t nother, int cus, hipStream_t s);
+// a.rb set: tiles[0, *nreg) (the regular ones) through k_femit_w, tiles[*nreg, nt) through k_femit_slow;
+// nreg is a device count
+void launch_femit(const FemitArgs &a, const uint32_t *tiles, const uint64_t *nreg, uint64_t nt, int cus,
+                  hipStream_t s);
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
 // head[i] = 1 where a run of equal sorted keys starts
 void launch_run_heads(const uint32_t *sorted, uint64_t n, uint8_t *head, hipStream_t s);
@@ -289,6 +292,9 @@ void launch_flag_no_neighbor(const uint32_t *src, uint64_t R, const DAdj &adj, c
 void launch_check_optional(const uint32_t *src, uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
                            uint32_t V, unsigned int *npe, hipStream_t s);
 void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out, hipStream_t s);
+// out[i] = src[idx[i]] for i < *nd (a device count ≤ cap)
+void launch_gather_u32_dev(const uint32_t *src, const uint32_t *idx, const uint64_t *nd, uint64_t cap, uint32_t *out,
+                           hipStream_t s);
 void launch_scatter_u32(const uint32_t *idx, const uint32_t *val, uint64_t n, uint32_t *out, hipStream_t s);
 void launch_flag_row_change(int ncols, const uint32_t *const *cols, uint64_t n, uint8_t *flags, hipStream_t s);
 // TRAVERSE: RID lookup of the target records; a level's history / WHILE filter with first-position

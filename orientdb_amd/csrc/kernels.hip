@@ -2702,6 +2702,17 @@ void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uin
   hipLaunchKernelGGL(k_gather_u32, dim3(nblocks(n, 256)), dim3(256), 0, s, src, idx, n, out);
   KCHECK("k_gather_u32");
 }
+// the same for a device count *nd ≤ cap (threads for cap entries)
+__global__ void k_gather_u32_dev(const uint32_t *src, const uint32_t *idx, const uint64_t *nd, uint32_t *out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < *nd) out[i] = src[idx[i]];
+}
+void launch_gather_u32_dev(const uint32_t *src, const uint32_t *idx, const uint64_t *nd, uint64_t cap, uint32_t *out,
+                           hipStream_t s) {
+  if (!cap) return;
+  hipLaunchKernelGGL(k_gather_u32_dev, dim3(nblocks(cap, 256)), dim3(256), 0, s, src, idx, nd, out);
+  KCHECK("k_gather_u32_dev");
+}
 
 __global__ void k_flag_row_change(int ncols, ColPtrs cp, uint64_t n, uint8_t *flags) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
