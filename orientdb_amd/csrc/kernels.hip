@@ -215,10 +215,31 @@ __device__ __forceinline__ bool atom_true(const DPred &P, int k, uint64_t raw, b
   const int64_t b = P.atom_i[k];
   return atom_cmp(P.atom_op[k], x < b ? -1 : (x > b ? 1 : 0));
 }
+// class c ∈ the predicate's polymorphic class set: the 4 mask words selected in registers (an index
+// into the kernel-argument array by a lane value is a memory load, and the wave waits for it)
+struct ClassMask {
+  uint64_t m[4];
+};
+__device__ __forceinline__ ClassMask class_mask_regs(const DPred &P) {
+  ClassMask r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)  // readfirstlane: values in SGPRs (a select of them cannot become a load)
+    r.m[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(P.class_mask[k] >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)P.class_mask[k]);
+  return r;
+}
+__device__ __forceinline__ bool class_in_mask(const ClassMask &cm, uint32_t c) {
+  const uint32_t w = c >> 6;
+  // masks, not selects (a select chain is turned back into an indexed load)
+  const uint64_t m = (cm.m[0] & (0ull - (uint64_t)(w == 0))) | (cm.m[1] & (0ull - (uint64_t)(w == 1))) |
+                     (cm.m[2] & (0ull - (uint64_t)(w == 2))) | (cm.m[3] & (0ull - (uint64_t)(w == 3)));
+  return (m >> (c & 63)) & 1ull;
+}
 __global__ __launch_bounds__(256) void k_eval_atoms(DPred P, uint32_t V, uint64_t *words, uint64_t nwords) {
   constexpr int EV = kEvalWords;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t w0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64 * EV;
+  const ClassMask cm = class_mask_regs(P);
   uint64_t vv[EV];
   uint32_t cls[EV];
   uint64_t raw[4][EV];
@@ -243,7 +264,7 @@ __global__ __launch_bounds__(256) void k_eval_atoms(DPred P, uint32_t V, uint64_
   for (int e = 0; e < EV; ++e) {
     const uint64_t v = (w0 + e) * 64 + lane;
     bool b = v < V;
-    if (P.use_class) b = b && ((P.class_mask[cls[e] >> 6] >> (cls[e] & 63)) & 1ull);
+    if (P.use_class) b = b && class_in_mask(cm, cls[e]);
     bool acc = P.conj != 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -263,26 +284,32 @@ __global__ __launch_bounds__(256) void k_eval_atoms4(DPred P, uint32_t V, uint64
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t w0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64 * 4;  // 4 words (256 vertices) per wave
   const uint64_t v0 = w0 * 64 + 4 * lane;
+  const ClassMask cm = class_mask_regs(P);
   uint32_t cls[4] = {0, 0, 0, 0};
-  uint32_t raw[4][4];
-  const bool full = v0 + 3 < V;
-  if (P.use_class) {
-    if (full) {
-      const uint2 c2 = *reinterpret_cast<const uint2 *>(P.vclass + v0);
-      cls[0] = c2.x & 0xFFFFu, cls[1] = c2.x >> 16, cls[2] = c2.y & 0xFFFFu, cls[3] = c2.y >> 16;
-    } else {
+  uint32_t raw[4][4] = {};
+  // wave-uniform: every wave but the last takes 16-byte column loads and 8-byte class loads, all issued
+  // before any is used (a per-lane test made the compiler select between both forms and wait in between)
+  const bool full = __builtin_amdgcn_readfirstlane((int)((w0 + 4) * 64 <= (uint64_t)V)) != 0;
+  if (full) {
+    uint2 c2 = make_uint2(0, 0);
+    if (P.use_class) c2 = *reinterpret_cast<const uint2 *>(P.vclass + v0);
+    uint4 x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < P.n_atoms) x[k] = *reinterpret_cast<const uint4 *>((const uint32_t *)P.atom_c[k].values + v0);
+    cls[0] = c2.x & 0xFFFFu, cls[1] = c2.x >> 16, cls[2] = c2.y & 0xFFFFu, cls[3] = c2.y >> 16;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < P.n_atoms) raw[k][0] = x[k].x, raw[k][1] = x[k].y, raw[k][2] = x[k].z, raw[k][3] = x[k].w;
+  } else {
+    if (P.use_class) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) cls[j] = P.vclass[v0 + j < V ? v0 + j : (uint64_t)V - 1];
     }
-  }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (k >= P.n_atoms) break;  // uniform
-    const uint32_t *c = (const uint32_t *)P.atom_c[k].values;
-    if (full) {
-      const uint4 x = *reinterpret_cast<const uint4 *>(c + v0);
-      raw[k][0] = x.x, raw[k][1] = x.y, raw[k][2] = x.z, raw[k][3] = x.w;
-    } else {
+    for (int k = 0; k < 4; ++k) {
+      if (k >= P.n_atoms) break;  // uniform
+      const uint32_t *c = (const uint32_t *)P.atom_c[k].values;
 #pragma unroll
       for (int j = 0; j < 4; ++j) raw[k][j] = c[v0 + j < V ? v0 + j : (uint64_t)V - 1];
     }
@@ -291,7 +318,7 @@ __global__ __launch_bounds__(256) void k_eval_atoms4(DPred P, uint32_t V, uint64
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     bool b = v0 + j < V;
-    if (P.use_class) b = b && ((P.class_mask[cls[j] >> 6] >> (cls[j] & 63)) & 1ull);
+    if (P.use_class) b = b && class_in_mask(cm, cls[j]);
     bool acc = P.conj != 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
