@@ -1039,15 +1039,45 @@ __device__ __forceinline__ void block_excl_scan_k(uint64_t (&x)[K], uint64_t (&t
   }
 }
 
+// The binning keys' block scan with the per-slice chunk counts packed two to a u64 (lo, hi halves):
+// 3 + MAXP/2 scans instead of 3 + MAXP, so the 16-slice kernels hold half the registers (226 VGPRs, 2
+// waves per SIMD, before). A half cannot carry into the other: a block's chunks of one slice stay far
+// below 2^32 (that would take > 2^41 edges in 256 rows).
+template <int MAXP>
+constexpr int bin_scan_keys() { return kBinKeys + (MAXP + 1) / 2; }
+template <int B, int MAXP>
+__device__ __forceinline__ void bin_block_scan(uint64_t (&x)[kBinKeys + MAXP], uint64_t (&tot)[kBinKeys + MAXP],
+                                               uint64_t *s_w) {
+  constexpr int NP = (MAXP + 1) / 2, K2 = kBinKeys + NP;
+  uint64_t y[K2], t2[K2];
+#pragma unroll
+  for (int k = 0; k < kBinKeys; ++k) y[k] = x[k];
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+    y[kBinKeys + i] = x[kBinKeys + 2 * i] | (2 * i + 1 < MAXP ? x[kBinKeys + 2 * i + 1] << 32 : 0ull);
+  block_excl_scan_k<B, K2>(y, t2, s_w);
+#pragma unroll
+  for (int k = 0; k < kBinKeys; ++k) x[k] = y[k], tot[k] = t2[k];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    x[kBinKeys + 2 * i] = (uint32_t)y[kBinKeys + i];
+    tot[kBinKeys + 2 * i] = (uint32_t)t2[kBinKeys + i];
+    if (2 * i + 1 < MAXP) {
+      x[kBinKeys + 2 * i + 1] = y[kBinKeys + i] >> 32;
+      tot[kBinKeys + 2 * i + 1] = t2[kBinKeys + i] >> 32;
+    }
+  }
+}
+
 template <bool SLICED, int MAXP>
 __global__ __launch_bounds__(kBinBlock) void k_bin_count(const uint32_t *src, uint64_t R, DAdj adj, DCuts cuts,
                                                           uint64_t heavy_deg, uint32_t P, uint64_t *blk, uint32_t cs) {
   constexpr int K = kBinKeys + MAXP;
-  __shared__ uint64_t s_w[K * (kBinBlock / 64)];
+  __shared__ uint64_t s_w[bin_scan_keys<MAXP>() * (kBinBlock / 64)];
   const uint64_t r = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x;
   uint64_t x[K], tot[K];
   row_bins<SLICED, MAXP>(src, r, R, adj, cuts, heavy_deg, P, x, cs);
-  block_excl_scan_k<kBinBlock, K>(x, tot, s_w);
+  bin_block_scan<kBinBlock, MAXP>(x, tot, s_w);
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < K; ++k)
@@ -1155,13 +1185,13 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_fill(const uint32_t *src, uin
                                                          LightRows lr, ChunkDesc *chunks, SliceChunk *schunks,
                                                          uint32_t cs) {
   constexpr int K = kBinKeys + MAXP;
-  __shared__ uint64_t s_w[K * (kBinBlock / 64)];
+  __shared__ uint64_t s_w[bin_scan_keys<MAXP>() * (kBinBlock / 64)];
   const uint64_t r = (uint64_t)blockIdx.x * kBinBlock + threadIdx.x;
   const uint32_t nb = gridDim.x;
   uint64_t x[K], tot[K];
   row_bins<SLICED, MAXP>(src, r, R, adj, cuts, heavy_deg, P, x, cs);
   const uint64_t heavy = x[1], light = x[2];
-  block_excl_scan_k<kBinBlock, K>(x, tot, s_w);
+  bin_block_scan<kBinBlock, MAXP>(x, tot, s_w);
   if (r > R) return;
   const uint64_t lo = x[0] + blk[blockIdx.x];
   if (lr.row) {
