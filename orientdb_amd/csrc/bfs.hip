@@ -56,26 +56,41 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
   __shared__ uint64_t s_r[4][kB / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint64_t te = 0, td = 0, tn = 0, tl = 0;
-  for (uint64_t v0 = vlo + (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
-    const uint64_t v = v0 + threadIdx.x;
-    const uint64_t f = v < V ? frontier[v] : 0;
-    uint64_t m = 0;
-    if (f) {
-      const uint64_t vis = visited[v];
-      m = f & ~vis;
-      if (m) visited[v] = vis | m;
-      if (expand && while_bm && !bm_test(while_bm, (uint32_t)v)) m = 0;
-      if (m != f) frontier[v] = m;
-      if (m && expand) {
-        const uint64_t d = adj_degree(adj, (uint32_t)v);
-        te += (uint64_t)__popcll(m) * d;
-        td += d;
-        tn += 1;
-        tl |= m;
-      }
+  // kPrepU block-strides per round, their frontier words loaded together (clamped, unconditional)
+  // before any store: one iteration at a time waited a memory round trip per 256 vertices, since each
+  // iteration's load came after the previous one's stores (vector memory completes in order)
+  constexpr int kPrepU = 4;
+  for (uint64_t b0 = vlo + (uint64_t)blockIdx.x * kB * kPrepU; b0 < V; b0 += (uint64_t)gridDim.x * kB * kPrepU) {
+    uint64_t fu[kPrepU];
+#pragma unroll
+    for (int u = 0; u < kPrepU; ++u) {
+      const uint64_t v = b0 + (uint64_t)u * kB + threadIdx.x;
+      const uint64_t x = frontier[v < V ? v : V - 1];
+      fu[u] = v < V ? x : 0;
     }
-    const uint64_t word = __ballot(m != 0);  // bit v of fbm: v's frontier mask is non-empty
-    if (fbm && lane == 0 && v0 + wave * 64 < V) fbm[(v0 >> 6) + wave] = word;
+#pragma unroll
+    for (int u = 0; u < kPrepU; ++u) {
+      const uint64_t v0 = b0 + (uint64_t)u * kB;
+      const uint64_t v = v0 + threadIdx.x;
+      const uint64_t f = fu[u];
+      uint64_t m = 0;
+      if (f) {
+        const uint64_t vis = visited[v];
+        m = f & ~vis;
+        if (m) visited[v] = vis | m;
+        if (expand && while_bm && !bm_test(while_bm, (uint32_t)v)) m = 0;
+        if (m != f) frontier[v] = m;
+        if (m && expand) {
+          const uint64_t d = adj_degree(adj, (uint32_t)v);
+          te += (uint64_t)__popcll(m) * d;
+          td += d;
+          tn += 1;
+          tl |= m;
+        }
+      }
+      const uint64_t word = __ballot(m != 0);  // bit v of fbm: v's frontier mask is non-empty
+      if (fbm && lane == 0 && v0 + wave * 64 < V) fbm[(v0 >> 6) + wave] = word;
+    }
   }
   if (!expand) return;
   te = wave_sum_u64(te);
@@ -104,7 +119,7 @@ void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const ui
                      const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s, uint32_t vlo) {
   if (vlo && fbm) fail(OMX_E_INVALID, "internal: the frontier bitmap covers whole words from vertex 0");
   if (V <= vlo) return;
-  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V - vlo, kB), (uint64_t)cus * 8);
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V - vlo, kB * 4), (uint64_t)cus * 8);
   hipLaunchKernelGGL(k_bfs_prep, dim3(g), dim3(kB), 0, s, frontier, visited, vlo, V, while_bm, (int)expand, adj, stats,
                      fbm);
   KCHECK("k_bfs_prep");
@@ -115,20 +130,35 @@ __global__ __launch_bounds__(kB) void k_bfs_list(const uint64_t *frontier, uint3
                                                  unsigned long long *count) {
   __shared__ uint32_t s_w[kB / 64];
   __shared__ uint32_t s_base;
-  for (uint64_t v0 = (uint64_t)blockIdx.x * kB; v0 < V; v0 += (uint64_t)gridDim.x * kB) {
-    const uint64_t v = v0 + threadIdx.x;
-    const bool act = v < V && frontier[v] != 0;
+  // 4 block-strides per round: their words loaded together, one scan and one atomic for all (the list's
+  // order inside a round is thread-major; the push does not depend on it)
+  constexpr int kListU = 4;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * kB * kListU; b0 < V; b0 += (uint64_t)gridDim.x * kB * kListU) {
+    uint64_t fu[kListU];
+#pragma unroll
+    for (int u = 0; u < kListU; ++u) {
+      const uint64_t v = b0 + (uint64_t)u * kB + threadIdx.x;
+      fu[u] = frontier[v < V ? v : V - 1];
+    }
+    uint32_t n = 0;
+#pragma unroll
+    for (int u = 0; u < kListU; ++u) n += (b0 + (uint64_t)u * kB + threadIdx.x < V && fu[u] != 0) ? 1u : 0u;
     uint32_t tot;
-    const uint32_t off = block_excl_scan<kB>(act ? 1u : 0u, s_w, &tot);
+    uint32_t off = block_excl_scan<kB>(n, s_w, &tot);
     if (threadIdx.x == 0 && tot) s_base = (uint32_t)atomicAdd(count, (unsigned long long)tot);
     __syncthreads();
-    if (act) list[s_base + off] = (uint32_t)v;
+#pragma unroll
+    for (int u = 0; u < kListU; ++u) {
+      const uint64_t v = b0 + (uint64_t)u * kB + threadIdx.x;
+      if (v < V && fu[u] != 0) list[s_base + off++] = (uint32_t)v;
+    }
     __syncthreads();
   }
 }
 void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsigned long long *count, int cus,
                      hipStream_t s) {
-  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 8);
+  if (!V) return;
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V, kB * 4), (uint64_t)cus * 8);
   hipLaunchKernelGGL(k_bfs_list, dim3(g), dim3(kB), 0, s, frontier, V, list, count);
   KCHECK("k_bfs_list");
 }
