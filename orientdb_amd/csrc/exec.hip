@@ -195,6 +195,7 @@ class Executor {
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
     if (const char *sj = std::getenv("OMX_SEMI")) semi_ok_ = std::strcmp(sj, "0") != 0;
     if (const char *gq = std::getenv("OMX_GRP32")) grp32_ = std::strcmp(gq, "0") != 0;
+    if (const char *gr = std::getenv("OMX_GRANK")) grank_ = std::strcmp(gr, "0") != 0;
     if (const char *fv = std::getenv("OMX_FEMIT_REVERSE"))
       femit_reverse_ = std::strcmp(fv, "force") == 0 ? 2 : std::strcmp(fv, "0") != 0 ? 1 : 0;
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
@@ -1520,6 +1521,10 @@ class Executor {
   // OMX_SEMI=0: write the rows as any other hop.
   bool semi_ = false, semi_ok_ = true;
   bool grp32_ = true;  // OMX_GRP32=0: 64-bit counters in the factorized grouping
+  // OMX_GRANK=1: the 32-bit grouping writes each entry's rank in the hist pass and places it without
+  // atomics. Off by default: at M1 the two passes took 78 + 136 µs against 72 + 121 µs for hist +
+  // cursor scatter (the scattered 4-byte writes are both placements' cost; profiles/r03/rank2)
+  bool grank_ = false;
   uint64_t semi_bindings_ = 0;
   bool semi_for(const Step &st) const {
     if (!semi_ok_ || p_.kind != Plan::MATCH || st.kind != S_EXPAND || st.optional || p_.optional[st.dst] ||
@@ -1978,12 +1983,18 @@ class Executor {
       h32 = DBuf<uint32_t>(&pool_, U + 1);
       HIP_CHECK(hipMemsetAsync(h32.p, 0, (U + 1) * 4, s_));
     }
+    // the lists written (not a semi-join): ranks in the hist pass, then placement without atomics
+    const bool ranked = c32 && grank_ && !(write && semi_);
+    DBuf<uint32_t> rank;
     if (l.n) {
       tm_.begin("k_key_hist");
-      if (c32) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, h32.p, s_);
+      if (ranked) {
+        rank = DBuf<uint32_t>(&pool_, l.carry[0].n);  // indexed like the keys: arena positions, not 0..n
+        launch_key_rank_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, h32.p, rank.p, s_);
+      } else if (c32) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, h32.p, s_);
       else if (l.segmented) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, s_);
       else launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
-      tm_.end(4ull * l.n + (c32 ? 4ull : 8ull) * U);
+      tm_.end((ranked ? 8ull : 4ull) * l.n + (c32 ? 4ull : 8ull) * U);
     }
     if (c32) {
       hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> hc(h32.p, CastU64());
@@ -2000,7 +2011,11 @@ class Executor {
       return true;
     }
     lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(l.n, 1));
-    if (l.n && c32) {
+    if (l.n && ranked) {
+      tm_.begin("k_key_scatter");
+      launch_key_place_seg(l.carry[0].p, l.dst.p, rank.p, l.seg_start.p, l.seg_count.p, l.nseg, loff.p, lcol.p, s_);
+      tm_.end(16ull * l.n);
+    } else if (l.n && c32) {
       DBuf<uint32_t> cur(&pool_, U + 1);
       cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, h32.p, cur.p, (int64_t)(U + 1), s_); });
       tm_.begin("k_key_scatter");

@@ -273,6 +273,12 @@ void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const u
                          unsigned long long *counts, hipStream_t s);
 void launch_key_scatter_seg(const uint32_t *key, const uint32_t *val, const uint64_t *seg_start, const uint32_t *seg_count,
                             uint32_t nseg, unsigned long long *cursor, uint32_t *out, hipStream_t s);
+// rank[i] = entry i's place in its key's group (counts[key] advanced by one atomic per run), then
+// out[loff[key[i]] + rank[i]] = val[i] (fewer than 2^32 entries)
+void launch_key_rank_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
+                         unsigned int *counts, uint32_t *rank, hipStream_t s);
+void launch_key_place_seg(const uint32_t *key, const uint32_t *val, const uint32_t *rank, const uint64_t *seg_start,
+                          const uint32_t *seg_count, uint32_t nseg, const uint64_t *loff, uint32_t *out, hipStream_t s);
 // 32-bit counters and cursors (fewer than 2^32 entries)
 void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
                          unsigned int *counts, hipStream_t s);

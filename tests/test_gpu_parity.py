@@ -392,7 +392,7 @@ def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, flist, monkeypatch
     assert rs.info["bindings"] == direct.info["bindings"]
 
 
-@pytest.mark.parametrize("emit", ["binned", "unsorted", "slow", "sources", "targets", "targets_slow", "grp64"])
+@pytest.mark.parametrize("emit", ["binned", "unsorted", "slow", "sources", "targets", "targets_slow", "grp64", "ranks"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
 def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, monkeypatch):
@@ -402,7 +402,8 @@ def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, mon
     k_femit_slow (a search of the row offsets per output row); sources = the lists always built from the
     sources' side; targets = always from the targets' side (the (b, c) pairs of the targets' in-rows
     written over the rows grouped by source, no lists), also through the slow tiles; grp64 = the lists
-    grouped with 64-bit counters and cursors (OMX_GRP32=0; 32-bit by default). Same rows, E_t and
+    grouped with 64-bit counters and cursors (OMX_GRP32=0; 32-bit by default); ranks = each entry's rank
+    written in the hist pass and placed without atomics (OMX_GRANK=1). Same rows, E_t and
     bindings as the direct expansion (P/OMatchStatement.java:491-497 per row)."""
     import orientdb_amd as o
     g, ref = rmat10 if graph == "simple" else rmat10_raw
@@ -412,8 +413,9 @@ def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, mon
     monkeypatch.setenv("OMX_FEMIT", "0" if emit == "binned" else "force")
     monkeypatch.setenv("OMX_FEMIT_SORT", "0" if emit == "unsorted" else "1")
     monkeypatch.setenv("OMX_FEMIT_SLOW", "1" if emit in ("slow", "targets_slow") else "0")
-    monkeypatch.setenv("OMX_FEMIT_REVERSE", "force" if emit.startswith("targets") else "0" if emit in ("sources", "grp64") else "1")
+    monkeypatch.setenv("OMX_FEMIT_REVERSE", "force" if emit.startswith("targets") else "0" if emit in ("sources", "grp64", "ranks") else "1")
     monkeypatch.setenv("OMX_GRP32", "0" if emit == "grp64" else "1")
+    monkeypatch.setenv("OMX_GRANK", "1" if emit == "ranks" else "0")
     rs = _parity(g, ref, q[1], q[2])
     assert rs.info["edges_traversed"] == direct.info["edges_traversed"]
     assert rs.info["bindings"] == direct.info["bindings"]
