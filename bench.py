@@ -76,7 +76,7 @@ HOT_KERNELS = ("k_femit", "k_expand_heavy", "k_expand_heavy_sliced", "k_expand_l
                "k_expand_light_check", "k_expand_heavy_check", "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit", "k_bfs_push", "k_bfs_prep", "k_bfs_emit",
                "k_gather_cols", "k_compact_segments")
 # timer records that are spans over other records or move no HBM bytes (not summed into a step)
-SPAN_RECORDS = ("expand_total", "documents", "exchange")
+SPAN_RECORDS = ("expand_total", "documents", "exchange", "deliver_d2h")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md §Chip-level parameters)
 
 
@@ -179,7 +179,7 @@ def cpu_baseline_shortest(g, query, target_s):
                       "1 thread)" % (reps, secs, seen[0])}
 
 
-def cpu_baseline(g, query, target_s=12.0):
+def cpu_baseline(g, query, target_s=12.0, single_thread_too=False):
     """The oracle's C DFS restatement (oracle/dfs_ref.c) on the host cores, on a bounded sample of
     the same workload's roots; GTEPS over the sampled roots."""
     import numpy as np
@@ -199,13 +199,22 @@ def cpu_baseline(g, query, target_s=12.0):
     if "." in ret:  # RETURN expressions: the DFS enumerates the same bindings of the aliases they read
         import re as _re
         query = head + "RETURN " + ",".join(sorted(set(_re.findall(r"\b([a-z]+)\.", ret))))
-    probe = dfs.run(cg, query, nthreads=threads, emit=False, root_sample=64)
     import re
     m = re.search(r"\((age|uid) < (\d+)\)", query.split("-")[0])
     nroots_total = int(np.count_nonzero(cg.columns[m.group(1)] < int(m.group(2)))) if m else g.V
+    out = dfs_sample(dfs, cg, query, threads, target_s, nroots_total)
+    out["cores_visible"] = visible
+    if single_thread_too:  # configs[0]: the faithful one-thread DFS beside the port on the job's cores
+        one = dfs_sample(dfs, cg, query, 1, target_s / 2, nroots_total)
+        out["single_thread"] = {k: one[k] for k in ("value", "unit", "cores", "kind", "sample", "bindings_per_s")}
+    return out
+
+
+def dfs_sample(dfs, cg, query, threads, target_s, nroots_total):
+    """oracle/dfs_ref.c over a bounded root sample, repeated until ≈ target_s of CPU work is timed."""
+    probe = dfs.run(cg, query, nthreads=threads, emit=False, root_sample=64)
     per_root = max(probe["seconds"] / max(probe["nroots"], 1), 1e-7)
     sample = int(min(nroots_total, max(64, target_s / per_root)))
-    # repeat the bounded sample until ≈ target_s of CPU work has been timed
     edges = bindings = 0
     secs = 0.0
     reps = 0
@@ -216,10 +225,10 @@ def cpu_baseline(g, query, target_s=12.0):
         secs += r["seconds"]
         reps += 1
     return {"value": edges / secs / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
-            "sample": "%d of %d roots x %d repetitions (%.1f s, %d edges, %d bindings; oracle/dfs_ref.c DFS, %d threads "
-                      "= the job's host-core share (OMP_NUM_THREADS), %d cores visible)" % (
-                sample, nroots_total, reps, secs, edges, bindings, threads, visible),
-            "bindings_per_s": bindings / secs, "cores_visible": visible}
+            "sample": "%d of %d roots x %d repetitions (%.1f s, %d edges, %d bindings; oracle/dfs_ref.c DFS, %d "
+                      "thread%s)" % (sample, nroots_total, reps, secs, edges, bindings, threads,
+                                     "" if threads == 1 else "s = the job's host-core share (OMP_NUM_THREADS)"),
+            "bindings_per_s": bindings / secs}
 
 
 def reduce_over_ranks(dist, dt, edges, bindings, rows):
@@ -270,6 +279,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--count", action="store_true", help="COUNT mode (the last hop counts its rows)")
+    ap.add_argument("--no-deliver", action="store_true", help="skip the RID map + D2H hand-over measurement")
     ap.add_argument("--replicated", action="store_true",
                     help="N > 1: replicate the graph and shard roots (weak scaling) instead of 1-D partitioning it")
     args = ap.parse_args()
@@ -354,6 +364,24 @@ def main():
     prof = st.execute(g, **dict(run_kw, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_KERNEL_TIMING))
     step_bytes = sum(k["alg_bytes"] for k in prof.kernel_launches if k["name"] not in SPAN_RECORDS)
     step_kernel_ms = sum(k["ms"] for k in prof.kernel_launches if k["name"] not in SPAN_RECORDS)
+    deliver = None
+    if world == 1 and mode == o.OMX_MODE_MATERIALIZE and not args.no_deliver and not infos[-1]["documents"]:
+        # the dense → RID map and the D2H hand-over of the rows, reported apart from the
+        # step: one more execution without KEEP_DEVICE (the rows mapped to RIDs on the device, then
+        # copied into libomx's host buffer, pageable memory, as an OResultSet fill would read them)
+        t1 = time.perf_counter()
+        d = st.execute(g, **dict(run_kw, flags=o.OMX_FLAG_KERNEL_TIMING, fetch_rows=False))
+        wall = (time.perf_counter() - t1) * 1e3
+        ks = {k["name"]: k for k in d.kernel_stats}
+        nrows, ncols = d.info["n_rows"], d.info["n_cols"]
+        mp, d2h = ks.get("k_map_rids", {"ms": 0.0}), ks.get("deliver_d2h", {"ms": 0.0})
+        deliver = {"rows": nrows, "cols": ncols, "bytes": nrows * ncols * 8, "wall_ms": wall,
+                   "map_rids_ms": mp["ms"], "d2h_ms": d2h["ms"],
+                   "d2h_GBps": nrows * ncols * 8 / (d2h["ms"] / 1e3) / 1e9 if d2h["ms"] > 0 else None,
+                   "note": "one execution outside the timed steps without OMX_FLAG_KEEP_DEVICE: rows mapped to u64 "
+                           "RIDs on the device (k_map_rids) and copied to a pageable host buffer (deliver_d2h); "
+                           "wall_ms is the whole execute including the step"}
+        del d
     edges = sum(i["edges_traversed"] for i in infos)
     edges_read = sum(i["edges_read"] for i in infos)
     bindings = sum(i["bindings"] for i in infos)
@@ -377,13 +405,19 @@ def main():
     per_step = [[k for k in sl if k["name"] == dom] for sl in step_launches]
     nslots = min((len(x) for x in per_step), default=0)
     slots = [{"ms": sum(x[j]["ms"] for x in per_step) / len(per_step),
-              "alg_bytes": sum(x[j]["alg_bytes"] for x in per_step) / len(per_step)} for j in range(nslots)]
+              "alg_bytes": sum(x[j]["alg_bytes"] for x in per_step) / len(per_step),
+              "hbm_bytes": sum(x[j].get("hbm_bytes", x[j]["alg_bytes"]) for x in per_step) / len(per_step)}
+             for j in range(nslots)]
     main_slot = max(range(nslots), key=lambda j: slots[j]["ms"]) if nslots else None
     if main_slot is not None and slots[main_slot]["ms"] > 0:
         launch = slots[main_slot]
     else:
         launch = {"ms": exp["ms"] / max(exp["launches"], 1), "alg_bytes": exp["alg_bytes"] / max(exp["launches"], 1)}
+        launch["hbm_bytes"] = launch["alg_bytes"]
     achieved = launch["alg_bytes"] / (launch["ms"] / 1e3) / 1e9 if launch["ms"] > 0 else 0.0
+    # the bytes HBM must move at least (each distinct byte once: a factorized hop's lists and a pull
+    # level's frontier masks are re-read from L2 by the rows / in-edges sharing them) per launch time
+    hbm_gbs = launch["hbm_bytes"] / (launch["ms"] / 1e3) / 1e9 if launch["ms"] > 0 else 0.0
     ms_step = dt_max / args.steps * 1e3
     out = {
         "metric": METRIC,
@@ -421,6 +455,10 @@ def main():
                      "launch": ("launch %d of %d per step (the one with the most device time)" % (main_slot + 1, nslots)
                                 if main_slot is not None else "all launches"),
                      "alg_bytes_per_launch": launch["alg_bytes"], "avg_launch_ms": launch["ms"],
+                     # achieved/frac count SURVEY §8(d)'s algorithmic bytes, L2 re-reads included; hbm_frac
+                     # counts each distinct byte once; pmc_frac is the measured PMC traffic (below)
+                     "hbm_bytes_per_launch": launch["hbm_bytes"], "hbm_achieved": hbm_gbs,
+                     "hbm_frac": hbm_gbs / HBM_PEAK_GBS, "pmc_frac": None,
                      "launches_per_step": slots,
                      "kernel_total": {"alg_bytes_per_step": exp["alg_bytes"] / args.steps,
                                       "ms_per_step": exp["ms"] / args.steps},
@@ -433,13 +471,16 @@ def main():
                         "GBps": (v["alg_bytes"] / (v["ms"] / 1e3) / 1e9) if v["ms"] > 0 else None}
                     for k, v in sorted(kst.items(), key=lambda kv: -kv[1]["ms"])},
         "cpu_baseline": None,
+        "deliver": deliver,
     }
     tr = measured_traffic(args, dom, default_scale, world)
     if tr is not None:
         out["roofline"]["traffic"] = tr["bytes_per_launch"]
         out["roofline"]["traffic_source"] = tr["source"] + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+        if launch["ms"] > 0:  # the PMC pass's bytes over this run's launch time
+            out["roofline"]["pmc_frac"] = tr["bytes_per_launch"] / (launch["ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(g, query, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(g, query, args.cpu_seconds, single_thread_too=args.query == "c1")
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -193,6 +193,10 @@ typedef struct omx_result_info {
                              /* 0: rows are RID tuples (omx_result_rows)                             */
   int32_t factorized_hops;   /* filtered hops run through the factorized expansion (distinct       */
                              /* sources → grouped filtered lists → rows over the lists; diagnostic) */
+  uint64_t rows_gathered;    /* partitioned runs whose projection needs the whole result (RETURN     */
+                             /* expressions, $elements, LIMIT): rows this rank received when the     */
+                             /* rows met on rank 0 — distinct tuples only, each rank de-duplicates   */
+                             /* its hash share first; 0 elsewhere (diagnostic)                       */
 } omx_result_info;
 
 /* A null binding (an unmatched optional node, P/OMatchStatement.java:448-458) in omx_result_rows. */
@@ -210,6 +214,10 @@ int omx_result_kernel_stat(const omx_result *r, int32_t i, const char **name, in
 /* The same timing launch by launch, in issue order (a kernel launched several times per execution,
  * e.g. a first hop and a row emission, is reported per launch). Returns OMX_E_INVALID past the end. */
 int omx_result_kernel_launch(const omx_result *r, int32_t i, const char **name, double *ms, uint64_t *alg_bytes);
+/* Launch i's byte counts: alg_bytes as above, and hbm_bytes, the bytes HBM must move at least — each
+ * distinct byte once, so data a kernel shares between work items and re-reads from L2 (a factorized
+ * hop's lists, a pull level's frontier masks) counts once. Returns OMX_E_INVALID past the end. */
+int omx_result_kernel_launch_bytes(const omx_result *r, int32_t i, uint64_t *alg_bytes, uint64_t *hbm_bytes);
 void omx_result_free(omx_result *r);
 
 /* One field of a result document (info.documents = 1): the value of RETURN item `col` (or of JSON key

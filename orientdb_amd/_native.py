@@ -61,7 +61,8 @@ class omx_result_info(C.Structure):
     _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_int32), ("deduplicated", C.c_int32),
                 ("edges_traversed", C.c_uint64), ("bindings", C.c_uint64), ("alg_bytes", C.c_uint64),
                 ("device_ms", C.c_double), ("total_ms", C.c_double), ("edges_read", C.c_uint64),
-                ("digest", C.c_uint64), ("documents", C.c_int32), ("factorized_hops", C.c_int32)]
+                ("digest", C.c_uint64), ("documents", C.c_int32), ("factorized_hops", C.c_int32),
+                ("rows_gathered", C.c_uint64)]
 
 
 OMX_NULL_RID = (1 << 64) - 1  # a null binding (unmatched optional node)
@@ -93,6 +94,7 @@ SIGNATURES = {
                                          C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "omx_result_kernel_launch": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_char_p), C.POINTER(C.c_double),
                                           C.POINTER(C.c_uint64)]),
+    "omx_result_kernel_launch_bytes": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "omx_result_free": (None, [C.c_void_p]),
     "omx_result_cell": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int32, C.POINTER(omx_cell)]),
     "omx_result_column": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),

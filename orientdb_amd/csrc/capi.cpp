@@ -341,7 +341,7 @@ void omx_exec_options_init(omx_exec_options *o) {
 
 int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, omx_result **out) {
   omx::Transport *t = opts && opts->comm ? opts->comm->t.get() : nullptr;
-  const uint64_t exchanges0 = t ? t->exchanges : 0;
+  bool running = false;
   const int rc = guard([&] {
     if (!g || !s || !out) omx::fail(OMX_E_INVALID, "null argument");
     omx_exec_options o;
@@ -357,14 +357,15 @@ int omx_execute(omx_graph *g, omx_statement *s, const omx_exec_options *opts, om
       s->plan_key = key;
     }
     std::lock_guard<std::mutex> lk(g->m);
-    *out = omx::execute_plan(*g->g, *s->plan, o, t);
+    *out = omx::execute_plan(*g->g, *s->plan, o, t, &running);
   });
   // A rank that fails releases the peers waiting for it in an exchange; the communicator is unusable
-  // afterwards. The exception is OMX_E_UNSUPPORTED raised before this call's first exchange: the
-  // planner and the plan's partition checks see the same statement, parameters and replicated schema
-  // on every rank, so every rank refused alike, nobody waits, the host falls back to the reference
-  // engine and the communicator stays usable for the next query.
-  if (rc != OMX_OK && t && (rc != OMX_E_UNSUPPORTED || t->exchanges != exchanges0)) t->abort();
+  // afterwards. The exception is OMX_E_UNSUPPORTED raised by the planner or the plan's partition checks,
+  // before execution starts: they see the same statement, parameters and replicated schema on every
+  // rank, so every rank refused alike, nobody waits, the host falls back to the reference engine and the
+  // communicator stays usable for the next query. A refusal raised during execution may depend on the
+  // rank's own rows (a size limit), so it aborts like any other failure.
+  if (rc != OMX_OK && t && (rc != OMX_E_UNSUPPORTED || running)) t->abort();
   return rc;
 }
 
@@ -435,6 +436,14 @@ int omx_result_kernel_launch(const omx_result *r, int32_t i, const char **name, 
   if (name) *name = k.name.c_str();
   if (ms) *ms = k.ms;
   if (alg_bytes) *alg_bytes = k.bytes;
+  return OMX_OK;
+}
+
+int omx_result_kernel_launch_bytes(const omx_result *r, int32_t i, uint64_t *alg_bytes, uint64_t *hbm_bytes) {
+  if (!r || i < 0 || (size_t)i >= r->klaunches.size()) return OMX_E_INVALID;
+  const auto &k = r->klaunches[i];
+  if (alg_bytes) *alg_bytes = k.bytes;
+  if (hbm_bytes) *hbm_bytes = k.hbm;
   return OMX_OK;
 }
 

@@ -18,6 +18,7 @@ struct omx_result {
     int64_t launches = 0;
     double ms = 0;
     uint64_t bytes = 0;
+    uint64_t hbm = 0;  // the bytes HBM must move at least (each distinct byte once; L2 re-reads excluded)
   };
   std::vector<KStat> kstats;
   std::vector<KStat> klaunches;  // every timed launch in issue order (launches = 1 each)
@@ -34,5 +35,7 @@ struct omx_result {
 namespace omx {
 class Transport;
 // tr: the ranks' communicator for a partitioned snapshot (nullptr otherwise)
-omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts, Transport *tr = nullptr);
+// *running (if given) is set once the plan's partition checks passed and execution started
+omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts, Transport *tr = nullptr,
+                         bool *running = nullptr);
 }

@@ -52,7 +52,8 @@ class Timer {
     static const char *const kHot[] = {"k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light",
                                        "k_expand_light_sliced", "k_expand_light_check", "k_expand_heavy_check",
                                        "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit", "k_bfs_push",
-                                       "k_bfs_emit", "k_trav_filter", "trav_select", "k_flist_tile", "k_femit"};
+                                       "k_bfs_emit", "k_trav_filter", "trav_select", "k_femit",
+                                       "k_isect_merge"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
     return false;
@@ -73,22 +74,31 @@ class Timer {
     recs_.push_back(r);
     open_.push_back(recs_.size() - 1);
   }
-  void end(uint64_t bytes = 0) {
+  // bytes: the algorithmic bytes; hbm: the bytes HBM must move at least, when a kernel
+  // re-reads data it shares between work items from L2 (default: the algorithmic bytes)
+  void end(uint64_t bytes = 0, uint64_t hbm = UINT64_MAX) {
     if (open_.empty()) return;
     last_ = open_.back();
     open_.pop_back();
     if (last_ == SIZE_MAX) return;
     recs_[last_].bytes = bytes;
+    recs_[last_].hbm = hbm == UINT64_MAX ? bytes : hbm;
     HIP_CHECK(hipEventRecord(recs_[last_].b, recs_[last_].s));
   }
   // algorithmic bytes of the region just closed, when they are only known after the launch
-  void amend(uint64_t bytes) {
-    if (last_ != SIZE_MAX) recs_[last_].bytes = bytes;
+  void amend(uint64_t bytes, uint64_t hbm = UINT64_MAX) {
+    if (last_ != SIZE_MAX) {
+      recs_[last_].bytes = bytes;
+      recs_[last_].hbm = hbm == UINT64_MAX ? bytes : hbm;
+    }
   }
   // index of the region just closed (SIZE_MAX when it was not recorded)
   size_t last() const { return last_; }
-  void amend_at(size_t i, uint64_t bytes) {
-    if (i < recs_.size()) recs_[i].bytes = bytes;
+  void amend_at(size_t i, uint64_t bytes, uint64_t hbm = UINT64_MAX) {
+    if (i < recs_.size()) {
+      recs_[i].bytes = bytes;
+      recs_[i].hbm = hbm == UINT64_MAX ? bytes : hbm;
+    }
   }
   // precondition: the stream has completed (Executor::run waits for its end event first)
   void collect(std::vector<omx_result::KStat> &out, std::vector<omx_result::KStat> &each) {
@@ -96,15 +106,16 @@ class Timer {
     for (auto &r : recs_) {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
-      each.push_back({r.name, 1, ms, r.bytes});
+      each.push_back({r.name, 1, ms, r.bytes, r.hbm});
       auto it = std::find_if(out.begin(), out.end(), [&](const omx_result::KStat &k) { return k.name == r.name; });
       if (it == out.end()) {
-        out.push_back({r.name, 0, 0, 0});
+        out.push_back({r.name, 0, 0, 0, 0});
         it = out.end() - 1;
       }
       it->launches++;
       it->ms += ms;
       it->bytes += r.bytes;
+      it->hbm += r.hbm;
     }
   }
 
@@ -123,7 +134,7 @@ class Timer {
     std::string name;
     hipEvent_t a, b;
     hipStream_t s;
-    uint64_t bytes = 0;
+    uint64_t bytes = 0, hbm = 0;
   };
   bool on_, hot_only_;
   std::vector<size_t> open_;
@@ -169,6 +180,10 @@ class Executor {
       slice_shift_ = (uint32_t)std::min<long>(20, std::max<long>(6, std::strtol(sh, nullptr, 10)));
     if (const char *f = std::getenv("OMX_FUSE_CHECK")) fuse_mode_ = f;  // "0" disables the intersection
     if (const char *sw = std::getenv("OMX_SWAP_CHECK")) swap_ = std::strcmp(sw, "0") != 0;
+    // OMX_MERGE: "0" keeps every closing check a binary-search probe; "force" merges every row whose two
+    // lists fit a tile (tests); OMX_MERGE_RATIO: merge when the longer list is ≤ ratio × the shorter
+    if (const char *mg = std::getenv("OMX_MERGE")) merge_ = std::strcmp(mg, "force") == 0 ? 2 : std::strcmp(mg, "0") != 0 ? 1 : 0;
+    if (const char *mr = std::getenv("OMX_MERGE_RATIO")) merge_ratio_ = std::max(1.0, std::strtod(mr, nullptr));
     if (const char *hb = std::getenv("OMX_PULL_HUBS")) pull_hubs_ = (uint32_t)std::strtoul(hb, nullptr, 10);
     if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max(1e-9, std::strtod(d, nullptr));
     if (const char *lv = std::getenv("OMX_PULL_LIVE")) pull_live_ = std::strcmp(lv, "0") != 0;
@@ -186,18 +201,11 @@ class Executor {
       factor_ = std::strcmp(fz, "0") != 0;
       if (std::strcmp(fz, "force") == 0) factor_min_rows_ = 1, factor_min_ratio_ = 0;
     }
-    if (const char *fl = std::getenv("OMX_FLIST")) flist_ = std::strcmp(fl, "0") != 0;
-    if (const char *fr = std::getenv("OMX_FLIST_REVERSE")) flist_reverse_ = std::strcmp(fr, "0") != 0;
-    if (const char *fp = std::getenv("OMX_FLIST_PAIRS")) flist_pairs_ = std::strcmp(fp, "0") != 0;
     if (const char *fe = std::getenv("OMX_FEMIT")) femit_ = std::strcmp(fe, "force") == 0 ? 2 : std::strcmp(fe, "0") != 0 ? 1 : 0;
     if (const char *fm = std::getenv("OMX_FEMIT_MIN_ET")) femit_min_et_ = std::strtoull(fm, nullptr, 10);
-    if (const char *fs = std::getenv("OMX_FEMIT_SORT")) femit_sort_ = std::strcmp(fs, "0") != 0;
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
     if (const char *sj = std::getenv("OMX_SEMI")) semi_ok_ = std::strcmp(sj, "0") != 0;
     if (const char *gq = std::getenv("OMX_GRP32")) grp32_ = std::strcmp(gq, "0") != 0;
-    if (const char *gr = std::getenv("OMX_GRANK")) grank_ = std::strcmp(gr, "0") != 0;
-    if (const char *fv = std::getenv("OMX_FEMIT_REVERSE"))
-      femit_reverse_ = std::strcmp(fv, "force") == 0 ? 2 : std::strcmp(fv, "0") != 0 ? 1 : 0;
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
     if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
     if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
@@ -227,7 +235,6 @@ class Executor {
     bool counted_only = false;
     std::vector<DBuf<uint32_t>> chain_out;
     if (chain) {
-      if (dist_ || o_.shard_world > 1) unsupported("TRAVERSE / SELECT expand() on a partitioned or sharded execution");
       chain_out.push_back(p_.kind == Plan::TRAVERSE ? traverse_bfs()
                           : p_.kind == Plan::SELECT ? select_expand()
                                                     : shortest_path());
@@ -282,7 +289,10 @@ class Executor {
     int ncols = 0;
     std::vector<DBuf<uint32_t>> out;
     // partitioned + distinct projection: equal tuples meet on one rank first
-    if (dist_ && !empty && !counted_only && gather0_) route_rank0();
+    if (dist_ && !empty && !counted_only && gather0_) {
+      pre_rank0_distinct();
+      route_rank0();
+    }
     else if (dist_ && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
     const bool sp_doc = p_.kind == Plan::SHORTEST_PATH && !p_.chain.expand_rows;
     const bool docs = p_.proj == Plan::PROJ_EXPR || p_.proj == Plan::PROJ_JSON || sp_doc;
@@ -321,7 +331,10 @@ class Executor {
       std::vector<const uint32_t *> cp;
       for (auto &c : out) cp.push_back(c.p);
       int64_t lim = p_.limit >= 0 ? p_.limit : o_.limit;
-      if (devproj_ && !p_.out_aliases.empty() && device_projection_ok(g_, p_, nullptr)) {
+      // with LIMIT the host evaluator runs: it stops at the limit-th distinct document, as
+      // addSingleResult :737-750 does, so an error in a later row is never raised (the device evaluates
+      // every row); row indices are u32 in the device dedup table
+      if (devproj_ && lim < 0 && n < UINT32_MAX && !p_.out_aliases.empty() && device_projection_ok(g_, p_, nullptr)) {
         // scalar items: evaluated and de-duplicated by content on the device (projdev.hip)
         tm_.begin("k_pj_eval");
         device_project(g_, p_, cp, n, lim, cus(), s_, *res);
@@ -360,7 +373,9 @@ class Executor {
       launch_map_rids(ncols, cp.data(), n, (o_.flags & OMX_FLAG_NO_RID_MAP) ? nullptr : g_.d_rids, rids.p, g_.V, s_);
       tm_.end(n * ncols * 12);
       res->rows.resize(n * ncols);
+      tm_.begin("deliver_d2h");  // the rows' hand-over to the host (reported apart from the step)
       HIP_CHECK(hipMemcpyAsync(res->rows.data(), rids.p, n * ncols * sizeof(uint64_t), hipMemcpyDeviceToHost, s_));
+      tm_.end(n * ncols * sizeof(uint64_t));
     }
     mark("launched");
     HIP_CHECK(hipEventRecord(eb, s_));
@@ -384,6 +399,7 @@ class Executor {
     res->info.edges_traversed = edges_;
     res->info.edges_read = edges_iter_;
     res->info.factorized_hops = (int32_t)factorized_hops_;
+    res->info.rows_gathered = rows_gathered_;
     res->info.digest = digest_;
     res->info.documents = docs ? 1 : 0;
     res->info.bindings = bindings_;
@@ -441,6 +457,8 @@ class Executor {
   std::string varlen_mode_ = "auto";
   std::string fuse_mode_ = "1";
   bool swap_ = true;  // fused closing check iterates the shorter of the two lists (OMX_SWAP_CHECK=0: off)
+  int merge_ = 1;     // fused closing check: merge path for lists of comparable lengths (isect.hip)
+  double merge_ratio_ = 8;
   // hub masks packed for the pull kernel in degree-rank order (8 MiB); 0 = plain col. 2^20 measured best
   // of 2^17…2^22 at C3 (profiles/r02/c3rank: pull 4.26 → 4.07 ms per step against 2^18 in vertex order)
   uint32_t pull_hubs_ = 1u << 20;
@@ -544,24 +562,30 @@ class Executor {
     const uint32_t V = g_.V, lo = g_.part_lo, hi = g_.part_hi;
     for (const auto &part : need) {
       EdgeSet &es = g_.esets[part.first];
-      DBuf<uint32_t> mine(&pool_, std::max<uint32_t>(hi - lo, 1)), all(&pool_, std::max<uint32_t>(V, 1));
-      DBuf<uint64_t> deg(&pool_, (uint64_t)V + 1);
+      // degrees travel as u64, two u32 words per vertex (the transport moves u32 columns)
+      DBuf<uint64_t> mine(&pool_, std::max<uint32_t>(hi - lo, 1)), all(&pool_, std::max<uint32_t>(V, 1));
       if (hi > lo) launch_row_degree_range(g_.rp(es, part.second), lo, hi, mine.p, s_);
-      std::vector<uint64_t> send(W, hi - lo), sdispl(W, 0), recv(W), rdispl(W);
+      std::vector<uint64_t> send(W, 2ull * (hi - lo)), sdispl(W, 0), recv(W), rdispl(W);
       for (int p = 0; p < W; ++p) {
-        recv[p] = phi[p] - plo[p];
-        rdispl[p] = plo[p];
+        recv[p] = 2 * (phi[p] - plo[p]);
+        rdispl[p] = 2 * plo[p];
       }
       tm_.begin("exchange");
-      tr_->alltoallv({mine.p}, send, sdispl, {all.p}, recv, rdispl, s_);
-      tm_.end(8ull * V);
-      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> d64(all.p, CastU64());
+      tr_->alltoallv({reinterpret_cast<const uint32_t *>(mine.p)}, send, sdispl,
+                     {reinterpret_cast<uint32_t *>(all.p)}, recv, rdispl, s_);
+      tm_.end(16ull * V);
       uint64_t *grp = nullptr;
       HIP_CHECK(hipMalloc((void **)&grp, ((uint64_t)V + 1) * 8));
-      HIP_CHECK(hipMemsetAsync(grp, 0, 8, s_));
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, d64, grp + 1, (int64_t)V, s_); });
-      HIP_CHECK(hipStreamSynchronize(s_));
+      try {
+        HIP_CHECK(hipMemsetAsync(grp, 0, 8, s_));
+        cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, all.p, grp + 1, (int64_t)V, s_); });
+        HIP_CHECK(hipStreamSynchronize(s_));
+      } catch (...) {
+        (void)hipFree(grp);
+        throw;
+      }
       es.d_global_rp[part.second] = grp;
+      g_.device_bytes += ((uint64_t)V + 1) * 8;
     }
   }
 
@@ -702,6 +726,8 @@ class Executor {
 
   // ---- 1-D partitioned execution (dist.h) ----------------------------------------------------------
   void dist_setup() {
+    if (p_.kind != Plan::MATCH && (tr_ || o_.shard_world > 1 || g_.partitioned()))
+      unsupported("TRAVERSE / SELECT expand() on a partitioned or sharded execution");
     if (!tr_) {
       if (g_.partitioned())
         fail(OMX_E_INVALID, "partitioned snapshot executed without a communicator (omx_exec_options.comm)");
@@ -751,7 +777,42 @@ class Executor {
       HIP_CHECK(hipStreamSynchronize(s_));  // (h0 is a local)
     }
     route_rows(dest, hist);
+    rows_gathered_ = R_;
   }
+  uint64_t rows_gathered_ = 0;  // rows this rank received in route_rank0 (omx_result_info.rows_gathered)
+
+  // before the rows meet on rank 0: equal tuples of the projected aliases meet on one rank
+  // (hash(tuple) % N) and each rank keeps its distinct ones, so rank 0 receives only distinct tuples;
+  // with LIMIT over plain alias rows (a distinct tuple is a distinct result row) a rank sends at most
+  // max(LIMIT, 1) of them (addSingleResult :737-750 keeps that many)
+  void pre_rank0_distinct() {
+    if (p_.out_aliases.empty()) return;
+    std::vector<int> al;
+    for (int a : p_.out_aliases)
+      if (std::find(al.begin(), al.end(), a) == al.end()) al.push_back(a);
+    // columns no projection reads do not travel
+    for (size_t a = 0; a < col_.size(); ++a)
+      if (std::find(al.begin(), al.end(), (int)a) == al.end() && bound_[a]) {
+        col_[a].reset();
+        bound_[a] = 0;
+      }
+    if (!p_.unique_by_construction && !marked_) {
+      route_hash(al);
+      std::vector<DBuf<uint32_t>> cs;
+      bool may_null = false;
+      for (int a : al) {
+        cs.push_back(std::move(col_[a]));
+        may_null = may_null || p_.optional[a];
+      }
+      uint64_t n = R_ ? distinct_rows(cs, (int)al.size(), may_null) : 0;
+      for (size_t i = 0; i < al.size(); ++i) col_[al[i]] = std::move(cs[i]);
+      R_ = n;
+      pre_distinct_ = true;
+    }
+    const int64_t limit = p_.limit >= 0 ? p_.limit : o_.limit;
+    if (limit >= 0 && p_.proj == Plan::PROJ_ALIASES) R_ = std::min<uint64_t>(R_, (uint64_t)std::max<int64_t>(limit, 1));
+  }
+  bool pre_distinct_ = false;  // pre_rank0_distinct de-duplicated the rows (rank 0 receives disjoint sets)
 
   // (row, vertex) pairs of an item's result sets (see traverse)
   struct PairSet {
@@ -1363,6 +1424,10 @@ class Executor {
   // fused: the following S_CHECK closes a cycle on this step's new column (sorted-
   // adjacency intersection instead of materialising the wedges and probing each)
   void expand_step(const Step &st, bool write, bool allow_segmented, const Step *check = nullptr) {
+    if (check && isect_ok(st, *check)) {
+      expand_check_isect(st, *check, write);
+      return;
+    }
     if (check && swap_ok(st, *check)) {
       expand_check_swapped(st, *check, write);
       return;
@@ -1492,24 +1557,21 @@ class Executor {
   // counts Σ_rows deg; edges_read counts what was iterated (Σ_U deg + the L entries).
   // Returns false (nothing done) when the rows repeat their sources less than kFactorMinRatio-fold.
   uint64_t factor_min_rows_ = 4096, factor_min_ratio_ = 4;
-  // OMX_FLIST=1: the lists by ordered tiles (factor.hip) instead of the filtered expansion + key grouping
-  // (measured at M1: forward tiles 1.6 ms for 200 M entries, from the targets' side 0.25 ms + a 0.6 ms
-  // pair sort — no faster than the grouped path's 1.3 ms, profiles/r03/flist; kept as an option)
-  bool flist_ = false;
-  bool flist_reverse_ = true;  // OMX_FLIST_REVERSE=0: never build the lists from the targets' in-rows
-  // OMX_FLIST_PAIRS=1: with the targets' side, expand the (source, target) pairs over the rows grouped by
-  // source instead of sorting the pairs (measured slower at M1: 21 M short expansions, 6.5 ms a step)
-  bool flist_pairs_ = false;
+  // Measured and removed (round 4, after rounds 2-3 kept them as options): the lists by ordered tiles of
+  // the flat entry space, from the sources' side (1.6 ms for M1's 200 M entries) or the targets' in-rows
+  // (0.25 ms + a 0.6 ms pair sort), the targets' (b, c) pairs written over the rows grouped by source
+  // (5.22 against 4.35 ms per step: the pairs re-read their groups from MALL), the entries placed by a
+  // rank written in the histogram pass (within box noise of the cursor scatter); profiles/r03/flist,
+  // femit/reverse.txt, rank2.
   // OMX_FEMIT=0: write the rows with the generic unfiltered expansion (binned heavy / merge-path rows)
-  // instead of k_femit's output tiles; OMX_FEMIT_SORT=0: keep the rows in their order (the lists are then
-  // re-read from HBM / MALL rather than L2)
+  // instead of k_femit's output tiles; k_femit's rows are grouped by source, so each list is re-read from
+  // L2 by its rows (in row order they came from HBM / MALL: 4.35 against 5.2 ms per M1 step, round 3)
   // OMX_FEMIT: 0 = never, 1 = when the hop traverses at least femit_min_et_ edges (E_t), force = always
   // (tests). Below that its fixed costs (the row sort, selections, tile lists: ≈ 0.2 ms) outweigh the
   // faster writes: C2 (RMAT-22, E_t 1.5e9) 1.21 ms against 1.15 binned; M1 (E_t 1.03e10) 4.2 against 5.2
   // (profiles/r03/femit/c2ab.txt)
   int femit_ = 1;
   uint64_t femit_min_et_ = 4000000000ull;
-  bool femit_sort_ = true;
   bool femit_slow_ = false;  // OMX_FEMIT_SLOW=1: every output tile through k_femit_slow (tests)
 
   // step 4 of expand_factorized when the rows are written: the output space Σ_rows |L(g[r])| is laid out
@@ -1521,10 +1583,6 @@ class Executor {
   // OMX_SEMI=0: write the rows as any other hop.
   bool semi_ = false, semi_ok_ = true;
   bool grp32_ = true;  // OMX_GRP32=0: 64-bit counters in the factorized grouping
-  // OMX_GRANK=1: the 32-bit grouping writes each entry's rank in the hist pass and places it without
-  // atomics. Off by default: at M1 the two passes took 78 + 136 µs against 72 + 121 µs for hist +
-  // cursor scatter (the scattered 4-byte writes are both placements' cost; profiles/r03/rank2)
-  bool grank_ = false;
   uint64_t semi_bindings_ = 0;
   bool semi_for(const Step &st) const {
     if (!semi_ok_ || p_.kind != Plan::MATCH || st.kind != S_EXPAND || st.optional || p_.optional[st.dst] ||
@@ -1558,10 +1616,10 @@ class Executor {
                    (unsigned long long)Rn, (unsigned long long)semi_bindings_);
   }
 
-  // perm_sorted: the rows are already sorted by source (g in that order); perm_sorted[i] = the row at
-  // sorted position i
+  // perm_sorted: the rows sorted by source (g in that order); perm_sorted[i] = the row at sorted
+  // position i. nlist: the entries of all U lists (each read from HBM once, then from L2 by its rows)
   void emit_factorized(DBuf<uint32_t> &g, uint64_t R, uint64_t U, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol,
-                       const std::vector<int> &cols, const Step &st, const uint32_t *perm_sorted = nullptr) {
+                       uint64_t nlist, const std::vector<int> &cols, const Step &st, const uint32_t *perm_sorted) {
     // 1. the rows whose list is not empty (the others write nothing), in row order or grouped by source.
     // Their count Rn stays on the device until the output size N is known: the kernels in between run
     // over R rows and read Rn, so one host round trip returns both
@@ -1575,26 +1633,10 @@ class Executor {
       cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cnt, fl, idx.p, nsel.p, (int64_t)R, s_); });
     }
     const uint64_t *rn = nsel.p;
-    DBuf<uint32_t> gs(&pool_, std::max<uint64_t>(R, 1)), perm;
-    if (perm_sorted) {  // grouped already: the non-empty rows keep their sorted order
-      perm = DBuf<uint32_t>(&pool_, std::max<uint64_t>(R, 1));
-      launch_gather_u32_dev(g.p, idx.p, rn, R, gs.p, s_);
-      launch_gather_u32_dev(perm_sorted, idx.p, rn, R, perm.p, s_);
-    } else if (femit_sort_ && R > 1) {  // grouped by source: a list is re-read from L2 by its rows
-      const uint64_t Rn = read1(nsel.p);
-      DBuf<uint32_t> gk(&pool_, std::max<uint64_t>(Rn, 1));
-      perm = DBuf<uint32_t>(&pool_, std::max<uint64_t>(Rn, 1));
-      if (Rn) launch_gather_u32(g.p, idx.p, Rn, gk.p, s_);
-      tm_.begin("femit_row_sort");
-      cub([&](void *t, size_t &b) {
-        return hipcub::DeviceRadixSort::SortPairs(t, b, gk.p, gs.p, idx.p, perm.p, (int64_t)Rn, 0,
-                                                  std::max(1, bits_for(U)), s_);
-      });
-      tm_.end(16ull * Rn * ((bits_for(U) + 7) / 8));
-    } else {
-      launch_gather_u32_dev(g.p, idx.p, rn, R, gs.p, s_);
-      perm = std::move(idx);
-    }
+    // (the rows are grouped by source already: the non-empty rows keep their sorted order)
+    DBuf<uint32_t> gs(&pool_, std::max<uint64_t>(R, 1)), perm(&pool_, std::max<uint64_t>(R, 1));
+    launch_gather_u32_dev(g.p, idx.p, rn, R, gs.p, s_);
+    launch_gather_u32_dev(perm_sorted, idx.p, rn, R, perm.p, s_);
     std::vector<DBuf<uint32_t>> sc;
     for (int c : cols) {
       sc.emplace_back(&pool_, std::max<uint64_t>(R, 1));
@@ -1614,9 +1656,8 @@ class Executor {
     R_ = N;
     factorized_hops_++;
     if (debug_expand_)
-      std::fprintf(stderr, "[omx factorized] emission R=%llu (non-empty %llu) U=%llu rows=%llu sorted=%d\n",
-                   (unsigned long long)R, (unsigned long long)Rn, (unsigned long long)U, (unsigned long long)N,
-                   (int)femit_sort_);
+      std::fprintf(stderr, "[omx factorized] emission R=%llu (non-empty %llu) U=%llu rows=%llu\n",
+                   (unsigned long long)R, (unsigned long long)Rn, (unsigned long long)U, (unsigned long long)N);
     if (N == 0) return;
     // 3. the output tiles (factor.hip k_femit_w): the rows' list entries → the new column, their
     // carried values → their columns
@@ -1638,7 +1679,7 @@ class Executor {
       a.cin[c] = sc[c].p;
       a.cout[c] = outc.back().p;
     }
-    femit_run(a);
+    femit_run(a, nlist);
     segmented_ = false;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(outc[i]);
     col_[st.dst] = std::move(dst);
@@ -1646,7 +1687,9 @@ class Executor {
 
   // the output tiles of a factorized emission (a's rows, offsets, lists and columns set): regular tiles
   // (full, ≤ 64 binding rows) through k_femit_w, the others through k_femit_slow
-  void femit_run(FemitArgs &a) {
+  // list_entries: the entries of a.lcol[0]'s lists when each is re-read from L2 by its rows (0: unknown,
+  // the HBM-necessary bytes are then the algorithmic ones)
+  void femit_run(FemitArgs &a, uint64_t list_entries = 0) {
     const uint64_t nt = femit_tiles(a.N);
     if (nt > 0xFFFFFFFFull) unsupported("a factorized emission of 2^42 or more rows");
     DBuf<uint64_t> rb(&pool_, 2 * nt), nreg(&pool_, 1);
@@ -1665,116 +1708,10 @@ class Executor {
     launch_femit(a, lists.p, nreg.p, nt, cus(), s_);  // the kernels read the partition's count (no host wait)
     // every list column read and every column written per output row; per binding row its offsets and
     // constants
-    tm_.end(a.N * 4ull * (2ull * a.nl + a.nc) + a.R * (24ull + 4ull * a.nc));
-  }
-
-  // The factorized hop from the targets' side, written without building the lists: for every target c
-  // passing the hop's filter, its in-neighbours b that are distinct sources give the (b, c) pairs (Σ
-  // indeg(C) entries read instead of Σ deg(U): M1's 10 % target window, 26 M against 200 M); the rows are
-  // grouped by source, and each pair writes the rows of its source's group with b and c — the same
-  // multiset of (…, b, c) rows as the rows over L(b) (a parallel edge b → c is one pair per edge, as it is
-  // one list entry). One GPU, a single-part adjacency, 2…4 carried columns. Returns false (nothing done)
-  // when the targets' side reads more than half the sources' entries.
-  // OMX_FEMIT_REVERSE=1: the targets' side when it reads fewer than half the sources' entries; =force:
-  // whenever it applies (tests). Off by default: at M1 it reads 26 M entries instead of 200 M and skips
-  // the lists (1.1 ms), but its pairs come in target order, so each re-reads its source's rows from MALL
-  // rather than L2, and the emission takes 2.93 instead of 2.15 ms: 5.22 against 4.35 ms per step
-  // (profiles/r03/femit/reverse.txt)
-  int femit_reverse_ = 0;
-  bool emit_factorized_reverse(const Step &st, const std::vector<int> &cols, DBuf<uint32_t> &g, uint64_t R,
-                               uint64_t U, const DBuf<uint64_t> &ubm, const DBuf<uint32_t> &iu,
-                               const DBuf<uint32_t> &pos, uint64_t EU) {
-    AdjSpec rs = st.adj;
-    rs.parts[0].second ^= 1;
-    const DAdj ra = make_adj(rs);
-    uint64_t nc = 0;
-    DBuf<uint32_t> cl = bitmap_list(bitmap(st.filter_bm), 0, 1, nc);
-    DBuf<uint64_t> cdeg(&pool_, nc + 1), cdoff(&pool_, nc + 1), castart(&pool_, std::max<uint64_t>(nc, 1));
-    launch_flist_prep(cl.p, nc, ra.p[0].rp, cdeg.p, castart.p, s_);
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, cdeg.p, cdoff.p, (int64_t)(nc + 1), s_); });
-    const uint64_t ER = read1(cdoff.p + nc);
-    if (ER * 2 >= EU && femit_reverse_ < 2) return false;
-    // 1. the (b, c) pairs: the targets' in-entries whose neighbour is a distinct source
-    const uint64_t nt = flist_tiles(ER);
-    DBuf<uint32_t> tmp(&pool_, std::max<uint64_t>(ER, 1)), trow(&pool_, std::max<uint64_t>(ER, 1)), tcnt(&pool_, nt + 1);
-    DBuf<uint64_t> toff(&pool_, nt + 1), rb(&pool_, 2 * nt + 2);
-    DBuf<unsigned long long> unused(&pool_, 1);
-    HIP_CHECK(hipMemsetAsync(tcnt.p + nt, 0, 4, s_));
-    tm_.begin("k_flist_tile");
-    launch_flist_tile(nc, cdoff.p, castart.p, ER, ra.p[0].col, ubm.p, tmp.p, tcnt.p, unused.p, rb.p, cus(), s_, cl.p, trow.p);
-    tm_.end(4ull * ER + 24ull * nc + 8ull * nt);
-    const size_t rec = tm_.last();
-    hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> tc(tcnt.p, CastU64());
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tc, toff.p, (int64_t)(nt + 1), s_); });
-    const uint64_t np = read1(toff.p + nt);
-    tm_.amend_at(rec, 4ull * ER + 24ull * nc + 8ull * nt + 8ull * np);
-    edges_iter_ += ER;
-    DBuf<uint32_t> pb(&pool_, std::max<uint64_t>(np, 1)), pc(&pool_, std::max<uint64_t>(np, 1));
-    tm_.begin("k_flist_gather");
-    launch_flist_gather(tmp.p, tcnt.p, toff.p, nt, pb.p, cus(), s_, trow.p, pc.p);
-    tm_.end(16ull * np + 12ull * nt);
-    // 2. the rows grouped by source: aoff[u] = first row of u's group; the other carried columns sorted
-    DBuf<uint32_t> sg(&pool_, R), perm(&pool_, R), idx(&pool_, R);
-    launch_iota(idx.p, R, s_);
-    tm_.begin("femit_row_sort");
-    cub([&](void *t, size_t &b) {
-      return hipcub::DeviceRadixSort::SortPairs(t, b, g.p, sg.p, idx.p, perm.p, (int64_t)R, 0, std::max(1, bits_for(U)), s_);
-    });
-    tm_.end(16ull * R * ((bits_for(U) + 7) / 8));
-    DBuf<uint64_t> aoff(&pool_, U + 1);
-    launch_flist_group_offsets(sg.p, R, iu.p, U, aoff.p, s_);
-    std::vector<int> other;
-    for (int c : cols)
-      if (c != st.src) other.push_back(c);
-    std::vector<DBuf<uint32_t>> sc;
-    for (int c : other) {
-      sc.emplace_back(&pool_, R);
-      launch_gather_u32(col_[c].p, perm.p, R, sc.back().p, s_);
-    }
-    // 3. every pair's group, its output rows (the scan of the group sizes) and list base
-    DBuf<uint32_t> pu(&pool_, std::max<uint64_t>(np, 1));
-    if (np) launch_gather_u32(pos.p, pb.p, np, pu.p, s_);
-    DBuf<uint64_t> len(&pool_, np + 1), roff(&pool_, np + 1), rbase(&pool_, std::max<uint64_t>(np, 1));
-    launch_femit_len(pu.p, np, aoff.p, len.p, s_);
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, len.p, roff.p, (int64_t)(np + 1), s_); });
-    if (np) launch_femit_base(pu.p, np, aoff.p, roff.p, rbase.p, s_);
-    const uint64_t N = read1(roff.p + np);
-    edges_iter_ += N;
-    alg_bytes_ += 8ull * R + 4ull * N * (cols.size() + 2);  // as expand_core's unfiltered written hop
-    R_ = N;
-    factorized_hops_++;
-    if (debug_expand_)
-      std::fprintf(stderr, "[omx factorized] targets' side: R=%llu U=%llu targets=%llu ER=%llu pairs=%llu rows=%llu\n",
-                   (unsigned long long)R, (unsigned long long)U, (unsigned long long)nc, (unsigned long long)ER,
-                   (unsigned long long)np, (unsigned long long)N);
-    if (N == 0) return true;
-    // 4. the output tiles: the group rows' other columns, the pair's b and c
-    FemitArgs a{};
-    a.g = pu.p;
-    a.roff = roff.p;
-    a.rbase = rbase.p;
-    a.loff = aoff.p;
-    a.R = np;
-    a.N = N;
-    a.nl = (int32_t)other.size();
-    std::vector<DBuf<uint32_t>> lo;
-    for (size_t m = 0; m < other.size(); ++m) {
-      lo.emplace_back(&pool_, N);
-      a.lcol[m] = sc[m].p;
-      a.lout[m] = lo.back().p;
-    }
-    a.nc = 2;
-    DBuf<uint32_t> ob(&pool_, N), oc(&pool_, N);
-    a.cin[0] = pb.p;
-    a.cout[0] = ob.p;
-    a.cin[1] = pc.p;
-    a.cout[1] = oc.p;
-    femit_run(a);
-    segmented_ = false;
-    for (size_t m = 0; m < other.size(); ++m) col_[other[m]] = std::move(lo[m]);
-    col_[st.src] = std::move(ob);
-    col_[st.dst] = std::move(oc);
-    return true;
+    const uint64_t alg = a.N * 4ull * (2ull * a.nl + a.nc) + a.R * (24ull + 4ull * a.nc);
+    // HBM-necessary: every column written per output row, each list entry and binding row read once
+    tm_.end(alg, list_entries && a.nl == 1 ? a.N * 4ull * (a.nl + a.nc) + 4ull * list_entries + a.R * (24ull + 4ull * a.nc)
+                                           : alg);
   }
 
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
@@ -1789,7 +1726,7 @@ class Executor {
     // rows emitted by k_femit_w from the sources' lists: the rows are sorted by source here (the emission
     // wants them grouped), so the distinct sources are the sorted runs' heads and a row's source index
     // is its run — no bitmap, position map or second sort
-    const bool presort = femit && femit_sort_ && !flist_ && femit_reverse_ == 0 && R > 0;
+    const bool presort = femit && R > 0;
     if (presort) {
       DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
       DBuf<uint8_t> head(&pool_, R);
@@ -1818,30 +1755,22 @@ class Executor {
       tm_.end(4ull * R + 8ull * nwords_);
       ub = bitmap_list(ubm.p, 0, 1, U);
     }
-    // the distinct sources' degrees, scanned: doff[u] = the first of u's entries in the flat list space
-    const bool tiles = flist_ && st.adj.parts.size() == 1;
-    DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1), astart;
-    if (tiles) {  // degrees and first col positions of the distinct sources, for the list tiles
-      astart = DBuf<uint64_t>(&pool_, std::max<uint64_t>(U, 1));
-      tm_.begin("k_flist_prep");
-      launch_flist_prep(ub.p, U, make_adj(st.adj).p[0].rp, udeg.p, astart.p, s_);
-      tm_.end(U * 36ull);
-    } else {
-      tm_.begin("k_row_degree");
-      launch_row_degree(ub.p, U, make_adj(st.adj), udeg.p, s_);
-      tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
-    }
+    // the distinct sources' degrees, scanned
+    DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1);
+    tm_.begin("k_row_degree");
+    launch_row_degree(ub.p, U, make_adj(st.adj), udeg.p, s_);
+    tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(U + 1), s_); });
     const uint64_t EU = read1(doff.p + U);
     if (Et < factor_min_ratio_ * EU) return false;
     edges_ += Et;
     // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
     // (presorted rows have theirs from the runs)
-    DBuf<uint32_t> iu(&pool_, std::max<uint64_t>(U, 1)), pos;
+    DBuf<uint32_t> iu(&pool_, std::max<uint64_t>(U, 1));
     launch_iota(iu.p, U, s_);
     if (!presort) {
       g = DBuf<uint32_t>(&pool_, R);
-      pos = DBuf<uint32_t>(&pool_, std::max<uint64_t>(g_.V, 1));
+      DBuf<uint32_t> pos(&pool_, std::max<uint64_t>(g_.V, 1));
       tm_.begin("k_scatter_u32");
       launch_scatter_u32(ub.p, iu.p, U, pos.p, s_);
       tm_.end(12ull * U);
@@ -1849,132 +1778,14 @@ class Executor {
       launch_gather_u32(pos.p, src, R, g.p, s_);
       tm_.end(12ull * R);
     }
-    if (!presort && femit && femit_reverse_ && !dist_ && st.adj.parts.size() == 1 && cols.size() >= 2 &&
-        femit_supported((int)cols.size() - 1, 2) && emit_factorized_reverse(st, cols, g, R, U, ubm, iu, pos, EU))
-      return true;
     DBuf<unsigned long long> cnt(&pool_, U + 1);
     DBuf<uint64_t> loff(&pool_, U + 1);
     HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));
-    DBuf<uint32_t> lcol;
-    uint64_t nlist = 0;
-    // the same lists from the targets' side: for every vertex c passing the target filter, its
-    // in-neighbours that are distinct sources — Σ indeg(C) entries instead of Σ deg(U) (M1: the 10 %
-    // target window, 26 M against 200 M), (source, target) pairs sorted by source. One GPU only (a
-    // partition holds the in-rows of its own targets).
-    bool reverse = false;
-    if (tiles && !dist_ && flist_reverse_) {
-      AdjSpec rs = st.adj;
-      rs.parts[0].second ^= 1;
-      const DAdj ra = make_adj(rs);
-      uint64_t nc = 0;
-      DBuf<uint32_t> cl = bitmap_list(bitmap(st.filter_bm), 0, 1, nc);
-      DBuf<uint64_t> cdeg(&pool_, nc + 1), cdoff(&pool_, nc + 1), castart(&pool_, std::max<uint64_t>(nc, 1));
-      tm_.begin("k_flist_prep");
-      launch_flist_prep(cl.p, nc, ra.p[0].rp, cdeg.p, castart.p, s_);
-      tm_.end(nc * 36ull);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, cdeg.p, cdoff.p, (int64_t)(nc + 1), s_); });
-      const uint64_t ER = read1(cdoff.p + nc);
-      if (ER * 2 < EU) {
-        reverse = true;
-        const uint64_t nt = flist_tiles(ER);
-        DBuf<uint32_t> tmp(&pool_, std::max<uint64_t>(ER, 1)), trow(&pool_, std::max<uint64_t>(ER, 1)), tcnt(&pool_, nt + 1);
-        DBuf<uint64_t> toff(&pool_, nt + 1), rb(&pool_, 2 * nt + 2);
-        HIP_CHECK(hipMemsetAsync(tcnt.p + nt, 0, 4, s_));
-        tm_.begin("k_flist_tile");
-        launch_flist_tile(nc, cdoff.p, castart.p, ER, ra.p[0].col, ubm.p, tmp.p, tcnt.p, cnt.p, rb.p, cus(), s_, cl.p,
-                          trow.p);
-        tm_.end(4ull * ER + 24ull * nc + 8ull * nt);
-        const size_t rec = tm_.last();
-        hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> tc(tcnt.p, CastU64());
-        cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tc, toff.p, (int64_t)(nt + 1), s_); });
-        nlist = read1(toff.p + nt);
-        tm_.amend_at(rec, 4ull * ER + 24ull * nc + 8ull * nt + 8ull * nlist);
-        DBuf<uint32_t> keys(&pool_, std::max<uint64_t>(nlist, 1)), vals(&pool_, std::max<uint64_t>(nlist, 1)),
-            skeys(&pool_, std::max<uint64_t>(nlist, 1));
-        lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(nlist, 1));
-        tm_.begin("k_flist_gather");
-        launch_flist_gather(tmp.p, tcnt.p, toff.p, nt, keys.p, cus(), s_, trow.p, vals.p);
-        tm_.end(16ull * nlist + 12ull * nt);
-        edges_iter_ += ER;
-        // rows of two columns, the source and one other X (M1 / C2: (a, b)): no grouping of the pairs —
-        // the rows are grouped by source instead (R, not Σ|L|, entries sorted), and every (b, c) pair
-        // is expanded over its source's X values: the same (X, b, c) rows
-        const int other = !flist_pairs_ || cols.size() != 2 ? -1 : cols[0] == st.src ? cols[1] : cols[1] == st.src ? cols[0] : -1;
-        if (other >= 0) {
-          DBuf<uint32_t> sg(&pool_, R), sx(&pool_, R), gp(&pool_, std::max<uint64_t>(nlist, 1));
-          DBuf<uint64_t> aoff(&pool_, U + 1);
-          tm_.begin("flist_row_sort");
-          cub([&](void *t, size_t &b) {
-            return hipcub::DeviceRadixSort::SortPairs(t, b, g.p, sg.p, col_[other].p, sx.p, (int64_t)R, 0,
-                                                      std::max(1, bits_for(U)), s_);
-          });
-          tm_.end(16ull * R * ((bits_for(U) + 7) / 8));
-          launch_flist_group_offsets(sg.p, R, iu.p, U, aoff.p, s_);
-          if (nlist) launch_gather_u32(pos.p, keys.p, nlist, gp.p, s_);
-          DAdj aadj{};
-          aadj.n = 1;
-          aadj.sorted = 0;
-          aadj.p[0].rp = aoff.p;
-          aadj.p[0].col = sx.p;
-          ExpandOut o = expand_core(gp.p, nlist, st.adj, nullptr, {keys.p, vals.p}, write, false, nullptr, nullptr,
-                                    nullptr, &aadj);
-          if (!o.counted_from_degrees) edges_iter_ += o.E;
-          R_ = o.n;
-          factorized_hops_++;
-          if (debug_expand_)
-            std::fprintf(stderr, "[omx factorized] pairs R=%llu U=%llu Et=%llu EU=%llu ER=%llu pairs=%llu rows=%llu\n",
-                         (unsigned long long)R, (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU,
-                         (unsigned long long)ER, (unsigned long long)nlist, (unsigned long long)o.n);
-          if (!write || R_ == 0) return true;
-          segmented_ = false;
-          col_[other] = std::move(o.dst);
-          col_[st.src] = std::move(o.carry[0]);
-          col_[st.dst] = std::move(o.carry[1]);
-          return true;
-        }
-        if (nlist) {
-          const int vbits = bits_for(g_.V);
-          tm_.begin("flist_sort");
-          cub([&](void *t, size_t &b) {
-            return hipcub::DeviceRadixSort::SortPairs(t, b, keys.p, skeys.p, vals.p, lcol.p, (int64_t)nlist, 0, vbits, s_);
-          });
-          tm_.end(16ull * nlist * ((vbits + 7) / 8));
-        }
-        launch_flist_group_offsets(skeys.p, nlist, ub.p, U, loff.p, s_);
-      }
-    }
-    if (reverse) {
-      // (lists built from the targets' side above)
-    } else if (tiles) {
-      // 2+3. the filtered lists, grouped by source in source order (factor.hip): tiles of the flat entry
-      // space compact their survivors in order, per-source counts give the offsets
-      const DAdj a = make_adj(st.adj);
-      const uint64_t nt = flist_tiles(EU);
-      DBuf<uint32_t> tmp(&pool_, std::max<uint64_t>(EU, 1)), tcnt(&pool_, nt + 1);
-      DBuf<uint64_t> toff(&pool_, nt + 1), rb(&pool_, 2 * nt + 2);
-      HIP_CHECK(hipMemsetAsync(tcnt.p + nt, 0, 4, s_));
-      tm_.begin("k_flist_tile");
-      launch_flist_tile(U, doff.p, astart.p, EU, a.p[0].col, bitmap(st.filter_bm), tmp.p, tcnt.p, cnt.p, rb.p, cus(), s_);
-      tm_.end(4ull * EU + 24ull * U + 8ull * nt);  // col per entry, row tables per source; amended below
-      const size_t rec = tm_.last();
-      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> tc(tcnt.p, CastU64());
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tc, toff.p, (int64_t)(nt + 1), s_); });
-      cub([&](void *t, size_t &b) {
-        return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
-      });
-      nlist = read1(toff.p + nt);
-      tm_.amend_at(rec, 4ull * EU + 24ull * U + 8ull * nt + 4ull * nlist);
-      lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(nlist, 1));
-      tm_.begin("k_flist_gather");
-      launch_flist_gather(tmp.p, tcnt.p, toff.p, nt, lcol.p, cus(), s_);
-      tm_.end(8ull * nlist + 12ull * nt);
-      edges_iter_ += EU;
-    } else {
     // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
     // (the filtered lists stay in the expansion's per-worker segments: grouping reads them in place)
     ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, true);
     edges_iter_ += l.E;
-    nlist = l.n;
+    const uint64_t nlist = l.n;
     // 3. grouped by source: offsets (U + 1) and the neighbours in group order (segmented lists under
     // 2^32 entries: 32-bit counters and cursors, half the atomics' footprint)
     const bool c32 = l.segmented && l.n < (1ull << 32) && grp32_;
@@ -1983,18 +1794,12 @@ class Executor {
       h32 = DBuf<uint32_t>(&pool_, U + 1);
       HIP_CHECK(hipMemsetAsync(h32.p, 0, (U + 1) * 4, s_));
     }
-    // the lists written (not a semi-join): ranks in the hist pass, then placement without atomics
-    const bool ranked = c32 && grank_ && !(write && semi_);
-    DBuf<uint32_t> rank;
     if (l.n) {
       tm_.begin("k_key_hist");
-      if (ranked) {
-        rank = DBuf<uint32_t>(&pool_, l.carry[0].n);  // indexed like the keys: arena positions, not 0..n
-        launch_key_rank_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, h32.p, rank.p, s_);
-      } else if (c32) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, h32.p, s_);
+      if (c32) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, h32.p, s_);
       else if (l.segmented) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, s_);
       else launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
-      tm_.end((ranked ? 8ull : 4ull) * l.n + (c32 ? 4ull : 8ull) * U);
+      tm_.end(4ull * l.n + (c32 ? 4ull : 8ull) * U);
     }
     if (c32) {
       hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> hc(h32.p, CastU64());
@@ -2010,12 +1815,8 @@ class Executor {
       semi_join(g, R, loff, cols);
       return true;
     }
-    lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(l.n, 1));
-    if (l.n && ranked) {
-      tm_.begin("k_key_scatter");
-      launch_key_place_seg(l.carry[0].p, l.dst.p, rank.p, l.seg_start.p, l.seg_count.p, l.nseg, loff.p, lcol.p, s_);
-      tm_.end(16ull * l.n);
-    } else if (l.n && c32) {
+    DBuf<uint32_t> lcol(&pool_, std::max<uint64_t>(l.n, 1));
+    if (l.n && c32) {
       DBuf<uint32_t> cur(&pool_, U + 1);
       cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, h32.p, cur.p, (int64_t)(U + 1), s_); });
       tm_.begin("k_key_scatter");
@@ -2029,10 +1830,9 @@ class Executor {
       else launch_key_scatter(l.carry[0].p, l.dst.p, l.n, cnt.p, lcol.p, s_);
       tm_.end(12ull * l.n + 8ull * U);
     }
-    }
     // 4. the rows over their sources' lists
     if (femit) {
-      emit_factorized(g, R, U, loff, lcol, cols, st, presort ? perm_s.p : nullptr);
+      emit_factorized(g, R, U, loff, lcol, nlist, cols, st, perm_s.p);
       return true;
     }
     DAdj ladj{};
@@ -2410,6 +2210,183 @@ class Executor {
       col_[cols[i]] = cat(og[0].n ? og[0].carry[i] : e0, og[0].n, og[1].n ? og[1].carry[i] : e1, og[1].n);
     }
     col_[ex.dst] = cat(og[0].dst, og[0].n, og[1].dst, og[1].n);
+  }
+
+  // The fused intersection N_x(x) ∩ N_y(y) with a merge path (isect.hip) for the rows whose lists have
+  // comparable lengths; the other rows probe: the shorter list iterated, the longer binary-searched
+  // (swapped only where that yields the same rows, see swap_ok), as expand_check_swapped. One part on
+  // each side, sorted rows, one GPU; the expansion's target filter and parallel edges are allowed (the
+  // merge keeps N_x's multiplicity, N_y is existence).
+  bool isect_ok(const Step &ex, const Step &ck) const {
+    return merge_ && !dist_ && ex.adj.parts.size() == 1 && ck.adj.parts.size() == 1 && ex.adj.sorted && ck.adj.sorted;
+  }
+  void expand_check_isect(const Step &ex, const Step &ck, bool write) {
+    require_u32_rows("a cycle-closing intersection");
+    const std::vector<int> cols = bound_cols();  // carried columns (ex.dst is not bound yet)
+    bound_[ex.dst] = 1;
+    const uint64_t R = R_;
+    const int ix = (int)(std::find(cols.begin(), cols.end(), ex.src) - cols.begin());
+    const int iy = (int)(std::find(cols.begin(), cols.end(), ck.src) - cols.begin());
+    const DAdj ax = make_adj(ex.adj), ay = make_adj(ck.adj);
+    const uint64_t *xfilter = bitmap(ex.filter_bm), *yfilter = bitmap(ck.filter_bm);
+    IsectPolicy pol{};
+    pol.merge = 1;
+    pol.force = merge_ == 2;
+    pol.swap = swap_ok(ex, ck);
+    pol.dup_free = ex.adj.dup_free;
+    pol.ratio = merge_ratio_;
+    // 1. each row's class, the E_t sums and the class sizes
+    DBuf<uint8_t> cls(&pool_, std::max<uint64_t>(R, 1));
+    DBuf<uint32_t> w(&pool_, std::max<uint64_t>(R, 1)), bnd(&pool_, std::max<uint64_t>(R, 1));
+    DBuf<unsigned long long> sums(&pool_, 6);
+    HIP_CHECK(hipMemsetAsync(sums.p, 0, 6 * sizeof(unsigned long long), s_));
+    tm_.begin("k_isect_class");
+    launch_isect_class(col_[ex.src].p, col_[ck.src].p, R, ax.p[0], ay.p[0], pol, cls.p, w.p, bnd.p, sums.p, cus(), s_);
+    tm_.end(R * (8ull + 32ull + 9ull));
+    launch_post_words(sums.p, 6, mail(), s_);
+    const uint64_t *hm = wait_mail();
+    const uint64_t hopE = hm[0], checkE = hm[1], nc[4] = {hm[2], hm[3], hm[4], hm[5]};
+    // 2. rows grouped by class (stable: each group keeps the row order)
+    DBuf<uint32_t> idx(&pool_, std::max<uint64_t>(R, 1));
+    if (R) {
+      DBuf<uint32_t> iota(&pool_, R);
+      DBuf<uint8_t> scls(&pool_, R);
+      launch_iota(iota.p, R, s_);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceRadixSort::SortPairs(t, b, cls.p, scls.p, iota.p, idx.p, (int64_t)R, 0, 2, s_); });
+    }
+    const uint64_t nM = nc[1];
+    const uint32_t *gi[3] = {idx.p + nc[0], idx.p + nc[0] + nc[1], idx.p + nc[0] + nc[1] + nc[2]};
+    // 3. the merged rows
+    uint64_t medges = 0, nmerged = 0, wtotal = 0;
+    DBuf<uint32_t> mdst;
+    std::vector<DBuf<uint32_t>> mcarry;
+    if (nM) {
+      DBuf<uint32_t> wm(&pool_, nM + 1), bm(&pool_, nM + 1);
+      launch_gather_u32(w.p, gi[0], nM, wm.p, s_);
+      launch_gather_u32(bnd.p, gi[0], nM, bm.p, s_);
+      DBuf<uint64_t> woff(&pool_, nM + 1), boff(&pool_, nM + 1), tot(&pool_, 2);
+      HIP_CHECK(hipMemsetAsync(wm.p + nM, 0, 4, s_));
+      HIP_CHECK(hipMemsetAsync(bm.p + nM, 0, 4, s_));
+      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> w64(wm.p, CastU64()), b64(bm.p, CastU64());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, w64, woff.p, (int64_t)(nM + 1), s_); });
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, b64, boff.p, (int64_t)(nM + 1), s_); });
+      HIP_CHECK(hipMemcpyAsync(tot.p, woff.p + nM, 8, hipMemcpyDeviceToDevice, s_));
+      HIP_CHECK(hipMemcpyAsync(tot.p + 1, boff.p + nM, 8, hipMemcpyDeviceToDevice, s_));
+      const auto wb = read2(tot.p);
+      wtotal = wb.first - (uint64_t)kIsRowPad * nM;  // the list entries the merge reads
+      const uint64_t cap = wb.second, ntiles = isect_tiles(wb.first);
+      if (ntiles > 0xFFFFFFFFull) unsupported("a merged intersection of 2^32 or more tiles");
+      DBuf<uint32_t> trow(&pool_, ntiles + 1), segc(&pool_, std::max<uint64_t>(ntiles, 1));
+      DBuf<uint64_t> segs(&pool_, std::max<uint64_t>(ntiles, 1));
+      DBuf<unsigned long long> ctr(&pool_, 2);
+      HIP_CHECK(hipMemsetAsync(ctr.p, 0, 2 * sizeof(unsigned long long), s_));
+      launch_isect_tiles(woff.p, nM, ntiles, trow.p, s_);
+      IsectArgs a{};
+      a.idx = gi[0];
+      a.boff = boff.p;
+      a.tile_row = trow.p;
+      a.nM = nM;
+      a.ntiles = ntiles;
+      a.xs = col_[ex.src].p;
+      a.ys = col_[ck.src].p;
+      a.ax = ax.p[0];
+      a.ay = ay.p[0];
+      a.xfilter = xfilter;
+      a.yfilter = yfilter;
+      a.counters = ctr.p;
+      a.seg_count = segc.p;
+      a.seg_start = segs.p;
+      DBuf<uint32_t> odst;
+      std::vector<DBuf<uint32_t>> ocar;
+      if (write) {
+        odst = DBuf<uint32_t>(&pool_, std::max<uint64_t>(cap, 1));
+        a.out_dst = odst.p;
+        a.ncarry = (int32_t)cols.size();
+        for (size_t c = 0; c < cols.size(); ++c) {
+          ocar.emplace_back(&pool_, std::max<uint64_t>(cap, 1));
+          a.carry_in[c] = col_[cols[c]].p;
+          a.carry_out[c] = ocar.back().p;
+        }
+      }
+      tm_.begin("k_isect_merge");
+      launch_isect_merge(a, write, cus(), s_);
+      // per merged row: its index, x and y, two row_ptr pairs; its lists; 4 B × columns per written row
+      // (amended below)
+      tm_.end(nM * 44ull + 4ull * wtotal);
+      const size_t rec = tm_.last();
+      if (write) {
+        DBuf<uint64_t> soffs(&pool_, ntiles + 1);
+        launch_seg_totals(segc.p, ntiles, ntiles, soffs.p, ctr.p, 0, 0, mail(), s_);
+        const uint64_t *mw = wait_mail();
+        nmerged = mw[1];
+        medges = mw[2];
+        mdst = DBuf<uint32_t>(&pool_, std::max<uint64_t>(nmerged, 1));
+        std::vector<uint32_t *> ins{odst.p}, outs{mdst.p};
+        for (size_t c = 0; c < cols.size(); ++c) {
+          mcarry.emplace_back(&pool_, std::max<uint64_t>(nmerged, 1));
+          ins.push_back(ocar[c].p);
+          outs.push_back(mcarry.back().p);
+        }
+        tm_.begin("k_compact_segments");
+        launch_compact_segments((int)ins.size(), ins.data(), outs.data(), segs.p, segc.p, soffs.p, (uint32_t)ntiles, s_);
+        tm_.end(8ull * ins.size() * nmerged);
+      } else {
+        const auto mr = read2(reinterpret_cast<const uint64_t *>(ctr.p));
+        medges = mr.first;
+        nmerged = mr.second;
+      }
+      tm_.amend_at(rec, nM * 44ull + 4ull * wtotal + 4ull * (cols.size() + 1) * (write ? nmerged : 0));
+    }
+    // 4. the probed rows: class 2 iterates N_x(x) and probes N_y(y), class 3 the other way round
+    ExpandOut og[2];
+    const uint64_t gn[2] = {nc[2], nc[3]};
+    for (int g = 0; g < 2; ++g) {
+      if (gn[g] == 0) continue;
+      std::vector<DBuf<uint32_t>> gc;
+      std::vector<const uint32_t *> in, carry;
+      std::vector<uint32_t *> out;
+      for (int c : cols) {
+        gc.emplace_back(&pool_, gn[g]);
+        in.push_back(col_[c].p);
+        out.push_back(gc.back().p);
+      }
+      launch_gather_cols(gi[1 + g], gn[g], (int)cols.size(), in.data(), out.data(), s_);
+      for (auto &b : gc) carry.push_back(b.p);
+      if (g == 0)
+        og[g] = expand_core(gc[ix].p, gn[g], ex.adj, xfilter, carry, write, false, gc[iy].p, &ck.adj, yfilter);
+      else  // (swapped rows exist only without an expansion filter: swap_ok)
+        og[g] = expand_core(gc[iy].p, gn[g], ck.adj, nullptr, carry, write, false, gc[ix].p, &ex.adj, yfilter);
+    }
+    // E_t: Σ|N_x(x)| for the hop, and for the check Σ|N_y(y)| over the hop's rows that
+    // reach it — every N_x entry without an expansion filter, else the entries passing it (counted by the
+    // merge kernel and the probing kernels)
+    edges_ += hopE + (xfilter ? medges + og[0].E_member : checkE);
+    edges_iter_ += wtotal + og[0].E + og[1].E;  // the merged lists (both read) and the iterated lists
+    R_ = nmerged + og[0].n + og[1].n;
+    if (!write || R_ == 0) return;
+    segmented_ = false;
+    // the three groups back to back
+    auto cat3 = [&](DBuf<uint32_t> *parts[3], const uint64_t *ns) {
+      const uint64_t n = ns[0] + ns[1] + ns[2];
+      for (int k = 0; k < 3; ++k)
+        if (ns[k] == n) return std::move(*parts[k]);
+      DBuf<uint32_t> o(&pool_, n);
+      uint64_t at = 0;
+      for (int k = 0; k < 3; ++k) {
+        if (ns[k]) HIP_CHECK(hipMemcpyAsync(o.p + at, parts[k]->p, ns[k] * 4, hipMemcpyDeviceToDevice, s_));
+        at += ns[k];
+      }
+      return o;
+    };
+    const uint64_t ns[3] = {nmerged, og[0].n, og[1].n};
+    for (size_t i = 0; i < cols.size(); ++i) {
+      DBuf<uint32_t> e0, e1, e2;
+      DBuf<uint32_t> *parts[3] = {nmerged ? &mcarry[i] : &e0, og[0].n ? &og[0].carry[i] : &e1, og[1].n ? &og[1].carry[i] : &e2};
+      col_[cols[i]] = cat3(parts, ns);
+    }
+    DBuf<uint32_t> e0, e1, e2;
+    DBuf<uint32_t> *parts[3] = {nmerged ? &mdst : &e0, og[0].n ? &og[0].dst : &e1, og[1].n ? &og[1].dst : &e2};
+    col_[ex.dst] = cat3(parts, ns);
   }
 
   // keep the rows whose flag is set (all bound columns)
@@ -2796,8 +2773,11 @@ class Executor {
               launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p], pull_E[p], lanes & live, fr.p, hub_fr[p].p,
                               probe ? fbm.p : nullptr, vis.p, nx.p, cus(), s_);
             }
-            // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask
-            tm_.end(16ull * V + 12ull * pull_E[p]);
+            // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask.
+            // HBM-necessary: the masks are shared by all the in-edges of a source, so each is needed once
+            // (probe levels: the frontier's masks and the frontier bitmap; else every vertex's mask)
+            tm_.end(16ull * V + 12ull * pull_E[p],
+                    16ull * V + 4ull * pull_E[p] + (probe ? 8ull * h[2] + V / 8 : 8ull * V));
             edges_iter_ += pull_E[p];
           }
         } else {
@@ -3158,13 +3138,19 @@ class Executor {
         HIP_CHECK(hipMemcpyAsync(out.back().p, out[taken[a]].p, R_ * 4, hipMemcpyDeviceToDevice, s_));
       }
     }
-    if (p_.unique_by_construction || marked_) return;  // (marked_: the rows are already the distinct set)
+    if (p_.unique_by_construction || marked_ || pre_distinct_) return;  // (marked_ / pre_distinct_: the rows are already the distinct set)
+    bool may_null = false;
+    for (int a : p_.out_aliases) may_null = may_null || p_.optional[a];
+    n = distinct_rows(out, k, may_null);
+  }
+
+  // the distinct tuples of the k columns `out` (R_ rows each, rewritten in place); returns their count
+  uint64_t distinct_rows(std::vector<DBuf<uint32_t>> &out, int k, bool may_null) {
     if (segmented_) fail(OMX_E_INVALID, "internal: segmented table reached dedup");
+    uint64_t n = R_;
     dedup_ran_ = 1;
     tm_.begin("dedup");
     const int vbits = bits_for(g_.V);
-    bool may_null = false;
-    for (int a : p_.out_aliases) may_null = may_null || p_.optional[a];
     if (k == 1 && !may_null) {
       // one column: the distinct vertices are the set bits of a V-bit bitmap (no sort)
       DBuf<uint64_t> bm(&pool_, nwords_);
@@ -3175,7 +3161,7 @@ class Executor {
       out[0] = std::move(lst);
       n = m;
       tm_.end(R_ * 4 + nwords_ * 16 + m * 4);
-      return;
+      return n;
     }
     if (k <= 3 && k * vbits <= 64) {
       // pack the tuple into one u64 key
@@ -3211,6 +3197,7 @@ class Executor {
       for (int c = 0; c < k; ++c) launch_gather_u32(sorted[c].p, idx.p, n, out[c].p, s_);
     }
     tm_.end(R_ * 4ull * k * 4);
+    return n;
   }
 
   void pack_tuple(std::vector<DBuf<uint32_t>> &cols, int k, int vbits, uint64_t *keys);
@@ -3250,12 +3237,16 @@ void Executor::unpack_tuple(const uint64_t *keys, uint64_t n, std::vector<DBuf<u
 
 }  // namespace
 
-omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts, Transport *tr) {
+omx_result *execute_plan(Graph &g, const Plan &p, const omx_exec_options &opts, Transport *tr, bool *running) {
+  if (running) *running = false;
   if (!g.on_device()) fail(OMX_E_DEVICE, "graph snapshot is host-only (device = -1)");
   HIP_CHECK(hipSetDevice(g.device));
   // a failure releases the peers waiting in an exchange with this rank: omx_execute (capi.cpp) aborts the
-  // communicator unless the failure is a refusal every rank made alike before exchanging anything
+  // communicator unless the failure is a refusal of the plan or of its partition checks (the constructor:
+  // the same statement and replicated schema on every rank, so every rank refused alike). Anything
+  // raised once run() started may depend on this rank's own rows, so its peers must be released.
   Executor ex(g, p, opts, tr);
+  if (running) *running = true;
   return ex.run();
 }
 

@@ -114,6 +114,42 @@ struct ExpandArgs {
   unsigned long long *member_edges;  // [0] Σ |N_member| of checked pairs, [1] col[] probes of the checks
 };
 
+// ---- isect.hip: the fused closing check as a sorted-list intersection (Executor::expand_check_isect) ----
+constexpr uint32_t kIsRowCap = 1024;  // m + n of a merged row (its two lists staged in LDS)
+constexpr uint32_t kIsRowPad = 8;     // a merged row's tile weight beyond m + n (bounds the rows a tile holds)
+struct IsectPolicy {
+  int32_t merge;     // merge rows of comparable lengths
+  int32_t force;     // merge every row with m + n ≤ kIsRowCap (tests)
+  int32_t swap;      // probe rows iterate the shorter list (simple adjacencies, no expansion filter)
+  int32_t dup_free;  // N_x has no parallel edges: a merged row matches at most min(m, n) times
+  double ratio;      // merge when max(m, n) ≤ ratio · min(m, n)
+};
+struct IsectArgs {
+  const uint32_t *idx;       // [nM] the merged rows' binding-table indices
+  const uint64_t *boff;      // [nM] scan of their output bounds (a tile writes at boff[its first row])
+  const uint32_t *tile_row;  // [ntiles + 1] first merged row of each tile
+  uint64_t nM, ntiles;
+  const uint32_t *xs, *ys;   // binding columns: expansion source x, check source y
+  DAdjPart ax, ay;           // N_x (iterated: the new column), N_y (membership)
+  const uint64_t *xfilter;   // the expansion's target bitmap, or nullptr
+  const uint64_t *yfilter;   // the check's target bitmap, or nullptr
+  int32_t ncarry;
+  const uint32_t *carry_in[kMaxCols];
+  uint32_t *carry_out[kMaxCols];
+  uint32_t *out_dst;
+  uint32_t *seg_count;       // [ntiles] rows tile t wrote, from seg_start[t]
+  uint64_t *seg_start;
+  unsigned long long *counters;  // [0] Σ |N_y(y)| over the A elements passing xfilter; [1] rows (count only)
+};
+// cls[r] ∈ {0 nothing, 1 merge, 2 probe N_y, 3 probe N_x}; w[r] = tile weight, bnd[r] = output bound of a
+// merged row (0 otherwise); sums (6 words, zeroed): Σ m, Σ m·n, rows of each class
+void launch_isect_class(const uint32_t *xs, const uint32_t *ys, uint64_t R, const DAdjPart &ax, const DAdjPart &ay,
+                        const IsectPolicy &pol, uint8_t *cls, uint32_t *w, uint32_t *bnd, unsigned long long *sums,
+                        int cus, hipStream_t s);
+uint64_t isect_tiles(uint64_t wtotal);
+void launch_isect_tiles(const uint64_t *woff, uint64_t nM, uint64_t ntiles, uint32_t *tile_row, hipStream_t s);
+void launch_isect_merge(const IsectArgs &a, bool write, int cus, hipStream_t s);
+
 // predicate VM → V-bit bitmap (u64 words); depth = value of $depth
 // nwords > ⌈V/64⌉ zero-fills the padding words (0: no padding)
 void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s,
@@ -139,7 +175,8 @@ void launch_route_bounds(const uint32_t *id, uint64_t R, const uint64_t *bounds,
 void launch_add_u32(uint32_t *x, uint64_t n, int64_t delta, hipStream_t s);
 
 void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t *deg, hipStream_t s);
-void launch_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint32_t *deg, hipStream_t s);
+// deg[v - lo] = degree of row v (u64: a multigraph row may hold 2^32 or more entries)
+void launch_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint64_t *deg, hipStream_t s);
 void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part,
                          hipStream_t s);
 // rows [vlo, vhi) (the owned rows of a partition; rp indexed by global vertex id)
@@ -221,22 +258,11 @@ void launch_iota(uint32_t *out, uint64_t n, hipStream_t s);
 void launch_fill_u32(uint32_t *out, uint64_t n, uint32_t x, hipStream_t s);
 // factorized expansion: position of each key in a sorted unique list; a key histogram; a scatter by key
 void launch_index_of(const uint32_t *sorted, uint64_t n, const uint32_t *keys, uint64_t m, uint32_t *out, hipStream_t s);
-// factor.hip: the filtered lists of a factorized hop's distinct sources (see there)
-uint64_t flist_tiles(uint64_t EU);
-void launch_flist_prep(const uint32_t *ub, uint64_t U, const uint64_t *rp, uint64_t *deg, uint64_t *astart, hipStream_t s);
-void launch_flist_tile(uint64_t U, const uint64_t *doff, const uint64_t *astart, uint64_t EU, const uint32_t *col,
-                       const uint64_t *filter, uint32_t *tmp, uint32_t *tile_cnt, unsigned long long *cnt, uint64_t *rb,
-                       int cus, hipStream_t s, const uint32_t *rowv = nullptr, uint32_t *tmp_row = nullptr);
-void launch_flist_gather(const uint32_t *tmp, const uint32_t *tile_cnt, const uint64_t *tile_off, uint64_t ntiles,
-                         uint32_t *out, int cus, hipStream_t s, const uint32_t *tmp_row = nullptr,
-                         uint32_t *out_row = nullptr);
-void launch_flist_group_offsets(const uint32_t *keys, uint64_t n, const uint32_t *ub, uint64_t U, uint64_t *loff,
-                                hipStream_t s);
 // factor.hip: the factorized hop's rows written over their sources' lists, by tiles of the output space
 // Binding row r owns the list entries [loff[g[r]], loff[g[r]+1]) of the list columns: output row o of it
 // takes every list column's entry at rbase[r] + o and every constant's value of row r.
 constexpr int kFemitCols = 4;   // constants per binding row
-constexpr int kFemitLists = 3;  // list columns
+constexpr int kFemitLists = 1;  // list columns
 struct FemitArgs {
   const uint32_t *g;     // [R] binding row → its list (group) index
   const uint64_t *roff;  // [R+1] first output row of every binding row (scan of its list length)
@@ -273,12 +299,6 @@ void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const u
                          unsigned long long *counts, hipStream_t s);
 void launch_key_scatter_seg(const uint32_t *key, const uint32_t *val, const uint64_t *seg_start, const uint32_t *seg_count,
                             uint32_t nseg, unsigned long long *cursor, uint32_t *out, hipStream_t s);
-// rank[i] = entry i's place in its key's group (counts[key] advanced by one atomic per run), then
-// out[loff[key[i]] + rank[i]] = val[i] (fewer than 2^32 entries)
-void launch_key_rank_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
-                         unsigned int *counts, uint32_t *rank, hipStream_t s);
-void launch_key_place_seg(const uint32_t *key, const uint32_t *val, const uint32_t *rank, const uint64_t *seg_start,
-                          const uint32_t *seg_count, uint32_t nseg, const uint64_t *loff, uint32_t *out, hipStream_t s);
 // 32-bit counters and cursors (fewer than 2^32 entries)
 void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
                          unsigned int *counts, hipStream_t s);

@@ -437,11 +437,11 @@ void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_
 
 // degrees of the rows [lo, hi) of one CSR (u32: a row of 2^32 or more entries does not occur in a
 // partition's snapshot)
-__global__ void k_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint32_t *deg) {
+__global__ void k_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint64_t *deg) {
   const uint64_t v = (uint64_t)lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v < hi) deg[v - lo] = (uint32_t)(rp[v + 1] - rp[v]);
+  if (v < hi) deg[v - lo] = rp[v + 1] - rp[v];
 }
-void launch_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint32_t *deg, hipStream_t s) {
+void launch_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint64_t *deg, hipStream_t s) {
   if (hi <= lo) return;
   hipLaunchKernelGGL(k_row_degree_range, dim3(nblocks(hi - lo, 256)), dim3(256), 0, s, rp, lo, hi, deg);
   KCHECK("k_row_degree_range");
@@ -2528,95 +2528,6 @@ void launch_key_scatter_seg(const uint32_t *key, const uint32_t *val, const uint
   key_scatter_seg(key, val, seg_start, seg_count, nseg, cursor, out, s);
 }
 
-// Grouping in two atomic-free-placement passes (the factorized lists at M1: the scatter's returning
-// atomics were its cost, 120 µs): k_key_rank_seg counts every key's entries with one returning atomic
-// per run and writes each entry's rank inside its key's group (rank[i] = the run's base + its place in
-// the run); after the offsets' scan, k_key_place_seg writes out[loff[key[i]] + rank[i]] = val[i] with
-// plain loads and stores.
-__global__ __launch_bounds__(256) void k_key_rank_seg(const uint32_t *__restrict__ key,
-                                                      const uint64_t *__restrict__ seg_start,
-                                                      const uint32_t *__restrict__ seg_count, uint32_t nseg,
-                                                      unsigned int *counts, uint32_t *rank) {
-  const uint32_t sg = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (sg >= nseg) return;
-  const int lane = threadIdx.x & 63;
-  const uint64_t b = seg_start[sg];
-  const uint32_t n = seg_count[sg];
-  for (uint32_t j = 0; j < n; j += 64 * kSegU) {
-    uint32_t k[kSegU];
-#pragma unroll
-    for (int u = 0; u < kSegU; ++u) {
-      const uint32_t jj = j + 64u * u + lane;
-      k[u] = key[b + (jj < n ? jj : 0)];
-    }
-    unsigned int base[kSegU];
-    uint64_t heads[kSegU];
-#pragma unroll
-    for (int u = 0; u < kSegU; ++u) {
-      const uint32_t j0 = j + 64u * u;
-      const bool valid = j0 + lane < n;
-      const uint32_t kk = valid ? k[u] : 0xFFFFFFFFu;
-      heads[u] = key_runs(kk, valid, lane);
-      const int nvalid = j0 < n ? (int)min(64u, n - j0) : 0;
-      base[u] = 0;
-      if (valid && ((heads[u] >> lane) & 1)) {
-        const uint64_t later = lane == 63 ? 0 : heads[u] & (~0ull << (lane + 1));
-        const int nxt = later ? __ffsll((unsigned long long)later) - 1 : 64;
-        base[u] = atomicAdd(&counts[kk], (unsigned int)(min(nxt, nvalid) - lane));
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kSegU; ++u) {
-      const uint32_t j0 = j + 64u * u;
-      const uint64_t upto = heads[u] & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-      const int hl = upto ? 63 - __clzll((long long)upto) : lane;
-      const unsigned int bs = __shfl(base[u], hl, 64);
-      if (j0 + lane < n) rank[b + j0 + lane] = bs + (unsigned int)(lane - hl);
-    }
-  }
-}
-__global__ __launch_bounds__(256) void k_key_place_seg(const uint32_t *__restrict__ key, const uint32_t *__restrict__ val,
-                                                       const uint32_t *__restrict__ rank,
-                                                       const uint64_t *__restrict__ seg_start,
-                                                       const uint32_t *__restrict__ seg_count, uint32_t nseg,
-                                                       const uint64_t *__restrict__ loff, uint32_t *out) {
-  const uint32_t sg = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (sg >= nseg) return;
-  const int lane = threadIdx.x & 63;
-  const uint64_t b = seg_start[sg];
-  const uint32_t n = seg_count[sg];
-  for (uint32_t j = 0; j < n; j += 64 * kSegU) {
-    uint32_t k[kSegU], v[kSegU], rk[kSegU];
-#pragma unroll
-    for (int u = 0; u < kSegU; ++u) {
-      const uint32_t jj = j + 64u * u + lane;
-      const uint64_t i = b + (jj < n ? jj : 0);
-      k[u] = key[i];
-      v[u] = val[i];
-      rk[u] = rank[i];
-    }
-    uint64_t o[kSegU];
-#pragma unroll
-    for (int u = 0; u < kSegU; ++u) o[u] = loff[k[u]];
-#pragma unroll
-    for (int u = 0; u < kSegU; ++u)
-      if (j + 64u * u + lane < n) out[o[u] + rk[u]] = v[u];
-  }
-}
-void launch_key_rank_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
-                         unsigned int *counts, uint32_t *rank, hipStream_t s) {
-  if (!nseg) return;
-  hipLaunchKernelGGL(k_key_rank_seg, dim3(nblocks(nseg, 4)), dim3(256), 0, s, key, seg_start, seg_count, nseg, counts,
-                     rank);
-  KCHECK("k_key_rank_seg");
-}
-void launch_key_place_seg(const uint32_t *key, const uint32_t *val, const uint32_t *rank, const uint64_t *seg_start,
-                          const uint32_t *seg_count, uint32_t nseg, const uint64_t *loff, uint32_t *out, hipStream_t s) {
-  if (!nseg) return;
-  hipLaunchKernelGGL(k_key_place_seg, dim3(nblocks(nseg, 4)), dim3(256), 0, s, key, val, rank, seg_start, seg_count,
-                     nseg, loff, out);
-  KCHECK("k_key_place_seg");
-}
 
 // ---- TRAVERSE (exec.hip Executor::traverse_bfs) -----------------------------------------------------
 // out[j] = the vertex whose RID is keys[j] (left untouched when no vertex has it; RIDs are unique)

@@ -325,6 +325,8 @@ bool device_projection_ok(const Graph &g, const Plan &p, std::string *why) {
 void device_project(Graph &g, const Plan &p, const std::vector<const uint32_t *> &cols, uint64_t n, int64_t limit,
                     int cus, hipStream_t s, omx_result &res) {
   const int nitems = (int)p.returns.size();
+  if (n >= UINT32_MAX) fail(OMX_E_INVALID, "internal: device projection of 2^32 or more tuples (u32 table slots)");
+  if (limit >= 0) fail(OMX_E_INVALID, "internal: device projection with LIMIT (the host evaluator stops at the limit)");
   std::vector<PjProgram> progs;
   for (const ReturnItem &ri : p.returns) {
     Compiler c{g, p};

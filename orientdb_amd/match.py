@@ -193,9 +193,10 @@ class OMatchStatement:
         return json.loads(buf.value.decode())
 
     def execute(self, graph, *args, mode=N.OMX_MODE_MATERIALIZE, flags=0, shard=(0, 1), documents=True, comm=None,
-                **named):
+                fetch_rows=True, **named):
         """comm: the ranks' Comm (orientdb_amd.dist) when `graph` is a partition; every rank then
-        returns its share of the distinct rows (their union is the result)."""
+        returns its share of the distinct rows (their union is the result). fetch_rows=False leaves the
+        RID rows libomx copied to the host unread (rs.rows stays empty; info and timings are read)."""
         arr, n = _values(args, named)
         o = N.omx_exec_options()
         N.lib().omx_exec_options_init(C.byref(o))
@@ -209,12 +210,12 @@ class OMatchStatement:
         r = C.c_void_p()
         N.check(N.lib().omx_execute(graph.handle, self._h, C.byref(o), C.byref(r)))
         try:
-            return self._collect(r, documents)
+            return self._collect(r, documents, fetch_rows)
         finally:
             N.lib().omx_result_free(r)
 
     @staticmethod
-    def _collect(r, documents):
+    def _collect(r, documents, fetch_rows=True):
         L = N.lib()
         info = N.omx_result_info()
         N.check(L.omx_result_info_get(r, C.byref(info)))
@@ -244,7 +245,9 @@ class OMatchStatement:
             name, ms, by = C.c_char_p(), C.c_double(), C.c_uint64()
             if L.omx_result_kernel_launch(r, i, C.byref(name), C.byref(ms), C.byref(by)) != 0:
                 break
-            launches.append({"name": name.value.decode(), "ms": ms.value, "alg_bytes": by.value})
+            hbm = C.c_uint64()
+            L.omx_result_kernel_launch_bytes(r, i, None, C.byref(hbm))
+            launches.append({"name": name.value.decode(), "ms": ms.value, "alg_bytes": by.value, "hbm_bytes": hbm.value})
             i += 1
         rs.kernel_launches = launches
         nrows, ncols = info.n_rows, info.n_cols
@@ -259,7 +262,7 @@ class OMatchStatement:
                 vals = [_column_values(r, c, *rs.cells[name]) for c, name in enumerate(cols)]
                 rs.extend(ODocument(zip(cols, row)) for row in zip(*vals))
             return rs
-        p = L.omx_result_rows(r)
+        p = L.omx_result_rows(r) if fetch_rows else None
         if p and nrows and ncols:
             rs.rows = np.ctypeslib.as_array(p, shape=(nrows * ncols,)).reshape(nrows, ncols).copy()
         else:

@@ -363,26 +363,17 @@ FACTOR_IDS = ("c2_both_ends", "c1_abc", "two_cols_dedup", "in_dir", "both_dir", 
               "paths", "elements", "fof_not_me", "matched_and_filter", "optional_free", "bound_candidate")
 
 
-@pytest.mark.parametrize("flist", ["tiles", "tiles_forward", "tiles_pairs", "grouped"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
-def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, flist, monkeypatch):
+def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, monkeypatch):
     """Every filtered hop through the factorized expansion (distinct sources → filtered lists → rows
-    over the lists, Executor::expand_factorized): same rows, same E_t — on the simple graph and on the
-    multigraph, whose parallel edges repeat a neighbour in a source's list (ridbag multiplicity,
-    OSBTreeRidBag.java:292-295) through the distinct-source grouping. tiles: the lists compacted in
-    order by tiles of the flat entry space (factor.hip), from the targets' in-rows when that reads fewer
-    entries (then sorted by source); tiles_forward: from the sources' rows; tiles_pairs: the (source,
-    target) pairs expanded over the rows grouped by source; grouped (the default): the generic filtered
-    expansion + key histogram / scatter (and every multi-part adjacency such as both())."""
+    over the lists, Executor::expand_factorized): same rows, same E_t and bindings as the direct
+    expansion — on the simple graph and on the multigraph, whose parallel edges repeat a neighbour in a
+    source's list (ridbag multiplicity, OSBTreeRidBag.java:292-295) through the distinct-source grouping.
+    The rows are written by the output-tiled emission at any size (OMX_FEMIT=force)."""
     import orientdb_amd as o
     g, ref = rmat10 if graph == "simple" else rmat10_raw
-    monkeypatch.setenv("OMX_FLIST", "0" if flist == "grouped" else "1")
-    monkeypatch.setenv("OMX_FLIST_PAIRS", "1" if flist == "tiles_pairs" else "0")
-    # tiles: the lists from the targets' in-rows whenever that reads fewer entries; tiles_forward: always
-    # from the sources' rows
-    monkeypatch.setenv("OMX_FLIST_REVERSE", "0" if flist == "tiles_forward" else "1")
-    monkeypatch.setenv("OMX_FEMIT", "force")  # the rows written by the output-tiled emission at any size
+    monkeypatch.setenv("OMX_FEMIT", "force")
     monkeypatch.setenv("OMX_FACTOR", "0")
     direct = o.OMatchStatement(q[1]).execute(g, documents=False)
     monkeypatch.setenv("OMX_FACTOR", "force")
@@ -392,39 +383,31 @@ def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, flist, monkeypatch
     assert rs.info["bindings"] == direct.info["bindings"]
 
 
-@pytest.mark.parametrize("emit", ["binned", "unsorted", "slow", "sources", "targets", "targets_slow", "grp64", "ranks"])
+@pytest.mark.parametrize("emit", ["binned", "slow", "grp64"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
 def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, monkeypatch):
-    """The factorized hop's rows written every way (the default — rows grouped by source, output tiles of
-    k_femit_w — is covered by test_rmat_parity_factorized): binned = the generic unfiltered expansion over
-    the lists (OMX_FEMIT=0); unsorted = the rows in their order; slow = every output tile through
-    k_femit_slow (a search of the row offsets per output row); sources = the lists always built from the
-    sources' side; targets = always from the targets' side (the (b, c) pairs of the targets' in-rows
-    written over the rows grouped by source, no lists), also through the slow tiles; grp64 = the lists
-    grouped with 64-bit counters and cursors (OMX_GRP32=0; 32-bit by default); ranks = each entry's rank
-    written in the hist pass and placed without atomics (OMX_GRANK=1). Same rows, E_t and
-    bindings as the direct expansion (P/OMatchStatement.java:491-497 per row)."""
+    """The factorized hop's rows written the other ways (the default — rows grouped by source, output
+    tiles of k_femit_w — is covered by test_rmat_parity_factorized): binned = the generic unfiltered
+    expansion over the lists (OMX_FEMIT=0); slow = every output tile through k_femit_slow (a search of
+    the row offsets per output row); grp64 = the lists grouped with 64-bit counters and cursors
+    (OMX_GRP32=0, the path of lists of 2^32 or more entries). Same rows, E_t and bindings as the direct
+    expansion (P/OMatchStatement.java:491-497 per row)."""
     import orientdb_amd as o
     g, ref = rmat10 if graph == "simple" else rmat10_raw
     monkeypatch.setenv("OMX_FACTOR", "0")
     direct = o.OMatchStatement(q[1]).execute(g, documents=False)
     monkeypatch.setenv("OMX_FACTOR", "force")
     monkeypatch.setenv("OMX_FEMIT", "0" if emit == "binned" else "force")
-    monkeypatch.setenv("OMX_FEMIT_SORT", "0" if emit == "unsorted" else "1")
-    monkeypatch.setenv("OMX_FEMIT_SLOW", "1" if emit in ("slow", "targets_slow") else "0")
-    monkeypatch.setenv("OMX_FEMIT_REVERSE", "force" if emit.startswith("targets") else "0" if emit in ("sources", "grp64", "ranks") else "1")
+    monkeypatch.setenv("OMX_FEMIT_SLOW", "1" if emit == "slow" else "0")
     monkeypatch.setenv("OMX_GRP32", "0" if emit == "grp64" else "1")
-    monkeypatch.setenv("OMX_GRANK", "1" if emit == "ranks" else "0")
     rs = _parity(g, ref, q[1], q[2])
     assert rs.info["edges_traversed"] == direct.info["edges_traversed"]
     assert rs.info["bindings"] == direct.info["bindings"]
 
 
-@pytest.mark.parametrize("side", ["sources", "targets"])
 @pytest.mark.parametrize("slow", ["0", "1"])
-@pytest.mark.parametrize("sort", ["0", "1"])
-def test_factorized_emission_many_tiles_rmat16(rmat16, side, slow, sort, monkeypatch):
+def test_factorized_emission_many_tiles_rmat16(rmat16, slow, monkeypatch):
     """Output tiles of the factorized emission across many tiles (RMAT-16 2-hop with WHERE on both ends:
     rows spanning tile boundaries, runs of short lists in one tile, a partial last tile): rows and digest
     equal with the emission through the generic expansion."""
@@ -436,9 +419,7 @@ def test_factorized_emission_many_tiles_rmat16(rmat16, side, slow, sort, monkeyp
     fl = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST
     base = o.OMatchStatement(q).execute(g, documents=False, flags=fl)
     monkeypatch.setenv("OMX_FEMIT", "force")
-    monkeypatch.setenv("OMX_FEMIT_SORT", sort)
     monkeypatch.setenv("OMX_FEMIT_SLOW", slow)
-    monkeypatch.setenv("OMX_FEMIT_REVERSE", "force" if side == "targets" else "0")
     rs = o.OMatchStatement(q).execute(g, documents=False, flags=fl)
     assert rs.info["factorized_hops"] >= 1 and rs.info["n_rows"] > 100000
     assert rs.info["n_rows"] == base.info["n_rows"] and rs.info["digest"] == base.info["digest"]

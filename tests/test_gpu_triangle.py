@@ -1,8 +1,11 @@
 """Cyclic patterns (configs[3]): the expansion that binds the last alias of a cycle and the
-check that closes it run fused — every expanded neighbour is kept only if it lies in the sorted adjacency
-of the row's closing vertex (binary search inside the expansion kernels), so wedges are never
-materialised. Parity: identical rows to the oracle and to the unfused expand + check path, and the same
-traversed-edge count (the fused kernels add Σ |N(closing vertex)| over the wedges, as the check would).
+check that closes it run fused as an intersection of two sorted adjacency lists, so wedges are never
+materialised: rows whose lists have comparable lengths through the merge path (isect.hip k_isect_merge),
+the others by binary search of the shorter list into the longer one inside the expansion kernels.
+Parity: identical rows to the oracle and to the unfused expand + check path, and the same traversed-edge
+count (the fused kernels add Σ |N(closing vertex)| over the wedges, as the check would), with the merge
+chosen by its length-ratio rule (merge), forced on every row that fits a tile (merge_force), and off
+(probe: every row binary-searches).
 """
 import numpy as np
 import pytest
@@ -26,10 +29,19 @@ def _cols(q):
     return [c.strip() for c in q.split("RETURN")[1].split(",")]
 
 
-@pytest.mark.parametrize("fuse", ["1", "0"])
-@pytest.mark.parametrize("q", CYCLES, ids=[q[0] for q in CYCLES])
-def test_cycle_parity(rmat10, q, fuse, monkeypatch):
+MODES = {"merge": ("1", "1"), "merge_force": ("1", "force"), "probe": ("1", "0"), "unfused": ("0", "1")}
+
+
+def _mode(monkeypatch, mode):
+    fuse, merge = MODES[mode]
     monkeypatch.setenv("OMX_FUSE_CHECK", fuse)
+    monkeypatch.setenv("OMX_MERGE", merge)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("q", CYCLES, ids=[q[0] for q in CYCLES])
+def test_cycle_parity(rmat10, q, mode, monkeypatch):
+    _mode(monkeypatch, mode)
     g, ref = rmat10
     _parity(g, ref, q[1], _cols(q[1]))
 
@@ -39,11 +51,12 @@ def test_fused_counts_equal_unfused(rmat10, q, monkeypatch):
     import orientdb_amd as o
     g, _ = rmat10
     info = {}
-    for fuse in ("1", "0"):
-        monkeypatch.setenv("OMX_FUSE_CHECK", fuse)
-        info[fuse] = o.OMatchStatement(q[1]).execute(g).info
-    for k in ("n_rows", "bindings", "edges_traversed"):
-        assert info["1"][k] == info["0"][k], k
+    for mode in MODES:
+        _mode(monkeypatch, mode)
+        info[mode] = o.OMatchStatement(q[1]).execute(g).info
+    for mode in ("merge", "merge_force", "probe"):
+        for k in ("n_rows", "bindings", "edges_traversed"):
+            assert info[mode][k] == info["unfused"][k], (mode, k)
 
 
 @pytest.mark.parametrize("q", CYCLES, ids=[q[0] for q in CYCLES])
@@ -61,12 +74,52 @@ def test_shorter_list_first_equals_plain_fused(rmat10, q, monkeypatch):
         assert info["1"][k] == info["0"][k], k
 
 
+@pytest.mark.parametrize("merge", ["0", "force"])
 @pytest.mark.parametrize("q", CYCLES[:3], ids=[q[0] for q in CYCLES[:3]])
-def test_cycle_parity_heavy_and_multigraph(rmat10, rmat10_raw, q, monkeypatch):
-    """every row of degree ≥ 2 through the chunked kernel's fused path; parallel edges kept."""
+def test_cycle_parity_heavy_and_multigraph(rmat10, rmat10_raw, q, merge, monkeypatch):
+    """every probed row of degree ≥ 2 through the chunked kernel's fused path, or every row merged;
+    parallel edges kept (a merged row keeps N_x's multiplicity: one row per edge x → t, P/OMatchStatement
+    .java:468-477 checks each of them for existence)."""
+    import orientdb_amd as o
     monkeypatch.setenv("OMX_HEAVY_DEG", "2")
+    monkeypatch.setenv("OMX_MERGE", merge)
     for g, ref in (rmat10, rmat10_raw):
-        _parity(g, ref, q[1], _cols(q[1]))
+        rs = _parity(g, ref, q[1], _cols(q[1]))
+        monkeypatch.setenv("OMX_FUSE_CHECK", "0")
+        un = o.OMatchStatement(q[1]).execute(g).info
+        monkeypatch.setenv("OMX_FUSE_CHECK", "1")
+        for k in ("n_rows", "bindings", "edges_traversed"):
+            assert rs.info[k] == un[k], k
+
+
+@pytest.mark.parametrize("k", [1, 7, 64, 200, 512, 600])
+def test_merge_long_and_short_rows(k, monkeypatch):
+    """Merged rows of every size against the probe and a brute-force enumeration: vertex 0 → 1, 1 → s
+    and s → 0 for the k vertices s of S, plus chords s → s + 1: the row (0, 1) intersects N_out(1) = S
+    ∪ … with N_in(0) = S (m + n = 2k: one row filling a tile half at k = 512, over the merge cap at 600),
+    the rows (1, s) and (s, 0) lists of one or two entries (many rows a tile, rows spanning a thread's
+    8 merged positions)."""
+    import orientdb_amd as o
+    V = k + 2
+    edges = {(0, 1)} | {(1, s) for s in range(2, V)} | {(s, 0) for s in range(2, V)}
+    edges |= {(s, s + 1) for s in range(2, V - 1)}
+    out = {v: sorted(t for (u, t) in edges if u == v) for v in range(V)}
+    rp = np.zeros(V + 1, np.uint64)
+    rp[1:] = np.cumsum([len(out[v]) for v in range(V)])
+    col = np.array([t for v in range(V) for t in out[v]], np.uint32)
+    g = o.GraphSnapshot.person_knows(rp, col, seed=1, device=0, keep_csr=True)
+    q = CYCLES[0][1]
+    want = sorted((a, b, c) for (a, b) in edges for c in out[b] if (c, a) in edges)
+    res = {}
+    for merge in ("force", "1", "0"):
+        monkeypatch.setenv("OMX_MERGE", merge)
+        rs = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_NO_RID_MAP)
+        idx = [rs.columns.index(c) for c in "abc"]
+        got = sorted(tuple(int(x) for x in row) for row in rs.rows[:, idx].tolist())
+        assert got == want, merge
+        res[merge] = (rs.info["edges_traversed"], rs.info["bindings"], rs.info["n_rows"])
+    assert res["force"] == res["1"] == res["0"]
+    g.close()
 
 
 @pytest.fixture(scope="module")
@@ -75,11 +128,14 @@ def ldbc():
     return o.GraphSnapshot.ldbc_like(device=0, keep_csr=True)
 
 
-def test_c4_ldbc_sf10_vs_c_oracle(ldbc):
+@pytest.mark.parametrize("merge", ["1", "force", "0"])
+def test_c4_ldbc_sf10_vs_c_oracle(ldbc, merge, monkeypatch):
     """configs[3] at full size: every directed triangle of the LDBC-like SF10 Knows graph, bit-exact
-    against oracle/dfs_ref.c, with the same traversed-edge count."""
+    against oracle/dfs_ref.c, with the same traversed-edge count — merge path by its ratio rule, on every
+    row that fits a tile, and off."""
     import orientdb_amd as o
     from oracle import dfs
+    monkeypatch.setenv("OMX_MERGE", merge)
     g = ldbc
     q = CYCLES[0][1]
     rs = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_NO_RID_MAP)
