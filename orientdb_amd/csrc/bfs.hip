@@ -163,6 +163,36 @@ void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsig
   KCHECK("k_bfs_list");
 }
 
+// partitioned sparse levels: the rank's frontier as (vertex, mask low word, mask high word) triples
+// (list: owned vertices relative to vlo, from k_bfs_list over fr + vlo), and their scatter on the peers
+__global__ void k_bfs_frontier_pack(uint32_t *list, uint64_t n, uint32_t vlo, const uint64_t *fr, uint32_t *mlo,
+                                    uint32_t *mhi) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t v = list[i] + vlo;
+  const uint64_t m = fr[v];
+  list[i] = v;
+  mlo[i] = (uint32_t)m;
+  mhi[i] = (uint32_t)(m >> 32);
+}
+__global__ void k_bfs_frontier_scatter(const uint32_t *v, const uint32_t *mlo, const uint32_t *mhi, uint64_t n,
+                                       uint64_t *fr) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) fr[v[i]] = ((uint64_t)mhi[i] << 32) | mlo[i];
+}
+void launch_bfs_frontier_pack(uint32_t *list, uint64_t n, uint32_t vlo, const uint64_t *fr, uint32_t *mlo, uint32_t *mhi,
+                              hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_bfs_frontier_pack, dim3(nblocks(n, kB)), dim3(kB), 0, s, list, n, vlo, fr, mlo, mhi);
+  KCHECK("k_bfs_frontier_pack");
+}
+void launch_bfs_frontier_scatter(const uint32_t *v, const uint32_t *mlo, const uint32_t *mhi, uint64_t n, uint64_t *fr,
+                                 hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_bfs_frontier_scatter, dim3(nblocks(n, kB)), dim3(kB), 0, s, v, mlo, mhi, n, fr);
+  KCHECK("k_bfs_frontier_scatter");
+}
+
 // degree of every listed vertex in one adjacency part (+ a trailing 0 for the exclusive scan)
 __global__ void k_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

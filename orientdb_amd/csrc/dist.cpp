@@ -23,7 +23,7 @@ namespace omx {
 
 // ---- threads ----------------------------------------------------------------------------------------
 
-ThreadHub::ThreadHub(int w) : world(w), counts(w, std::vector<uint64_t>(w, 0)), sbuf(w), sdispl(w), gathered(w, 0) {}
+ThreadHub::ThreadHub(int w) : world(w), counts(w, std::vector<uint64_t>(w, 0)), sbuf(w), sdispl(w), gathered(w) {}
 
 void ThreadHub::barrier() {
   std::unique_lock<std::mutex> lk(m);
@@ -99,7 +99,7 @@ class ThreadTransport : public Transport {
 
   void abort() override { hub_->abort(); }
 
-  std::vector<uint64_t> allgather(uint64_t x, hipStream_t) override {
+  std::vector<uint64_t> allgather_n(const std::vector<uint64_t> &x, hipStream_t) override {
     ++exchanges;
     {
       std::lock_guard<std::mutex> lk(hub_->m);
@@ -109,7 +109,10 @@ class ThreadTransport : public Transport {
     std::vector<uint64_t> out;
     {
       std::lock_guard<std::mutex> lk(hub_->m);
-      out = hub_->gathered;
+      for (const auto &g : hub_->gathered) {
+        if (g.size() != x.size()) fail(OMX_E_INVALID, "internal: allgather_n sizes differ between ranks");
+        out.insert(out.end(), g.begin(), g.end());
+      }
     }
     hub_->barrier();  // the slots may be reused
     return out;
@@ -131,8 +134,8 @@ class RcclTransport : public Transport {
     HIP_OK(hipSetDevice(device));
     NCCL_OK(ncclCommInitRank(&comm_, world, uid, rank));
     HIP_OK(hipMalloc((void **)&d_recv_, std::max(1, world) * sizeof(uint64_t)));
-    HIP_OK(hipMalloc((void **)&d_one_, sizeof(uint64_t)));
-    HIP_OK(hipMalloc((void **)&d_all_, std::max(1, world) * sizeof(uint64_t)));
+    HIP_OK(hipMalloc((void **)&d_one_, kMaxGather * sizeof(uint64_t)));
+    HIP_OK(hipMalloc((void **)&d_all_, std::max(1, world) * kMaxGather * sizeof(uint64_t)));
   }
   ~RcclTransport() override {
     (void)hipSetDevice(device_);
@@ -147,14 +150,17 @@ class RcclTransport : public Transport {
     comm_ = nullptr;
   }
 
-  std::vector<uint64_t> allgather(uint64_t x, hipStream_t s) override {
+  std::vector<uint64_t> allgather_n(const std::vector<uint64_t> &x, hipStream_t s) override {
     ++exchanges;
     if (!comm_) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: the communicator was aborted");
-    HIP_OK(hipMemcpyAsync(d_one_, &x, sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    NCCL_OK(ncclAllGather(d_one_, d_all_, 1, ncclUint64, comm_, s));
-    std::vector<uint64_t> out(world_);
-    HIP_OK(hipMemcpyAsync(out.data(), d_all_, world_ * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
+    const size_t n = x.size();
+    if (n > kMaxGather) fail(OMX_E_INVALID, "internal: allgather_n of more than 8 words");
+    if (n == 0) return {};
+    HIP_OK(hipMemcpyAsync(d_one_, x.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    NCCL_OK(ncclAllGather(d_one_, d_all_, n, ncclUint64, comm_, s));
+    std::vector<uint64_t> out(world_ * n);
+    HIP_OK(hipMemcpyAsync(out.data(), d_all_, world_ * n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));  // (x and out are host locals)
     return out;
   }
   int rank() const override { return rank_; }
@@ -186,6 +192,7 @@ class RcclTransport : public Transport {
   }
 
  private:
+  static constexpr size_t kMaxGather = 8;  // words per rank in one allgather_n
   int rank_, world_, device_;
   ncclComm_t comm_ = nullptr;
   uint64_t *d_recv_ = nullptr;

@@ -42,7 +42,10 @@ class Transport {
   // instead of waiting forever. The communicator is unusable afterwards.
   virtual void abort() = 0;
   // every rank's x (host values), in rank order
-  virtual std::vector<uint64_t> allgather(uint64_t x, hipStream_t s) = 0;
+  std::vector<uint64_t> allgather(uint64_t x, hipStream_t s) { return allgather_n({x}, s); }
+  // every rank's words x[0..n) (the same n on every rank), rank-major: out[p·n + i] = rank p's x[i] —
+  // several per-level values in one host round trip
+  virtual std::vector<uint64_t> allgather_n(const std::vector<uint64_t> &x, hipStream_t s) = 0;
   // collectives this rank has entered (counts / alltoallv / allgather): an execute that fails before
   // its first exchange failed the same way on every rank (the plan and its checks are replicated), so
   // nobody waits for it and the communicator stays usable
@@ -63,7 +66,7 @@ struct ThreadHub {
   std::vector<std::vector<uint64_t>> counts;                // [src][dst]
   std::vector<std::vector<const uint32_t *>> sbuf;          // [src][column]
   std::vector<std::vector<uint64_t>> sdispl;                // [src][dst]
-  std::vector<uint64_t> gathered;                           // [src] (allgather)
+  std::vector<std::vector<uint64_t>> gathered;              // [src] (allgather_n)
 };
 
 std::unique_ptr<Transport> make_thread_transport(std::shared_ptr<ThreadHub> hub, int rank);

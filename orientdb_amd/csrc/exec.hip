@@ -144,6 +144,16 @@ class Timer {
   std::vector<Rec> recs_;
 };
 
+// head[i] = 1 where a run of equal sorted keys starts
+__global__ void k_u64_heads(const uint64_t *k, uint64_t n, uint8_t *head) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) head[i] = i == 0 || k[i] != k[i - 1];
+}
+static void launch_u64_heads(const uint64_t *k, uint64_t n, uint8_t *head, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_u64_heads, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, k, n, head);
+}
+
 __global__ void k_invert_flags(const uint8_t *in, uint8_t *out, uint64_t n) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = in[i] ? 0 : 1;
@@ -180,6 +190,8 @@ class Executor {
       slice_shift_ = (uint32_t)std::min<long>(20, std::max<long>(6, std::strtol(sh, nullptr, 10)));
     if (const char *f = std::getenv("OMX_FUSE_CHECK")) fuse_mode_ = f;  // "0" disables the intersection
     if (const char *sw = std::getenv("OMX_SWAP_CHECK")) swap_ = std::strcmp(sw, "0") != 0;
+    if (const char *de = std::getenv("OMX_DENSE_EXCHANGE")) dense_exchange_ = std::strcmp(de, "0") != 0;
+    if (const char *tl = std::getenv("OMX_TLIST")) tlist_ = std::strcmp(tl, "force") == 0 ? 2 : std::strcmp(tl, "0") != 0 ? 1 : 0;
     // OMX_MERGE: "0" keeps every closing check a binary-search probe; "force" merges every row whose two
     // lists fit a tile (tests); OMX_MERGE_RATIO: merge when the longer list is ≤ ratio × the shorter
     if (const char *mg = std::getenv("OMX_MERGE")) merge_ = std::strcmp(mg, "force") == 0 ? 2 : std::strcmp(mg, "0") != 0 ? 1 : 0;
@@ -468,6 +480,9 @@ class Executor {
   double pull_probe_ = 0.1;
   bool pull_wave_ = true;  // OMX_PULL_WAVE=0: the workgroup-tiled k_bfs_pull for the tiled bottom-up levels
   bool pull_exit_ = true;  // denser levels pull per vertex with an early exit (OMX_PULL_EXIT=0: tiles)
+  // partitioned BFS: levels whose frontier holds fewer than V/12 vertices exchange (vertex, mask) triples
+  // instead of the frontier blocks (OMX_DENSE_EXCHANGE=1: always the blocks)
+  bool dense_exchange_ = false;
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
   // sliced hops size their arenas from the target bitmap's density (OMX_ARENA_ESTIMATE=0: exact bound;
   // OMX_ARENA_MARGIN scales the estimate, 0 forces the short-arena re-run in tests)
@@ -558,7 +573,12 @@ class Executor {
             need.push_back(part);
     if (need.empty()) return;
     const int W = tr_->world();
-    const std::vector<uint64_t> plo = tr_->allgather(g_.part_lo, s_), phi = tr_->allgather(g_.part_hi, s_);
+    const std::vector<uint64_t> lohi = tr_->allgather_n({g_.part_lo, g_.part_hi}, s_);
+    std::vector<uint64_t> plo(W), phi(W);
+    for (int p = 0; p < W; ++p) {
+      plo[p] = lohi[2 * p];
+      phi[p] = lohi[2 * p + 1];
+    }
     const uint32_t V = g_.V, lo = g_.part_lo, hi = g_.part_hi;
     for (const auto &part : need) {
       EdgeSet &es = g_.esets[part.first];
@@ -593,7 +613,9 @@ class Executor {
     DPred d{};
     d.cols = g_.d_cols;
     d.vclass = g_.d_vclass;
-    if (class_id >= 0) {
+    // (a class whose polymorphic set holds every vertex of the snapshot — configs' class:Person — tests
+    // nothing: the bitmap kernels then read no class ids)
+    if (class_id >= 0 && g_.count(class_id) < (uint64_t)g_.V) {
       d.use_class = 1;
       g_.class_mask(class_id, d.class_mask);
     }
@@ -1458,12 +1480,32 @@ class Executor {
     bound_[st.dst] = 1;
     std::vector<const uint32_t *> carry;
     for (int c : cols) carry.push_back(col_[c].p);
+    // a set-valued hop over an adjacency that may repeat a neighbour: the input row index rides along
+    // and the (row, neighbour) pairs are made distinct (a count-only hop writes its rows for that)
+    const bool nbset = st.distinct_nb && !st.adj.dup_free && !check;
+    DBuf<uint32_t> rid;
+    if (nbset) {
+      write = true;
+      allow_segmented = false;
+      rid = DBuf<uint32_t>(&pool_, std::max<uint64_t>(R_, 1));
+      launch_iota(rid.p, R_, s_);
+      carry.push_back(rid.p);
+    }
     ExpandOut o = expand_core(col_[st.src].p, R_, st.adj, bitmap(st.filter_bm), carry, write, allow_segmented,
                               check ? col_[check->src].p : nullptr, check ? &check->adj : nullptr,
                               check ? bitmap(check->filter_bm) : nullptr);
     edges_ += o.E + o.E_member;
     if (!o.counted_from_degrees) edges_iter_ += o.E;
     R_ = o.n;
+    if (nbset && o.n) {
+      DBuf<uint32_t> orid = std::move(o.carry.back());
+      o.carry.pop_back();
+      std::vector<DBuf<uint32_t> *> oc;
+      for (auto &c : o.carry) oc.push_back(&c);
+      R_ = o.n = distinct_pairs(orid, o.dst, oc, o.n);
+    } else if (nbset) {
+      o.carry.pop_back();
+    }
     if (n_empty) {  // append the null-target rows
       const uint64_t n = R_ + n_empty;
       auto cat = [&](DBuf<uint32_t> *a, const uint32_t *b) {
@@ -1714,6 +1756,47 @@ class Executor {
                                            : alg);
   }
 
+  // The same (source index, neighbour) pairs from the targets' side: the vertices c passing the hop's
+  // filter expanded over their in-rows, filtered by the bitmap of the distinct sources (the sliced
+  // filtered expansion, its bitmap slices in LDS), each surviving in-neighbour b replaced by its index
+  // among the sources. Σ indeg(C) entries are read instead of Σ deg(U) (M1: the 10 % target window, 26 M
+  // against 200 M; the pairs are the lists' entries, one per edge b → c, so parallel edges keep their
+  // multiplicity). One GPU, one adjacency part; taken when it reads fewer than half the entries
+  // (OMX_TLIST=0: never, =force: whenever it applies). Returns false (nothing done) otherwise.
+  int tlist_ = 1;
+  bool targets_side_lists(const Step &st, uint64_t U, const DBuf<uint32_t> &ub, const DBuf<uint32_t> &iu, uint64_t EU,
+                          bool nbset, ExpandOut &l) {
+    if (!tlist_ || dist_ || st.adj.parts.size() != 1 || st.filter_bm < 0 || U == 0) return false;
+    AdjSpec rs = st.adj;
+    rs.parts[0].second ^= 1;
+    uint64_t nc = 0;
+    DBuf<uint32_t> cl = bitmap_list(bitmap(st.filter_bm), 0, 1, nc);
+    const uint64_t ER = degree_sum(cl.p, nc, rs);
+    if (tlist_ != 2 && ER * 2 >= EU) return false;
+    // the distinct sources as a (slice-padded) bitmap and their positions
+    DBuf<uint64_t> ubm(&pool_, padded_words());
+    HIP_CHECK(hipMemsetAsync(ubm.p, 0, padded_words() * 8, s_));
+    DBuf<uint32_t> pos(&pool_, std::max<uint64_t>(g_.V, 1));
+    tm_.begin("k_mark_bitmap");
+    launch_mark_bitmap(ub.p, U, ubm.p, g_.V, s_);
+    launch_scatter_u32(ub.p, iu.p, U, pos.p, s_);
+    tm_.end(16ull * U);
+    l = expand_core(cl.p, nc, rs, ubm.p, {cl.p}, true, !nbset);
+    edges_iter_ += l.E;
+    if (l.n) {  // (c, b) → (index of b, c): the grouping keys the first carried column
+      tm_.begin("k_seg_map");
+      if (l.segmented) launch_seg_map_u32(l.dst.p, l.seg_start.p, l.seg_count.p, l.nseg, pos.p, s_);
+      else launch_gather_u32(pos.p, l.dst.p, l.n, l.dst.p, s_);
+      tm_.end(12ull * l.n);
+      std::swap(l.carry[0], l.dst);
+    }
+    if (debug_expand_)
+      std::fprintf(stderr, "[omx factorized] lists from the targets' side: U=%llu targets=%llu ER=%llu EU=%llu pairs=%llu\n",
+                   (unsigned long long)U, (unsigned long long)nc, (unsigned long long)ER, (unsigned long long)EU,
+                   (unsigned long long)l.n);
+    return true;
+  }
+
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
@@ -1783,8 +1866,14 @@ class Executor {
     HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));
     // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
     // (the filtered lists stay in the expansion's per-worker segments: grouping reads them in place)
-    ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, true);
-    edges_iter_ += l.E;
+    // (a set-valued hop over an adjacency that may repeat a neighbour: each list made distinct first)
+    const bool nbset = st.distinct_nb && !st.adj.dup_free;
+    ExpandOut l;
+    if (!targets_side_lists(st, U, ub, iu, EU, nbset, l)) {
+      l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, !nbset);
+      edges_iter_ += l.E;
+    }
+    if (nbset && l.n) l.n = distinct_pairs(l.carry[0], l.dst, {}, l.n);
     const uint64_t nlist = l.n;
     // 3. grouped by source: offsets (U + 1) and the neighbours in group order (segmented lists under
     // 2^32 entries: 32-bit counters and cursors, half the atomics' footprint)
@@ -2389,6 +2478,49 @@ class Executor {
     col_[ex.dst] = cat3(parts, ns);
   }
 
+  // The rows (…, n) of a set-valued hop (Step::distinct_nb) over an adjacency that may repeat a neighbour:
+  // one row per distinct (input row, n) — rid is the input row index carried through the expansion.
+  // Radix sort of the packed pairs, run heads, then every column (rid and dst included) gathered.
+  // Returns the rows kept.
+  uint64_t distinct_pairs(DBuf<uint32_t> &rid, DBuf<uint32_t> &dst, std::vector<DBuf<uint32_t> *> others, uint64_t n) {
+    if (n <= 1) return n;
+    const int vb = std::max(bits_for(g_.V), bits_for(n));  // (rid < n, dst ≤ V: both below 2^32)
+    tm_.begin("distinct_pairs");
+    DBuf<uint64_t> keys(&pool_, n), skeys(&pool_, n);
+    std::vector<DBuf<uint32_t>> kc;
+    kc.push_back(std::move(rid));
+    kc.push_back(std::move(dst));
+    const uint64_t R0 = R_;
+    R_ = n;  // pack_tuple reads R_ rows
+    pack_tuple(kc, 2, vb, keys.p);
+    R_ = R0;
+    rid = std::move(kc[0]);
+    dst = std::move(kc[1]);
+    DBuf<uint32_t> iota(&pool_, n), perm(&pool_, n);
+    launch_iota(iota.p, n, s_);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceRadixSort::SortPairs(t, b, keys.p, skeys.p, iota.p, perm.p, (int64_t)n, 0, 2 * vb, s_); });
+    DBuf<uint8_t> head(&pool_, n);
+    launch_u64_heads(skeys.p, n, head.p, s_);
+    DBuf<uint32_t> sel(&pool_, n);
+    DBuf<uint64_t> nsel(&pool_, 1);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, perm.p, head.p, sel.p, nsel.p, (int64_t)n, s_); });
+    const uint64_t m = read1(nsel.p);
+    others.push_back(&dst);
+    others.push_back(&rid);
+    std::vector<DBuf<uint32_t>> nc;
+    std::vector<const uint32_t *> in;
+    std::vector<uint32_t *> out;
+    for (DBuf<uint32_t> *c : others) {
+      nc.emplace_back(&pool_, std::max<uint64_t>(m, 1));
+      in.push_back(c->p);
+      out.push_back(nc.back().p);
+    }
+    launch_gather_cols(sel.p, m, (int)in.size(), in.data(), out.data(), s_);
+    for (size_t i = 0; i < others.size(); ++i) *others[i] = std::move(nc[i]);
+    tm_.end(n * 40ull + m * 8ull * others.size());
+    return m;
+  }
+
   // keep the rows whose flag is set (all bound columns)
   void select_rows(const uint8_t *flags, uint64_t R) {
     if (R == 0) {  // (a partitioned rank without rows: nothing to select)
@@ -2430,6 +2562,7 @@ class Executor {
     if (ck.kind != S_CHECK || ck.dst != ex.dst || ck.src == ex.dst || !col_[ck.src].p) return false;
     if (ex.optional || ck.optional) return false;
     if (!ck.adj.sorted || ck.adj.parts.empty()) return false;
+    if (ex.distinct_nb && !ex.adj.dup_free) return false;  // the expansion's neighbours form a set first
     return true;
   }
 
@@ -2580,9 +2713,15 @@ class Executor {
     uint32_t vlo = 0, vhi = V;
     if (dist_) {
       const int W = tr_->world(), me = tr_->rank();
-      const std::vector<uint64_t> rs = tr_->allgather(R_, s_);
-      plo = tr_->allgather(g_.part_lo, s_);
-      phi = tr_->allgather(g_.part_hi, s_);
+      const std::vector<uint64_t> g3 = tr_->allgather_n({R_, g_.part_lo, g_.part_hi}, s_);
+      std::vector<uint64_t> rs(W);
+      plo.assign(W, 0);
+      phi.assign(W, 0);
+      for (int p = 0; p < W; ++p) {
+        rs[p] = g3[3 * p];
+        plo[p] = g3[3 * p + 1];
+        phi[p] = g3[3 * p + 2];
+      }
       vlo = g_.part_lo;
       vhi = g_.part_hi;
       std::vector<uint64_t> send(W, R_), sdispl(W, 0), recv(rs), rdispl(W, 0);
@@ -2689,10 +2828,16 @@ class Executor {
         uint64_t h[4] = {hm[0], hm[1], hm[2], hm[3]};
         tm_.amend(8ull * (vhi - vlo) + 24ull * h[2]);  // frontier scan + visited and row_ptr pair of the active vertices
         uint64_t live_or = h[3];
+        uint64_t active = h[2];
+        std::vector<uint64_t> al;
         if (dist_) {  // every rank continues while any rank has an active vertex; live lanes over all ranks
-          const uint64_t active = global_sum(h[2]);
+          al = tr_->allgather_n({h[2], h[3]}, s_);
+          active = 0;
           live_or = 0;
-          for (uint64_t x : tr_->allgather(h[3], s_)) live_or |= x;
+          for (int p = 0; p < tr_->world(); ++p) {
+            active += al[2 * p];
+            live_or |= al[2 * p + 1];
+          }
           if (active == 0) break;
         } else if (h[2] == 0) {
           break;
@@ -2709,18 +2854,47 @@ class Executor {
                        (unsigned long long)row0, (long long)d, (double)h[1] * pull_div_ > (double)eadj ? "pull" : "push",
                        (unsigned long long)h[2], (unsigned long long)h[1], (unsigned long long)h[0]);
         if (dist_) {
-          // the frontier blocks of every rank (u64 masks sent as u32 word pairs; nothing to itself)
           const int W = tr_->world(), me = tr_->rank();
-          std::vector<uint64_t> send(W, 2ull * (vhi - vlo)), sdispl(W, 0), recv(W), rdispl(W);
-          for (int p = 0; p < W; ++p) {
-            recv[p] = 2ull * (phi[p] - plo[p]);
-            rdispl[p] = 2ull * plo[p];
+          if (12 * active < (uint64_t)V && !dense_exchange_) {
+            // a sparse level: every rank sends its frontier vertices with their masks (12 B each) to every
+            // peer instead of its whole block (8 B per owned vertex); the peers' entries of fr are zero
+            // before they are scattered in (a rank's pull writes only its own vertices)
+            const uint64_t n = h[2];
+            DBuf<uint32_t> lv(&pool_, std::max<uint64_t>(n, 1)), mlo(&pool_, std::max<uint64_t>(n, 1)),
+                mhi(&pool_, std::max<uint64_t>(n, 1));
+            DBuf<unsigned long long> lc(&pool_, 1);
+            HIP_CHECK(hipMemsetAsync(lc.p, 0, sizeof(unsigned long long), s_));
+            if (n) launch_bfs_list(fr.p + vlo, vhi - vlo, lv.p, lc.p, cus(), s_);
+            launch_bfs_frontier_pack(lv.p, n, vlo, fr.p, mlo.p, mhi.p, s_);
+            std::vector<uint64_t> send(W, n), sdispl(W, 0), recv(W), rdispl(W);
+            uint64_t nr = 0;
+            for (int p = 0; p < W; ++p) {
+              recv[p] = p == me ? 0 : al[2 * p];
+              rdispl[p] = nr;
+              nr += recv[p];
+            }
+            send[me] = 0;
+            DBuf<uint32_t> rv(&pool_, std::max<uint64_t>(nr, 1)), rlo(&pool_, std::max<uint64_t>(nr, 1)),
+                rhi(&pool_, std::max<uint64_t>(nr, 1));
+            tm_.begin("exchange");
+            tr_->alltoallv({lv.p, mlo.p, mhi.p}, send, sdispl, {rv.p, rlo.p, rhi.p}, recv, rdispl, s_);
+            tm_.end(12ull * (n * (W - 1) + nr));
+            if (vlo) HIP_CHECK(hipMemsetAsync(fr.p, 0, (size_t)vlo * 8, s_));
+            if (vhi < V) HIP_CHECK(hipMemsetAsync(fr.p + vhi, 0, (size_t)(V - vhi) * 8, s_));
+            launch_bfs_frontier_scatter(rv.p, rlo.p, rhi.p, nr, fr.p, s_);
+          } else {
+            // the frontier blocks of every rank (u64 masks sent as u32 word pairs; nothing to itself)
+            std::vector<uint64_t> send(W, 2ull * (vhi - vlo)), sdispl(W, 0), recv(W), rdispl(W);
+            for (int p = 0; p < W; ++p) {
+              recv[p] = 2ull * (phi[p] - plo[p]);
+              rdispl[p] = 2ull * plo[p];
+            }
+            send[me] = recv[me] = 0;
+            tm_.begin("exchange");
+            tr_->alltoallv({reinterpret_cast<const uint32_t *>(fr.p + vlo)}, send, sdispl,
+                           {reinterpret_cast<uint32_t *>(fr.p)}, recv, rdispl, s_);
+            tm_.end(8ull * V);
           }
-          send[me] = recv[me] = 0;
-          tm_.begin("exchange");
-          tr_->alltoallv({reinterpret_cast<const uint32_t *>(fr.p + vlo)}, send, sdispl,
-                         {reinterpret_cast<uint32_t *>(fr.p)}, recv, rdispl, s_);
-          tm_.end(8ull * V);
           for (int p = 0; p < radj.n; ++p) {
             if (!rest.p) {
               rest = DBuf<uint32_t>(&pool_, V);

@@ -318,6 +318,9 @@ void launch_flag_no_neighbor(const uint32_t *src, uint64_t R, const DAdj &adj, c
 void launch_check_optional(const uint32_t *src, uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
                            uint32_t V, unsigned int *npe, hipStream_t s);
 void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out, hipStream_t s);
+// v[i] = map[v[i]] over the rows of a block-segmented column
+void launch_seg_map_u32(uint32_t *v, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
+                        const uint32_t *map, hipStream_t s);
 // out[i] = src[idx[i]] for i < *nd (a device count ≤ cap)
 void launch_gather_u32_dev(const uint32_t *src, const uint32_t *idx, const uint64_t *nd, uint64_t cap, uint32_t *out,
                            hipStream_t s);
@@ -354,6 +357,12 @@ void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const ui
 void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsigned long long *count, int cus,
                      hipStream_t s);
 void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg, hipStream_t s);
+// partitioned sparse levels: list[i] (relative to vlo) → the vertex and its mask split into two words; and
+// fr[v[i]] = the mask on the receiving rank
+void launch_bfs_frontier_pack(uint32_t *list, uint64_t n, uint32_t vlo, const uint64_t *fr, uint32_t *mlo, uint32_t *mhi,
+                              hipStream_t s);
+void launch_bfs_frontier_scatter(const uint32_t *v, const uint32_t *mlo, const uint32_t *mhi, uint64_t n, uint64_t *fr,
+                                 hipStream_t s);
 void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, uint64_t etot, const uint64_t *rp,
                      const uint32_t *col, const uint64_t *frontier, const uint64_t *visited, uint64_t *next,
                      int cus, hipStream_t s);

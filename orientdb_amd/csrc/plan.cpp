@@ -1078,6 +1078,7 @@ class Planner {
         } else {
           st.kind = S_EXPAND;
           st.filter_bm = st.mode == T_CAND ? bitmap(nodes_[t].alias, 1) : bitmap(nodes_[t].alias, 0);
+          st.distinct_nb = fwd && where_of(nodes_[t].alias) != nullptr;
         }
       }
       st.desc = std::string(st.kind == S_VARLEN ? "varlen " : st.kind == S_MULTI ? "multi " : st.kind == S_CHECK ? "check " : "expand ") +

@@ -78,6 +78,10 @@ struct Step {
   TravSpec trav;           // S_MULTI
   bool optional = false;   // S_EXPAND / S_CHECK into an optional node
   int where_bm = -1;       // optional target: the node's WHERE alone (the emptiness test of the traversal)
+  // S_EXPAND: the traversal returns a set (a forward single hop into a node with a WHERE: the HashSet of
+  // P/OMatchPathItem.java:61,71-78), so a neighbour reached over several edges (parallel edges, or both()
+  // over u → v and v → u) binds once; reverse traversals and hops without a WHERE keep every edge
+  bool distinct_nb = false;
   std::string desc;
 };
 

@@ -172,15 +172,18 @@ def test_partitioned_varlen_edges_match_replicated(rmat10_full, q, monkeypatch):
     assert sum(r.info["n_rows"] for r in res) == full.info["n_rows"]
 
 
+@pytest.mark.parametrize("exchange", ["auto", "dense"])
 @pytest.mark.parametrize("world", [2, 3, 4])
 @pytest.mark.parametrize("q", [q for q in DIST_VARLEN if q[0] in ("depth_only", "two_batches", "while_prop", "both_dir",
                                                                   "where_target", "maxdepth")], ids=lambda q: q[0])
-def test_partitioned_msbfs_matches_replicated(rmat10_full, q, world, monkeypatch):
+def test_partitioned_msbfs_matches_replicated(rmat10_full, q, world, exchange, monkeypatch):
     """The partitioned multi-source BFS (every level pulled over the rank's own vertices from the
-    allgathered frontier) finds the replicated BFS's rows, level by level the same E_t."""
+    exchanged frontier: (vertex, mask) triples on sparse levels, whole blocks on dense ones — or always
+    the blocks, OMX_DENSE_EXCHANGE=1) finds the replicated BFS's rows, level by level the same E_t."""
     import orientdb_amd as o
     g, _ = rmat10_full
     monkeypatch.setenv("OMX_VARLEN", "bfs")
+    monkeypatch.setenv("OMX_DENSE_EXCHANGE", "1" if exchange == "dense" else "0")
     full = o.OMatchStatement(q[1]).execute(g, documents=False)
     res = run_ranks(_parts(world), q[1], documents=False)
     assert sum(r.info["edges_traversed"] for r in res) == full.info["edges_traversed"]
@@ -301,6 +304,12 @@ def test_partitioned_documents(rmat10_full, world, q):
     assert all(len(r) == 0 for r in res[1:])
     assert res[0].info["documents"] == 1
     assert doc_set(res[0]) == doc_set(want)
+    # each rank de-duplicated its hash share of the alias tuples first: rank 0 received distinct tuples
+    # only, at most the distinct bindings of every alias ($matches of the same pattern)
+    import orientdb_amd as o
+    head = q[1].split(" RETURN ")[0]
+    m = o.OMatchStatement(head + " RETURN $matches").execute(g, documents=False)
+    assert res[0].info["rows_gathered"] <= m.info["n_rows"]
 
 
 def test_partitioned_return_adjacency_is_unsupported():
@@ -326,6 +335,8 @@ def test_partitioned_limit(rmat10_full, world, limit):
     got = gpu_set(res[0], cols)
     assert len(got) == min(max(limit, 1), len(want))
     assert got <= want
+    # every rank sent at most max(LIMIT, 1) of its distinct rows to rank 0
+    assert res[0].info["rows_gathered"] <= min(world * max(limit, 1), len(want))
 
 
 def test_partitioned_optional_null_reached_again_raises(rmat10_full):

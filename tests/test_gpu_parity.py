@@ -100,6 +100,7 @@ class _Ref:
         self.cg = dfs.CsrGraph(g.csr[0], g.csr[1], {"uid": np.arange(g.V, dtype=np.int64), "age": g.age},
                                simple=simple)
         self._db = None
+        self.bindings = None  # the C DFS's complete matches of the last expected() it answered
 
     @property
     def db(self):
@@ -110,10 +111,12 @@ class _Ref:
 
     def expected(self, query, cols):
         from oracle import dfs
+        self.bindings = None
         if cols is not None:
             try:
                 r = dfs.run(self.cg, query, nthreads=8)
                 idx = [r["aliases"].index(c) for c in cols]
+                self.bindings = r["bindings"]
                 return {tuple((11 << 48) | int(v) for v in row[idx]) for row in r["rows"]}
             except NotImplementedError:
                 pass
@@ -236,6 +239,29 @@ def test_return_division_by_zero_fails(rmat10, devproj, monkeypatch):
         o.OMatchStatement("MATCH {class:Person,as:a,where:(uid < 5)} RETURN a.uid / 0 as x").execute(g)
 
 
+@pytest.mark.parametrize("devproj", ["1", "0"])
+def test_return_division_by_zero_past_limit(rmat10, devproj, monkeypatch):
+    """LIMIT stops the projection at the limit-th distinct document (OMatchStatement.addSingleResult
+    :737-750), so a division by zero in a later row is never evaluated: the rows of one alias come in
+    ascending vertex order, the zero divisor sits on the last root, and LIMIT 1 returns the first root's
+    document on both evaluators (the device one hands LIMIT to the host, which stops early); without the
+    LIMIT both fail."""
+    import orientdb_amd as o
+    from oracle.match_ref import MatchOracle
+    monkeypatch.setenv("OMX_DEVPROJ", devproj)
+    g, ref = rmat10
+    rp = g.csr[0].astype(np.int64)
+    roots = [v for v in range(30) if rp[v + 1] > rp[v]]
+    last = roots[-1]
+    q = "MATCH {class:Person,as:a,where:(uid < 30)}-Knows->{as:b} RETURN 1000 / (a.uid - %d) as x" % last
+    rs = o.OMatchStatement(q + " LIMIT 1").execute(g)
+    assert len(rs) == 1
+    want = MatchOracle(ref.db, q + " LIMIT 1").execute()
+    assert doc_set(rs) == doc_set(want)
+    with pytest.raises(o.OmxExecutionError):
+        o.OMatchStatement(q).execute(g)
+
+
 def test_optional_null_reached_again_raises(rmat10):
     """A null optional alias reached again by a non-empty traversal is the reference's
     NullPointerException (matched.get(alias).getIdentity(), P/OMatchStatement.java:468): an execution error."""
@@ -256,6 +282,10 @@ def _parity(g, ref, query, cols, **kw):
     rs = o.OMatchStatement(query).execute(g, **kw)
     assert rs.info["n_rows"] == len(want)
     assert gpu_set(rs, cols if cols and rs.columns[0] not in ("$elements", "$pathElements") else None) == want
+    if ref.bindings is not None and "LIMIT" not in query.upper():
+        # complete matches before the de-duplication: a set-valued hop binds a repeated neighbour once
+        # (P/OMatchPathItem.java:61,71-78), reverse hops and hops without a WHERE once per edge
+        assert rs.info["bindings"] == ref.bindings
     return rs
 
 
@@ -363,16 +393,20 @@ FACTOR_IDS = ("c2_both_ends", "c1_abc", "two_cols_dedup", "in_dir", "both_dir", 
               "paths", "elements", "fof_not_me", "matched_and_filter", "optional_free", "bound_candidate")
 
 
+@pytest.mark.parametrize("lists", ["sources", "targets"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
-def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, monkeypatch):
+def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, lists, monkeypatch):
     """Every filtered hop through the factorized expansion (distinct sources → filtered lists → rows
     over the lists, Executor::expand_factorized): same rows, same E_t and bindings as the direct
     expansion — on the simple graph and on the multigraph, whose parallel edges repeat a neighbour in a
     source's list (ridbag multiplicity, OSBTreeRidBag.java:292-295) through the distinct-source grouping.
-    The rows are written by the output-tiled emission at any size (OMX_FEMIT=force)."""
+    The lists built from the sources' rows (OMX_TLIST=0) or from the targets' in-rows filtered by the
+    distinct sources (OMX_TLIST=force, Executor::targets_side_lists); the rows written by the
+    output-tiled emission at any size (OMX_FEMIT=force)."""
     import orientdb_amd as o
     g, ref = rmat10 if graph == "simple" else rmat10_raw
+    monkeypatch.setenv("OMX_TLIST", "0" if lists == "sources" else "force")
     monkeypatch.setenv("OMX_FEMIT", "force")
     monkeypatch.setenv("OMX_FACTOR", "0")
     direct = o.OMatchStatement(q[1]).execute(g, documents=False)
@@ -480,12 +514,10 @@ def test_factorized_auto_threshold_rmat14(simple):
     want = {tuple(int(v) for v in row) for row in ref["rows"]}
     assert got == want and rs.info["n_rows"] == len(want)
     assert rs.info["edges_traversed"] == ref["edges"]
-    if simple:
-        assert rs.info["bindings"] == ref["bindings"]
-    # (multigraph: a filtered forward hop returns a HashSet in the reference (OMatchPathItem.java:61,75),
-    # so its DFS binds a repeated neighbour once; the device counts one binding row per parallel edge and
-    # the final content de-duplication removes the repeats — the result rows above are equal, only this
-    # diagnostic count differs)
+    # (multigraph: a forward hop into a node with a WHERE returns a HashSet in the reference
+    # (OMatchPathItem.java:61,71-78), so a neighbour reached over parallel edges binds once; the device
+    # makes each source's filtered list distinct, Step::distinct_nb, while E_t still counts every edge)
+    assert rs.info["bindings"] == ref["bindings"]
     import os
     os.environ["OMX_FACTOR"] = "0"
     try:
