@@ -790,10 +790,19 @@ class Evaluator:
                 return a - b
             if op == "*":
                 return a * b
+            # Java arithmetic (P/OMathExpression.java:105-147): integer / truncates toward zero and % takes
+            # the dividend's sign (Python's // and % floor); a double % is fmod
             if op == "/":
-                return a // b if isinstance(a, int) and isinstance(b, int) else a / b
+                if isinstance(a, int) and isinstance(b, int):
+                    q = abs(a) // abs(b)
+                    return -q if (a < 0) != (b < 0) else q
+                return a / b
             if op == "%":
-                return a % b
+                if isinstance(a, int) and isinstance(b, int):
+                    r = abs(a) % abs(b)
+                    return -r if a < 0 else r
+                import math
+                return math.fmod(a, b)
         if k == "call":
             return self.call(e[1], e[2], rec, rec)
         if k == "chain":

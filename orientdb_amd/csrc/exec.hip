@@ -368,6 +368,13 @@ class Executor {
       ncols = (int)p_.out_aliases.size();
     }
     int64_t limit = p_.limit >= 0 ? p_.limit : o_.limit;
+    if (dist_ && counted_only && limit > -1) {
+      // COUNT with LIMIT over a partitioned snapshot: the ranks' counted rows are disjoint (distinct by
+      // construction), so the result is min(Σ ranks, max(LIMIT, 1)), reported by rank 0
+      uint64_t total = 0;
+      for (uint64_t x : tr_->allgather(n, s_)) total += x;
+      n = tr_->rank() == 0 ? total : 0;
+    }
     if (limit > -1 && n > (uint64_t)std::max<int64_t>(limit, 1)) n = (uint64_t)std::max<int64_t>(limit, 1);
     if (n > 0 && !counted_only && !docs && (o_.flags & OMX_FLAG_DIGEST)) {
       std::vector<const uint32_t *> cp;
@@ -772,7 +779,6 @@ class Executor {
     if (!p_.ret_adj.empty())
       unsupported("out()/in()/both() in a RETURN expression is not supported on a partitioned snapshot");
     const bool limited = p_.limit >= 0 || o_.limit >= 0;
-    if (limited && o_.mode == OMX_MODE_COUNT) unsupported("LIMIT in COUNT mode on a partitioned snapshot");
     // optional nodes need nothing more: a row is flagged or checked on the owner of the vertex whose
     // adjacency it reads (a traversal never starts from an optional alias, plan.cpp); RETURN expressions,
     // $elements / $pathElements and LIMIT are evaluated over the content-distinct result as a whole, so
@@ -1497,14 +1503,15 @@ class Executor {
     edges_ += o.E + o.E_member;
     if (!o.counted_from_degrees) edges_iter_ += o.E;
     R_ = o.n;
-    if (nbset && o.n) {
+    // (an expansion with no rows or no adjacency returns no carried columns at all)
+    if (nbset && o.carry.size() > cols.size()) {
       DBuf<uint32_t> orid = std::move(o.carry.back());
       o.carry.pop_back();
-      std::vector<DBuf<uint32_t> *> oc;
-      for (auto &c : o.carry) oc.push_back(&c);
-      R_ = o.n = distinct_pairs(orid, o.dst, oc, o.n);
-    } else if (nbset) {
-      o.carry.pop_back();
+      if (o.n) {
+        std::vector<DBuf<uint32_t> *> oc;
+        for (auto &c : o.carry) oc.push_back(&c);
+        R_ = o.n = distinct_pairs(orid, o.dst, oc, o.n);
+      }
     }
     if (n_empty) {  // append the null-target rows
       const uint64_t n = R_ + n_empty;

@@ -339,6 +339,20 @@ def test_partitioned_limit(rmat10_full, world, limit):
     assert res[0].info["rows_gathered"] <= min(world * max(limit, 1), len(want))
 
 
+@pytest.mark.parametrize("limit", [0, 5, 10 ** 9])
+def test_partitioned_count_limit(rmat10_full, limit):
+    """COUNT mode with LIMIT on a partitioned snapshot: the ranks' counted rows are disjoint, so rank 0
+    reports min(Σ ranks, max(LIMIT, 1)) (OMatchStatement.java:741-746), the others 0 — equal to the
+    single-snapshot count under the same LIMIT."""
+    import orientdb_amd as o
+    g, _ = rmat10_full
+    q = [x for x in RMAT_QUERIES if x[0] == "three_hop"][0][1] + " LIMIT %d" % limit
+    full = o.OMatchStatement(q).execute(g, mode=o.OMX_MODE_COUNT, documents=False)
+    res = run_ranks(_parts(3), q, mode=o.OMX_MODE_COUNT, documents=False)
+    assert res[0].info["n_rows"] == full.info["n_rows"] == min(max(limit, 1), full.info["bindings"])
+    assert all(r.info["n_rows"] == 0 for r in res[1:])
+
+
 def test_partitioned_optional_null_reached_again_raises(rmat10_full):
     """The NPE of a null optional alias reached again (P/OMatchStatement.java:468) fails the partitioned
     execution on every rank (the rank that finds it aborts the exchanges of the others)."""

@@ -207,6 +207,8 @@ DOC_QUERIES += [
     ("math_dbl", "MATCH {class:Person,as:a,where:(uid < 40)}-Knows->{as:b} RETURN b.age / 2.0 as h, b.age % 7 as m"),
     ("rid_and_const", "MATCH {class:Person,as:a,where:(uid < 25)}-Knows->{as:b} RETURN b.@rid as r, 3 as k, a.nope as z"),
     ("int_div", "MATCH {class:Person,as:a,where:(uid < 25)}-Knows->{as:b} RETURN (a.uid + 7) / 3 as q, -a.uid as n"),
+    # Java integer arithmetic on negatives: / truncates toward zero, % keeps the dividend's sign
+    ("neg_div_mod", "MATCH {class:Person,as:a,where:(uid < 40)}-Knows->{as:b} RETURN (a.uid - 20) / 7 as q, (a.uid - 20) % 7 as m"),
 ]
 
 

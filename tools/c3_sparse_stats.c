@@ -16,7 +16,7 @@ int main(int argc, char **argv) {
   uint32_t *col = malloc(E * 4);
   if (fread(rp, 8, V + 1, f) != V + 1 || fread(col, 4, E, f) != E) return 1;
   fclose(f);
-  const uint64_t lds_hubs = argc > 2 ? strtoull(argv[2], 0, 10) : 11500, hubs = 1u << 20;
+  const uint64_t lds_hubs = argc > 2 ? strtoull(argv[2], 0, 10) : 11500, hubs = argc > 3 ? strtoull(argv[3], 0, 10) : 1u << 20;
   // out-degree rank of every vertex (counting sort, descending)
   uint64_t maxd = 0;
   for (uint64_t v = 0; v < V; ++v) if (rp[v + 1] - rp[v] > maxd) maxd = rp[v + 1] - rp[v];
