@@ -1770,7 +1770,7 @@ class Executor {
   // against 200 M; the pairs are the lists' entries, one per edge b → c, so parallel edges keep their
   // multiplicity). One GPU, one adjacency part; taken when it reads fewer than half the entries
   // (OMX_TLIST=0: never, =force: whenever it applies). Returns false (nothing done) otherwise.
-  int tlist_ = 1;
+  int tlist_ = 0;
   bool targets_side_lists(const Step &st, uint64_t U, const DBuf<uint32_t> &ub, const DBuf<uint32_t> &iu, uint64_t EU,
                           bool nbset, ExpandOut &l) {
     if (!tlist_ || dist_ || st.adj.parts.size() != 1 || st.filter_bm < 0 || U == 0) return false;
@@ -2377,8 +2377,14 @@ class Executor {
       DBuf<unsigned long long> ctr(&pool_, 2);
       HIP_CHECK(hipMemsetAsync(ctr.p, 0, 2 * sizeof(unsigned long long), s_));
       launch_isect_tiles(woff.p, nM, ntiles, trow.p, s_);
+      DBuf<uint64_t> pa(&pool_, nM), pb(&pool_, nM);
+      DBuf<uint32_t> pmn(&pool_, nM);
+      launch_isect_prep(gi[0], nM, col_[ex.src].p, col_[ck.src].p, ax.p[0], ay.p[0], pa.p, pb.p, pmn.p, s_);
       IsectArgs a{};
       a.idx = gi[0];
+      a.pa = pa.p;
+      a.pb = pb.p;
+      a.pmn = pmn.p;
       a.boff = boff.p;
       a.tile_row = trow.p;
       a.nM = nM;

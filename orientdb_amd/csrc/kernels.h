@@ -115,7 +115,7 @@ struct ExpandArgs {
 };
 
 // ---- isect.hip: the fused closing check as a sorted-list intersection (Executor::expand_check_isect) ----
-constexpr uint32_t kIsRowCap = 1024;  // m + n of a merged row (its two lists staged in LDS)
+constexpr uint32_t kIsRowCap = 256;   // m + n of a merged row (its two lists staged in a wave's LDS tile)
 constexpr uint32_t kIsRowPad = 8;     // a merged row's tile weight beyond m + n (bounds the rows a tile holds)
 struct IsectPolicy {
   int32_t merge;     // merge rows of comparable lengths
@@ -126,6 +126,8 @@ struct IsectPolicy {
 };
 struct IsectArgs {
   const uint32_t *idx;       // [nM] the merged rows' binding-table indices
+  const uint64_t *pa, *pb;   // [nM] their N_x and N_y list starts (launch_isect_prep)
+  const uint32_t *pmn;       // [nM] m | n << 16
   const uint64_t *boff;      // [nM] scan of their output bounds (a tile writes at boff[its first row])
   const uint32_t *tile_row;  // [ntiles + 1] first merged row of each tile
   uint64_t nM, ntiles;
@@ -148,6 +150,8 @@ void launch_isect_class(const uint32_t *xs, const uint32_t *ys, uint64_t R, cons
                         int cus, hipStream_t s);
 uint64_t isect_tiles(uint64_t wtotal);
 void launch_isect_tiles(const uint64_t *woff, uint64_t nM, uint64_t ntiles, uint32_t *tile_row, hipStream_t s);
+void launch_isect_prep(const uint32_t *idx, uint64_t nM, const uint32_t *xs, const uint32_t *ys, const DAdjPart &ax,
+                       const DAdjPart &ay, uint64_t *pa, uint64_t *pb, uint32_t *pmn, hipStream_t s);
 void launch_isect_merge(const IsectArgs &a, bool write, int cus, hipStream_t s);
 
 // predicate VM → V-bit bitmap (u64 words); depth = value of $depth
