@@ -191,7 +191,6 @@ class Executor {
     if (const char *f = std::getenv("OMX_FUSE_CHECK")) fuse_mode_ = f;  // "0" disables the intersection
     if (const char *sw = std::getenv("OMX_SWAP_CHECK")) swap_ = std::strcmp(sw, "0") != 0;
     if (const char *de = std::getenv("OMX_DENSE_EXCHANGE")) dense_exchange_ = std::strcmp(de, "0") != 0;
-    if (const char *tl = std::getenv("OMX_TLIST")) tlist_ = std::strcmp(tl, "force") == 0 ? 2 : std::strcmp(tl, "0") != 0 ? 1 : 0;
     // OMX_MERGE: "0" keeps every closing check a binary-search probe; "force" merges every row whose two
     // lists fit a tile (tests); OMX_MERGE_RATIO: merge when the longer list is ≤ ratio × the shorter
     if (const char *mg = std::getenv("OMX_MERGE")) merge_ = std::strcmp(mg, "force") == 0 ? 2 : std::strcmp(mg, "0") != 0 ? 1 : 0;
@@ -476,11 +475,16 @@ class Executor {
   std::string varlen_mode_ = "auto";
   std::string fuse_mode_ = "1";
   bool swap_ = true;  // fused closing check iterates the shorter of the two lists (OMX_SWAP_CHECK=0: off)
-  int merge_ = 1;     // fused closing check: merge path for lists of comparable lengths (isect.hip)
+  // fused closing check: merge path for lists of comparable lengths (isect.hip). Off by default: at C4
+  // (LDBC SF10, lists of ≈ 30) the binary-search probe of an L1-resident list takes 0.74 ms a step and the
+  // wave-tiled merge 1.38 ms (it reads both lists, 210 M entries against 65 M iterated; round 4,
+  // profiles/r04/isect); OMX_MERGE=1 merges rows by the ratio rule, =force every row that fits a tile
+  int merge_ = 0;
   double merge_ratio_ = 8;
-  // hub masks packed for the pull kernel in degree-rank order (8 MiB); 0 = plain col. 2^20 measured best
-  // of 2^17…2^22 at C3 (profiles/r02/c3rank: pull 4.26 → 4.07 ms per step against 2^18 in vertex order)
-  uint32_t pull_hubs_ = 1u << 20;
+  // hub masks packed for the pull kernel in degree-rank order (4 MiB: one XCD's L2); 0 = plain col. 2^20
+  // measured best of 2^17…2^22 at C3 in round 2 (profiles/r02/c3rank); with the LDS hubs and the frontier
+  // probe of round 3, 2^19 (sparse level 1.546 ms) edges out 2^20 (1.598) and 2^18 (1.594) (r04/c3h)
+  uint32_t pull_hubs_ = 1u << 19;
   double pull_div_ = 20;  // bottom-up when the frontier's edges exceed 1/pull_div_ of the adjacency
   bool pull_live_ = true;  // the pull waits only for lanes whose frontier is non-empty
   // levels whose frontier holds fewer than this fraction of the vertices pull through the frontier bitmap
@@ -1763,47 +1767,6 @@ class Executor {
                                            : alg);
   }
 
-  // The same (source index, neighbour) pairs from the targets' side: the vertices c passing the hop's
-  // filter expanded over their in-rows, filtered by the bitmap of the distinct sources (the sliced
-  // filtered expansion, its bitmap slices in LDS), each surviving in-neighbour b replaced by its index
-  // among the sources. Σ indeg(C) entries are read instead of Σ deg(U) (M1: the 10 % target window, 26 M
-  // against 200 M; the pairs are the lists' entries, one per edge b → c, so parallel edges keep their
-  // multiplicity). One GPU, one adjacency part; taken when it reads fewer than half the entries
-  // (OMX_TLIST=0: never, =force: whenever it applies). Returns false (nothing done) otherwise.
-  int tlist_ = 0;
-  bool targets_side_lists(const Step &st, uint64_t U, const DBuf<uint32_t> &ub, const DBuf<uint32_t> &iu, uint64_t EU,
-                          bool nbset, ExpandOut &l) {
-    if (!tlist_ || dist_ || st.adj.parts.size() != 1 || st.filter_bm < 0 || U == 0) return false;
-    AdjSpec rs = st.adj;
-    rs.parts[0].second ^= 1;
-    uint64_t nc = 0;
-    DBuf<uint32_t> cl = bitmap_list(bitmap(st.filter_bm), 0, 1, nc);
-    const uint64_t ER = degree_sum(cl.p, nc, rs);
-    if (tlist_ != 2 && ER * 2 >= EU) return false;
-    // the distinct sources as a (slice-padded) bitmap and their positions
-    DBuf<uint64_t> ubm(&pool_, padded_words());
-    HIP_CHECK(hipMemsetAsync(ubm.p, 0, padded_words() * 8, s_));
-    DBuf<uint32_t> pos(&pool_, std::max<uint64_t>(g_.V, 1));
-    tm_.begin("k_mark_bitmap");
-    launch_mark_bitmap(ub.p, U, ubm.p, g_.V, s_);
-    launch_scatter_u32(ub.p, iu.p, U, pos.p, s_);
-    tm_.end(16ull * U);
-    l = expand_core(cl.p, nc, rs, ubm.p, {cl.p}, true, !nbset);
-    edges_iter_ += l.E;
-    if (l.n) {  // (c, b) → (index of b, c): the grouping keys the first carried column
-      tm_.begin("k_seg_map");
-      if (l.segmented) launch_seg_map_u32(l.dst.p, l.seg_start.p, l.seg_count.p, l.nseg, pos.p, s_);
-      else launch_gather_u32(pos.p, l.dst.p, l.n, l.dst.p, s_);
-      tm_.end(12ull * l.n);
-      std::swap(l.carry[0], l.dst);
-    }
-    if (debug_expand_)
-      std::fprintf(stderr, "[omx factorized] lists from the targets' side: U=%llu targets=%llu ER=%llu EU=%llu pairs=%llu\n",
-                   (unsigned long long)U, (unsigned long long)nc, (unsigned long long)ER, (unsigned long long)EU,
-                   (unsigned long long)l.n);
-    return true;
-  }
-
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
@@ -1875,11 +1838,8 @@ class Executor {
     // (the filtered lists stay in the expansion's per-worker segments: grouping reads them in place)
     // (a set-valued hop over an adjacency that may repeat a neighbour: each list made distinct first)
     const bool nbset = st.distinct_nb && !st.adj.dup_free;
-    ExpandOut l;
-    if (!targets_side_lists(st, U, ub, iu, EU, nbset, l)) {
-      l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, !nbset);
-      edges_iter_ += l.E;
-    }
+    ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, !nbset);
+    edges_iter_ += l.E;
     if (nbset && l.n) l.n = distinct_pairs(l.carry[0], l.dst, {}, l.n);
     const uint64_t nlist = l.n;
     // 3. grouped by source: offsets (U + 1) and the neighbours in group order (segmented lists under

@@ -322,9 +322,6 @@ void launch_flag_no_neighbor(const uint32_t *src, uint64_t R, const DAdj &adj, c
 void launch_check_optional(const uint32_t *src, uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
                            uint32_t V, unsigned int *npe, hipStream_t s);
 void launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out, hipStream_t s);
-// v[i] = map[v[i]] over the rows of a block-segmented column
-void launch_seg_map_u32(uint32_t *v, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
-                        const uint32_t *map, hipStream_t s);
 // out[i] = src[idx[i]] for i < *nd (a device count ≤ cap)
 void launch_gather_u32_dev(const uint32_t *src, const uint32_t *idx, const uint64_t *nd, uint64_t cap, uint32_t *out,
                            hipStream_t s);

@@ -280,72 +280,102 @@ __global__ __launch_bounds__(256) void k_eval_atoms(DPred P, uint32_t V, uint64_
 // The same for atoms over 4-byte columns without absent values (the common WHERE: `age < 1`): a lane
 // takes 4 consecutive vertices with one 16-byte load per column (and 8 bytes of class ids), so a wave
 // instruction moves 1 KiB instead of 256 B; a word's 16 nibbles are OR-reduced across 16 lanes.
-// Persistent: a wave takes kAtomU groups of 4 words a round, all their loads issued first (a wave per
-// group waited one memory round trip for 1 KiB: 36 µs for RMAT-24's 67 MB column, 1.9 TB/s).
-constexpr int kAtomU = 4;
 __global__ __launch_bounds__(256) void k_eval_atoms4(DPred P, uint32_t V, uint64_t *words, uint64_t nwords) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64, nwv = (uint64_t)gridDim.x * 4;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64 * 4;  // 4 words (256 vertices) per wave
+  const uint64_t v0 = w0 * 64 + 4 * lane;
   const ClassMask cm = class_mask_regs(P);
-  const uint64_t ngroups = (nwords + 3) / 4;
-  for (uint64_t g0 = wave * kAtomU; g0 < ngroups; g0 += nwv * kAtomU) {
-    uint4 xs[kAtomU][4];
-    uint2 cs[kAtomU];
-    bool fulls[kAtomU];
+  uint32_t cls[4] = {0, 0, 0, 0};
+  uint32_t raw[4][4] = {};
+  // wave-uniform: every wave but the last takes 16-byte column loads and 8-byte class loads, all issued
+  // before any is used (a per-lane test made the compiler select between both forms and wait in between)
+  const bool full = __builtin_amdgcn_readfirstlane((int)((w0 + 4) * 64 <= (uint64_t)V)) != 0;
+  if (full) {
+    uint2 c2 = make_uint2(0, 0);
+    if (P.use_class) c2 = *reinterpret_cast<const uint2 *>(P.vclass + v0);
+    uint4 x[4];
 #pragma unroll
-    for (int u = 0; u < kAtomU; ++u) {
-      const uint64_t w0 = (g0 + u) * 4, v0 = w0 * 64 + 4 * lane;
-      fulls[u] = (w0 + 4) * 64 <= (uint64_t)V;  // wave-uniform
-      cs[u] = make_uint2(0, 0);
-      if (fulls[u]) {
-        if (P.use_class) cs[u] = *reinterpret_cast<const uint2 *>(P.vclass + v0);
+    for (int k = 0; k < 4; ++k)
+      if (k < P.n_atoms) x[k] = *reinterpret_cast<const uint4 *>((const uint32_t *)P.atom_c[k].values + v0);
+    cls[0] = c2.x & 0xFFFFu, cls[1] = c2.x >> 16, cls[2] = c2.y & 0xFFFFu, cls[3] = c2.y >> 16;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (k < P.n_atoms) xs[u][k] = *reinterpret_cast<const uint4 *>((const uint32_t *)P.atom_c[k].values + v0);
+    for (int k = 0; k < 4; ++k)
+      if (k < P.n_atoms) raw[k][0] = x[k].x, raw[k][1] = x[k].y, raw[k][2] = x[k].z, raw[k][3] = x[k].w;
+  } else {
+    if (P.use_class) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cls[j] = P.vclass[v0 + j < V ? v0 + j : (uint64_t)V - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= P.n_atoms) break;  // uniform
+      const uint32_t *c = (const uint32_t *)P.atom_c[k].values;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) raw[k][j] = c[v0 + j < V ? v0 + j : (uint64_t)V - 1];
+    }
+  }
+  uint64_t nib = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bool b = v0 + j < V;
+    if (P.use_class) b = b && class_in_mask(cm, cls[j]);
+    bool acc = P.conj != 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= P.n_atoms) break;
+      const bool r = atom_true(P, k, raw[k][j], true);
+      acc = P.conj ? (acc && r) : (acc || r);
+    }
+    nib |= (uint64_t)(b && acc) << j;
+  }
+  uint64_t x = nib << (4 * (lane & 15));
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) x |= __shfl_xor(x, off, 64);
+  if ((lane & 15) == 0 && w0 + lane / 16 < nwords) words[w0 + lane / 16] = x;
+}
+
+// One comparison of an int32 column with an integer constant, no class test (M1's `age < 1`, `age >=
+// 90`): the comparison is a range test lo <= x <= hi (negated for !=), and a wave takes 16 words (1,024
+// vertices) a round with four 16-byte loads a lane in flight. The general kernel above holds 150 VGPRs
+// when compiled for four groups a wave (3 waves a SIMD: 55 µs for RMAT-24's 67 MB column); this one
+// holds few.
+constexpr int kAtom1U = 4;
+__global__ __launch_bounds__(256) void k_eval_atom1_i32(const int32_t *col, int64_t lo, int64_t hi, int neg, uint32_t V,
+                                                        uint64_t *words, uint64_t nwords) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64, nwv = (uint64_t)gridDim.x * 4;
+  const uint64_t nrounds = (nwords + 4 * kAtom1U - 1) / (4 * kAtom1U);
+  for (uint64_t rd = wave; rd < nrounds; rd += nwv) {
+    const uint64_t w0 = rd * 4 * kAtom1U;
+    const bool full = (w0 + 4 * kAtom1U) * 64 <= (uint64_t)V;  // wave-uniform
+    int4 x[kAtom1U];
+#pragma unroll
+    for (int u = 0; u < kAtom1U; ++u) {
+      const uint64_t v0 = (w0 + 4 * u) * 64 + 4 * lane;
+      if (full) {
+        x[u] = *reinterpret_cast<const int4 *>(col + v0);
+      } else {
+        x[u].x = col[v0 + 0 < V ? v0 + 0 : V - 1];
+        x[u].y = col[v0 + 1 < V ? v0 + 1 : V - 1];
+        x[u].z = col[v0 + 2 < V ? v0 + 2 : V - 1];
+        x[u].w = col[v0 + 3 < V ? v0 + 3 : V - 1];
       }
     }
 #pragma unroll
-    for (int u = 0; u < kAtomU; ++u) {
-      const uint64_t w0 = (g0 + u) * 4, v0 = w0 * 64 + 4 * lane;
-      if (g0 + u >= ngroups) break;  // uniform
-      uint32_t cls[4] = {0, 0, 0, 0};
-      uint32_t raw[4][4] = {};
-      if (fulls[u]) {
-        cls[0] = cs[u].x & 0xFFFFu, cls[1] = cs[u].x >> 16, cls[2] = cs[u].y & 0xFFFFu, cls[3] = cs[u].y >> 16;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (k < P.n_atoms) raw[k][0] = xs[u][k].x, raw[k][1] = xs[u][k].y, raw[k][2] = xs[u][k].z, raw[k][3] = xs[u][k].w;
-      } else {
-        if (P.use_class) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) cls[j] = P.vclass[v0 + j < V ? v0 + j : (uint64_t)V - 1];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (k >= P.n_atoms) break;  // uniform
-          const uint32_t *c = (const uint32_t *)P.atom_c[k].values;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) raw[k][j] = c[v0 + j < V ? v0 + j : (uint64_t)V - 1];
-        }
-      }
+    for (int u = 0; u < kAtom1U; ++u) {
+      const uint64_t v0 = (w0 + 4 * u) * 64 + 4 * lane;
+      const int32_t e[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
       uint64_t nib = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        bool b = v0 + j < V;
-        if (P.use_class) b = b && class_in_mask(cm, cls[j]);
-        bool acc = P.conj != 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (k >= P.n_atoms) break;
-          const bool r = atom_true(P, k, raw[k][j], true);
-          acc = P.conj ? (acc && r) : (acc || r);
-        }
-        nib |= (uint64_t)(b && acc) << j;
+        const bool r = ((int64_t)e[j] >= lo && (int64_t)e[j] <= hi) != (neg != 0);
+        nib |= (uint64_t)(r && v0 + j < V) << j;
       }
-      uint64_t x = nib << (4 * (lane & 15));
+      uint64_t w = nib << (4 * (lane & 15));
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1) x |= __shfl_xor(x, off, 64);
-      if ((lane & 15) == 0 && w0 + lane / 16 < nwords) words[w0 + lane / 16] = x;
+      for (int off = 1; off < 16; off <<= 1) w |= __shfl_xor(w, off, 64);
+      const uint64_t wi = w0 + 4 * u + lane / 16;
+      if ((lane & 15) == 0 && wi < nwords) words[wi] = w;
     }
   }
 }
@@ -358,8 +388,20 @@ void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *
   for (int k = 0; four && k < pred.n_atoms; ++k)
     four = pred.atom_c[k].present == nullptr && pred.atom_c[k].type != OMX_PROP_INT64 &&
            pred.atom_c[k].type != OMX_PROP_DOUBLE;
-  if (four) {
-    const uint64_t groups = (nwords + 3) / 4;
+  // one int32 comparison with an integer constant, no class test: the range-test kernel
+  if (four && pred.n_atoms == 1 && !pred.use_class && pred.atom_c[0].type == OMX_PROP_INT32 && !pred.atom_dbl[0] &&
+      pred.atom_op[0] >= P_EQ && pred.atom_op[0] <= P_GE) {
+    const int64_t b = pred.atom_i[0];
+    int64_t lo = INT64_MIN, hi = INT64_MAX;
+    int neg = 0;
+    switch (pred.atom_op[0]) {
+      case P_EQ: lo = hi = b; break;
+      case P_NE: lo = hi = b; neg = 1; break;
+      case P_LT: if (b == INT64_MIN) lo = 1, hi = 0; else hi = b - 1; break;  // (lo > hi: nothing)
+      case P_LE: hi = b; break;
+      case P_GT: if (b == INT64_MAX) lo = 1, hi = 0; else lo = b + 1; break;
+      default: lo = b; break;  // P_GE
+    }
     static int cus_of[64] = {};  // CUs of each device (queried once)
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
@@ -367,8 +409,16 @@ void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *
         cus_of[dev] = 256;
       cus = cus_of[dev];
     }
-    const uint64_t waves = std::min<uint64_t>((groups + kAtomU - 1) / kAtomU, (uint64_t)std::max(cus, 1) * 32);
-    hipLaunchKernelGGL(k_eval_atoms4, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s, pred, V, words, nwords);
+    const uint64_t rounds = (nwords + 4 * kAtom1U - 1) / (4 * kAtom1U);
+    const uint64_t waves = std::min<uint64_t>(rounds, (uint64_t)std::max(cus, 1) * 32);
+    hipLaunchKernelGGL(k_eval_atom1_i32, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s,
+                       (const int32_t *)pred.atom_c[0].values, lo, hi, neg, V, words, nwords);
+    KCHECK("k_eval_atom1_i32");
+    return;
+  }
+  if (four) {
+    const uint64_t groups = (nwords + 3) / 4;
+    hipLaunchKernelGGL(k_eval_atoms4, dim3(nblocks(groups * 64, 256)), dim3(256), 0, s, pred, V, words, nwords);
     KCHECK("k_eval_atoms4");
     return;
   }
@@ -2775,32 +2825,6 @@ void launch_scatter_u32(const uint32_t *idx, const uint32_t *val, uint64_t n, ui
   hipLaunchKernelGGL(k_scatter_u32, dim3(nblocks(n, 256)), dim3(256), 0, s, idx, val, n, out);
   KCHECK("k_scatter_u32");
 }
-// v[i] = map[v[i]] over the rows of a block-segmented column (segment s: [seg_start[s], + seg_count[s])),
-// one wave per segment, four rows a lane in flight
-__global__ __launch_bounds__(256) void k_seg_map_u32(uint32_t *v, const uint64_t *seg_start, const uint32_t *seg_count,
-                                                     uint32_t nseg, const uint32_t *map) {
-  const uint32_t sg = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (sg >= nseg) return;
-  const uint32_t lane = threadIdx.x & 63, n = seg_count[sg];
-  uint32_t *b = v + seg_start[sg];
-  for (uint32_t j = lane; j < n; j += 256) {
-    uint32_t x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = j + 64u * u < n ? b[j + 64u * u] : 0u;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = j + 64u * u < n ? map[x[u]] : 0u;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (j + 64u * u < n) b[j + 64u * u] = x[u];
-  }
-}
-void launch_seg_map_u32(uint32_t *v, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
-                        const uint32_t *map, hipStream_t s) {
-  if (!nseg) return;
-  hipLaunchKernelGGL(k_seg_map_u32, dim3(nblocks(nseg, 4)), dim3(256), 0, s, v, seg_start, seg_count, nseg, map);
-  KCHECK("k_seg_map_u32");
-}
-
 __global__ void k_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = src[idx[i]];

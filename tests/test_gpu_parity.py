@@ -395,20 +395,16 @@ FACTOR_IDS = ("c2_both_ends", "c1_abc", "two_cols_dedup", "in_dir", "both_dir", 
               "paths", "elements", "fof_not_me", "matched_and_filter", "optional_free", "bound_candidate")
 
 
-@pytest.mark.parametrize("lists", ["sources", "targets"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
-def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, lists, monkeypatch):
+def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, monkeypatch):
     """Every filtered hop through the factorized expansion (distinct sources → filtered lists → rows
     over the lists, Executor::expand_factorized): same rows, same E_t and bindings as the direct
     expansion — on the simple graph and on the multigraph, whose parallel edges repeat a neighbour in a
     source's list (ridbag multiplicity, OSBTreeRidBag.java:292-295) through the distinct-source grouping.
-    The lists built from the sources' rows (OMX_TLIST=0) or from the targets' in-rows filtered by the
-    distinct sources (OMX_TLIST=force, Executor::targets_side_lists); the rows written by the
-    output-tiled emission at any size (OMX_FEMIT=force)."""
+    The rows are written by the output-tiled emission at any size (OMX_FEMIT=force)."""
     import orientdb_amd as o
     g, ref = rmat10 if graph == "simple" else rmat10_raw
-    monkeypatch.setenv("OMX_TLIST", "0" if lists == "sources" else "force")
     monkeypatch.setenv("OMX_FEMIT", "force")
     monkeypatch.setenv("OMX_FACTOR", "0")
     direct = o.OMatchStatement(q[1]).execute(g, documents=False)
