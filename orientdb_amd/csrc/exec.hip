@@ -144,6 +144,16 @@ class Timer {
   std::vector<Rec> recs_;
 };
 
+// out[i] = (u32) in[i] (degrees of a partition's rows: below 2^32)
+__global__ void k_u64_to_u32(const uint64_t *in, uint64_t n, uint32_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (uint32_t)in[i];
+}
+static void launch_u64_to_u32(const uint64_t *in, uint64_t n, uint32_t *out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_u64_to_u32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, n, out);
+}
+
 // head[i] = 1 where a run of equal sorted keys starts
 __global__ void k_u64_heads(const uint64_t *k, uint64_t n, uint8_t *head) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -307,6 +317,9 @@ class Executor {
     else if (dist_ && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
     const bool sp_doc = p_.kind == Plan::SHORTEST_PATH && !p_.chain.expand_rows;
     const bool docs = p_.proj == Plan::PROJ_EXPR || p_.proj == Plan::PROJ_JSON || sp_doc;
+    // partitioned: the lists out()/in()/both() read in RETURN expressions, from the vertices' owners
+    RetAdj fetched;
+    if (dist_ && !empty && !counted_only && docs && !p_.ret_adj_alias.empty()) fetch_return_adjacency(fetched);
     if (sp_doc) {  // SELECT shortestPath(...): one document whose field is the list of the path's RIDs
       HVal list;
       list.k = HVal::LIST;
@@ -353,7 +366,7 @@ class Executor {
         n = res->n_pcol_rows;
       } else {
         tm_.begin("documents");
-        res->docs = build_documents(g_, p_, cp, n, lim, s_);
+        res->docs = build_documents(g_, p_, cp, n, lim, s_, dist_ ? &fetched : nullptr);
         tm_.end();
         n = res->docs.size();
       }
@@ -780,8 +793,11 @@ class Executor {
     // predicates read the gathered degrees (gather_global_degrees, at the start of run()).
     // RETURN expressions read the replicated property columns, but out()/in()/both() inside them read
     // adjacency rows a partition may not hold
-    if (!p_.ret_adj.empty())
-      unsupported("out()/in()/both() in a RETURN expression is not supported on a partitioned snapshot");
+    // out()/in()/both() applied to an alias is fetched from the owners before the projection
+    // (fetch_return_adjacency); applied to a list or a field its vertices are only known while rank 0
+    // evaluates the expression
+    if (p_.ret_adj_deep)
+      unsupported("out()/in()/both() of a list or a field in a RETURN expression is not supported on a partitioned snapshot");
     const bool limited = p_.limit >= 0 || o_.limit >= 0;
     // optional nodes need nothing more: a row is flagged or checked on the owner of the vertex whose
     // adjacency it reads (a traversal never starts from an optional alias, plan.cpp); RETURN expressions,
@@ -845,6 +861,77 @@ class Executor {
     if (limit >= 0 && p_.proj == Plan::PROJ_ALIASES) R_ = std::min<uint64_t>(R_, (uint64_t)std::max<int64_t>(limit, 1));
   }
   bool pre_distinct_ = false;  // pre_rank0_distinct de-duplicated the rows (rank 0 receives disjoint sets)
+
+  // every rank's rows (cols, n of them) to rank 0; returns the rows this rank holds afterwards
+  uint64_t to_rank0(const std::vector<DBuf<uint32_t> *> &cols, uint64_t n) {
+    const int W = tr_->world();
+    DBuf<uint32_t> dest(&pool_, std::max<uint64_t>(n, 1));
+    DBuf<uint64_t> hist(&pool_, W);
+    HIP_CHECK(hipMemsetAsync(hist.p, 0, W * sizeof(uint64_t), s_));
+    if (n) {
+      HIP_CHECK(hipMemsetAsync(dest.p, 0, n * sizeof(uint32_t), s_));
+      HIP_CHECK(hipMemcpyAsync(hist.p, &n, sizeof(uint64_t), hipMemcpyHostToDevice, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));  // (n is a local)
+    }
+    return exchange_cols(cols, n, dest, hist);
+  }
+
+  // out()/in()/both() applied to an alias in a RETURN expression, on a partitioned snapshot: rank 0
+  // (which holds every row after route_rank0) sends the alias's distinct vertices to their owners, each
+  // owner answers with their degrees and lists (the ordered expansion: parts in the AdjSpec's order, as
+  // OrientVertex.getVertices iterates its fields), and rank 0 keeps them for the document builder. Every
+  // rank takes part, in the plan's order of the suffixes.
+  void fetch_return_adjacency(RetAdj &out) {
+    const int W = tr_->world();
+    for (const auto &sa : p_.ret_adj_alias) {
+      const AdjSpec &as = p_.ret_adj.at(sa.first);
+      // 1. the distinct vertices of the alias (rank 0; nulls skipped)
+      uint64_t n = 0;
+      DBuf<uint32_t> ids;
+      if (R_ && col_[sa.second].p) {
+        DBuf<uint64_t> bm(&pool_, std::max<uint64_t>(nwords_, 1));
+        HIP_CHECK(hipMemsetAsync(bm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+        launch_mark_bitmap(col_[sa.second].p, R_, bm.p, g_.V, s_);
+        ids = bitmap_list(bm.p, 0, 1, n);
+      } else {
+        ids = DBuf<uint32_t>(&pool_, 1);
+      }
+      // 2. to their owners
+      DBuf<uint32_t> dest(&pool_, std::max<uint64_t>(n, 1));
+      DBuf<uint64_t> hist(&pool_, W);
+      HIP_CHECK(hipMemsetAsync(hist.p, 0, W * sizeof(uint64_t), s_));
+      if (n) launch_route_owner(ids.p, n, block_, (uint32_t)W, dest.p, hist.p, s_);
+      n = exchange_cols({&ids}, n, dest, hist);
+      // 3. the owners' degrees and lists, in id order
+      DBuf<uint32_t> deg32(&pool_, std::max<uint64_t>(n, 1)), lists;
+      uint64_t nl = 0;
+      if (n) {
+        DBuf<uint64_t> deg(&pool_, n + 1);
+        launch_row_degree(ids.p, n, make_adj(as), deg.p, s_);
+        launch_u64_to_u32(deg.p, n, deg32.p, s_);
+        ExpandOut o = expand_core(ids.p, n, as, nullptr, {}, true, false, nullptr, nullptr, nullptr, nullptr, true);
+        nl = o.n;
+        lists = nl ? std::move(o.dst) : DBuf<uint32_t>(&pool_, 1);
+      } else {
+        lists = DBuf<uint32_t>(&pool_, 1);
+      }
+      // 4. back to rank 0: (vertex, degree) rows, then the lists (both in rank order, then id order)
+      n = to_rank0({&ids, &deg32}, n);
+      nl = to_rank0({&lists}, nl);
+      if (tr_->rank() != 0 || n == 0) continue;
+      std::vector<uint32_t> hid(n), hdeg(n), hl(nl);
+      HIP_CHECK(hipMemcpyAsync(hid.data(), ids.p, n * 4, hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipMemcpyAsync(hdeg.data(), deg32.p, n * 4, hipMemcpyDeviceToHost, s_));
+      if (nl) HIP_CHECK(hipMemcpyAsync(hl.data(), lists.p, nl * 4, hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+      uint64_t at = 0;
+      for (uint64_t i = 0; i < n; ++i) {
+        if (at + hdeg[i] > nl) fail(OMX_E_INVALID, "internal: fetched adjacency lists are short");
+        out[{sa.first, hid[i]}] = std::vector<uint32_t>(hl.begin() + at, hl.begin() + at + hdeg[i]);
+        at += hdeg[i];
+      }
+    }
+  }
 
   // (row, vertex) pairs of an item's result sets (see traverse)
   struct PairSet {

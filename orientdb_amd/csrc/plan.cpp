@@ -1184,7 +1184,8 @@ class Planner {
       case Expr::CALL: unsupported("function call " + e->name + "() in a RETURN expression");
       case Expr::CHAIN:
         check_return(e->kids[0], refs);
-        for (auto &s : e->suffixes) {
+        for (size_t si = 0; si < e->suffixes.size(); ++si) {
+          const Suffix &s = e->suffixes[si];
           if (s.kind == Suffix::METHOD) {
             const std::string m = lower(s.name);
             if (m == "out" || m == "in" || m == "both") {
@@ -1195,6 +1196,10 @@ class Planner {
                 labels.push_back(v->s);
               }
               plan_->ret_adj[&s] = adjacency(m, labels);
+              auto ai = e->kids[0] && e->kids[0]->kind == Expr::FIELD ? alias_idx_.find(e->kids[0]->name)
+                                                                          : alias_idx_.end();
+              if (si == 0 && ai != alias_idx_.end()) plan_->ret_adj_alias.emplace_back(&s, ai->second);
+              else plan_->ret_adj_deep = true;
             } else if (!((m == "size" || m == "touppercase" || m == "tolowercase") && s.args.empty())) {
               unsupported("method " + s.name + "() in a RETURN expression");
             }

@@ -127,6 +127,11 @@ struct Plan {
   std::vector<std::string> out_names;
   std::vector<ReturnItem> returns;                 // PROJ_EXPR / PROJ_JSON
   std::map<const Suffix *, AdjSpec> ret_adj;       // out()/in()/both() suffixes inside RETURN expressions
+  // the ones applied to an alias directly (`a.out('L')…`), in RETURN order (the same on every rank): a
+  // partitioned run fetches those vertices' lists from their owners; ret_adj_deep: some out()/in()/both()
+  // applies to a list or a field (its vertices are only known while the expression is evaluated)
+  std::vector<std::pair<const Suffix *, int>> ret_adj_alias;
+  bool ret_adj_deep = false;
   std::vector<char> optional;                      // per alias: an optional pattern node (null when unmatched)
   Params params;                                   // the query parameters (RETURN expressions read them)
   bool unique_by_construction = false;

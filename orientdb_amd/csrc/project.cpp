@@ -156,6 +156,9 @@ class Evaluator {
   const Plan &p_;
   std::map<std::pair<const Suffix *, uint32_t>, std::vector<uint32_t>> adj_cache_;
 
+ public:
+  const RetAdj *fetched_ = nullptr;
+
   static HVal lit(const Value &v) {
     switch (v.kind) {
       case Value::INT: return mk_int(v.i);
@@ -280,6 +283,11 @@ class Evaluator {
   // out()/in()/both() of one vertex: the adjacency parts of the plan's AdjSpec, read from the device CSR
   std::vector<uint32_t> neighbours(const Suffix *s, uint32_t v) {
     auto key = std::make_pair(s, v);
+    if (fetched_) {  // a partitioned run: every list the expressions read was fetched from its owner
+      auto f = fetched_->find(key);
+      if (f == fetched_->end()) fail(OMX_E_INVALID, "internal: a RETURN adjacency list was not fetched");
+      return f->second;
+    }
     auto it = adj_cache_.find(key);
     if (it != adj_cache_.end()) return it->second;
     std::vector<uint32_t> out;
@@ -438,7 +446,7 @@ std::string to_json(const HVal &x) {
 }  // namespace
 
 std::vector<Document> build_documents(Graph &g, const Plan &p, const std::vector<const uint32_t *> &cols, uint64_t n,
-                                      int64_t limit, hipStream_t s) {
+                                      int64_t limit, hipStream_t s, const RetAdj *fetched) {
   const size_t k = cols.size();
   std::vector<uint32_t> h(n * k);
   for (size_t c = 0; c < k; ++c)
@@ -446,6 +454,7 @@ std::vector<Document> build_documents(Graph &g, const Plan &p, const std::vector
   HIP_CHECK(hipStreamSynchronize(s));
   ensure_rids(g);
   Evaluator ev(g, p);
+  ev.fetched_ = fetched;
   std::vector<Document> docs;
   std::unordered_set<std::string> seen;
   const uint64_t cap = limit > -1 ? (uint64_t)std::max<int64_t>(limit, 1) : UINT64_MAX;

@@ -11,7 +11,9 @@
 // de-duplicates the documents by content. Property values, RIDs and classes come from host mirrors of
 // the snapshot's columns (copied once per graph), out()/in()/both() lists from the device CSR.
 #pragma once
+#include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "graph.h"
@@ -33,9 +35,14 @@ struct HVal {
 };
 using Document = std::vector<HVal>;  // one value per Plan::out_names
 
+// the lists of out()/in()/both() suffixes of RETURN expressions, per (suffix, vertex)
+using RetAdj = std::map<std::pair<const Suffix *, uint32_t>, std::vector<uint32_t>>;
+
 // cols: n distinct tuples of Plan::out_aliases (device columns, dense ids; V = null). limit: LIMIT
-// (after content de-duplication; -1 none; 0 keeps one, as addSingleResult does).
+// (after content de-duplication; -1 none; 0 keeps one, as addSingleResult does). fetched: a partitioned
+// run's lists fetched from their owners (Executor::fetch_return_adjacency); every list is then read from
+// it (a partition's CSR holds its own rows only), else from the device CSR.
 std::vector<Document> build_documents(Graph &g, const Plan &p, const std::vector<const uint32_t *> &cols, uint64_t n,
-                                      int64_t limit, hipStream_t s);
+                                      int64_t limit, hipStream_t s, const RetAdj *fetched = nullptr);
 
 }  // namespace omx

@@ -293,11 +293,12 @@ def test_partitioned_optional_and_elements(rmat10_full, world, q):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("q", [q for q in DOC_QUERIES if q[0] != "out_list"], ids=lambda q: q[0])
+@pytest.mark.parametrize("q", DOC_QUERIES, ids=lambda q: q[0])
 def test_partitioned_documents(rmat10_full, world, q):
     """RETURN expressions / JSON over a partitioned snapshot: every rank's rows meet on rank 0, which
     builds the documents from the replicated property columns and de-duplicates them by content
-    (addResult :698-719, ODocumentEqualityWrapper); the other ranks return nothing."""
+    (addResult :698-719, ODocumentEqualityWrapper); the other ranks return nothing. out()/in()/both() of
+    an alias (out_list) reads lists rank 0 fetched from their owners (Executor::fetch_return_adjacency)."""
     g, ref = rmat10_full
     want = oracle_rows(ref.db, q[1])
     res = run_ranks(_parts(world), q[1])
@@ -313,10 +314,11 @@ def test_partitioned_documents(rmat10_full, world, q):
 
 
 def test_partitioned_return_adjacency_is_unsupported():
-    """out()/in() inside a RETURN expression reads adjacency rows a partition does not hold: refused
-    alike on every rank before any exchange (the host runs the reference engine)."""
+    """out()/in() of a list inside a RETURN expression (a.out('Knows').out('Knows')) reads lists whose
+    vertices are only known while rank 0 evaluates it: refused alike on every rank before any exchange
+    (the host runs the reference engine)."""
     import orientdb_amd as o
-    q = [x for x in DOC_QUERIES if x[0] == "out_list"][0][1]
+    q = "MATCH {class:Person,as:a,where:(uid < 15)} RETURN a.out('Knows').out('Knows').size() as d2"
     with pytest.raises(o.OmxUnsupported):
         run_ranks(_parts(2), q)
 
