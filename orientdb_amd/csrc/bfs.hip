@@ -163,6 +163,31 @@ void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsig
   KCHECK("k_bfs_list");
 }
 
+// the frontier vertices that are not hubs (hub_bm: V bits), listed for a push beside a hubs-only pull;
+// one atomic per block
+__global__ __launch_bounds__(kB) void k_bfs_list_nonhub(const uint64_t *frontier, const uint64_t *hub_bm, uint32_t V,
+                                                        uint32_t *list, unsigned long long *count) {
+  __shared__ uint32_t s_w[kB / 64];
+  __shared__ uint32_t s_base;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * kB; b0 < V; b0 += (uint64_t)gridDim.x * kB) {
+    const uint64_t v = b0 + threadIdx.x;
+    const bool keep = v < V && frontier[v] != 0 && !bm_test(hub_bm, (uint32_t)v);
+    uint32_t tot;
+    const uint32_t off = block_excl_scan<kB>(keep ? 1u : 0u, s_w, &tot);
+    if (threadIdx.x == 0 && tot) s_base = (uint32_t)atomicAdd(count, (unsigned long long)tot);
+    __syncthreads();
+    if (keep) list[s_base + off] = (uint32_t)v;
+    __syncthreads();
+  }
+}
+void launch_bfs_list_nonhub(const uint64_t *frontier, const uint64_t *hub_bm, uint32_t V, uint32_t *list,
+                            unsigned long long *count, int cus, hipStream_t s) {
+  if (!V) return;
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 8);
+  hipLaunchKernelGGL(k_bfs_list_nonhub, dim3(g), dim3(kB), 0, s, frontier, hub_bm, V, list, count);
+  KCHECK("k_bfs_list_nonhub");
+}
+
 // partitioned sparse levels: the rank's frontier as (vertex, mask low word, mask high word) triples
 // (list: owned vertices relative to vlo, from k_bfs_list over fr + vlo), and their scatter on the peers
 __global__ void k_bfs_frontier_pack(uint32_t *list, uint64_t n, uint32_t vlo, const uint64_t *fr, uint32_t *mlo,
@@ -423,7 +448,9 @@ struct PwTable {
   unsigned long long acc[kPwRows];
 };
 
-template <bool PROBE>
+// HUBS (a sparse level whose non-hub frontier is pushed instead, exec.hip varlen_msbfs): non-hub in-edges
+// are skipped without any memory access
+template <bool PROBE, bool HUBS>
 __global__ __launch_bounds__(64 * kPwWaves) void k_bfs_pull_w(const uint64_t *rp, const uint32_t *col,
                                                              const uint32_t *__restrict__ tiles,
                                                              const uint64_t *__restrict__ rb, uint64_t n,
@@ -500,7 +527,7 @@ __global__ __launch_bounds__(64 * kPwWaves) void k_bfs_pull_w(const uint64_t *rp
         const uint32_t hx = xv & 0x7FFFFFFFu;
         if ((xv >> 31) && hx < nlds) g = s_hub[hx] & nd;
         else if (xv >> 31) g = hub_fr[hx] & nd;
-        else if (!PROBE || ((fbm[xv >> 6] >> (xv & 63)) & 1)) g = frontier[xv] & nd;
+        else if (!HUBS && (!PROBE || ((fbm[xv >> 6] >> (xv & 63)) & 1))) g = frontier[xv] & nd;
       }
       f[j] = g;
       kk[j] = k;
@@ -522,7 +549,7 @@ __global__ __launch_bounds__(64 * kPwWaves) void k_bfs_pull_w(const uint64_t *rp
 }
 
 // the other tiles: one thread per in-edge, its vertex by a search of the row pointers
-template <bool PROBE>
+template <bool PROBE, bool HUBS>
 __global__ __launch_bounds__(256) void k_bfs_pull_w_slow(const uint64_t *rp, const uint32_t *col, uint64_t E,
                                                         const uint32_t *tiles, const uint64_t *rb, uint64_t n,
                                                         uint64_t lanes, const uint64_t *frontier,
@@ -542,7 +569,7 @@ __global__ __launch_bounds__(256) void k_bfs_pull_w_slow(const uint64_t *rp, con
       const uint32_t xv = col[e];
       uint64_t g = 0;
       if (xv >> 31) g = hub_fr[xv & 0x7FFFFFFFu] & nd;
-      else if (!PROBE || ((fbm[xv >> 6] >> (xv & 63)) & 1)) g = frontier[xv] & nd;
+      else if (!HUBS && (!PROBE || ((fbm[xv >> 6] >> (xv & 63)) & 1))) g = frontier[xv] & nd;
       if (g) atomicOr((unsigned long long *)&next[lo], (unsigned long long)g);
     }
   }
@@ -578,7 +605,7 @@ void launch_pull_w_bounds(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t *
 void launch_bfs_pull_w(const uint64_t *rp, const uint32_t *col, uint64_t E, const uint32_t *tiles, uint64_t nreg,
                        const uint64_t *rb, uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr,
                        uint32_t nhubs, const uint64_t *fbm, const uint64_t *visited, uint64_t *next, int cus,
-                       hipStream_t s) {
+                       hipStream_t s, bool hubs_only) {
   const uint64_t nt = bfs_pull_w_tiles(E);
   if (!nt || !lanes) return;
   static const int per = [] {  // workgroups per CU (4 waves each)
@@ -597,14 +624,16 @@ void launch_bfs_pull_w(const uint64_t *rp, const uint32_t *col, uint64_t E, cons
   if (slow_all) nreg = 0;
   if (nreg) {
     const dim3 g((unsigned)std::min<uint64_t>((nreg + kPwWaves - 1) / kPwWaves, (uint64_t)cus * per));
-    if (fbm) hipLaunchKernelGGL(k_bfs_pull_w<true>, g, dim3(64 * kPwWaves), 0, s, rp, col, tiles, rb, nreg, lanes, frontier, hub_fr, fbm, visited, next, nlds);
-    else hipLaunchKernelGGL(k_bfs_pull_w<false>, g, dim3(64 * kPwWaves), 0, s, rp, col, tiles, rb, nreg, lanes, frontier, hub_fr, fbm, visited, next, nlds);
+    if (hubs_only) hipLaunchKernelGGL((k_bfs_pull_w<false, true>), g, dim3(64 * kPwWaves), 0, s, rp, col, tiles, rb, nreg, lanes, frontier, hub_fr, fbm, visited, next, nlds);
+    else if (fbm) hipLaunchKernelGGL((k_bfs_pull_w<true, false>), g, dim3(64 * kPwWaves), 0, s, rp, col, tiles, rb, nreg, lanes, frontier, hub_fr, fbm, visited, next, nlds);
+    else hipLaunchKernelGGL((k_bfs_pull_w<false, false>), g, dim3(64 * kPwWaves), 0, s, rp, col, tiles, rb, nreg, lanes, frontier, hub_fr, fbm, visited, next, nlds);
     KCHECK("k_bfs_pull_w");
   }
   if (nt > nreg) {
     const dim3 g((unsigned)std::min<uint64_t>(nt - nreg, (uint64_t)cus * 8));
-    if (fbm) hipLaunchKernelGGL(k_bfs_pull_w_slow<true>, g, dim3(256), 0, s, rp, col, E, tiles + nreg, rb, nt - nreg, lanes, frontier, hub_fr, fbm, visited, next);
-    else hipLaunchKernelGGL(k_bfs_pull_w_slow<false>, g, dim3(256), 0, s, rp, col, E, tiles + nreg, rb, nt - nreg, lanes, frontier, hub_fr, fbm, visited, next);
+    if (hubs_only) hipLaunchKernelGGL((k_bfs_pull_w_slow<false, true>), g, dim3(256), 0, s, rp, col, E, tiles + nreg, rb, nt - nreg, lanes, frontier, hub_fr, fbm, visited, next);
+    else if (fbm) hipLaunchKernelGGL((k_bfs_pull_w_slow<true, false>), g, dim3(256), 0, s, rp, col, E, tiles + nreg, rb, nt - nreg, lanes, frontier, hub_fr, fbm, visited, next);
+    else hipLaunchKernelGGL((k_bfs_pull_w_slow<false, false>), g, dim3(256), 0, s, rp, col, E, tiles + nreg, rb, nt - nreg, lanes, frontier, hub_fr, fbm, visited, next);
     KCHECK("k_bfs_pull_w_slow");
   }
 }

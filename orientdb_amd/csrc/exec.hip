@@ -201,6 +201,7 @@ class Executor {
     if (const char *f = std::getenv("OMX_FUSE_CHECK")) fuse_mode_ = f;  // "0" disables the intersection
     if (const char *sw = std::getenv("OMX_SWAP_CHECK")) swap_ = std::strcmp(sw, "0") != 0;
     if (const char *de = std::getenv("OMX_DENSE_EXCHANGE")) dense_exchange_ = std::strcmp(de, "0") != 0;
+    if (const char *hp = std::getenv("OMX_HUB_PUSH")) hub_push_ = std::strcmp(hp, "force") == 0 ? 2 : std::strcmp(hp, "0") != 0 ? 1 : 0;
     // OMX_MERGE: "0" keeps every closing check a binary-search probe; "force" merges every row whose two
     // lists fit a tile (tests); OMX_MERGE_RATIO: merge when the longer list is ≤ ratio × the shorter
     if (const char *mg = std::getenv("OMX_MERGE")) merge_ = std::strcmp(mg, "force") == 0 ? 2 : std::strcmp(mg, "0") != 0 ? 1 : 0;
@@ -504,6 +505,9 @@ class Executor {
   double pull_probe_ = 0.1;
   bool pull_wave_ = true;  // OMX_PULL_WAVE=0: the workgroup-tiled k_bfs_pull for the tiled bottom-up levels
   bool pull_exit_ = true;  // denser levels pull per vertex with an early exit (OMX_PULL_EXIT=0: tiles)
+  // sparse levels: hubs-only pull + push of the non-hub frontier when that pushes under 1/8 of the pull's
+  // entries (OMX_HUB_PUSH=0: off, =force: at every sparse level; tests)
+  int hub_push_ = 1;
   // partitioned BFS: levels whose frontier holds fewer than V/12 vertices exchange (vertex, mask) triples
   // instead of the frontier blocks (OMX_DENSE_EXCHANGE=1: always the blocks)
   bool dense_exchange_ = false;
@@ -2848,7 +2852,7 @@ class Executor {
     DBuf<uint32_t> list;
     DBuf<unsigned long long> stats(&pool_, 5);
     // bottom-up partitions of every reversed part (once per traversal; built on the first pull level)
-    std::vector<DBuf<uint64_t>> hub_fr(radj.n);
+    std::vector<DBuf<uint64_t>> hub_fr(radj.n), hub_bm(radj.n);
     std::vector<const uint64_t *> pull_part(radj.n, nullptr);
     std::vector<const uint32_t *> pull_col(radj.n, nullptr), pull_hubs(radj.n, nullptr);
     std::vector<uint32_t> pull_nh(radj.n, 0);
@@ -2996,13 +3000,45 @@ class Executor {
               if (tm_.last() != SIZE_MAX) exit_recs.push_back(tm_.last());
               continue;
             }
+            // A sparse level whose frontier is mostly hubs (C3's third level: 1.2 K of its 54 M non-hub
+            // in-edges come from frontier vertices) pulls over the hub entries only — a non-hub entry costs
+            // no memory access instead of a frontier-bitmap probe — and the few non-hub frontier vertices push
+            // their out-edges instead (OMX_HUB_PUSH=0: the probing pull for every entry)
+            bool hubs_only = false;
+            if (probe && pull_wave_ && hub_push_ && pull_nh[p] > 0) {
+              if (!hub_bm[p].p) {  // the part's hubs as a V-bit set (once per traversal)
+                hub_bm[p] = DBuf<uint64_t>(&pool_, std::max<uint64_t>(nwords_, 1));
+                HIP_CHECK(hipMemsetAsync(hub_bm[p].p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+                launch_mark_bitmap(pull_hubs[p], pull_nh[p], hub_bm[p].p, V, s_);
+              }
+              if (!list.p) list = DBuf<uint32_t>(&pool_, V);
+              DBuf<unsigned long long> nc(&pool_, 1);
+              HIP_CHECK(hipMemsetAsync(nc.p, 0, sizeof(unsigned long long), s_));
+              tm_.begin("k_bfs_list");
+              launch_bfs_list_nonhub(fr.p, hub_bm[p].p, V, list.p, nc.p, cus(), s_);
+              tm_.end(8ull * V + V / 8);
+              const uint64_t nn = read1(reinterpret_cast<const uint64_t *>(nc.p));
+              DBuf<uint64_t> deg(&pool_, nn + 1), loffs(&pool_, nn + 1);
+              launch_bfs_list_deg(list.p, nn, adj.p[p].rp, deg.p, s_);
+              cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, deg.p, loffs.p, (int64_t)(nn + 1), s_); });
+              const uint64_t etot = read1(loffs.p + nn);
+              if (hub_push_ == 2 || etot * 8 < pull_E[p]) {
+                hubs_only = true;
+                if (etot) {
+                  tm_.begin("k_bfs_push");
+                  launch_bfs_push(list.p, loffs.p, nn, etot, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, cus(), s_);
+                  tm_.end(20ull * etot + 24ull * nn);
+                  edges_iter_ += etot;
+                }
+              }
+            }
             tm_.begin(probe ? "k_bfs_pull_sparse" : "k_bfs_pull");
             if (pull_wave_) {  // wave tiles over the in-edges
               const uint64_t *wrb = nullptr;
               uint64_t nreg = 0;
               const uint32_t *wt = pullw_of(rspec.parts[p].first, rspec.parts[p].second, radj.p[p].rp, pull_E[p], &wrb, &nreg);
               launch_bfs_pull_w(radj.p[p].rp, pull_col[p], pull_E[p], wt, nreg, wrb, lanes & live, fr.p, hub_fr[p].p,
-                                pull_nh[p], probe ? fbm.p : nullptr, vis.p, nx.p, cus(), s_);
+                                pull_nh[p], probe && !hubs_only ? fbm.p : nullptr, vis.p, nx.p, cus(), s_, hubs_only);
             } else {
               launch_bfs_pull(V, radj.p[p].rp, pull_col[p], pull_part[p], pull_E[p], lanes & live, fr.p, hub_fr[p].p,
                               probe ? fbm.p : nullptr, vis.p, nx.p, cus(), s_);
@@ -3011,7 +3047,7 @@ class Executor {
             // HBM-necessary: the masks are shared by all the in-edges of a source, so each is needed once
             // (probe levels: the frontier's masks and the frontier bitmap; else every vertex's mask)
             tm_.end(16ull * V + 12ull * pull_E[p],
-                    16ull * V + 4ull * pull_E[p] + (probe ? 8ull * h[2] + V / 8 : 8ull * V));
+                    16ull * V + 4ull * pull_E[p] + (probe ? 8ull * h[2] + (hubs_only ? 0 : V / 8) : 8ull * V));
             edges_iter_ += pull_E[p];
           }
         } else {

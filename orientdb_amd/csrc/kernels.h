@@ -358,6 +358,9 @@ void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const ui
 void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsigned long long *count, int cus,
                      hipStream_t s);
 void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg, hipStream_t s);
+// frontier vertices not in hub_bm (a sparse level's push beside a hubs-only pull)
+void launch_bfs_list_nonhub(const uint64_t *frontier, const uint64_t *hub_bm, uint32_t V, uint32_t *list,
+                            unsigned long long *count, int cus, hipStream_t s);
 // partitioned sparse levels: list[i] (relative to vlo) → the vertex and its mask split into two words; and
 // fr[v[i]] = the mask on the receiving rank
 void launch_bfs_frontier_pack(uint32_t *list, uint64_t n, uint32_t vlo, const uint64_t *fr, uint32_t *mlo, uint32_t *mhi,
@@ -379,7 +382,7 @@ void launch_pull_w_bounds(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t *
 void launch_bfs_pull_w(const uint64_t *rp, const uint32_t *col, uint64_t E, const uint32_t *tiles, uint64_t nreg,
                        const uint64_t *rb, uint64_t lanes, const uint64_t *frontier, const uint64_t *hub_fr,
                        uint32_t nhubs, const uint64_t *fbm, const uint64_t *visited, uint64_t *next, int cus,
-                       hipStream_t s);
+                       hipStream_t s, bool hubs_only = false);
 // dense levels: per-vertex pull with an early exit (k_bfs_pull_exit + k_bfs_pull_rest) over vertices
 // [vlo, V); rest u32[V]
 // scratch; counts[0] += in-edges read, counts[1] = vertices handed to the per-wave pass (zeroed by the caller)

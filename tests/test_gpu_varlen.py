@@ -41,7 +41,9 @@ MODES = {
     "bfs_push": {"OMX_VARLEN": "bfs", "OMX_BFS_PULL_DIV": "1"},
     "bfs_pull": dict(_PULL, OMX_PULL_PROBE="0"),  # dense levels: per-vertex early-exit pull
     "bfs_pull_tiles": dict(_PULL, OMX_PULL_PROBE="0", OMX_PULL_EXIT="0"),  # dense levels: in-edge wave tiles
-    "bfs_pull_probe": dict(_PULL, OMX_PULL_PROBE="2"),
+    "bfs_pull_probe": dict(_PULL, OMX_PULL_PROBE="2", OMX_HUB_PUSH="0"),
+    # sparse levels: the hub entries pulled, the non-hub frontier pushed (every level: OMX_PULL_PROBE=2)
+    "bfs_pull_hubs_push": dict(_PULL, OMX_PULL_PROBE="2", OMX_HUB_PUSH="force"),
     # the workgroup-tiled k_bfs_pull, and every wave tile through the slow path
     "bfs_pull_tiles_wg": dict(_PULL, OMX_PULL_PROBE="0", OMX_PULL_EXIT="0", OMX_PULL_WAVE="0"),
     "bfs_pull_probe_wg": dict(_PULL, OMX_PULL_PROBE="2", OMX_PULL_WAVE="0"),
@@ -115,7 +117,8 @@ def rmat14():
     return o.GraphSnapshot.rmat(14, device=0, keep_csr=True)
 
 
-@pytest.mark.parametrize("pull", ["auto", "pull", "pull_tiles", "pull_probe", "pull_tiles_wg", "pull_probe_wg"])
+@pytest.mark.parametrize("pull", ["auto", "pull", "pull_tiles", "pull_probe", "pull_hubs_push", "pull_tiles_wg",
+                                  "pull_probe_wg"])
 def test_varlen_rmat14_hub_root_vs_c_bfs(rmat14, pull, monkeypatch):
     """RMAT-14 from the highest-degree vertex and 63 others (rows straddle pull tiles; the hub
     threshold picks a strict subset of the sources) against oracle/bfs_ref.c, all levels bottom-up
@@ -127,7 +130,8 @@ def test_varlen_rmat14_hub_root_vs_c_bfs(rmat14, pull, monkeypatch):
     monkeypatch.setenv("OMX_PULL_HUBS", "512")
     if pull != "auto":
         monkeypatch.setenv("OMX_BFS_PULL_DIV", "1000000000000")
-    monkeypatch.setenv("OMX_PULL_PROBE", "2" if pull.startswith("pull_probe") else "0")
+    monkeypatch.setenv("OMX_PULL_PROBE", "2" if pull.startswith(("pull_probe", "pull_hubs")) else "0")
+    monkeypatch.setenv("OMX_HUB_PUSH", "force" if pull == "pull_hubs_push" else "0")
     monkeypatch.setenv("OMX_PULL_EXIT", "0" if pull.startswith("pull_tiles") else "1")
     monkeypatch.setenv("OMX_PULL_WAVE", "0" if pull.endswith("_wg") else "1")
     g = rmat14
