@@ -128,19 +128,25 @@ def ldbc():
     return o.GraphSnapshot.ldbc_like(device=0, keep_csr=True)
 
 
+@pytest.fixture(scope="module")
+def ldbc_ref(ldbc):
+    """oracle/dfs_ref.c over the SF10 triangles, computed once for the parametrized device runs"""
+    from oracle import dfs
+    g = ldbc
+    cg = dfs.CsrGraph(g.csr[0], g.csr[1], {"uid": np.arange(g.V, dtype=np.int64), "age": g.age})
+    return dfs.run(cg, CYCLES[0][1], nthreads=8)
+
+
 @pytest.mark.parametrize("merge", ["1", "force", "0"])
-def test_c4_ldbc_sf10_vs_c_oracle(ldbc, merge, monkeypatch):
+def test_c4_ldbc_sf10_vs_c_oracle(ldbc, ldbc_ref, merge, monkeypatch):
     """configs[3] at full size: every directed triangle of the LDBC-like SF10 Knows graph, bit-exact
     against oracle/dfs_ref.c, with the same traversed-edge count — merge path by its ratio rule, on every
-    row that fits a tile, and off."""
+    row that fits a tile, and off (the probe, the default)."""
     import orientdb_amd as o
-    from oracle import dfs
     monkeypatch.setenv("OMX_MERGE", merge)
-    g = ldbc
+    g, ref = ldbc, ldbc_ref
     q = CYCLES[0][1]
     rs = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_NO_RID_MAP)
-    cg = dfs.CsrGraph(g.csr[0], g.csr[1], {"uid": np.arange(g.V, dtype=np.int64), "age": g.age})
-    ref = dfs.run(cg, q, nthreads=8)
     assert rs.info["n_rows"] == len(ref["rows"])
     assert rs.info["edges_traversed"] == ref["edges"]
     idx = [rs.columns.index(c) for c in ref["aliases"]]
