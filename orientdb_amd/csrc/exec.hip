@@ -144,6 +144,16 @@ class Timer {
   std::vector<Rec> recs_;
 };
 
+// out[id[i]] = deg[i] (a fetched adjacency's degrees placed at their vertices)
+__global__ void k_scatter_deg(const uint32_t *id, const uint32_t *deg, uint64_t n, uint64_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[id[i]] = deg[i];
+}
+static void launch_scatter_deg(const uint32_t *id, const uint32_t *deg, uint64_t n, uint64_t *out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_scatter_deg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, id, deg, n, out);
+}
+
 // out[i] = (u32) in[i] (degrees of a partition's rows: below 2^32)
 __global__ void k_u64_to_u32(const uint64_t *in, uint64_t n, uint32_t *out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -252,14 +262,20 @@ class Executor {
     HIP_CHECK(hipEventRecord(ea, s_));
     mark("events");
     const bool chain = p_.kind != Plan::MATCH;
-    if (dist_ && !chain) gather_global_degrees();
+    if (dist_) gather_global_degrees();  // (degree predicates; a chain's WHERE / WHILE too)
     bool empty = !chain && (p_.empty || !check_candidates());
     bool counted_only = false;
     std::vector<DBuf<uint32_t>> chain_out;
-    if (chain) {
+    if (chain && dist_ && tr_->rank() != 0) {
+      // a partitioned chain runs on rank 0; the others serve the adjacency lists it asks for
+      serve_chain();
+      R_ = 0;
+      chain_out.push_back(DBuf<uint32_t>(&pool_, 1));
+    } else if (chain) {
       chain_out.push_back(p_.kind == Plan::TRAVERSE ? traverse_bfs()
                           : p_.kind == Plan::SELECT ? select_expand()
                                                     : shortest_path());
+      if (dist_) tr_->allgather_n({0, 0}, s_);  // the servers stop
     } else if (!empty) {
       // a partitioned run keeps stepping with no local rows: every rank takes part in every exchange
       for (size_t i = 0; i < p_.steps.size() && (R_ > 0 || dist_); ++i) {
@@ -776,8 +792,8 @@ class Executor {
 
   // ---- 1-D partitioned execution (dist.h) ----------------------------------------------------------
   void dist_setup() {
-    if (p_.kind != Plan::MATCH && (tr_ || o_.shard_world > 1 || g_.partitioned()))
-      unsupported("TRAVERSE / SELECT expand() on a partitioned or sharded execution");
+    if (p_.kind != Plan::MATCH && o_.shard_world > 1)
+      unsupported("TRAVERSE / SELECT expand() / shortestPath() with root shards");
     if (!tr_) {
       if (g_.partitioned())
         fail(OMX_E_INVALID, "partitioned snapshot executed without a communicator (omx_exec_options.comm)");
@@ -2051,8 +2067,10 @@ class Executor {
   DBuf<uint32_t> ordered_hop(const uint32_t *cur, uint64_t n, const AdjSpec &adj, uint64_t &out_n,
                              const uint64_t *filter = nullptr) {
     out_n = 0;
+    FetchedAdj f;
+    if (dist_) chain_fetch(adj, cur, n, f);  // (every call, n = 0 included: the servers count on it)
     if (!n) return DBuf<uint32_t>(&pool_, 1);
-    ExpandOut o = expand_core(cur, n, adj, filter, {}, true, false, nullptr, nullptr, nullptr, nullptr, true);
+    ExpandOut o = expand_core(cur, n, adj, filter, {}, true, false, nullptr, nullptr, nullptr, dist_ ? &f.adj : nullptr, true);
     edges_ += o.E;
     edges_iter_ += o.E;
     out_n = o.n;
@@ -2061,6 +2079,88 @@ class Executor {
   }
 
   int64_t chain_limit() const { return p_.limit >= 0 ? p_.limit : o_.limit; }
+
+  // ---- partitioned TRAVERSE / SELECT / shortestPath: rank 0 walks, the owners serve adjacency lists ---
+  // Before each ordered move rank 0 asks for the lists of the move's vertices (chain_fetch): the request
+  // (1, the AdjSpec's index in chain_specs) travels in an allgather_n round, the vertices go to their
+  // owners, which answer with degrees and lists (the ordered expansion: parts in the AdjSpec's order), and
+  // rank 0 lays them out as a V-row CSR (zero rows for the vertices not asked for) that the unchanged
+  // single-GPU code expands. A (0, 0) round ends the service. The work list, history, WHILE / WHERE
+  // bitmaps (replicated columns) and the result stay on rank 0.
+  struct FetchedAdj {
+    DBuf<uint64_t> rp;
+    DBuf<uint32_t> col;
+    DAdj adj{};
+  };
+  std::vector<const AdjSpec *> chain_specs() const {
+    std::vector<const AdjSpec *> v;
+    for (const AdjSpec &h : p_.chain.hops) v.push_back(&h);
+    v.push_back(&p_.chain.sp_left);
+    v.push_back(&p_.chain.sp_right);
+    return v;
+  }
+  void chain_fetch(const AdjSpec &as, const uint32_t *list, uint64_t n, FetchedAdj &f) {
+    const std::vector<const AdjSpec *> specs = chain_specs();
+    const uint64_t id = (uint64_t)(std::find(specs.begin(), specs.end(), &as) - specs.begin());
+    if (id >= specs.size()) fail(OMX_E_INVALID, "internal: a chain adjacency outside the plan");
+    tr_->allgather_n({1, id}, s_);
+    fetch_lists(as, list, n, &f);
+  }
+  void serve_chain() {
+    const std::vector<const AdjSpec *> specs = chain_specs();
+    for (;;) {
+      const std::vector<uint64_t> w = tr_->allgather_n({0, 0}, s_);
+      if (w[0] == 0) return;  // rank 0's word: the walk ended
+      if (w[1] >= specs.size()) fail(OMX_E_INVALID, "internal: a chain adjacency request out of range");
+      fetch_lists(*specs[w[1]], nullptr, 0, nullptr);
+    }
+  }
+  // collective: rank 0's vertices (list, n) → their lists from the owners; out (rank 0) gets the CSR
+  void fetch_lists(const AdjSpec &as, const uint32_t *list, uint64_t n, FetchedAdj *out) {
+    const int W = tr_->world();
+    DBuf<uint32_t> ids;
+    uint64_t m = 0;
+    if (n) {  // distinct, ascending (so the owners' answers concatenate in vertex order)
+      DBuf<uint64_t> bm(&pool_, std::max<uint64_t>(nwords_, 1));
+      HIP_CHECK(hipMemsetAsync(bm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+      launch_mark_bitmap(list, n, bm.p, g_.V, s_);
+      ids = bitmap_list(bm.p, 0, 1, m);
+    } else {
+      ids = DBuf<uint32_t>(&pool_, 1);
+    }
+    DBuf<uint32_t> dest(&pool_, std::max<uint64_t>(m, 1));
+    DBuf<uint64_t> hist(&pool_, W);
+    HIP_CHECK(hipMemsetAsync(hist.p, 0, W * sizeof(uint64_t), s_));
+    if (m) launch_route_owner(ids.p, m, block_, (uint32_t)W, dest.p, hist.p, s_);
+    m = exchange_cols({&ids}, m, dest, hist);
+    DBuf<uint32_t> deg32(&pool_, std::max<uint64_t>(m, 1)), lists;
+    uint64_t nl = 0;
+    if (m) {
+      DBuf<uint64_t> deg(&pool_, m + 1);
+      launch_row_degree(ids.p, m, make_adj(as), deg.p, s_);
+      launch_u64_to_u32(deg.p, m, deg32.p, s_);
+      ExpandOut o = expand_core(ids.p, m, as, nullptr, {}, true, false, nullptr, nullptr, nullptr, nullptr, true);
+      nl = o.n;
+      lists = nl ? std::move(o.dst) : DBuf<uint32_t>(&pool_, 1);
+    } else {
+      lists = DBuf<uint32_t>(&pool_, 1);
+    }
+    m = to_rank0({&ids, &deg32}, m);
+    nl = to_rank0({&lists}, nl);
+    if (!out) return;
+    // rank 0: rp[v + 1] - rp[v] = the fetched degree of v (0 for the others), col = the lists in order
+    DBuf<uint64_t> dv(&pool_, (uint64_t)g_.V + 1);
+    HIP_CHECK(hipMemsetAsync(dv.p, 0, ((uint64_t)g_.V + 1) * 8, s_));
+    if (m) launch_scatter_deg(ids.p, deg32.p, m, dv.p, s_);
+    out->rp = DBuf<uint64_t>(&pool_, (uint64_t)g_.V + 1);
+    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, dv.p, out->rp.p, (int64_t)g_.V + 1, s_); });
+    out->col = std::move(lists);
+    out->adj = DAdj{};
+    out->adj.n = 1;
+    out->adj.sorted = as.parts.size() == 1 && as.sorted;
+    out->adj.p[0].rp = out->rp.p;
+    out->adj.p[0].col = out->col.p;
+  }
 
   // TRAVERSE <fields> FROM <target> [WHILE <cond>] [MAXDEPTH d] [LIMIT n] STRATEGY BREADTH_FIRST.
   // OTraverse's queue (OTraverseContext.QueueMemory) holds, level by level, the records the previous
@@ -2172,7 +2272,10 @@ class Executor {
     if (A.n >= UINT32_MAX) unsupported("a shortestPath() level of 2^32 or more vertices");
     DBuf<uint32_t> rows(&pool_, A.n);
     launch_iota(rows.p, A.n, s_);
-    ExpandOut o = expand_core(A.queue.p, A.n, *A.adj, nullptr, {rows.p}, true, false, nullptr, nullptr, nullptr, nullptr, true);
+    FetchedAdj f;
+    if (dist_) chain_fetch(*A.adj, A.queue.p, A.n, f);
+    ExpandOut o = expand_core(A.queue.p, A.n, *A.adj, nullptr, {rows.p}, true, false, nullptr, nullptr, nullptr,
+                              dist_ ? &f.adj : nullptr, true);
     edges_ += o.E;
     edges_iter_ += o.E;
     if (!o.n) {

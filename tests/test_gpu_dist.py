@@ -229,7 +229,7 @@ def test_unsupported_keeps_communicator_usable(rmat10_full):
     parts = _parts(2)
     comms = o.Comm.threads(2)
     name, query, cols = [q for q in RMAT_QUERIES if q[0] == "c2_both_ends"][0]
-    unsup = "TRAVERSE out('Knows') FROM #11:0 STRATEGY BREADTH_FIRST"
+    unsup = "TRAVERSE out('Knows') FROM #11:0 STRATEGY DEPTH_FIRST"  # (the planner refuses it everywhere)
     out, errs = [None, None], [[], []]
 
     def work(r):
@@ -388,3 +388,37 @@ def test_partitioned_cartesian_and_degrees(rmat10_full, world, q):
     res = run_ranks(_parts(world), query)
     got = [gpu_set(r, cols) for r in res]
     assert set().union(*got) == want and len(want) > 0
+
+
+# ---- partitioned TRAVERSE / SELECT expand() / shortestPath(): rank 0 walks, the owners serve lists ----
+def _chain_queries(g):
+    rp = g.csr[0].astype(np.int64)
+    deg = np.diff(rp)
+    hub, leaf = int(np.argmax(deg)), int(np.argmax(deg == 1))
+    return [
+        ("traverse_while", "TRAVERSE out('Knows') FROM #11:%d WHILE $depth < 3 STRATEGY BREADTH_FIRST" % hub),
+        ("traverse_maxdepth", "TRAVERSE out('Knows') FROM [#11:3, #11:7, #11:3] MAXDEPTH 2 STRATEGY BREADTH_FIRST"),
+        ("traverse_limit_both", "TRAVERSE both('Knows') FROM #11:%d MAXDEPTH 3 LIMIT 50 STRATEGY BREADTH_FIRST" % leaf),
+        ("traverse_prop", "TRAVERSE in('Knows') FROM #11:%d WHILE age < 70 STRATEGY BREADTH_FIRST" % hub),
+        ("select_chain", "SELECT expand(out('Knows').out('Knows')) FROM #11:%d" % hub),
+        ("select_where", "SELECT expand(in('Knows').out('Knows')) FROM Person WHERE uid < 20"),
+        ("shortest_out", "SELECT expand(shortestPath(#11:%d, #11:%d, 'OUT', 'Knows'))" % (leaf, hub)),
+        ("shortest_both", "SELECT expand(shortestPath(#11:%d, #11:%d, 'BOTH'))" % (hub, leaf)),
+    ]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("qi", range(8), ids=["traverse_while", "traverse_maxdepth", "traverse_limit_both", "traverse_prop",
+                                              "select_chain", "select_where", "shortest_out", "shortest_both"])
+def test_partitioned_chains(rmat10_full, world, qi):
+    """TRAVERSE / SELECT expand() / shortestPath() on a partitioned snapshot (Executor::serve_chain): rank 0
+    runs the ordered walk over lists its peers fetch from their rows, so the records come in the
+    reference's order, equal to the single-snapshot run's; the other ranks return nothing."""
+    import orientdb_amd as o
+    g, _ = rmat10_full
+    name, q = _chain_queries(g)[qi]
+    full = o.OMatchStatement(q).execute(g, documents=False)
+    res = run_ranks(_parts(world), q, documents=False)
+    assert np.array_equal(np.asarray(res[0].rows), np.asarray(full.rows)), name
+    assert res[0].info["edges_traversed"] == full.info["edges_traversed"]
+    assert all(r.info["n_rows"] == 0 for r in res[1:])
