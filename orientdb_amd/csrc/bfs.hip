@@ -762,19 +762,12 @@ __global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, u
 }
 
 // Result emission from the visited masks: (row0 + lane, v) for every set lane of v with emit(v).
-// Two threads per vertex, one per 32-lane half of its mask: a thread stages its pairs one set bit at a
-// time, so a wave waits for its fullest mask — a vertex every root reached holds 64 — and halves halve
-// that wait (the rows' order inside a block is a set's: vertex-major, then the halves).
-constexpr uint32_t kEmitV = kB / 2;  // vertices per emission block
-__device__ __forceinline__ uint64_t emit_half(uint64_t m, uint32_t t) {
-  return (t & 1) ? (m & 0xFFFFFFFF00000000ull) : (m & 0xFFFFFFFFull);
-}
 __global__ __launch_bounds__(kB) void k_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V,
                                                        uint32_t *blk) {
   __shared__ uint32_t s_w[kB / 64];
-  const uint64_t v = (uint64_t)blockIdx.x * kEmitV + threadIdx.x / 2;
+  const uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x;
   uint32_t c = 0;
-  if (v < V && (!emit_bm || bm_test(emit_bm, (uint32_t)v))) c = (uint32_t)__popcll(emit_half(visited[v], threadIdx.x));
+  if (v < V && (!emit_bm || bm_test(emit_bm, (uint32_t)v))) c = (uint32_t)__popcll(visited[v]);
   uint32_t tot;
   block_excl_scan<kB>(c, s_w, &tot);
   if (threadIdx.x == 0) blk[blockIdx.x] = tot;
@@ -796,11 +789,11 @@ __global__ __launch_bounds__(kB) void k_bfs_emit_write(const uint64_t *visited, 
   __shared__ uint8_t s_t[kEmitWin];
   __shared__ uint32_t s_cv[BfsCarry::kMax][64];
   static_assert(kB <= 256, "s_t holds a thread index in 8 bits");
-  const uint64_t v = (uint64_t)blockIdx.x * kEmitV + threadIdx.x / 2;
+  const uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x;
   for (int c = 0; c < cc.n; ++c)
     if (threadIdx.x < cc.nl) s_cv[c][threadIdx.x] = cc.in[c][row0 + threadIdx.x];
   uint64_t m = 0;
-  if (v < V && (!emit_bm || bm_test(emit_bm, (uint32_t)v))) m = emit_half(visited[v], threadIdx.x);
+  if (v < V && (!emit_bm || bm_test(emit_bm, (uint32_t)v))) m = visited[v];
   uint32_t tot;
   const uint32_t c = (uint32_t)__popcll(m);
   const uint32_t off = block_excl_scan<kB>(c, s_w, &tot);  // (its barrier also publishes s_cv)
@@ -822,22 +815,22 @@ __global__ __launch_bounds__(kB) void k_bfs_emit_write(const uint64_t *visited, 
       const uint32_t l = s_row[i];
       if (cc.n == 0) out_row[base + w0 + i] = row0 + l;
       for (int k = 0; k < cc.n; ++k) cc.out[k][base + w0 + i] = s_cv[k][l];
-      out_v[base + w0 + i] = (uint32_t)((uint64_t)blockIdx.x * kEmitV + s_t[i] / 2);
+      out_v[base + w0 + i] = (uint32_t)((uint64_t)blockIdx.x * kB + s_t[i]);
     }
     __syncthreads();
   }
 }
 void launch_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, uint32_t *blk, hipStream_t s) {
-  hipLaunchKernelGGL(k_bfs_emit_count, dim3(nblocks(V, kEmitV)), dim3(kB), 0, s, visited, emit_bm, V, blk);
+  hipLaunchKernelGGL(k_bfs_emit_count, dim3(nblocks(V, kB)), dim3(kB), 0, s, visited, emit_bm, V, blk);
   KCHECK("k_bfs_emit_count");
 }
 void launch_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, const uint64_t *blk_offs,
                            uint32_t row0, uint32_t *out_row, uint32_t *out_v, const BfsCarry &cc, hipStream_t s) {
-  hipLaunchKernelGGL(k_bfs_emit_write, dim3(nblocks(V, kEmitV)), dim3(kB), 0, s, visited, emit_bm, V, blk_offs, row0,
+  hipLaunchKernelGGL(k_bfs_emit_write, dim3(nblocks(V, kB)), dim3(kB), 0, s, visited, emit_bm, V, blk_offs, row0,
                      out_row, out_v, cc);
   KCHECK("k_bfs_emit_write");
 }
-unsigned bfs_blocks(uint32_t V) { return nblocks(V, kEmitV); }
+unsigned bfs_blocks(uint32_t V) { return nblocks(V, kB); }
 
 // T_BOUND: row r (lane r - row0) keeps its binding iff its bound target was reached and passes emit
 __global__ void k_bfs_bound(const uint32_t *dst, uint64_t row0, int nl, const uint64_t *visited,
