@@ -13,6 +13,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -237,6 +238,8 @@ class Executor {
     if (const char *fm = std::getenv("OMX_FEMIT_MIN_ET")) femit_min_et_ = std::strtoull(fm, nullptr, 10);
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
     if (const char *sj = std::getenv("OMX_SEMI")) semi_ok_ = std::strcmp(sj, "0") != 0;
+    if (const char *rl = std::getenv("OMX_RLIST")) rlist_ = std::strcmp(rl, "force") == 0 ? 2 : std::strcmp(rl, "0") != 0 ? 1 : 0;
+    if (const char *rr = std::getenv("OMX_RLIST_RATIO")) rlist_ratio_ = std::strtoull(rr, nullptr, 10);
     if (const char *gq = std::getenv("OMX_GRP32")) grp32_ = std::strcmp(gq, "0") != 0;
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
     if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
@@ -570,6 +573,12 @@ class Executor {
     launch_post_words(dptr, 2, mail(), s_, 8);
     const uint64_t *w = wait_mail();
     return {w[0], w[1]};
+  }
+  // three u64 words in one host round trip
+  std::array<uint64_t, 3> read3(const uint64_t *dptr) {
+    launch_post_words(dptr, 3, mail(), s_, 8);
+    const uint64_t *w = wait_mail();
+    return {w[0], w[1], w[2]};
   }
   template <class T>
   T read1(const T *dptr) {
@@ -1732,6 +1741,11 @@ class Executor {
   // (profiles/r03/femit/c2ab.txt)
   int femit_ = 1;
   uint64_t femit_min_et_ = 4000000000ull;
+  // OMX_RLIST: 1 = the lists from the targets' side (factor.hip k_rlist_tile) when the targets' in-entries
+  // are fewer than 1/rlist_ratio_ of the sources' entries (OMX_RLIST_RATIO), force = whenever it applies
+  // (tests), 0 = never
+  int rlist_ = 1;
+  uint64_t rlist_ratio_ = 3;
   bool femit_slow_ = false;  // OMX_FEMIT_SLOW=1: every output tile through k_femit_slow (tests)
 
   // step 4 of expand_factorized when the rows are written: the output space Σ_rows |L(g[r])| is laid out
@@ -1779,14 +1793,14 @@ class Executor {
   // perm_sorted: the rows sorted by source (g in that order); perm_sorted[i] = the row at sorted
   // position i. nlist: the entries of all U lists (each read from HBM once, then from L2 by its rows)
   void emit_factorized(DBuf<uint32_t> &g, uint64_t R, uint64_t U, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol,
-                       uint64_t nlist, const std::vector<int> &cols, const Step &st, const uint32_t *perm_sorted) {
+                       uint64_t nlist /* UINT64_MAX: read from loff[U] */, const std::vector<int> &cols, const Step &st, const uint32_t *perm_sorted) {
     // 1. the rows whose list is not empty (the others write nothing), in row order or grouped by source.
     // Their count Rn stays on the device until the output size N is known: the kernels in between run
     // over R rows and read Rn, so one host round trip returns both
     DBuf<uint64_t> len(&pool_, R + 1);
     launch_femit_len(g.p, R, loff.p, len.p, s_);
     DBuf<uint32_t> idx(&pool_, R);
-    DBuf<uint64_t> nsel(&pool_, 2);
+    DBuf<uint64_t> nsel(&pool_, 3);
     {
       hipcub::CountingInputIterator<uint32_t> cnt(0);
       hipcub::TransformInputIterator<uint8_t, NonZeroU64, const uint64_t *> fl(len.p, NonZeroU64());
@@ -1809,8 +1823,17 @@ class Executor {
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, len.p, roff.p, (int64_t)(R + 1), s_); });
     launch_femit_base(gs.p, R, loff.p, roff.p, rbase.p, s_, rn);
     HIP_CHECK(hipMemcpyAsync(nsel.p + 1, roff.p + R, 8, hipMemcpyDeviceToDevice, s_));
-    const auto rn_n = read2(nsel.p);
-    const uint64_t Rn = rn_n.first, N = rn_n.second;
+    uint64_t Rn = 0, N = 0;
+    if (nlist == UINT64_MAX) {  // the lists' total from the device too (lists from the targets' side)
+      HIP_CHECK(hipMemcpyAsync(nsel.p + 2, loff.p + U, 8, hipMemcpyDeviceToDevice, s_));
+      const auto w = read3(nsel.p);
+      Rn = w[0], N = w[1], nlist = w[2];
+      if (rlist_rec_ != SIZE_MAX) tm_.amend_at(rlist_rec_, nlist * 8ull + nct_rec_ * 12ull + 4ull * er_rec_);
+      rlist_rec_ = SIZE_MAX;
+    } else {
+      const auto rn_n = read2(nsel.p);
+      Rn = rn_n.first, N = rn_n.second;
+    }
     edges_iter_ += N;
     alg_bytes_ += 8ull * R + 4ull * N * (cols.size() + 2);  // as expand_core's unfiltered written hop
     R_ = N;
@@ -1874,6 +1897,73 @@ class Executor {
                                            : alg);
   }
 
+  // steps 2-4 of expand_factorized with the lists from the targets' side (factor.hip k_rlist_tile): the
+  // targets tl (the hop's filter bitmap, ascending) and their in-entries' offsets tdoff over the reversed
+  // adjacency rs; the distinct sources ub ascending, g the rows' source indices
+  bool expand_factorized_rev(const Step &st, bool write, const std::vector<int> &cols, uint64_t R, uint64_t U,
+                             DBuf<uint32_t> &ub, DBuf<uint32_t> &g, DBuf<uint32_t> &perm_s, bool presort, bool femit,
+                             const DBuf<uint32_t> &tl, uint64_t nct, const DBuf<uint64_t> &tdoff, uint64_t ER,
+                             const AdjSpec &rs) {
+    if (!presort) {  // the rows' source indices: the rank of their source among ub
+      g = DBuf<uint32_t>(&pool_, R);
+      launch_index_of(ub.p, U, col_[st.src].p, R, g.p, s_);
+    }
+    const DAdj ra = make_adj(rs);
+    const uint64_t nwords = ((uint64_t)g_.V + 63) / 64;
+    DBuf<uint4> rw(&pool_, std::max<uint64_t>(nwords, 1));
+    launch_rank_words(ub.p, U, nwords, rw.p, s_);
+    DBuf<uint32_t> h32(&pool_, U + 1), eidx(&pool_, std::max<uint64_t>(ER, 1));
+    DBuf<uint64_t> rb(&pool_, 2 * rlist_tiles(ER) + 2), loff(&pool_, U + 1);
+    HIP_CHECK(hipMemsetAsync(h32.p, 0, (U + 1) * 4, s_));
+    RListArgs ra_{};
+    ra_.doff = tdoff.p;
+    ra_.tv = tl.p;
+    ra_.rp = ra.p[0].rp;
+    ra_.col = ra.p[0].col;
+    ra_.rb = rb.p;
+    ra_.rw = rw.p;
+    ra_.nc = nct;
+    ra_.ER = ER;
+    ra_.eidx = eidx.p;
+    ra_.cnt = h32.p;
+    tm_.begin("k_rlist_count");
+    launch_rlist(ra_, true, cus(), s_);
+    // per in-entry its col word, its rank word, its source index; per target its offsets and row pointer
+    tm_.end(ER * (4ull + 16ull + 4ull) + nct * 28ull);
+    edges_iter_ += ER;
+    {
+      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> hc(h32.p, CastU64());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, hc, loff.p, (int64_t)(U + 1), s_); });
+    }
+    if (write && semi_) {
+      semi_join(g, R, loff, cols);
+      return true;
+    }
+    // the lists' total stays on the device (the emission reads it with its own counts)
+    DBuf<uint32_t> lcol(&pool_, std::max<uint64_t>(ER, 1));
+    {
+      DBuf<uint32_t> cur(&pool_, U + 1);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, h32.p, cur.p, (int64_t)(U + 1), s_); });
+      ra_.cnt = cur.p;
+      ra_.lcol = lcol.p;
+      tm_.begin("k_rlist_place");
+      launch_rlist(ra_, false, cus(), s_);
+      tm_.end(ER * 4ull + nct * 12ull);  // amended with the placed entries once known
+      rlist_rec_ = tm_.last();
+      nct_rec_ = nct;
+      er_rec_ = ER;
+    }
+    if (femit) {
+      emit_factorized(g, R, U, loff, lcol, UINT64_MAX, cols, st, perm_s.p);
+      return true;
+    }
+    DBuf<uint32_t> rowsrc = std::move(g);
+    return expand_over_lists(st, write, cols, R, U, rowsrc, loff, lcol, UINT64_MAX);
+  }
+  // the placement pass's timer record, its targets and in-entries (amended in emit_factorized)
+  size_t rlist_rec_ = SIZE_MAX;
+  uint64_t nct_rec_ = 0, er_rec_ = 0;
+
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
@@ -1915,15 +2005,46 @@ class Executor {
       tm_.end(4ull * R + 8ull * nwords_);
       ub = bitmap_list(ubm.p, 0, 1, U);
     }
+    const bool nbset = st.distinct_nb && !st.adj.dup_free;
+    // the targets' side (below): the targets' list and in-degrees, scanned beside the sources' degrees
+    const bool rev_ok = rlist_ && !nbset && !dist_ && st.adj.parts.size() == 1 && U > 0;
+    AdjSpec rs = st.adj;
+    if (rev_ok) rs.parts[0].second ^= 1;
+    uint64_t nct = 0;
+    DBuf<uint32_t> tl;
+    DBuf<uint64_t> tdoff;
+    if (rev_ok) {
+      tl = bitmap_list(bitmap(st.filter_bm), 0, 1, nct);
+      DBuf<uint64_t> tdeg(&pool_, nct + 1);
+      tdoff = DBuf<uint64_t>(&pool_, nct + 1);
+      launch_row_degree(tl.p, nct, make_adj(rs), tdeg.p, s_);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tdeg.p, tdoff.p, (int64_t)(nct + 1), s_); });
+    }
     // the distinct sources' degrees, scanned
     DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1);
     tm_.begin("k_row_degree");
     launch_row_degree(ub.p, U, make_adj(st.adj), udeg.p, s_);
     tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(U + 1), s_); });
-    const uint64_t EU = read1(doff.p + U);
+    uint64_t EU = 0, ER = UINT64_MAX;
+    if (rev_ok) {  // both totals in one host round trip
+      DBuf<uint64_t> two(&pool_, 2);
+      HIP_CHECK(hipMemcpyAsync(two.p, doff.p + U, 8, hipMemcpyDeviceToDevice, s_));
+      HIP_CHECK(hipMemcpyAsync(two.p + 1, tdoff.p + nct, 8, hipMemcpyDeviceToDevice, s_));
+      const auto eu_er = read2(two.p);
+      EU = eu_er.first;
+      ER = eu_er.second;
+    } else {
+      EU = read1(doff.p + U);
+    }
     if (Et < factor_min_ratio_ * EU) return false;
     edges_ += Et;
+    const bool rev = rev_ok && ER < 0xFFFFFFFFull && (rlist_ == 2 || ER * rlist_ratio_ < EU);
+    if (debug_expand_)
+      std::fprintf(stderr, "[omx factorized] R=%llu U=%llu Et=%llu EU=%llu targets' in-entries=%lld -> %s side\n",
+                   (unsigned long long)R, (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU,
+                   rev_ok ? (long long)ER : -1ll, rev ? "targets'" : "sources'");
+    if (rev) return expand_factorized_rev(st, write, cols, R, U, ub, g, perm_s, presort, femit, tl, nct, tdoff, ER, rs);
     // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
     // (presorted rows have theirs from the runs)
     DBuf<uint32_t> iu(&pool_, std::max<uint64_t>(U, 1));
@@ -1944,7 +2065,6 @@ class Executor {
     // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
     // (the filtered lists stay in the expansion's per-worker segments: grouping reads them in place)
     // (a set-valued hop over an adjacency that may repeat a neighbour: each list made distinct first)
-    const bool nbset = st.distinct_nb && !st.adj.dup_free;
     ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, !nbset);
     edges_iter_ += l.E;
     if (nbset && l.n) l.n = distinct_pairs(l.carry[0], l.dst, {}, l.n);
@@ -1998,6 +2118,13 @@ class Executor {
       emit_factorized(g, R, U, loff, lcol, nlist, cols, st, perm_s.p);
       return true;
     }
+    return expand_over_lists(st, write, cols, R, U, g, loff, lcol, nlist);
+  }
+
+  // step 4 without the factorized emission: an unfiltered expansion of the rows (source index g) over the
+  // lists (loff, lcol)
+  bool expand_over_lists(const Step &st, bool write, const std::vector<int> &cols, uint64_t R, uint64_t U,
+                         DBuf<uint32_t> &g, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol, uint64_t nlist) {
     DAdj ladj{};
     ladj.n = 1;
     ladj.sorted = 0;
@@ -2010,9 +2137,8 @@ class Executor {
     R_ = o.n;
     factorized_hops_++;
     if (debug_expand_)
-      std::fprintf(stderr, "[omx factorized] R=%llu U=%llu Et=%llu EU=%llu lists=%llu rows=%llu\n", (unsigned long long)R,
-                   (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU, (unsigned long long)nlist,
-                   (unsigned long long)o.n);
+      std::fprintf(stderr, "[omx factorized] R=%llu U=%llu lists=%lld rows=%llu\n", (unsigned long long)R,
+                   (unsigned long long)U, nlist == UINT64_MAX ? -1ll : (long long)nlist, (unsigned long long)o.n);
     if (!write || R_ == 0) return true;
     segmented_ = false;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);

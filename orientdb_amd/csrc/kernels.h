@@ -282,6 +282,24 @@ struct FemitArgs {
 };
 bool femit_supported(int nl, int nc);
 uint64_t femit_tiles(uint64_t N);
+// the factorized hop's lists from the targets' side (factor.hip k_rlist_tile): the targets' in-entries
+// whose neighbour is a distinct source, grouped by that source
+struct RListArgs {
+  const uint64_t *doff;  // [nc+1] exclusive scan of the targets' in-degrees
+  const uint32_t *tv;    // [nc] target vertices
+  const uint64_t *rp;    // the reversed adjacency (single part): target → in-neighbours
+  const uint32_t *col;
+  const uint64_t *rb;    // [2·rlist_tiles(ER)] first / last target of every tile (the COUNT pass writes it)
+  const uint4 *rw;       // rank words of the distinct sources (launch_rank_words)
+  uint64_t nc, ER;
+  uint32_t *eidx;        // [ER] source index of every entry (~0u: none); COUNT writes, placement reads
+  uint32_t *cnt;         // COUNT: per-source entry counts (zeroed); placement: cursors (their exclusive scan)
+  uint32_t *lcol;        // placement: the lists
+};
+uint64_t rlist_tiles(uint64_t ER);
+// rw[w] = {bits of the sources in [64w, 64w+64) (lo, hi), sources below 64w, 0}; ub ascending, distinct
+void launch_rank_words(const uint32_t *ub, uint64_t U, uint64_t nwords, uint4 *rw, hipStream_t s);
+void launch_rlist(RListArgs &a, bool count, int cus, hipStream_t s);
 // len[r] = |L(g[r])| for r < R, len[R] = 0
 // nd: a device row count ≤ R (rows past it: length 0, no base); nullptr: all R rows
 void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s,
