@@ -1903,15 +1903,18 @@ class Executor {
   bool expand_factorized_rev(const Step &st, bool write, const std::vector<int> &cols, uint64_t R, uint64_t U,
                              DBuf<uint32_t> &ub, DBuf<uint32_t> &g, DBuf<uint32_t> &perm_s, bool presort, bool femit,
                              const DBuf<uint32_t> &tl, uint64_t nct, const DBuf<uint64_t> &tdoff, uint64_t ER,
-                             const AdjSpec &rs) {
+                             const AdjSpec &rs, DBuf<uint4> &rw) {
+    const uint64_t nwords = ((uint64_t)g_.V + 63) / 64;
+    if (!rw.p) {
+      rw = DBuf<uint4>(&pool_, std::max<uint64_t>(nwords, 1));
+      launch_rank_words(ub.p, U, nwords, rw.p, s_);
+    }
     if (!presort) {  // the rows' source indices: the rank of their source among ub
+      DBuf<uint32_t> unused(&pool_, U + 1);
       g = DBuf<uint32_t>(&pool_, R);
-      launch_index_of(ub.p, U, col_[st.src].p, R, g.p, s_);
+      launch_row_rank(rw.p, col_[st.src].p, R, g.p, unused.p, s_);
     }
     const DAdj ra = make_adj(rs);
-    const uint64_t nwords = ((uint64_t)g_.V + 63) / 64;
-    DBuf<uint4> rw(&pool_, std::max<uint64_t>(nwords, 1));
-    launch_rank_words(ub.p, U, nwords, rw.p, s_);
     DBuf<uint32_t> h32(&pool_, U + 1), eidx(&pool_, std::max<uint64_t>(ER, 1));
     DBuf<uint64_t> rb(&pool_, 2 * rlist_tiles(ER) + 2), loff(&pool_, U + 1);
     HIP_CHECK(hipMemsetAsync(h32.p, 0, (U + 1) * 4, s_));
@@ -1977,26 +1980,28 @@ class Executor {
     // wants them grouped), so the distinct sources are the sorted runs' heads and a row's source index
     // is its run — no bitmap, position map or second sort
     const bool presort = femit && R > 0;
+    DBuf<uint4> rw;  // rank words of the distinct sources (grouped rows, lists from the targets' side)
+    const uint64_t nrw = ((uint64_t)g_.V + 63) / 64;
     if (presort) {
-      DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
-      DBuf<uint8_t> head(&pool_, R);
-      DBuf<uint64_t> nsel(&pool_, 1);
+      // grouped by a counting sort over the source indices (the index of a row's source is its rank in
+      // the source bitmap): ≈ 0.1 ms less than a radix sort of the rows by source at M1
+      ubm = DBuf<uint64_t>(&pool_, std::max<uint64_t>(nwords_, 1));
+      HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
+      tm_.begin("k_mark_bitmap");
+      launch_mark_bitmap(src, R, ubm.p, g_.V, s_);
+      tm_.end(4ull * R + 8ull * nwords_);
+      ub = bitmap_list(ubm.p, 0, 1, U);
+      rw = DBuf<uint4>(&pool_, std::max<uint64_t>(nrw, 1));
+      DBuf<uint32_t> gr(&pool_, R), cnt(&pool_, U + 1), cur(&pool_, U + 1);
+      HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 4, s_));
+      tm_.begin("femit_row_group");
+      launch_rank_words(ub.p, U, nrw, rw.p, s_);
+      launch_row_rank(rw.p, src, R, gr.p, cnt.p, s_);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, cur.p, (int64_t)(U + 1), s_); });
       perm_s = DBuf<uint32_t>(&pool_, R);
-      ub = DBuf<uint32_t>(&pool_, R);
       g = DBuf<uint32_t>(&pool_, R);
-      launch_iota(iota.p, R, s_);
-      tm_.begin("femit_row_sort");
-      cub([&](void *t, size_t &b) {
-        return hipcub::DeviceRadixSort::SortPairs(t, b, src, ss.p, iota.p, perm_s.p, (int64_t)R, 0,
-                                                  std::max(1, bits_for(g_.V)), s_);
-      });
-      tm_.end(16ull * R * ((bits_for(g_.V) + 7) / 8));
-      launch_run_heads(ss.p, R, head.p, s_);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, ss.p, head.p, ub.p, nsel.p, (int64_t)R, s_); });
-      hipcub::TransformInputIterator<uint32_t, CastU8U32, const uint8_t *> hc(head.p, CastU8U32());
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, hc, g.p, (int64_t)R, s_); });
-      launch_add_u32(g.p, R, -1, s_);
-      U = read1(nsel.p);
+      launch_row_place(gr.p, R, cur.p, perm_s.p, g.p, s_);
+      tm_.end(16ull * nrw + 4ull * U + R * (4ull + 16ull + 4ull) + R * (4ull + 8ull));
     } else {
       ubm = DBuf<uint64_t>(&pool_, std::max<uint64_t>(nwords_, 1));
       HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
@@ -2044,7 +2049,7 @@ class Executor {
       std::fprintf(stderr, "[omx factorized] R=%llu U=%llu Et=%llu EU=%llu targets' in-entries=%lld -> %s side\n",
                    (unsigned long long)R, (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU,
                    rev_ok ? (long long)ER : -1ll, rev ? "targets'" : "sources'");
-    if (rev) return expand_factorized_rev(st, write, cols, R, U, ub, g, perm_s, presort, femit, tl, nct, tdoff, ER, rs);
+    if (rev) return expand_factorized_rev(st, write, cols, R, U, ub, g, perm_s, presort, femit, tl, nct, tdoff, ER, rs, rw);
     // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
     // (presorted rows have theirs from the runs)
     DBuf<uint32_t> iu(&pool_, std::max<uint64_t>(U, 1));

@@ -60,6 +60,29 @@ __global__ void k_rank_words(const uint32_t *ub, uint64_t U, uint64_t nwords, ui
   rw[w] = make_uint4((uint32_t)bits, (uint32_t)(bits >> 32), (uint32_t)lo, 0u);
 }
 
+// the rows grouped by source without a sort: g[r] = the index of src[r] among the distinct sources (its
+// rank word), cnt[g[r]] += 1; then every row placed at its group's cursor (perm: sorted position → row,
+// gs: sorted position → group). The order inside a group is the atomics' order: the emission writes a
+// group's rows in any order (the result is a multiset, as the reference's rows are per source).
+__global__ void k_row_rank(const uint4 *rw, const uint32_t *src, uint64_t R, uint32_t *g, uint32_t *cnt) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint32_t v = src[r];
+  const uint4 q = rw[v >> 6];
+  const uint64_t bits = ((uint64_t)q.y << 32) | q.x;
+  const uint32_t id = q.z + (uint32_t)__popcll(bits & ((1ull << (v & 63u)) - 1ull));
+  g[r] = id;
+  atomicAdd(&cnt[id], 1u);
+}
+__global__ void k_row_place(const uint32_t *g, uint64_t R, uint32_t *cur, uint32_t *perm, uint32_t *gs) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint32_t id = g[r];
+  const uint32_t p = atomicAdd(&cur[id], 1u);
+  perm[p] = (uint32_t)r;
+  gs[p] = id;
+}
+
 // the first and last target of every tile
 __global__ void k_rlist_bounds(const uint64_t *doff, uint64_t nc, uint64_t ER, uint64_t ntiles, uint64_t *rb) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -436,6 +459,18 @@ void launch_rank_words(const uint32_t *ub, uint64_t U, uint64_t nwords, uint4 *r
   if (!nwords) return;
   hipLaunchKernelGGL(k_rank_words, dim3(nblocks(nwords, 256)), dim3(256), 0, s, ub, U, nwords, rw);
   KCHECK("k_rank_words");
+}
+
+void launch_row_rank(const uint4 *rw, const uint32_t *src, uint64_t R, uint32_t *g, uint32_t *cnt, hipStream_t s) {
+  if (!R) return;
+  hipLaunchKernelGGL(k_row_rank, dim3(nblocks(R, 256)), dim3(256), 0, s, rw, src, R, g, cnt);
+  KCHECK("k_row_rank");
+}
+
+void launch_row_place(const uint32_t *g, uint64_t R, uint32_t *cur, uint32_t *perm, uint32_t *gs, hipStream_t s) {
+  if (!R) return;
+  hipLaunchKernelGGL(k_row_place, dim3(nblocks(R, 256)), dim3(256), 0, s, g, R, cur, perm, gs);
+  KCHECK("k_row_place");
 }
 
 void launch_rlist(RListArgs &a, bool count, int cus, hipStream_t s) {
