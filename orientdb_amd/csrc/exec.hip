@@ -1903,7 +1903,7 @@ class Executor {
   bool expand_factorized_rev(const Step &st, bool write, const std::vector<int> &cols, uint64_t R, uint64_t U,
                              DBuf<uint32_t> &ub, DBuf<uint32_t> &g, DBuf<uint32_t> &perm_s, bool presort, bool femit,
                              const DBuf<uint32_t> &tl, uint64_t nct, const DBuf<uint64_t> &tdoff, uint64_t ER,
-                             const AdjSpec &rs, DBuf<uint4> &rw) {
+                             const AdjSpec &rs, DBuf<uint4> &rw, bool dedup) {
     const uint64_t nwords = ((uint64_t)g_.V + 63) / 64;
     if (!rw.p) {
       rw = DBuf<uint4>(&pool_, std::max<uint64_t>(nwords, 1));
@@ -1930,7 +1930,7 @@ class Executor {
     ra_.eidx = eidx.p;
     ra_.cnt = h32.p;
     tm_.begin("k_rlist_count");
-    launch_rlist(ra_, true, cus(), s_);
+    launch_rlist(ra_, true, dedup, cus(), s_);
     // per in-entry its col word, its rank word, its source index; per target its offsets and row pointer
     tm_.end(ER * (4ull + 16ull + 4ull) + nct * 28ull);
     edges_iter_ += ER;
@@ -1950,7 +1950,7 @@ class Executor {
       ra_.cnt = cur.p;
       ra_.lcol = lcol.p;
       tm_.begin("k_rlist_place");
-      launch_rlist(ra_, false, cus(), s_);
+      launch_rlist(ra_, false, false, cus(), s_);
       tm_.end(ER * 4ull + nct * 12ull);  // amended with the placed entries once known
       rlist_rec_ = tm_.last();
       nct_rec_ = nct;
@@ -2012,9 +2012,10 @@ class Executor {
     }
     const bool nbset = st.distinct_nb && !st.adj.dup_free;
     // the targets' side (below): the targets' list and in-degrees, scanned beside the sources' degrees
-    const bool rev_ok = rlist_ && !nbset && !dist_ && st.adj.parts.size() == 1 && U > 0;
     AdjSpec rs = st.adj;
-    if (rev_ok) rs.parts[0].second ^= 1;
+    if (st.adj.parts.size() == 1) rs.parts[0].second ^= 1;
+    // (a set-valued hop over parallel edges: the sorted in-lists hold a pair's entries side by side)
+    const bool rev_ok = rlist_ && !dist_ && st.adj.parts.size() == 1 && U > 0 && (!nbset || make_adj(rs).sorted);
     uint64_t nct = 0;
     DBuf<uint32_t> tl;
     DBuf<uint64_t> tdoff;
@@ -2049,7 +2050,7 @@ class Executor {
       std::fprintf(stderr, "[omx factorized] R=%llu U=%llu Et=%llu EU=%llu targets' in-entries=%lld -> %s side\n",
                    (unsigned long long)R, (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU,
                    rev_ok ? (long long)ER : -1ll, rev ? "targets'" : "sources'");
-    if (rev) return expand_factorized_rev(st, write, cols, R, U, ub, g, perm_s, presort, femit, tl, nct, tdoff, ER, rs, rw);
+    if (rev) return expand_factorized_rev(st, write, cols, R, U, ub, g, perm_s, presort, femit, tl, nct, tdoff, ER, rs, rw, nbset);
     // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
     // (presorted rows have theirs from the runs)
     DBuf<uint32_t> iu(&pool_, std::max<uint64_t>(U, 1));

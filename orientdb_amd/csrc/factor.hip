@@ -95,7 +95,9 @@ __global__ void k_rlist_bounds(const uint64_t *doff, uint64_t nc, uint64_t ER, u
 // COUNT: eidx[e] = the source index of entry e (~0u: not a distinct source), cnt[index] += 1.
 // !COUNT: lcol[cnt[eidx[e]]++] = the entry's target. A tile over more than kRlRows targets (a run of
 // in-degree-0/1 targets) searches the global offsets instead of staging.
-template <bool COUNT>
+// DEDUP (a set-valued hop, sorted in-lists): an entry equal to its predecessor in its target's in-list
+// (a parallel edge) is skipped, so every (source, target) pair is listed once.
+template <bool COUNT, bool DEDUP>
 __global__ __launch_bounds__(kRlB) void k_rlist_tile(RListArgs a) {
   constexpr int W = kRlB / 64;
   __shared__ uint64_t s_base[kRlRows];  // COUNT: col position of a target's entry e, minus e
@@ -153,19 +155,24 @@ __global__ __launch_bounds__(kRlB) void k_rlist_tile(RListArgs a) {
     __syncthreads();
     if (COUNT) {
       // every step's col word requested, then every rank word, before any is consumed
-      uint32_t x[kRlSteps];
+      uint32_t x[kRlSteps], px[DEDUP ? kRlSteps : 1];
 #pragma unroll
       for (int k = 0; k < kRlSteps; ++k) {
         const uint32_t jl = (uint32_t)k * kRlB + tid;
-        const uint64_t e = t0 + (jl < ne ? jl : 0);
+        const uint32_t jc = jl < ne ? jl : 0;
+        const uint64_t e = t0 + jc;
         uint64_t pos;
+        bool first;  // the first entry of its target's in-list
         if (staged) {
-          pos = s_base[s_seg[jl < ne ? jl : 0]] + e;
+          pos = s_base[s_seg[jc]] + e;
+          first = jc == 0 ? a.doff[r0] == t0 : s_seg[jc - 1] != s_seg[jc];
         } else {
           const uint64_t r = last_le_range(a.doff, r0, r0 + nr - 1, e);
           pos = a.rp[a.tv[r]] + (e - a.doff[r]);
+          first = a.doff[r] == e;
         }
         x[k] = a.col[pos];
+        if (DEDUP) px[k] = first ? ~x[k] : a.col[pos - (first ? 0 : 1)];
       }
       uint4 q[kRlSteps];
 #pragma unroll
@@ -177,7 +184,7 @@ __global__ __launch_bounds__(kRlB) void k_rlist_tile(RListArgs a) {
         const uint64_t bits = ((uint64_t)q[k].y << 32) | q[k].x;
         const uint32_t b = x[k] & 63u;
         uint32_t id = ~0u;
-        if ((bits >> b) & 1ull) {
+        if ((bits >> b) & 1ull && (!DEDUP || px[k] != x[k])) {
           id = q[k].z + (uint32_t)__popcll(bits & ((1ull << b) - 1ull));
           atomicAdd(&a.cnt[id], 1u);
         }
@@ -473,7 +480,7 @@ void launch_row_place(const uint32_t *g, uint64_t R, uint32_t *cur, uint32_t *pe
   KCHECK("k_row_place");
 }
 
-void launch_rlist(RListArgs &a, bool count, int cus, hipStream_t s) {
+void launch_rlist(RListArgs &a, bool count, bool dedup, int cus, hipStream_t s) {
   const uint64_t nt = rlist_tiles(a.ER);
   if (!nt || !a.nc) return;
   if (count) {
@@ -482,8 +489,9 @@ void launch_rlist(RListArgs &a, bool count, int cus, hipStream_t s) {
     KCHECK("k_rlist_bounds");
   }
   const dim3 grid((unsigned)std::min<uint64_t>(nt, (uint64_t)cus * 8)), blk(kRlB);
-  if (count) hipLaunchKernelGGL(k_rlist_tile<true>, grid, blk, 0, s, a);
-  else hipLaunchKernelGGL(k_rlist_tile<false>, grid, blk, 0, s, a);
+  if (count && dedup) hipLaunchKernelGGL((k_rlist_tile<true, true>), grid, blk, 0, s, a);
+  else if (count) hipLaunchKernelGGL((k_rlist_tile<true, false>), grid, blk, 0, s, a);
+  else hipLaunchKernelGGL((k_rlist_tile<false, false>), grid, blk, 0, s, a);
   KCHECK("k_rlist_tile");
 }
 

@@ -299,7 +299,8 @@ struct RListArgs {
 uint64_t rlist_tiles(uint64_t ER);
 // rw[w] = {bits of the sources in [64w, 64w+64) (lo, hi), sources below 64w, 0}; ub ascending, distinct
 void launch_rank_words(const uint32_t *ub, uint64_t U, uint64_t nwords, uint4 *rw, hipStream_t s);
-void launch_rlist(RListArgs &a, bool count, int cus, hipStream_t s);
+// dedup (COUNT pass, sorted in-lists): a parallel edge's repeated in-entry is not listed
+void launch_rlist(RListArgs &a, bool count, bool dedup, int cus, hipStream_t s);
 // g[r] = index of src[r] among the distinct sources (rank words rw), cnt[g[r]] += 1 (cnt zeroed)
 void launch_row_rank(const uint4 *rw, const uint32_t *src, uint64_t R, uint32_t *g, uint32_t *cnt, hipStream_t s);
 // every row at its group's cursor (cur = the exclusive scan of cnt): perm[p] = r, gs[p] = g[r]

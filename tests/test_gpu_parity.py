@@ -418,7 +418,9 @@ def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, side, monkeypatch)
     assert direct.info["factorized_hops"] == 0
     assert rs.info["edges_traversed"] == direct.info["edges_traversed"]
     assert rs.info["bindings"] == direct.info["bindings"]
-    if side == "targets" and q[0] in ("c2_both_ends", "c1_abc", "in_dir", "three_hop"):
+    # (on the multigraph a set-valued hop's parallel edges are side by side in the sorted in-lists: the
+    # count pass lists each (source, target) pair once)
+    if side == "targets" and q[0] in ("c2_both_ends", "in_dir", "three_hop"):
         t = o.OMatchStatement(q[1]).execute(g, documents=False, flags=o.OMX_FLAG_KERNEL_TIMING)
         assert any(k["name"] == "k_rlist_place" for k in t.kernel_stats)
 
