@@ -329,12 +329,13 @@ class Executor {
     uint64_t n = 0;
     int ncols = 0;
     std::vector<DBuf<uint32_t>> out;
-    // partitioned + distinct projection: equal tuples meet on one rank first
-    if (dist_ && !empty && !counted_only && gather0_) {
+    // partitioned + distinct projection: equal tuples meet on one rank first (a chain's records are
+    // on rank 0 already, in their order)
+    if (dist_ && !chain && !empty && !counted_only && gather0_) {
       pre_rank0_distinct();
       route_rank0();
     }
-    else if (dist_ && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
+    else if (dist_ && !chain && !empty && !counted_only && !p_.unique_by_construction) route_hash(p_.out_aliases);
     const bool sp_doc = p_.kind == Plan::SHORTEST_PATH && !p_.chain.expand_rows;
     const bool docs = p_.proj == Plan::PROJ_EXPR || p_.proj == Plan::PROJ_JSON || sp_doc;
     // partitioned: the lists out()/in()/both() read in RETURN expressions, from the vertices' owners
