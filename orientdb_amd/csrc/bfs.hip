@@ -163,28 +163,34 @@ void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsig
   KCHECK("k_bfs_list");
 }
 
-// the frontier vertices that are not hubs (hub_bm: V bits), listed for a push beside a hubs-only pull;
-// one atomic per block
-__global__ __launch_bounds__(kB) void k_bfs_list_nonhub(const uint64_t *frontier, const uint64_t *hub_bm, uint32_t V,
+// the frontier vertices that are not hubs, listed for a push beside a hubs-only pull: one thread per
+// 64-vertex word of the frontier bitmap (fbm & ~hub_bm, 2 MB each at RMAT-24 instead of the V·8-B
+// masks), one atomic per block (a block per 256 vertices made 65 K atomics on one counter: 0.78 ms)
+__global__ __launch_bounds__(kB) void k_bfs_list_nonhub(const uint64_t *fbm, const uint64_t *hub_bm, uint32_t V,
                                                         uint32_t *list, unsigned long long *count) {
   __shared__ uint32_t s_w[kB / 64];
   __shared__ uint32_t s_base;
-  for (uint64_t b0 = (uint64_t)blockIdx.x * kB; b0 < V; b0 += (uint64_t)gridDim.x * kB) {
-    const uint64_t v = b0 + threadIdx.x;
-    const bool keep = v < V && frontier[v] != 0 && !bm_test(hub_bm, (uint32_t)v);
+  const uint64_t nw = ((uint64_t)V + 63) / 64;
+  for (uint64_t w0 = (uint64_t)blockIdx.x * kB; w0 < nw; w0 += (uint64_t)gridDim.x * kB) {
+    const uint64_t w = w0 + threadIdx.x;
+    uint64_t bits = 0;
+    if (w < nw) {
+      bits = fbm[w] & ~hub_bm[w];
+      if (w == nw - 1 && (V & 63u)) bits &= (1ull << (V & 63u)) - 1ull;
+    }
     uint32_t tot;
-    const uint32_t off = block_excl_scan<kB>(keep ? 1u : 0u, s_w, &tot);
+    uint32_t off = block_excl_scan<kB>((uint32_t)__popcll(bits), s_w, &tot);
     if (threadIdx.x == 0 && tot) s_base = (uint32_t)atomicAdd(count, (unsigned long long)tot);
     __syncthreads();
-    if (keep) list[s_base + off] = (uint32_t)v;
+    for (; bits; bits &= bits - 1) list[s_base + off++] = (uint32_t)(w * 64 + __builtin_ctzll(bits));
     __syncthreads();
   }
 }
-void launch_bfs_list_nonhub(const uint64_t *frontier, const uint64_t *hub_bm, uint32_t V, uint32_t *list,
+void launch_bfs_list_nonhub(const uint64_t *fbm, const uint64_t *hub_bm, uint32_t V, uint32_t *list,
                             unsigned long long *count, int cus, hipStream_t s) {
   if (!V) return;
-  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V, kB), (uint64_t)cus * 8);
-  hipLaunchKernelGGL(k_bfs_list_nonhub, dim3(g), dim3(kB), 0, s, frontier, hub_bm, V, list, count);
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(((uint64_t)V + 63) / 64, kB), (uint64_t)cus * 8);
+  hipLaunchKernelGGL(k_bfs_list_nonhub, dim3(g), dim3(kB), 0, s, fbm, hub_bm, V, list, count);
   KCHECK("k_bfs_list_nonhub");
 }
 

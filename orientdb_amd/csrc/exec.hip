@@ -575,12 +575,6 @@ class Executor {
     const uint64_t *w = wait_mail();
     return {w[0], w[1]};
   }
-  // three u64 words in one host round trip
-  std::array<uint64_t, 3> read3(const uint64_t *dptr) {
-    launch_post_words(dptr, 3, mail(), s_, 8);
-    const uint64_t *w = wait_mail();
-    return {w[0], w[1], w[2]};
-  }
   template <class T>
   T read1(const T *dptr) {
     static_assert(sizeof(T) == 4 || sizeof(T) == 8, "read1 reads one 4- or 8-byte word");
@@ -1794,14 +1788,14 @@ class Executor {
   // perm_sorted: the rows sorted by source (g in that order); perm_sorted[i] = the row at sorted
   // position i. nlist: the entries of all U lists (each read from HBM once, then from L2 by its rows)
   void emit_factorized(DBuf<uint32_t> &g, uint64_t R, uint64_t U, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol,
-                       uint64_t nlist /* UINT64_MAX: read from loff[U] */, const std::vector<int> &cols, const Step &st, const uint32_t *perm_sorted) {
+                       uint64_t nlist, const std::vector<int> &cols, const Step &st, const uint32_t *perm_sorted) {
     // 1. the rows whose list is not empty (the others write nothing), in row order or grouped by source.
     // Their count Rn stays on the device until the output size N is known: the kernels in between run
     // over R rows and read Rn, so one host round trip returns both
     DBuf<uint64_t> len(&pool_, R + 1);
     launch_femit_len(g.p, R, loff.p, len.p, s_);
     DBuf<uint32_t> idx(&pool_, R);
-    DBuf<uint64_t> nsel(&pool_, 3);
+    DBuf<uint64_t> nsel(&pool_, 2);
     {
       hipcub::CountingInputIterator<uint32_t> cnt(0);
       hipcub::TransformInputIterator<uint8_t, NonZeroU64, const uint64_t *> fl(len.p, NonZeroU64());
@@ -1824,17 +1818,8 @@ class Executor {
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, len.p, roff.p, (int64_t)(R + 1), s_); });
     launch_femit_base(gs.p, R, loff.p, roff.p, rbase.p, s_, rn);
     HIP_CHECK(hipMemcpyAsync(nsel.p + 1, roff.p + R, 8, hipMemcpyDeviceToDevice, s_));
-    uint64_t Rn = 0, N = 0;
-    if (nlist == UINT64_MAX) {  // the lists' total from the device too (lists from the targets' side)
-      HIP_CHECK(hipMemcpyAsync(nsel.p + 2, loff.p + U, 8, hipMemcpyDeviceToDevice, s_));
-      const auto w = read3(nsel.p);
-      Rn = w[0], N = w[1], nlist = w[2];
-      if (rlist_rec_ != SIZE_MAX) tm_.amend_at(rlist_rec_, nlist * 8ull + nct_rec_ * 12ull + 4ull * er_rec_);
-      rlist_rec_ = SIZE_MAX;
-    } else {
-      const auto rn_n = read2(nsel.p);
-      Rn = rn_n.first, N = rn_n.second;
-    }
+    const auto rn_n = read2(nsel.p);
+    const uint64_t Rn = rn_n.first, N = rn_n.second;
     edges_iter_ += N;
     alg_bytes_ += 8ull * R + 4ull * N * (cols.size() + 2);  // as expand_core's unfiltered written hop
     R_ = N;
@@ -1911,62 +1896,62 @@ class Executor {
       launch_rank_words(ub.p, U, nwords, rw.p, s_);
     }
     if (!presort) {  // the rows' source indices: the rank of their source among ub
-      DBuf<uint32_t> unused(&pool_, U + 1);
       g = DBuf<uint32_t>(&pool_, R);
-      launch_row_rank(rw.p, col_[st.src].p, R, g.p, unused.p, s_);
+      launch_row_rank(rw.p, col_[st.src].p, R, g.p, s_);
     }
     const DAdj ra = make_adj(rs);
-    DBuf<uint32_t> h32(&pool_, U + 1), eidx(&pool_, std::max<uint64_t>(ER, 1));
-    DBuf<uint64_t> rb(&pool_, 2 * rlist_tiles(ER) + 2), loff(&pool_, U + 1);
-    HIP_CHECK(hipMemsetAsync(h32.p, 0, (U + 1) * 4, s_));
-    RListArgs ra_{};
-    ra_.doff = tdoff.p;
-    ra_.tv = tl.p;
-    ra_.rp = ra.p[0].rp;
-    ra_.col = ra.p[0].col;
-    ra_.rb = rb.p;
-    ra_.rw = rw.p;
-    ra_.nc = nct;
-    ra_.ER = ER;
-    ra_.eidx = eidx.p;
-    ra_.cnt = h32.p;
+    const uint64_t nt = rlist_tiles(ER);
+    DBuf<uint32_t> eidx(&pool_, std::max<uint64_t>(ER, 1)), tcnt(&pool_, nt + 1);
+    DBuf<uint64_t> rb(&pool_, 2 * nt + 2), toff(&pool_, nt + 1), loff(&pool_, U + 1);
+    HIP_CHECK(hipMemsetAsync(tcnt.p + nt, 0, 4, s_));
+    RListArgs a{};
+    a.doff = tdoff.p;
+    a.tv = tl.p;
+    a.rp = ra.p[0].rp;
+    a.col = ra.p[0].col;
+    a.rb = rb.p;
+    a.rw = rw.p;
+    a.nc = nct;
+    a.ER = ER;
+    a.eidx = eidx.p;
+    a.tcnt = tcnt.p;
+    a.toff = toff.p;
     tm_.begin("k_rlist_count");
-    launch_rlist(ra_, true, dedup, cus(), s_);
+    launch_rlist(a, true, dedup, cus(), s_);
     // per in-entry its col word, its rank word, its source index; per target its offsets and row pointer
     tm_.end(ER * (4ull + 16ull + 4ull) + nct * 28ull);
     edges_iter_ += ER;
     {
-      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> hc(h32.p, CastU64());
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, hc, loff.p, (int64_t)(U + 1), s_); });
+      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> tc(tcnt.p, CastU64());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tc, toff.p, (int64_t)(nt + 1), s_); });
     }
+    const uint64_t np = read1(toff.p + nt);
+    DBuf<uint32_t> pid(&pool_, std::max<uint64_t>(np, 1)), pc(&pool_, std::max<uint64_t>(np, 1));
+    a.pid = pid.p;
+    a.pc = pc.p;
+    tm_.begin("k_rlist_place");
+    launch_rlist(a, false, false, cus(), s_);
+    tm_.end(ER * 4ull + nct * 12ull + np * 8ull);
+    // grouped by source index: a radix sort of the pairs, the offsets by a search per source
+    DBuf<uint32_t> sk(&pool_, std::max<uint64_t>(np, 1)), lcol(&pool_, std::max<uint64_t>(np, 1));
+    const int kb = std::max(1, bits_for(U));
+    tm_.begin("rlist_sort");
+    cub([&](void *t, size_t &b) {
+      return hipcub::DeviceRadixSort::SortPairs(t, b, pid.p, sk.p, pc.p, lcol.p, (int64_t)np, 0, kb, s_);
+    });
+    tm_.end(16ull * np * ((kb + 7) / 8));
+    launch_group_offsets(sk.p, np, U, loff.p, s_);
     if (write && semi_) {
       semi_join(g, R, loff, cols);
       return true;
     }
-    // the lists' total stays on the device (the emission reads it with its own counts)
-    DBuf<uint32_t> lcol(&pool_, std::max<uint64_t>(ER, 1));
-    {
-      DBuf<uint32_t> cur(&pool_, U + 1);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, h32.p, cur.p, (int64_t)(U + 1), s_); });
-      ra_.cnt = cur.p;
-      ra_.lcol = lcol.p;
-      tm_.begin("k_rlist_place");
-      launch_rlist(ra_, false, false, cus(), s_);
-      tm_.end(ER * 4ull + nct * 12ull);  // amended with the placed entries once known
-      rlist_rec_ = tm_.last();
-      nct_rec_ = nct;
-      er_rec_ = ER;
-    }
     if (femit) {
-      emit_factorized(g, R, U, loff, lcol, UINT64_MAX, cols, st, perm_s.p);
+      emit_factorized(g, R, U, loff, lcol, np, cols, st, perm_s.p);
       return true;
     }
     DBuf<uint32_t> rowsrc = std::move(g);
-    return expand_over_lists(st, write, cols, R, U, rowsrc, loff, lcol, UINT64_MAX);
+    return expand_over_lists(st, write, cols, R, U, rowsrc, loff, lcol, np);
   }
-  // the placement pass's timer record, its targets and in-entries (amended in emit_factorized)
-  size_t rlist_rec_ = SIZE_MAX;
-  uint64_t nct_rec_ = 0, er_rec_ = 0;
 
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
@@ -1981,28 +1966,29 @@ class Executor {
     // wants them grouped), so the distinct sources are the sorted runs' heads and a row's source index
     // is its run — no bitmap, position map or second sort
     const bool presort = femit && R > 0;
-    DBuf<uint4> rw;  // rank words of the distinct sources (grouped rows, lists from the targets' side)
-    const uint64_t nrw = ((uint64_t)g_.V + 63) / 64;
+    DBuf<uint4> rw;  // rank words of the distinct sources (the lists from the targets' side)
     if (presort) {
-      // grouped by a counting sort over the source indices (the index of a row's source is its rank in
-      // the source bitmap): ≈ 0.1 ms less than a radix sort of the rows by source at M1
-      ubm = DBuf<uint64_t>(&pool_, std::max<uint64_t>(nwords_, 1));
-      HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
-      tm_.begin("k_mark_bitmap");
-      launch_mark_bitmap(src, R, ubm.p, g_.V, s_);
-      tm_.end(4ull * R + 8ull * nwords_);
-      ub = bitmap_list(ubm.p, 0, 1, U);
-      rw = DBuf<uint4>(&pool_, std::max<uint64_t>(nrw, 1));
-      DBuf<uint32_t> gr(&pool_, R), cnt(&pool_, U + 1), cur(&pool_, U + 1);
-      HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 4, s_));
-      tm_.begin("femit_row_group");
-      launch_rank_words(ub.p, U, nrw, rw.p, s_);
-      launch_row_rank(rw.p, src, R, gr.p, cnt.p, s_);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, cur.p, (int64_t)(U + 1), s_); });
+      // (a counting sort over the sources' ranks measured 0.34 ms against this sort's 0.17: its cursor
+      // atomics land on random counters at the memory side)
+      DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
+      DBuf<uint8_t> head(&pool_, R);
+      DBuf<uint64_t> nsel(&pool_, 1);
       perm_s = DBuf<uint32_t>(&pool_, R);
+      ub = DBuf<uint32_t>(&pool_, R);
       g = DBuf<uint32_t>(&pool_, R);
-      launch_row_place(gr.p, R, cur.p, perm_s.p, g.p, s_);
-      tm_.end(16ull * nrw + 4ull * U + R * (4ull + 16ull + 4ull) + R * (4ull + 8ull));
+      launch_iota(iota.p, R, s_);
+      tm_.begin("femit_row_sort");
+      cub([&](void *t, size_t &b) {
+        return hipcub::DeviceRadixSort::SortPairs(t, b, src, ss.p, iota.p, perm_s.p, (int64_t)R, 0,
+                                                  std::max(1, bits_for(g_.V)), s_);
+      });
+      tm_.end(16ull * R * ((bits_for(g_.V) + 7) / 8));
+      launch_run_heads(ss.p, R, head.p, s_);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, ss.p, head.p, ub.p, nsel.p, (int64_t)R, s_); });
+      hipcub::TransformInputIterator<uint32_t, CastU8U32, const uint8_t *> hc(head.p, CastU8U32());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, hc, g.p, (int64_t)R, s_); });
+      launch_add_u32(g.p, R, -1, s_);
+      U = read1(nsel.p);
     } else {
       ubm = DBuf<uint64_t>(&pool_, std::max<uint64_t>(nwords_, 1));
       HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
@@ -2144,8 +2130,8 @@ class Executor {
     R_ = o.n;
     factorized_hops_++;
     if (debug_expand_)
-      std::fprintf(stderr, "[omx factorized] R=%llu U=%llu lists=%lld rows=%llu\n", (unsigned long long)R,
-                   (unsigned long long)U, nlist == UINT64_MAX ? -1ll : (long long)nlist, (unsigned long long)o.n);
+      std::fprintf(stderr, "[omx factorized] R=%llu U=%llu lists=%llu rows=%llu\n", (unsigned long long)R,
+                   (unsigned long long)U, (unsigned long long)nlist, (unsigned long long)o.n);
     if (!write || R_ == 0) return true;
     segmented_ = false;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
@@ -3241,7 +3227,7 @@ class Executor {
             // no memory access instead of a frontier-bitmap probe — and the few non-hub frontier vertices push
             // their out-edges instead (OMX_HUB_PUSH=0: the probing pull for every entry)
             bool hubs_only = false;
-            if (probe && pull_wave_ && hub_push_ && pull_nh[p] > 0) {
+            if (probe && !dist_ && pull_wave_ && hub_push_ && pull_nh[p] > 0) {  // (fbm: one GPU)
               if (!hub_bm[p].p) {  // the part's hubs as a V-bit set (once per traversal)
                 hub_bm[p] = DBuf<uint64_t>(&pool_, std::max<uint64_t>(nwords_, 1));
                 HIP_CHECK(hipMemsetAsync(hub_bm[p].p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
@@ -3251,8 +3237,8 @@ class Executor {
               DBuf<unsigned long long> nc(&pool_, 1);
               HIP_CHECK(hipMemsetAsync(nc.p, 0, sizeof(unsigned long long), s_));
               tm_.begin("k_bfs_list");
-              launch_bfs_list_nonhub(fr.p, hub_bm[p].p, V, list.p, nc.p, cus(), s_);
-              tm_.end(8ull * V + V / 8);
+              launch_bfs_list_nonhub(fbm.p, hub_bm[p].p, V, list.p, nc.p, cus(), s_);
+              tm_.end(V / 4);
               const uint64_t nn = read1(reinterpret_cast<const uint64_t *>(nc.p));
               DBuf<uint64_t> deg(&pool_, nn + 1), loffs(&pool_, nn + 1);
               launch_bfs_list_deg(list.p, nn, adj.p[p].rp, deg.p, s_);

@@ -293,18 +293,19 @@ struct RListArgs {
   const uint4 *rw;       // rank words of the distinct sources (launch_rank_words)
   uint64_t nc, ER;
   uint32_t *eidx;        // [ER] source index of every entry (~0u: none); COUNT writes, placement reads
-  uint32_t *cnt;         // COUNT: per-source entry counts (zeroed); placement: cursors (their exclusive scan)
-  uint32_t *lcol;        // placement: the lists
+  uint32_t *tcnt;        // [tiles] COUNT: the tiles' listed entries
+  const uint64_t *toff;  // [tiles+1] their exclusive scan
+  uint32_t *pid, *pc;    // placement: the (source index, target) pairs, compacted per tile
 };
 uint64_t rlist_tiles(uint64_t ER);
+// loff[u] = first position of key u in keys[0, n) (ascending), u ≤ U
+void launch_group_offsets(const uint32_t *keys, uint64_t n, uint64_t U, uint64_t *loff, hipStream_t s);
 // rw[w] = {bits of the sources in [64w, 64w+64) (lo, hi), sources below 64w, 0}; ub ascending, distinct
 void launch_rank_words(const uint32_t *ub, uint64_t U, uint64_t nwords, uint4 *rw, hipStream_t s);
 // dedup (COUNT pass, sorted in-lists): a parallel edge's repeated in-entry is not listed
 void launch_rlist(RListArgs &a, bool count, bool dedup, int cus, hipStream_t s);
-// g[r] = index of src[r] among the distinct sources (rank words rw), cnt[g[r]] += 1 (cnt zeroed)
-void launch_row_rank(const uint4 *rw, const uint32_t *src, uint64_t R, uint32_t *g, uint32_t *cnt, hipStream_t s);
-// every row at its group's cursor (cur = the exclusive scan of cnt): perm[p] = r, gs[p] = g[r]
-void launch_row_place(const uint32_t *g, uint64_t R, uint32_t *cur, uint32_t *perm, uint32_t *gs, hipStream_t s);
+// g[r] = index of src[r] among the distinct sources (rank words rw)
+void launch_row_rank(const uint4 *rw, const uint32_t *src, uint64_t R, uint32_t *g, hipStream_t s);
 // len[r] = |L(g[r])| for r < R, len[R] = 0
 // nd: a device row count ≤ R (rows past it: length 0, no base); nullptr: all R rows
 void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s,
@@ -382,7 +383,7 @@ void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsig
                      hipStream_t s);
 void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg, hipStream_t s);
 // frontier vertices not in hub_bm (a sparse level's push beside a hubs-only pull)
-void launch_bfs_list_nonhub(const uint64_t *frontier, const uint64_t *hub_bm, uint32_t V, uint32_t *list,
+void launch_bfs_list_nonhub(const uint64_t *fbm, const uint64_t *hub_bm, uint32_t V, uint32_t *list,
                             unsigned long long *count, int cus, hipStream_t s);
 // partitioned sparse levels: list[i] (relative to vlo) → the vertex and its mask split into two words; and
 // fr[v[i]] = the mask on the receiving rank
