@@ -13,7 +13,6 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
-#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -238,8 +237,6 @@ class Executor {
     if (const char *fm = std::getenv("OMX_FEMIT_MIN_ET")) femit_min_et_ = std::strtoull(fm, nullptr, 10);
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
     if (const char *sj = std::getenv("OMX_SEMI")) semi_ok_ = std::strcmp(sj, "0") != 0;
-    if (const char *rl = std::getenv("OMX_RLIST")) rlist_ = std::strcmp(rl, "force") == 0 ? 2 : std::strcmp(rl, "0") != 0 ? 1 : 0;
-    if (const char *rr = std::getenv("OMX_RLIST_RATIO")) rlist_ratio_ = std::strtoull(rr, nullptr, 10);
     if (const char *gq = std::getenv("OMX_GRP32")) grp32_ = std::strcmp(gq, "0") != 0;
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
     if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
@@ -1736,11 +1733,6 @@ class Executor {
   // (profiles/r03/femit/c2ab.txt)
   int femit_ = 1;
   uint64_t femit_min_et_ = 4000000000ull;
-  // OMX_RLIST: 1 = the lists from the targets' side (factor.hip k_rlist_tile) when the targets' in-entries
-  // are fewer than 1/rlist_ratio_ of the sources' entries (OMX_RLIST_RATIO), force = whenever it applies
-  // (tests), 0 = never
-  int rlist_ = 1;
-  uint64_t rlist_ratio_ = 3;
   bool femit_slow_ = false;  // OMX_FEMIT_SLOW=1: every output tile through k_femit_slow (tests)
 
   // step 4 of expand_factorized when the rows are written: the output space Σ_rows |L(g[r])| is laid out
@@ -1883,76 +1875,6 @@ class Executor {
                                            : alg);
   }
 
-  // steps 2-4 of expand_factorized with the lists from the targets' side (factor.hip k_rlist_tile): the
-  // targets tl (the hop's filter bitmap, ascending) and their in-entries' offsets tdoff over the reversed
-  // adjacency rs; the distinct sources ub ascending, g the rows' source indices
-  bool expand_factorized_rev(const Step &st, bool write, const std::vector<int> &cols, uint64_t R, uint64_t U,
-                             DBuf<uint32_t> &ub, DBuf<uint32_t> &g, DBuf<uint32_t> &perm_s, bool presort, bool femit,
-                             const DBuf<uint32_t> &tl, uint64_t nct, const DBuf<uint64_t> &tdoff, uint64_t ER,
-                             const AdjSpec &rs, DBuf<uint4> &rw, bool dedup) {
-    const uint64_t nwords = ((uint64_t)g_.V + 63) / 64;
-    if (!rw.p) {
-      rw = DBuf<uint4>(&pool_, std::max<uint64_t>(nwords, 1));
-      launch_rank_words(ub.p, U, nwords, rw.p, s_);
-    }
-    if (!presort) {  // the rows' source indices: the rank of their source among ub
-      g = DBuf<uint32_t>(&pool_, R);
-      launch_row_rank(rw.p, col_[st.src].p, R, g.p, s_);
-    }
-    const DAdj ra = make_adj(rs);
-    const uint64_t nt = rlist_tiles(ER);
-    DBuf<uint32_t> eidx(&pool_, std::max<uint64_t>(ER, 1)), tcnt(&pool_, nt + 1);
-    DBuf<uint64_t> rb(&pool_, 2 * nt + 2), toff(&pool_, nt + 1), loff(&pool_, U + 1);
-    HIP_CHECK(hipMemsetAsync(tcnt.p + nt, 0, 4, s_));
-    RListArgs a{};
-    a.doff = tdoff.p;
-    a.tv = tl.p;
-    a.rp = ra.p[0].rp;
-    a.col = ra.p[0].col;
-    a.rb = rb.p;
-    a.rw = rw.p;
-    a.nc = nct;
-    a.ER = ER;
-    a.eidx = eidx.p;
-    a.tcnt = tcnt.p;
-    a.toff = toff.p;
-    tm_.begin("k_rlist_count");
-    launch_rlist(a, true, dedup, cus(), s_);
-    // per in-entry its col word, its rank word, its source index; per target its offsets and row pointer
-    tm_.end(ER * (4ull + 16ull + 4ull) + nct * 28ull);
-    edges_iter_ += ER;
-    {
-      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> tc(tcnt.p, CastU64());
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tc, toff.p, (int64_t)(nt + 1), s_); });
-    }
-    const uint64_t np = read1(toff.p + nt);
-    DBuf<uint32_t> pid(&pool_, std::max<uint64_t>(np, 1)), pc(&pool_, std::max<uint64_t>(np, 1));
-    a.pid = pid.p;
-    a.pc = pc.p;
-    tm_.begin("k_rlist_place");
-    launch_rlist(a, false, false, cus(), s_);
-    tm_.end(ER * 4ull + nct * 12ull + np * 8ull);
-    // grouped by source index: a radix sort of the pairs, the offsets by a search per source
-    DBuf<uint32_t> sk(&pool_, std::max<uint64_t>(np, 1)), lcol(&pool_, std::max<uint64_t>(np, 1));
-    const int kb = std::max(1, bits_for(U));
-    tm_.begin("rlist_sort");
-    cub([&](void *t, size_t &b) {
-      return hipcub::DeviceRadixSort::SortPairs(t, b, pid.p, sk.p, pc.p, lcol.p, (int64_t)np, 0, kb, s_);
-    });
-    tm_.end(16ull * np * ((kb + 7) / 8));
-    launch_group_offsets(sk.p, np, U, loff.p, s_);
-    if (write && semi_) {
-      semi_join(g, R, loff, cols);
-      return true;
-    }
-    if (femit) {
-      emit_factorized(g, R, U, loff, lcol, np, cols, st, perm_s.p);
-      return true;
-    }
-    DBuf<uint32_t> rowsrc = std::move(g);
-    return expand_over_lists(st, write, cols, R, U, rowsrc, loff, lcol, np);
-  }
-
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
@@ -1966,10 +1888,7 @@ class Executor {
     // wants them grouped), so the distinct sources are the sorted runs' heads and a row's source index
     // is its run — no bitmap, position map or second sort
     const bool presort = femit && R > 0;
-    DBuf<uint4> rw;  // rank words of the distinct sources (the lists from the targets' side)
     if (presort) {
-      // (a counting sort over the sources' ranks measured 0.34 ms against this sort's 0.17: its cursor
-      // atomics land on random counters at the memory side)
       DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
       DBuf<uint8_t> head(&pool_, R);
       DBuf<uint64_t> nsel(&pool_, 1);
@@ -1997,47 +1916,15 @@ class Executor {
       tm_.end(4ull * R + 8ull * nwords_);
       ub = bitmap_list(ubm.p, 0, 1, U);
     }
-    const bool nbset = st.distinct_nb && !st.adj.dup_free;
-    // the targets' side (below): the targets' list and in-degrees, scanned beside the sources' degrees
-    AdjSpec rs = st.adj;
-    if (st.adj.parts.size() == 1) rs.parts[0].second ^= 1;
-    // (a set-valued hop over parallel edges: the sorted in-lists hold a pair's entries side by side)
-    const bool rev_ok = rlist_ && !dist_ && st.adj.parts.size() == 1 && U > 0 && (!nbset || make_adj(rs).sorted);
-    uint64_t nct = 0;
-    DBuf<uint32_t> tl;
-    DBuf<uint64_t> tdoff;
-    if (rev_ok) {
-      tl = bitmap_list(bitmap(st.filter_bm), 0, 1, nct);
-      DBuf<uint64_t> tdeg(&pool_, nct + 1);
-      tdoff = DBuf<uint64_t>(&pool_, nct + 1);
-      launch_row_degree(tl.p, nct, make_adj(rs), tdeg.p, s_);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tdeg.p, tdoff.p, (int64_t)(nct + 1), s_); });
-    }
     // the distinct sources' degrees, scanned
     DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1);
     tm_.begin("k_row_degree");
     launch_row_degree(ub.p, U, make_adj(st.adj), udeg.p, s_);
     tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(U + 1), s_); });
-    uint64_t EU = 0, ER = UINT64_MAX;
-    if (rev_ok) {  // both totals in one host round trip
-      DBuf<uint64_t> two(&pool_, 2);
-      HIP_CHECK(hipMemcpyAsync(two.p, doff.p + U, 8, hipMemcpyDeviceToDevice, s_));
-      HIP_CHECK(hipMemcpyAsync(two.p + 1, tdoff.p + nct, 8, hipMemcpyDeviceToDevice, s_));
-      const auto eu_er = read2(two.p);
-      EU = eu_er.first;
-      ER = eu_er.second;
-    } else {
-      EU = read1(doff.p + U);
-    }
+    const uint64_t EU = read1(doff.p + U);
     if (Et < factor_min_ratio_ * EU) return false;
     edges_ += Et;
-    const bool rev = rev_ok && ER < 0xFFFFFFFFull && (rlist_ == 2 || ER * rlist_ratio_ < EU);
-    if (debug_expand_)
-      std::fprintf(stderr, "[omx factorized] R=%llu U=%llu Et=%llu EU=%llu targets' in-entries=%lld -> %s side\n",
-                   (unsigned long long)R, (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU,
-                   rev_ok ? (long long)ER : -1ll, rev ? "targets'" : "sources'");
-    if (rev) return expand_factorized_rev(st, write, cols, R, U, ub, g, perm_s, presort, femit, tl, nct, tdoff, ER, rs, rw, nbset);
     // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
     // (presorted rows have theirs from the runs)
     DBuf<uint32_t> iu(&pool_, std::max<uint64_t>(U, 1));
@@ -2058,6 +1945,7 @@ class Executor {
     // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
     // (the filtered lists stay in the expansion's per-worker segments: grouping reads them in place)
     // (a set-valued hop over an adjacency that may repeat a neighbour: each list made distinct first)
+    const bool nbset = st.distinct_nb && !st.adj.dup_free;
     ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, !nbset);
     edges_iter_ += l.E;
     if (nbset && l.n) l.n = distinct_pairs(l.carry[0], l.dst, {}, l.n);
@@ -2111,13 +1999,6 @@ class Executor {
       emit_factorized(g, R, U, loff, lcol, nlist, cols, st, perm_s.p);
       return true;
     }
-    return expand_over_lists(st, write, cols, R, U, g, loff, lcol, nlist);
-  }
-
-  // step 4 without the factorized emission: an unfiltered expansion of the rows (source index g) over the
-  // lists (loff, lcol)
-  bool expand_over_lists(const Step &st, bool write, const std::vector<int> &cols, uint64_t R, uint64_t U,
-                         DBuf<uint32_t> &g, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol, uint64_t nlist) {
     DAdj ladj{};
     ladj.n = 1;
     ladj.sorted = 0;
@@ -2130,8 +2011,9 @@ class Executor {
     R_ = o.n;
     factorized_hops_++;
     if (debug_expand_)
-      std::fprintf(stderr, "[omx factorized] R=%llu U=%llu lists=%llu rows=%llu\n", (unsigned long long)R,
-                   (unsigned long long)U, (unsigned long long)nlist, (unsigned long long)o.n);
+      std::fprintf(stderr, "[omx factorized] R=%llu U=%llu Et=%llu EU=%llu lists=%llu rows=%llu\n", (unsigned long long)R,
+                   (unsigned long long)U, (unsigned long long)Et, (unsigned long long)EU, (unsigned long long)nlist,
+                   (unsigned long long)o.n);
     if (!write || R_ == 0) return true;
     segmented_ = false;
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);

@@ -26,199 +26,6 @@ __device__ __forceinline__ uint64_t last_le_range(const T *off, uint64_t lo, uin
   return lo;
 }
 
-// ---- the lists from the targets' side ------------------------------------------------------------------
-// L(u) = the targets c passing the hop's WHERE with an edge u → c, once per edge — and c's in-list holds u
-// once per such edge. So L is also the targets' in-entries whose neighbour is a distinct source, grouped by
-// that source: at M1 (RMAT-24, a 10 % target window) 26 M in-entries instead of the sources' 200 M
-// entries. The targets' in-entries are one flat range [0, ER) in target order (doff = the exclusive scan
-// of their in-degrees), cut into tiles of kRlTile entries; a tile's targets are staged in LDS and every
-// entry finds its target through a max-scan of the targets' first entries (no per-entry search).
-// The distinct sources are probed through rank words — per 64-vertex word the U-bitmap bits and the
-// number of sources below the word, 16 B: the bit and the source index come in one request to an
-// L2-resident 4 MB table (RMAT-24). Pass 1 (COUNT) records every entry's source index and counts each
-// tile's listed entries; pass 2 writes the (source index, target) pairs compacted per tile; a radix sort
-// by source index groups them into the lists.
-constexpr int kRlB = 256, kRlSteps = 16, kRlTile = kRlB * kRlSteps, kRlRows = 1024;
-
-// rank words of a sorted distinct source list: word w = {bits of the sources in [64w, 64w + 64), the
-// number of sources below 64w}
-__global__ void k_rank_words(const uint32_t *ub, uint64_t U, uint64_t nwords, uint4 *rw) {
-  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= nwords) return;
-  auto lower = [&](uint64_t x) {
-    uint64_t lo = 0, hi = U;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if ((uint64_t)ub[mid] < x) lo = mid + 1;
-      else hi = mid;
-    }
-    return lo;
-  };
-  const uint64_t lo = lower(w << 6), hi = lower((w + 1) << 6);
-  uint64_t bits = 0;
-  for (uint64_t i = lo; i < hi; ++i) bits |= 1ull << (ub[i] & 63u);
-  rw[w] = make_uint4((uint32_t)bits, (uint32_t)(bits >> 32), (uint32_t)lo, 0u);
-}
-
-// g[r] = the index of src[r] among the distinct sources (its rank word)
-__global__ void k_row_rank(const uint4 *rw, const uint32_t *src, uint64_t R, uint32_t *g) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  const uint32_t v = src[r];
-  const uint4 q = rw[v >> 6];
-  const uint64_t bits = ((uint64_t)q.y << 32) | q.x;
-  const uint32_t id = q.z + (uint32_t)__popcll(bits & ((1ull << (v & 63u)) - 1ull));
-  g[r] = id;
-}
-// the first and last target of every tile
-__global__ void k_rlist_bounds(const uint64_t *doff, uint64_t nc, uint64_t ER, uint64_t ntiles, uint64_t *rb) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntiles) return;
-  const uint64_t t0 = t * kRlTile, t1 = min(t0 + (uint64_t)kRlTile, ER) - 1;
-  rb[2 * t] = last_le_range(doff, 0, nc - 1, t0);
-  rb[2 * t + 1] = last_le_range(doff, rb[2 * t], nc - 1, t1);
-}
-
-// COUNT: eidx[e] = the source index of entry e (~0u: not a distinct source), tcnt[tile] = the tile's
-// listed entries. Placement: the (source index, target) pairs of tile t compacted from toff[t] (a
-// wave-aggregated LDS cursor); a radix sort by source index then groups them. (Cursor atomics per entry
-// measured 0.92 + 1.94 ms at M1: device-scope atomics run at the memory side, one 64-B request per lane
-// on random counters.) A tile over more than kRlRows targets (a run of in-degree-0/1 targets) searches
-// the global offsets instead of staging.
-// DEDUP (a set-valued hop, sorted in-lists): an entry equal to its predecessor in its target's in-list
-// (a parallel edge) is skipped, so every (source, target) pair is listed once.
-template <bool COUNT, bool DEDUP>
-__global__ __launch_bounds__(kRlB) void k_rlist_tile(RListArgs a) {
-  constexpr int W = kRlB / 64;
-  __shared__ uint32_t s_tc;
-  __shared__ uint64_t s_base[kRlRows];  // COUNT: col position of a target's entry e, minus e
-  __shared__ uint32_t s_tv[kRlRows];    // !COUNT: the target vertex
-  __shared__ uint16_t s_seg[kRlTile];   // tile-local target of every entry
-  __shared__ uint32_t s_wmax[W];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t ntiles = (a.ER + kRlTile - 1) / kRlTile;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t t0 = tile * kRlTile, t1 = min(t0 + (uint64_t)kRlTile, a.ER) - 1;
-    const uint32_t ne = (uint32_t)(t1 - t0 + 1);
-    const uint64_t r0 = a.rb[2 * tile], nr = a.rb[2 * tile + 1] - r0 + 1;
-    const bool staged = nr <= kRlRows;
-    if (staged) {
-      for (uint32_t x = tid; x < ne; x += kRlB) s_seg[x] = 0;
-      __syncthreads();
-      for (uint32_t lr = tid; lr < nr; lr += kRlB) {
-        const uint64_t rs = a.doff[r0 + lr], re = a.doff[r0 + lr + 1];
-        const uint64_t st = rs > t0 ? rs - t0 : 0;
-        if (re > rs && st < ne) s_seg[st] = (uint16_t)lr;
-        const uint32_t v = a.tv[r0 + lr];
-        if (COUNT) s_base[lr] = a.rp[v] - rs;
-        else s_tv[lr] = v;
-      }
-      __syncthreads();
-      // max-scan of the marks: thread t holds entries [t·kRlSteps, t·kRlSteps + kRlSteps)
-      uint32_t vals[kRlSteps];
-      uint32_t mx = 0;
-#pragma unroll
-      for (int i = 0; i < kRlSteps; ++i) {
-        const uint32_t idx = tid * kRlSteps + i;
-        const uint32_t v = idx < ne ? s_seg[idx] : 0;
-        mx = mx > v ? mx : v;
-        vals[i] = mx;
-      }
-      uint32_t incl = mx;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= (uint32_t)off) incl = incl > y ? incl : y;
-      }
-      if (lane == 63) s_wmax[wave] = incl;
-      uint32_t excl = __shfl_up(incl, 1, 64);
-      if (lane == 0) excl = 0;
-      __syncthreads();
-      uint32_t wp = 0;
-      for (uint32_t w = 0; w < wave; ++w) wp = wp > s_wmax[w] ? wp : s_wmax[w];
-      const uint32_t pre = excl > wp ? excl : wp;
-#pragma unroll
-      for (int i = 0; i < kRlSteps; ++i) {
-        const uint32_t idx = tid * kRlSteps + i;
-        if (idx < ne) s_seg[idx] = (uint16_t)(pre > vals[i] ? pre : vals[i]);
-      }
-    }
-    if (tid == 0) s_tc = 0;
-    __syncthreads();
-    if (COUNT) {
-      // every step's col word requested, then every rank word, before any is consumed
-      uint32_t x[kRlSteps], px[DEDUP ? kRlSteps : 1];
-#pragma unroll
-      for (int k = 0; k < kRlSteps; ++k) {
-        const uint32_t jl = (uint32_t)k * kRlB + tid;
-        const uint32_t jc = jl < ne ? jl : 0;
-        const uint64_t e = t0 + jc;
-        uint64_t pos;
-        bool first;  // the first entry of its target's in-list
-        if (staged) {
-          pos = s_base[s_seg[jc]] + e;
-          first = jc == 0 ? a.doff[r0] == t0 : s_seg[jc - 1] != s_seg[jc];
-        } else {
-          const uint64_t r = last_le_range(a.doff, r0, r0 + nr - 1, e);
-          pos = a.rp[a.tv[r]] + (e - a.doff[r]);
-          first = a.doff[r] == e;
-        }
-        x[k] = a.col[pos];
-        if (DEDUP) px[k] = first ? ~x[k] : a.col[pos - (first ? 0 : 1)];
-      }
-      uint4 q[kRlSteps];
-#pragma unroll
-      for (int k = 0; k < kRlSteps; ++k) q[k] = a.rw[x[k] >> 6];
-#pragma unroll
-      for (int k = 0; k < kRlSteps; ++k) {
-        const uint32_t jl = (uint32_t)k * kRlB + tid;
-        if (jl >= ne) continue;
-        const uint64_t bits = ((uint64_t)q[k].y << 32) | q[k].x;
-        const uint32_t b = x[k] & 63u;
-        uint32_t id = ~0u;
-        if ((bits >> b) & 1ull && (!DEDUP || px[k] != x[k])) {
-          id = q[k].z + (uint32_t)__popcll(bits & ((1ull << b) - 1ull));
-        }
-        a.eidx[t0 + jl] = id;
-        const uint64_t m = __ballot(id != ~0u);
-        if (lane == 0 && m) atomicAdd(&s_tc, (uint32_t)__popcll(m));
-      }
-      __syncthreads();
-      if (tid == 0) a.tcnt[tile] = s_tc;
-    } else {
-      uint32_t id[kRlSteps];
-#pragma unroll
-      for (int k = 0; k < kRlSteps; ++k) {
-        const uint32_t jl = (uint32_t)k * kRlB + tid;
-        id[k] = a.eidx[t0 + (jl < ne ? jl : 0)];
-      }
-      const uint64_t tb = a.toff[tile];
-#pragma unroll
-      for (int k = 0; k < kRlSteps; ++k) {
-        const uint32_t jl = (uint32_t)k * kRlB + tid;
-        const bool live = jl < ne && id[k] != ~0u;
-        const uint64_t m = __ballot(live);
-        if (!m) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&s_tc, (uint32_t)__popcll(m));
-        base = __shfl(base, 0, 64);
-        if (!live) continue;
-        uint32_t c;
-        if (staged) {
-          c = s_tv[s_seg[jl]];
-        } else {
-          const uint64_t r = last_le_range(a.doff, r0, r0 + nr - 1, t0 + jl);
-          c = a.tv[r];
-        }
-        const uint64_t o = tb + base + lane_prefix(m);
-        a.pid[o] = id[k];
-        a.pc[o] = c;
-      }
-    }
-    __syncthreads();  // the LDS tables are restaged by the next tile
-  }
-}
-
 // ---- the factorized emission: every row (…, u) written over L(u) -------------------------------------
 // The result rows of a factorized hop are Σ_rows |L(g[r])| — known before anything is written — so they
 // are laid out densely, row by row (roff = the exclusive scan of the rows' list lengths; the rows are
@@ -463,54 +270,6 @@ __global__ __launch_bounds__(256) void k_femit_slow(FemitArgs a, const uint32_t 
 }
 
 }  // namespace
-
-uint64_t rlist_tiles(uint64_t ER) { return (ER + kRlTile - 1) / kRlTile; }
-
-void launch_rank_words(const uint32_t *ub, uint64_t U, uint64_t nwords, uint4 *rw, hipStream_t s) {
-  if (!nwords) return;
-  hipLaunchKernelGGL(k_rank_words, dim3(nblocks(nwords, 256)), dim3(256), 0, s, ub, U, nwords, rw);
-  KCHECK("k_rank_words");
-}
-
-void launch_row_rank(const uint4 *rw, const uint32_t *src, uint64_t R, uint32_t *g, hipStream_t s) {
-  if (!R) return;
-  hipLaunchKernelGGL(k_row_rank, dim3(nblocks(R, 256)), dim3(256), 0, s, rw, src, R, g);
-  KCHECK("k_row_rank");
-}
-
-
-// the lists' offsets from the pairs sorted by source index: loff[u] = the first pair of source u (u ≤ U)
-__global__ void k_group_offsets(const uint32_t *keys, uint64_t n, uint64_t U, uint64_t *loff) {
-  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u > U) return;
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if ((uint64_t)keys[mid] < u) lo = mid + 1;
-    else hi = mid;
-  }
-  loff[u] = lo;
-}
-
-void launch_group_offsets(const uint32_t *keys, uint64_t n, uint64_t U, uint64_t *loff, hipStream_t s) {
-  hipLaunchKernelGGL(k_group_offsets, dim3(nblocks(U + 1, 256)), dim3(256), 0, s, keys, n, U, loff);
-  KCHECK("k_group_offsets");
-}
-
-void launch_rlist(RListArgs &a, bool count, bool dedup, int cus, hipStream_t s) {
-  const uint64_t nt = rlist_tiles(a.ER);
-  if (!nt || !a.nc) return;
-  if (count) {
-    hipLaunchKernelGGL(k_rlist_bounds, dim3(nblocks(nt, 256)), dim3(256), 0, s, a.doff, a.nc, a.ER, nt,
-                       const_cast<uint64_t *>(a.rb));
-    KCHECK("k_rlist_bounds");
-  }
-  const dim3 grid((unsigned)std::min<uint64_t>(nt, (uint64_t)cus * 8)), blk(kRlB);
-  if (count && dedup) hipLaunchKernelGGL((k_rlist_tile<true, true>), grid, blk, 0, s, a);
-  else if (count) hipLaunchKernelGGL((k_rlist_tile<true, false>), grid, blk, 0, s, a);
-  else hipLaunchKernelGGL((k_rlist_tile<false, false>), grid, blk, 0, s, a);
-  KCHECK("k_rlist_tile");
-}
 
 uint64_t femit_tiles(uint64_t N) { return (N + kEwTile - 1) / kEwTile; }
 

@@ -282,30 +282,6 @@ struct FemitArgs {
 };
 bool femit_supported(int nl, int nc);
 uint64_t femit_tiles(uint64_t N);
-// the factorized hop's lists from the targets' side (factor.hip k_rlist_tile): the targets' in-entries
-// whose neighbour is a distinct source, grouped by that source
-struct RListArgs {
-  const uint64_t *doff;  // [nc+1] exclusive scan of the targets' in-degrees
-  const uint32_t *tv;    // [nc] target vertices
-  const uint64_t *rp;    // the reversed adjacency (single part): target → in-neighbours
-  const uint32_t *col;
-  const uint64_t *rb;    // [2·rlist_tiles(ER)] first / last target of every tile (the COUNT pass writes it)
-  const uint4 *rw;       // rank words of the distinct sources (launch_rank_words)
-  uint64_t nc, ER;
-  uint32_t *eidx;        // [ER] source index of every entry (~0u: none); COUNT writes, placement reads
-  uint32_t *tcnt;        // [tiles] COUNT: the tiles' listed entries
-  const uint64_t *toff;  // [tiles+1] their exclusive scan
-  uint32_t *pid, *pc;    // placement: the (source index, target) pairs, compacted per tile
-};
-uint64_t rlist_tiles(uint64_t ER);
-// loff[u] = first position of key u in keys[0, n) (ascending), u ≤ U
-void launch_group_offsets(const uint32_t *keys, uint64_t n, uint64_t U, uint64_t *loff, hipStream_t s);
-// rw[w] = {bits of the sources in [64w, 64w+64) (lo, hi), sources below 64w, 0}; ub ascending, distinct
-void launch_rank_words(const uint32_t *ub, uint64_t U, uint64_t nwords, uint4 *rw, hipStream_t s);
-// dedup (COUNT pass, sorted in-lists): a parallel edge's repeated in-entry is not listed
-void launch_rlist(RListArgs &a, bool count, bool dedup, int cus, hipStream_t s);
-// g[r] = index of src[r] among the distinct sources (rank words rw)
-void launch_row_rank(const uint4 *rw, const uint32_t *src, uint64_t R, uint32_t *g, hipStream_t s);
 // len[r] = |L(g[r])| for r < R, len[R] = 0
 // nd: a device row count ≤ R (rows past it: length 0, no base); nullptr: all R rows
 void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s,

@@ -395,37 +395,27 @@ FACTOR_IDS = ("c2_both_ends", "c1_abc", "two_cols_dedup", "in_dir", "both_dir", 
               "paths", "elements", "fof_not_me", "matched_and_filter", "optional_free", "bound_candidate")
 
 
-@pytest.mark.parametrize("side", ["sources", "targets"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
-def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, side, monkeypatch):
+def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, monkeypatch):
     """Every filtered hop through the factorized expansion (distinct sources → filtered lists → rows
     over the lists, Executor::expand_factorized): same rows, same E_t and bindings as the direct
     expansion — on the simple graph and on the multigraph, whose parallel edges repeat a neighbour in a
     source's list (ridbag multiplicity, OSBTreeRidBag.java:292-295) through the distinct-source grouping.
-    The lists from the sources' filtered adjacency (OMX_RLIST=0) or from the targets' in-entries whose
-    neighbour is a distinct source (OMX_RLIST=force, factor.hip k_rlist_tile; a parallel edge is one
-    in-entry as it is one list entry). The rows are written by the output-tiled emission at any size
-    (OMX_FEMIT=force)."""
+    The rows are written by the output-tiled emission at any size (OMX_FEMIT=force)."""
     import orientdb_amd as o
     g, ref = rmat10 if graph == "simple" else rmat10_raw
     monkeypatch.setenv("OMX_FEMIT", "force")
     monkeypatch.setenv("OMX_FACTOR", "0")
     direct = o.OMatchStatement(q[1]).execute(g, documents=False)
     monkeypatch.setenv("OMX_FACTOR", "force")
-    monkeypatch.setenv("OMX_RLIST", "force" if side == "targets" else "0")
     rs = _parity(g, ref, q[1], q[2])
     assert direct.info["factorized_hops"] == 0
     assert rs.info["edges_traversed"] == direct.info["edges_traversed"]
     assert rs.info["bindings"] == direct.info["bindings"]
-    # (on the multigraph a set-valued hop's parallel edges are side by side in the sorted in-lists: the
-    # count pass lists each (source, target) pair once)
-    if side == "targets" and q[0] in ("c2_both_ends", "in_dir", "three_hop"):
-        t = o.OMatchStatement(q[1]).execute(g, documents=False, flags=o.OMX_FLAG_KERNEL_TIMING)
-        assert any(k["name"] == "k_rlist_place" for k in t.kernel_stats)
 
 
-@pytest.mark.parametrize("emit", ["binned", "slow", "grp64", "binned_targets"])
+@pytest.mark.parametrize("emit", ["binned", "slow", "grp64"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
 def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, monkeypatch):
@@ -443,15 +433,12 @@ def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, mon
     monkeypatch.setenv("OMX_FEMIT", "0" if emit == "binned" else "force")
     monkeypatch.setenv("OMX_FEMIT_SLOW", "1" if emit == "slow" else "0")
     monkeypatch.setenv("OMX_GRP32", "0" if emit == "grp64" else "1")
-    monkeypatch.setenv("OMX_RLIST", "force" if emit == "binned_targets" else "0")
-    if emit == "binned_targets":
-        monkeypatch.setenv("OMX_FEMIT", "0")
     rs = _parity(g, ref, q[1], q[2])
     assert rs.info["edges_traversed"] == direct.info["edges_traversed"]
     assert rs.info["bindings"] == direct.info["bindings"]
 
 
-@pytest.mark.parametrize("slow", ["0", "1", "targets"])
+@pytest.mark.parametrize("slow", ["0", "1"])
 def test_factorized_emission_many_tiles_rmat16(rmat16, slow, monkeypatch):
     """Output tiles of the factorized emission across many tiles (RMAT-16 2-hop with WHERE on both ends:
     rows spanning tile boundaries, runs of short lists in one tile, a partial last tile): rows and digest
@@ -462,12 +449,9 @@ def test_factorized_emission_many_tiles_rmat16(rmat16, slow, monkeypatch):
     monkeypatch.setenv("OMX_FACTOR", "force")
     monkeypatch.setenv("OMX_FEMIT", "0")
     fl = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST
-    monkeypatch.setenv("OMX_RLIST", "0")
     base = o.OMatchStatement(q).execute(g, documents=False, flags=fl)
-    # targets: the lists from the targets' in-entries (tiles over many targets, hub in-lists across tiles)
     monkeypatch.setenv("OMX_FEMIT", "force")
-    monkeypatch.setenv("OMX_FEMIT_SLOW", "1" if slow == "1" else "0")
-    monkeypatch.setenv("OMX_RLIST", "force" if slow == "targets" else "0")
+    monkeypatch.setenv("OMX_FEMIT_SLOW", slow)
     rs = o.OMatchStatement(q).execute(g, documents=False, flags=fl)
     assert rs.info["factorized_hops"] >= 1 and rs.info["n_rows"] > 100000
     assert rs.info["n_rows"] == base.info["n_rows"] and rs.info["digest"] == base.info["digest"]
@@ -485,10 +469,9 @@ SEMI_QUERIES = [
 ]
 
 
-@pytest.mark.parametrize("side", ["sources", "targets"])
 @pytest.mark.parametrize("graph", ["simple", "multigraph"])
 @pytest.mark.parametrize("q", SEMI_QUERIES, ids=[q[0] for q in SEMI_QUERIES])
-def test_semi_join_last_hop(rmat10, rmat10_raw, q, graph, side, monkeypatch):
+def test_semi_join_last_hop(rmat10, rmat10_raw, q, graph, monkeypatch):
     """A factorized last hop whose new alias the projection never reads is a semi-join (the rows whose
     source has a non-empty filtered list; no row per target is written): the same documents / rows as
     the oracle and as writing every row (OMX_SEMI=0), the same E_t and bindings (Σ |L(b)|, parallel edges
@@ -496,7 +479,6 @@ def test_semi_join_last_hop(rmat10, rmat10_raw, q, graph, side, monkeypatch):
     import orientdb_amd as o
     g, ref = rmat10 if graph == "simple" else rmat10_raw
     monkeypatch.setenv("OMX_FACTOR", "force")
-    monkeypatch.setenv("OMX_RLIST", "force" if side == "targets" else "0")
     monkeypatch.setenv("OMX_SEMI", "0")
     full = o.OMatchStatement(q[1]).execute(g, documents=q[2] is None)
     monkeypatch.setenv("OMX_SEMI", "1")
