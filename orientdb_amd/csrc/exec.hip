@@ -1878,17 +1878,23 @@ class Executor {
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
-    // the distinct sources, ascending: marked in a V-bit bitmap and listed (no sort of the R rows)
-    uint64_t U = 0;
+    uint64_t U = 0, Et = 0, EU = 0;
     DBuf<uint32_t> ub, g, perm_s;
     DBuf<uint64_t> ubm;
-    const uint64_t Et = degree_sum(src, R, st.adj);
-    const bool femit = write && !semi_ && femit_ && (femit_ == 2 || Et >= femit_min_et_) && cols.size() <= (size_t)kFemitCols;
+    const DAdj adj = make_adj(st.adj);
     // rows emitted by k_femit_w from the sources' lists: the rows are sorted by source here (the emission
     // wants them grouped), so the distinct sources are the sorted runs' heads and a row's source index
-    // is its run — no bitmap, position map or second sort
-    const bool presort = femit && R > 0;
-    if (presort) {
+    // is its run — no bitmap, position map or second sort. Whether the emission runs depends on E_t (its
+    // threshold), which the device computes beside the sort: E_t, the distinct sources U and their
+    // adjacency total EU come back in one host round trip (three before: 0.06-0.09 ms of idle device)
+    const bool femit_ok = write && !semi_ && femit_ && cols.size() <= (size_t)kFemitCols && R > 0 && adj.n > 0;
+    bool femit = false;
+    if (femit_ok) {
+      DBuf<uint64_t> rdeg(&pool_, R + 1), et(&pool_, 1);
+      tm_.begin("k_row_degree");
+      launch_row_degree(src, R, adj, rdeg.p, s_);
+      tm_.end(R * (4ull + 8ull * adj.n + 8ull));
+      cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, rdeg.p, et.p, (int64_t)(R + 1), s_); });
       DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
       DBuf<uint8_t> head(&pool_, R);
       DBuf<uint64_t> nsel(&pool_, 1);
@@ -1907,29 +1913,46 @@ class Executor {
       hipcub::TransformInputIterator<uint32_t, CastU8U32, const uint8_t *> hc(head.p, CastU8U32());
       cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, hc, g.p, (int64_t)R, s_); });
       launch_add_u32(g.p, R, -1, s_);
-      U = read1(nsel.p);
+      // the distinct sources' degrees over the R-row bound (rows past U count 0), scanned
+      DBuf<uint64_t> udeg(&pool_, R + 1), doff(&pool_, R + 1);
+      tm_.begin("k_row_degree");
+      launch_row_degree_dev(ub.p, nsel.p, R, adj, udeg.p, s_);
+      tm_.end(R * 8ull);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(R + 1), s_); });
+      const uint64_t *words[3] = {et.p, nsel.p, doff.p + R};
+      launch_post_ptrs(words, 3, mail(), s_);
+      const uint64_t *m = wait_mail();
+      Et = m[0], U = m[1], EU = m[2];
+      femit = femit_ == 2 || Et >= femit_min_et_;
+      if (!femit) {  // below the threshold: the rows' source indices back in row order
+        DBuf<uint32_t> gr(&pool_, R);
+        launch_scatter_u32(perm_s.p, g.p, R, gr.p, s_);
+        g = std::move(gr);
+      }
     } else {
+      Et = degree_sum(src, R, st.adj);
+      // the distinct sources, ascending: marked in a V-bit bitmap and listed (no sort of the R rows)
       ubm = DBuf<uint64_t>(&pool_, std::max<uint64_t>(nwords_, 1));
       HIP_CHECK(hipMemsetAsync(ubm.p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
       tm_.begin("k_mark_bitmap");
       launch_mark_bitmap(src, R, ubm.p, g_.V, s_);
       tm_.end(4ull * R + 8ull * nwords_);
       ub = bitmap_list(ubm.p, 0, 1, U);
+      // the distinct sources' degrees, scanned
+      DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1);
+      tm_.begin("k_row_degree");
+      launch_row_degree(ub.p, U, adj, udeg.p, s_);
+      tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(U + 1), s_); });
+      EU = read1(doff.p + U);
     }
-    // the distinct sources' degrees, scanned
-    DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1);
-    tm_.begin("k_row_degree");
-    launch_row_degree(ub.p, U, make_adj(st.adj), udeg.p, s_);
-    tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(U + 1), s_); });
-    const uint64_t EU = read1(doff.p + U);
     if (Et < factor_min_ratio_ * EU) return false;
     edges_ += Et;
     // 1. row → distinct source index: a V-sized position map scattered from the list, gathered per row
-    // (presorted rows have theirs from the runs)
+    // (sorted rows have theirs from the runs)
     DBuf<uint32_t> iu(&pool_, std::max<uint64_t>(U, 1));
     launch_iota(iu.p, U, s_);
-    if (!presort) {
+    if (!g.p) {
       g = DBuf<uint32_t>(&pool_, R);
       DBuf<uint32_t> pos(&pool_, std::max<uint64_t>(g_.V, 1));
       tm_.begin("k_scatter_u32");

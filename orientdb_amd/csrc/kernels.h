@@ -179,6 +179,9 @@ void launch_route_bounds(const uint32_t *id, uint64_t R, const uint64_t *bounds,
 void launch_add_u32(uint32_t *x, uint64_t n, int64_t delta, hipStream_t s);
 
 void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t *deg, hipStream_t s);
+// deg[r] = degree of src[r] for r < *n (a device count ≤ R), 0 for *n ≤ r ≤ R
+void launch_row_degree_dev(const uint32_t *src, const uint64_t *n, uint64_t R, const DAdj &adj, uint64_t *deg,
+                           hipStream_t s);
 // deg[v - lo] = degree of row v (u64: a multigraph row may hold 2^32 or more entries)
 void launch_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint64_t *deg, hipStream_t s);
 void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part,
@@ -247,6 +250,8 @@ void launch_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h, uint
                        hipStream_t s);
 // mail[i] = word i at p (words of `bytes` = 4 or 8, zero-extended), i < n < kMailSeq
 void launch_post_words(const void *p, int n, const Mail &mail, hipStream_t s, int bytes = 8);
+// mail word i = *p[i] (u64 words anywhere on the device, up to 4)
+void launch_post_ptrs(const uint64_t *const *p, int n, const Mail &mail, hipStream_t s);
 
 void launch_check(const uint32_t *src, const uint32_t *dst, uint64_t R, const DAdj &adj, const uint64_t *filter,
                   uint8_t *flags, hipStream_t s);

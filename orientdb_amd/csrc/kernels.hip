@@ -509,6 +509,17 @@ void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_
   KCHECK("k_row_degree");
 }
 
+__global__ void k_row_degree_dev(const uint32_t *src, const uint64_t *nd, uint64_t R, DAdj adj, uint64_t *deg) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > R) return;
+  deg[r] = r < *nd ? adj_degree(adj, src[r]) : 0;
+}
+void launch_row_degree_dev(const uint32_t *src, const uint64_t *n, uint64_t R, const DAdj &adj, uint64_t *deg,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_row_degree_dev, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, n, R, adj, deg);
+  KCHECK("k_row_degree_dev");
+}
+
 // degrees of the rows [lo, hi) of one CSR (u32: a row of 2^32 or more entries does not occur in a
 // partition's snapshot)
 __global__ void k_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint64_t *deg) {
@@ -2296,6 +2307,20 @@ void launch_seg_totals(const uint32_t *cnt, uint64_t nseg, uint64_t nseg_h, uint
 __global__ void k_post_words(const void *p, int n, int bytes, Mail mail) {
   for (int i = 0; i < n; ++i) mail.p[i] = bytes == 8 ? ((const uint64_t *)p)[i] : (uint64_t)((const uint32_t *)p)[i];
   mail_post(mail);
+}
+struct PostPtrs {
+  const uint64_t *p[4];
+};
+__global__ void k_post_ptrs(PostPtrs pp, int n, Mail mail) {
+  for (int i = 0; i < n; ++i) mail.p[i] = *pp.p[i];
+  mail_post(mail);
+}
+void launch_post_ptrs(const uint64_t *const *p, int n, const Mail &mail, hipStream_t s) {
+  if (n <= 0 || n > 4) fail(OMX_E_INVALID, "post_ptrs: bad word count");
+  PostPtrs pp{};
+  for (int i = 0; i < n; ++i) pp.p[i] = p[i];
+  hipLaunchKernelGGL(k_post_ptrs, dim3(1), dim3(1), 0, s, pp, n, mail);
+  KCHECK("k_post_ptrs");
 }
 void launch_post_words(const void *p, int n, const Mail &mail, hipStream_t s, int bytes) {
   if (n <= 0 || n >= kMailSeq) fail(OMX_E_INVALID, "post_words: bad word count");
