@@ -20,7 +20,7 @@ CYCLES = [
     ("triangle_where_b", "MATCH {class:Person,as:a}-Knows->{as:b,where:(age < 50)}-Knows->{as:c}-Knows->{as:a} RETURN a,b,c"),
     ("triangle_in", "MATCH {class:Person,as:a,where:(uid < 300)}<-Knows-{as:b}<-Knows-{as:c}<-Knows-{as:a} RETURN a,b,c"),
     ("triangle_both", "MATCH {class:Person,as:a,where:(uid < 40)}-Knows-{as:b}-Knows-{as:c}-Knows-{as:a} RETURN a,b,c"),
-    ("square", "MATCH {class:Person,as:a,where:(uid < 100)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d}-Knows->{as:a} RETURN a,b,c,d"),
+    ("square", "MATCH {class:Person,as:a,where:(uid < 25)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d}-Knows->{as:a} RETURN a,b,c,d"),
     ("triangle_project", "MATCH {class:Person,as:a}-Knows->{as:b}-Knows->{as:c}-Knows->{as:a} RETURN a"),
 ]
 
@@ -130,18 +130,25 @@ def ldbc():
 
 @pytest.fixture(scope="module")
 def ldbc_ref(ldbc):
-    """oracle/dfs_ref.c over the SF10 triangles, computed once for the parametrized device runs"""
+    """oracle/dfs_ref.c over the SF10 triangles, computed once for the parametrized device runs (with
+    the rows' sorted packed keys)"""
     from oracle import dfs
     g = ldbc
     cg = dfs.CsrGraph(g.csr[0], g.csr[1], {"uid": np.arange(g.V, dtype=np.int64), "age": g.age})
-    return dfs.run(cg, CYCLES[0][1], nthreads=8)
+    ref = dfs.run(cg, CYCLES[0][1], nthreads=8)
+    ref["key"] = _tri_key(ref["rows"].astype(np.uint64))
+    return ref
 
 
-@pytest.mark.parametrize("merge", ["1", "force", "0"])
+def _tri_key(m):
+    return np.sort((m[:, 0] << np.uint64(42)) | (m[:, 1] << np.uint64(21)) | m[:, 2])
+
+
+@pytest.mark.parametrize("merge", ["force", "0"])
 def test_c4_ldbc_sf10_vs_c_oracle(ldbc, ldbc_ref, merge, monkeypatch):
     """configs[3] at full size: every directed triangle of the LDBC-like SF10 Knows graph, bit-exact
-    against oracle/dfs_ref.c, with the same traversed-edge count — merge path by its ratio rule, on every
-    row that fits a tile, and off (the probe, the default)."""
+    against oracle/dfs_ref.c, with the same traversed-edge count — merge path on every row that fits a
+    tile, and off (the probe, the default; the ratio rule between them is covered at RMAT-10)."""
     import orientdb_amd as o
     monkeypatch.setenv("OMX_MERGE", merge)
     g, ref = ldbc, ldbc_ref
@@ -151,5 +158,4 @@ def test_c4_ldbc_sf10_vs_c_oracle(ldbc, ldbc_ref, merge, monkeypatch):
     assert rs.info["edges_traversed"] == ref["edges"]
     idx = [rs.columns.index(c) for c in ref["aliases"]]
     got = rs.rows[:, idx].astype(np.uint64)
-    key = lambda m: np.sort((m[:, 0] << np.uint64(42)) | (m[:, 1] << np.uint64(21)) | m[:, 2])
-    assert np.array_equal(key(got), key(ref["rows"].astype(np.uint64)))
+    assert np.array_equal(_tri_key(got), ref["key"])
