@@ -1176,6 +1176,18 @@ class Executor {
         DBuf<unsigned long long> cnt(&pool_, 1);
         nh = build_pull_col(g_.rp(es, dir), g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, pull_hubs_, hub_idx.p, hist.p,
                             cnt.p, hubs, pcol, cus(), s_);
+        // the hubs' entries (a hubs-only pull reads these alone): Σ their degree in the opposite CSR
+        uint64_t he = 0;
+        if (nh) {
+          DAdj oa{};
+          oa.n = 1;
+          oa.p[0].rp = g_.rp(es, dir ^ 1);
+          DBuf<uint64_t> hd(&pool_, (uint64_t)nh + 1), hs(&pool_, 1);
+          launch_row_degree(hubs, nh, oa, hd.p, s_);
+          cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, hd.p, hs.p, (int64_t)nh + 1, s_); });
+          he = read1(hs.p);
+        }
+        es.hub_entries[dir] = he;
         HIP_CHECK(hipStreamSynchronize(s_));
       } catch (...) {
         if (pcol) (void)hipFree(pcol);
@@ -3173,7 +3185,9 @@ class Executor {
             // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask.
             // HBM-necessary: the masks are shared by all the in-edges of a source, so each is needed once
             // (probe levels: the frontier's masks and the frontier bitmap; else every vertex's mask)
-            tm_.end(16ull * V + 12ull * pull_E[p],
+            // (hubs-only: every col word is read, a mask gathered for the hub entries alone)
+            const uint64_t pg = hubs_only ? g_.esets[rspec.parts[p].first].hub_entries[rspec.parts[p].second] : pull_E[p];
+            tm_.end(16ull * V + 4ull * pull_E[p] + 8ull * pg,
                     16ull * V + 4ull * pull_E[p] + (probe ? 8ull * h[2] + (hubs_only ? 0 : V / 8) : 8ull * V));
             edges_iter_ += pull_E[p];
           }
