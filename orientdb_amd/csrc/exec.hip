@@ -3165,7 +3165,7 @@ class Executor {
                 hubs_only = true;
                 if (etot) {
                   tm_.begin("k_bfs_push");
-                  launch_bfs_push(list.p, loffs.p, nn, etot, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, cus(), s_);
+                  launch_bfs_push_v(list.p, nn, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, s_);
                   tm_.end(20ull * etot + 24ull * nn);
                   edges_iter_ += etot;
                 }
