@@ -49,13 +49,15 @@ void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *front
 // statistics are accumulated (one atomic per block and counter): stats[0] = Σ popc(m)·deg (the edges
 // the reference traverses, SURVEY §8(d) E_t), stats[1] = Σ deg over active vertices (push work),
 // stats[2] = active vertices, stats[3] = OR of m (the live lanes: a lane whose frontier is empty
-// reaches nothing more, so the pull does not wait for it).
+// reaches nothing more, so the pull does not wait for it); with hub_bm (the pull's hubs, V bits)
+// stats[4] / stats[5] = the same push work / count over the active vertices that are not hubs (what a
+// hubs-only pull leaves to a push).
 __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t vlo, uint32_t V,
                                                  const uint64_t *while_bm, int expand, DAdj adj,
-                                                 unsigned long long *stats, uint64_t *fbm) {
-  __shared__ uint64_t s_r[4][kB / 64];
+                                                 unsigned long long *stats, uint64_t *fbm, const uint64_t *hub_bm) {
+  __shared__ uint64_t s_r[6][kB / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint64_t te = 0, td = 0, tn = 0, tl = 0;
+  uint64_t te = 0, td = 0, tn = 0, tl = 0, hd = 0, hn = 0;
   // kPrepU block-strides per round, their frontier words loaded together (clamped, unconditional)
   // before any store: one iteration at a time waited a memory round trip per 256 vertices, since each
   // iteration's load came after the previous one's stores (vector memory completes in order)
@@ -86,6 +88,10 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
           td += d;
           tn += 1;
           tl |= m;
+          if (hub_bm && !bm_test(hub_bm, (uint32_t)v)) {
+            hd += d;
+            hn += 1;
+          }
         }
       }
       const uint64_t word = __ballot(m != 0);  // bit v of fbm: v's frontier mask is non-empty
@@ -96,6 +102,8 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
   te = wave_sum_u64(te);
   td = wave_sum_u64(td);
   tn = wave_sum_u64(tn);
+  hd = wave_sum_u64(hd);
+  hn = wave_sum_u64(hn);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) tl |= __shfl_xor(tl, off, 64);
   if (lane == 0) {
@@ -103,9 +111,11 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
     s_r[1][wave] = td;
     s_r[2][wave] = tn;
     s_r[3][wave] = tl;
+    s_r[4][wave] = hd;
+    s_r[5][wave] = hn;
   }
   __syncthreads();
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < 3 || (hub_bm && (threadIdx.x == 4 || threadIdx.x == 5))) {
     uint64_t x = 0;
     for (int w = 0; w < kB / 64; ++w) x += s_r[threadIdx.x][w];
     if (x) atomicAdd(&stats[threadIdx.x], (unsigned long long)x);
@@ -116,12 +126,13 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
   }
 }
 void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
-                     const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s, uint32_t vlo) {
+                     const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s, uint32_t vlo,
+                     const uint64_t *hub_bm) {
   if (vlo && fbm) fail(OMX_E_INVALID, "internal: the frontier bitmap covers whole words from vertex 0");
   if (V <= vlo) return;
   const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V - vlo, kB * 4), (uint64_t)cus * 8);
   hipLaunchKernelGGL(k_bfs_prep, dim3(g), dim3(kB), 0, s, frontier, visited, vlo, V, while_bm, (int)expand, adj, stats,
-                     fbm);
+                     fbm, hub_bm);
   KCHECK("k_bfs_prep");
 }
 
@@ -261,29 +272,6 @@ void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, u
   const unsigned g = (unsigned)std::min<uint64_t>(nblocks(etot, kB), (uint64_t)cus * 16);
   hipLaunchKernelGGL(k_bfs_push, dim3(g), dim3(kB), 0, s, list, loffs, nl, etot, rp, col, frontier, visited, next);
   KCHECK("k_bfs_push");
-}
-
-// the non-hub frontier's push beside a hubs-only pull: one thread per listed vertex walks its out-edges
-// (a non-hub's out-degree is small by definition: below the 2^19th-highest), no per-edge search of the
-// list's offsets (the edge-parallel k_bfs_push: 20 dependent loads an edge, 0.26 ms at C3)
-__global__ __launch_bounds__(kB) void k_bfs_push_v(const uint32_t *list, uint64_t nl, const uint64_t *rp,
-                                                   const uint32_t *col, const uint64_t *frontier,
-                                                   const uint64_t *visited, uint64_t *next) {
-  const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
-  if (i >= nl) return;
-  const uint32_t v = list[i];
-  const uint64_t m = frontier[v], b = rp[v], e = rp[v + 1];
-  for (uint64_t k = b; k < e; ++k) {
-    const uint32_t w = col[k];
-    const uint64_t mm = m & ~visited[w];
-    if (mm && (next[w] & mm) != mm) atomicOr((unsigned long long *)&next[w], (unsigned long long)mm);
-  }
-}
-void launch_bfs_push_v(const uint32_t *list, uint64_t nl, const uint64_t *rp, const uint32_t *col,
-                       const uint64_t *frontier, const uint64_t *visited, uint64_t *next, hipStream_t s) {
-  if (!nl) return;
-  hipLaunchKernelGGL(k_bfs_push_v, dim3(nblocks(nl, kB)), dim3(kB), 0, s, list, nl, rp, col, frontier, visited, next);
-  KCHECK("k_bfs_push_v");
 }
 
 __global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part);

@@ -1152,10 +1152,12 @@ class Executor {
   }
 
   // the hub-annotated col of one CSR for the bottom-up BFS (built once per CSR, bfs.hip)
-  const uint32_t *pull_col_of(int eset, int dir, uint32_t *nhubs, const uint32_t **hubs) {
+  const uint32_t *pull_col_of(int eset, int dir, uint32_t *nhubs, const uint32_t **hubs,
+                              const uint64_t **hub_bm = nullptr) {
     EdgeSet &es = g_.esets[eset];
     *nhubs = 0;
     *hubs = nullptr;
+    if (hub_bm) *hub_bm = nullptr;
     // k_bfs_pull reads bit 31 of a col entry as the hub tag: vertex ids must stay below 2^31
     if (g_.V >= 0x80000000u) unsupported("variable-length traversal over 2^31 or more vertices");
     if (pull_hubs_ == 0 || g_.partitioned()) return g_.col(es, dir);
@@ -1163,15 +1165,19 @@ class Executor {
       HIP_CHECK(hipStreamSynchronize(s_));
       (void)hipFree(es.d_pull_col[dir]);
       (void)hipFree(es.d_hubs[dir]);
+      if (es.d_hub_bm[dir]) (void)hipFree(es.d_hub_bm[dir]);
       es.d_pull_col[dir] = nullptr;
       es.d_hubs[dir] = nullptr;
+      es.d_hub_bm[dir] = nullptr;
     }
     if (!es.d_pull_col[dir]) {  // built into local buffers, published once complete
       const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
       uint32_t *pcol = nullptr, *hubs = nullptr, nh = 0;
+      uint64_t *hbm = nullptr;
       try {
         HIP_CHECK(hipMalloc((void **)&pcol, std::max<size_t>(E * 4, 4)));
         HIP_CHECK(hipMalloc((void **)&hubs, std::max<size_t>((size_t)pull_hubs_ * 4, 4)));
+        HIP_CHECK(hipMalloc((void **)&hbm, std::max<size_t>(nwords_ * 8, 8)));
         DBuf<uint32_t> hub_idx(&pool_, g_.V), hist(&pool_, 4096);
         DBuf<unsigned long long> cnt(&pool_, 1);
         nh = build_pull_col(g_.rp(es, dir), g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, pull_hubs_, hub_idx.p, hist.p,
@@ -1188,20 +1194,26 @@ class Executor {
           he = read1(hs.p);
         }
         es.hub_entries[dir] = he;
+        HIP_CHECK(hipMemsetAsync(hbm, 0, std::max<size_t>(nwords_ * 8, 8), s_));
+        if (nh) launch_mark_bitmap(hubs, nh, hbm, g_.V, s_);
         HIP_CHECK(hipStreamSynchronize(s_));
       } catch (...) {
         if (pcol) (void)hipFree(pcol);
         if (hubs) (void)hipFree(hubs);
+        if (hbm) (void)hipFree(hbm);
         throw;
       }
       es.d_pull_col[dir] = pcol;
       es.d_hubs[dir] = hubs;
+      es.d_hub_bm[dir] = hbm;
+      g_.device_bytes += nwords_ * 8;
       es.n_hubs[dir] = nh;
       es.hubs_requested[dir] = pull_hubs_;
       g_.device_bytes += E * 4 + (uint64_t)pull_hubs_ * 4;
     }
     *nhubs = es.n_hubs[dir];
     *hubs = es.d_hubs[dir];
+    if (hub_bm) *hub_bm = es.d_hub_bm[dir];
     return es.d_pull_col[dir];
   }
 
@@ -2989,9 +3001,18 @@ class Executor {
     if (depth_only_while) wconst = make_pred(st.while_prog, -1);
     DBuf<uint64_t> fr(&pool_, V), nx(&pool_, V), vis(&pool_, V), fbm(&pool_, nwords_);
     DBuf<uint32_t> list;
-    DBuf<unsigned long long> stats(&pool_, 5);
+    DBuf<unsigned long long> stats(&pool_, 6);
     // bottom-up partitions of every reversed part (once per traversal; built on the first pull level)
-    std::vector<DBuf<uint64_t>> hub_fr(radj.n), hub_bm(radj.n);
+    std::vector<DBuf<uint64_t>> hub_fr(radj.n);
+    // sparse levels pull over the hub entries only and push the non-hub frontier (one GPU, one part): the
+    // hubs' V-bit set lets the level prologue count that frontier and its out-edges (OMX_HUB_PUSH=0: off)
+    const uint64_t *hub_bm = nullptr;
+    if (!dist_ && pull_wave_ && hub_push_ && radj.n == 1) {
+      uint32_t nh = 0;
+      const uint32_t *hb = nullptr;
+      pull_col_of(rspec.parts[0].first, rspec.parts[0].second, &nh, &hb, &hub_bm);
+      if (!nh) hub_bm = nullptr;
+    }
     std::vector<const uint64_t *> pull_part(radj.n, nullptr);
     std::vector<const uint32_t *> pull_col(radj.n, nullptr), pull_hubs(radj.n, nullptr);
     std::vector<uint32_t> pull_nh(radj.n, 0);
@@ -3021,14 +3042,14 @@ class Executor {
         if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate");
         bool expand = !(st.has_max_depth && d >= st.max_depth);
         if (expand && depth_only_while) expand = !while_never && eval_pred_const(wconst, d);
-        HIP_CHECK(hipMemsetAsync(stats.p, 0, 5 * sizeof(unsigned long long), s_));
+        HIP_CHECK(hipMemsetAsync(stats.p, 0, 6 * sizeof(unsigned long long), s_));
         tm_.begin("k_bfs_prep");
-        launch_bfs_prep(fr.p, vis.p, vhi, while_bm, expand, adj, stats.p, dist_ ? nullptr : fbm.p, cus(), s_, vlo);
+        launch_bfs_prep(fr.p, vis.p, vhi, while_bm, expand, adj, stats.p, dist_ ? nullptr : fbm.p, cus(), s_, vlo, hub_bm);
         tm_.end(8ull * (vhi - vlo));
         if (!expand) break;
-        launch_post_words(stats.p, 4, mail(), s_);
+        launch_post_words(stats.p, 6, mail(), s_);
         const uint64_t *hm = wait_mail();
-        uint64_t h[4] = {hm[0], hm[1], hm[2], hm[3]};
+        uint64_t h[6] = {hm[0], hm[1], hm[2], hm[3], hm[4], hm[5]};
         tm_.amend(8ull * (vhi - vlo) + 24ull * h[2]);  // frontier scan + visited and row_ptr pair of the active vertices
         uint64_t live_or = h[3];
         uint64_t active = h[2];
@@ -3140,35 +3161,28 @@ class Executor {
               continue;
             }
             // A sparse level whose frontier is mostly hubs (C3's third level: 1.2 K of its 54 M non-hub
-            // in-edges come from frontier vertices) pulls over the hub entries only — a non-hub entry costs
-            // no memory access instead of a frontier-bitmap probe — and the few non-hub frontier vertices push
-            // their out-edges instead (OMX_HUB_PUSH=0: the probing pull for every entry)
+            // in-edges come from frontier vertices) gathers masks for the hub entries only — a non-hub entry
+            // costs its col word, no frontier-bitmap probe — and the non-hub frontier (h[5] vertices, h[4]
+            // out-edges: counted by the prologue, no host round trip) pushes its out-edges instead, when
+            // those are under 1/8 of the level's in-edges
             bool hubs_only = false;
-            if (probe && !dist_ && pull_wave_ && hub_push_ && pull_nh[p] > 0) {  // (fbm: one GPU)
-              if (!hub_bm[p].p) {  // the part's hubs as a V-bit set (once per traversal)
-                hub_bm[p] = DBuf<uint64_t>(&pool_, std::max<uint64_t>(nwords_, 1));
-                HIP_CHECK(hipMemsetAsync(hub_bm[p].p, 0, std::max<uint64_t>(nwords_, 1) * 8, s_));
-                launch_mark_bitmap(pull_hubs[p], pull_nh[p], hub_bm[p].p, V, s_);
-              }
-              if (!list.p) list = DBuf<uint32_t>(&pool_, V);
-              DBuf<unsigned long long> nc(&pool_, 1);
-              HIP_CHECK(hipMemsetAsync(nc.p, 0, sizeof(unsigned long long), s_));
-              tm_.begin("k_bfs_list");
-              launch_bfs_list_nonhub(fbm.p, hub_bm[p].p, V, list.p, nc.p, cus(), s_);
-              tm_.end(V / 4);
-              const uint64_t nn = read1(reinterpret_cast<const uint64_t *>(nc.p));
-              DBuf<uint64_t> deg(&pool_, nn + 1), loffs(&pool_, nn + 1);
-              launch_bfs_list_deg(list.p, nn, adj.p[p].rp, deg.p, s_);
-              cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, deg.p, loffs.p, (int64_t)(nn + 1), s_); });
-              const uint64_t etot = read1(loffs.p + nn);
-              if (hub_push_ == 2 || etot * 8 < pull_E[p]) {
-                hubs_only = true;
-                if (etot) {
-                  tm_.begin("k_bfs_push");
-                  launch_bfs_push_v(list.p, nn, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, s_);
-                  tm_.end(20ull * etot + 24ull * nn);
-                  edges_iter_ += etot;
-                }
+            if (probe && hub_bm && (hub_push_ == 2 || h[4] * 8 < pull_E[p])) {
+              hubs_only = true;
+              const uint64_t nn = h[5], etot = h[4];
+              if (etot) {
+                if (!list.p) list = DBuf<uint32_t>(&pool_, V);
+                DBuf<unsigned long long> nc(&pool_, 1);
+                HIP_CHECK(hipMemsetAsync(nc.p, 0, sizeof(unsigned long long), s_));
+                tm_.begin("k_bfs_list");
+                launch_bfs_list_nonhub(fbm.p, hub_bm, V, list.p, nc.p, cus(), s_);
+                tm_.end(V / 4);
+                DBuf<uint64_t> deg(&pool_, nn + 1), loffs(&pool_, nn + 1);
+                launch_bfs_list_deg(list.p, nn, adj.p[p].rp, deg.p, s_);
+                cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, deg.p, loffs.p, (int64_t)(nn + 1), s_); });
+                tm_.begin("k_bfs_push");
+                launch_bfs_push(list.p, loffs.p, nn, etot, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, cus(), s_);
+                tm_.end(20ull * etot + 24ull * nn);
+                edges_iter_ += etot;
               }
             }
             tm_.begin(probe ? "k_bfs_pull_sparse" : "k_bfs_pull");

@@ -359,13 +359,10 @@ void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *front
 // vertices [vlo, V) (a partition's own rows: vlo = part_lo, V = part_hi; fbm only from vertex 0)
 void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
                      const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s,
-                     uint32_t vlo = 0);
+                     uint32_t vlo = 0, const uint64_t *hub_bm = nullptr);
 void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsigned long long *count, int cus,
                      hipStream_t s);
 void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg, hipStream_t s);
-// one thread per listed (non-hub) frontier vertex pushes its out-edges' masks
-void launch_bfs_push_v(const uint32_t *list, uint64_t nl, const uint64_t *rp, const uint32_t *col,
-                       const uint64_t *frontier, const uint64_t *visited, uint64_t *next, hipStream_t s);
 // frontier vertices not in hub_bm (a sparse level's push beside a hubs-only pull)
 void launch_bfs_list_nonhub(const uint64_t *fbm, const uint64_t *hub_bm, uint32_t V, uint32_t *list,
                             unsigned long long *count, int cus, hipStream_t s);
