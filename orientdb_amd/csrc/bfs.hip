@@ -248,28 +248,68 @@ void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, 
 
 // Top-down: one thread per frontier edge (consecutive threads → consecutive col[] entries); the
 // owning list entry is found by binary search in the degree prefix.
+// top-down level: every out-edge of the listed frontier pushes its source's mask. A block takes
+// kPushIT·kB consecutive edges; their sources' list offsets are staged in LDS (two global searches a
+// block), so an edge finds its source with an LDS binary search (a global search per edge was ≈20
+// dependent loads); a range over more than kPushStage sources searches the global offsets.
+constexpr int kPushIT = 8, kPushStage = 2048;
 __global__ __launch_bounds__(kB) void k_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl,
                                                  uint64_t etot, const uint64_t *rp, const uint32_t *col,
                                                  const uint64_t *frontier, const uint64_t *visited, uint64_t *next) {
-  const uint64_t stride = (uint64_t)gridDim.x * kB;
-  for (uint64_t e = (uint64_t)blockIdx.x * kB + threadIdx.x; e < etot; e += stride) {
-    uint64_t lo = 0, hi = nl;  // largest i with loffs[i] <= e
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) >> 1;
+  __shared__ uint64_t s_off[kPushStage + 1];
+  __shared__ uint64_t s_lo, s_hi;
+  auto search = [&](uint64_t lo, uint64_t hi, uint64_t e) {  // largest i in [lo, hi] with loffs[i] <= e
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi + 1) >> 1;
       if (loffs[mid] <= e) lo = mid;
-      else hi = mid;
+      else hi = mid - 1;
     }
-    const uint32_t v = list[lo];
-    const uint32_t w = col[rp[v] + (e - loffs[lo])];
-    const uint64_t m = frontier[v] & ~visited[w];
-    if (m && (next[w] & m) != m) atomicOr((unsigned long long *)&next[w], (unsigned long long)m);
+    return lo;
+  };
+  constexpr uint64_t per = (uint64_t)kB * kPushIT;
+  for (uint64_t e0 = (uint64_t)blockIdx.x * per; e0 < etot; e0 += (uint64_t)gridDim.x * per) {
+    const uint64_t e1 = e0 + per < etot ? e0 + per : etot;
+    if (threadIdx.x == 0) {
+      const uint64_t lo = search(0, nl - 1, e0);
+      s_lo = lo;
+      s_hi = search(lo, nl - 1, e1 - 1);
+    }
+    __syncthreads();
+    const uint64_t lo = s_lo, hi = s_hi, n = hi - lo + 1;
+    const bool staged = n + 1 <= (uint64_t)kPushStage;
+    if (staged)
+      for (uint64_t i = threadIdx.x; i <= n; i += kB) s_off[i] = loffs[lo + i];
+    __syncthreads();
+    for (int k = 0; k < kPushIT; ++k) {
+      const uint64_t e = e0 + (uint64_t)k * kB + threadIdx.x;
+      if (e >= e1) break;
+      uint64_t j, base;
+      if (staged) {
+        uint32_t a = 0, b = (uint32_t)(n - 1);
+        while (a < b) {
+          const uint32_t mid = (a + b + 1) >> 1;
+          if (s_off[mid] <= e) a = mid;
+          else b = mid - 1;
+        }
+        j = lo + a;
+        base = s_off[a];
+      } else {
+        j = search(lo, hi, e);
+        base = loffs[j];
+      }
+      const uint32_t v = list[j];
+      const uint32_t w = col[rp[v] + (e - base)];
+      const uint64_t m = frontier[v] & ~visited[w];
+      if (m && (next[w] & m) != m) atomicOr((unsigned long long *)&next[w], (unsigned long long)m);
+    }
+    __syncthreads();  // s_off and s_lo are restaged by the next range
   }
 }
 void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, uint64_t etot, const uint64_t *rp,
                      const uint32_t *col, const uint64_t *frontier, const uint64_t *visited, uint64_t *next,
                      int cus, hipStream_t s) {
-  if (!etot) return;
-  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(etot, kB), (uint64_t)cus * 16);
+  if (!etot || !nl) return;
+  const unsigned g = (unsigned)std::min<uint64_t>(nblocks(etot, (uint64_t)kB * kPushIT), (uint64_t)cus * 16);
   hipLaunchKernelGGL(k_bfs_push, dim3(g), dim3(kB), 0, s, list, loffs, nl, etot, rp, col, frontier, visited, next);
   KCHECK("k_bfs_push");
 }

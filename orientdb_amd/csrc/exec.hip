@@ -3001,7 +3001,8 @@ class Executor {
     if (depth_only_while) wconst = make_pred(st.while_prog, -1);
     DBuf<uint64_t> fr(&pool_, V), nx(&pool_, V), vis(&pool_, V), fbm(&pool_, nwords_);
     DBuf<uint32_t> list;
-    DBuf<unsigned long long> stats(&pool_, 6);
+    // the level prologue's six words (k_bfs_prep) and, in stats[6], the push level's list counter
+    DBuf<unsigned long long> stats(&pool_, 7);
     // bottom-up partitions of every reversed part (once per traversal; built on the first pull level)
     std::vector<DBuf<uint64_t>> hub_fr(radj.n);
     // sparse levels pull over the hub entries only and push the non-hub frontier (one GPU, one part): the
@@ -3042,7 +3043,7 @@ class Executor {
         if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate");
         bool expand = !(st.has_max_depth && d >= st.max_depth);
         if (expand && depth_only_while) expand = !while_never && eval_pred_const(wconst, d);
-        HIP_CHECK(hipMemsetAsync(stats.p, 0, 6 * sizeof(unsigned long long), s_));
+        HIP_CHECK(hipMemsetAsync(stats.p, 0, 7 * sizeof(unsigned long long), s_));
         tm_.begin("k_bfs_prep");
         launch_bfs_prep(fr.p, vis.p, vhi, while_bm, expand, adj, stats.p, dist_ ? nullptr : fbm.p, cus(), s_, vlo, hub_bm);
         tm_.end(8ull * (vhi - vlo));
@@ -3208,7 +3209,7 @@ class Executor {
         } else {
           if (!list.p) list = DBuf<uint32_t>(&pool_, V);
           tm_.begin("k_bfs_list");
-          launch_bfs_list(fr.p, V, list.p, stats.p + 4, cus(), s_);
+          launch_bfs_list(fr.p, V, list.p, stats.p + 6, cus(), s_);
           tm_.end(8ull * V + 4ull * h[2]);
           const uint64_t nl_act = h[2];
           DBuf<uint64_t> deg(&pool_, nl_act + 1), loffs(&pool_, nl_act + 1);
