@@ -305,8 +305,12 @@ def test_rmat_parity_all_rows_chunked(rmat10, q, monkeypatch):
     _parity(g, ref, q[1], q[2])
 
 
+CHUNK_IDS = ("c2_both_ends", "c1_fof", "c1_abc", "both_dir", "three_hop", "paths", "varlen_depth", "cartesian",
+             "optional_free", "multi_two_hops")
+
+
 @pytest.mark.parametrize("chunk", ["256", "512", "2048"])
-@pytest.mark.parametrize("q", RMAT_QUERIES, ids=[q[0] for q in RMAT_QUERIES])
+@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in CHUNK_IDS], ids=lambda q: q[0])
 def test_rmat_parity_dense_chunk_windows(rmat10, q, chunk, monkeypatch):
     """Unfiltered written hops with every row of degree ≥ 2 cut into 256-, 512- or 2048-entry aligned
     chunk windows (k_expand_heavy with 4 / 8 / 32 slots), factorized hops forced so their row emission
@@ -415,9 +419,12 @@ def test_rmat_parity_factorized(rmat10, rmat10_raw, q, graph, monkeypatch):
     assert rs.info["bindings"] == direct.info["bindings"]
 
 
-@pytest.mark.parametrize("emit", ["binned", "slow", "grp64"])
-@pytest.mark.parametrize("graph", ["simple", "multigraph"])
-@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
+EMIT_CASES = [(q, g, e) for q in RMAT_QUERIES if q[0] in FACTOR_IDS for g in ("simple", "multigraph") for e in ("binned",)] + \
+    [(q, "multigraph", e) for q in RMAT_QUERIES if q[0] in ("c2_both_ends", "in_dir", "three_hop", "paths", "matched_and_filter")
+     for e in ("slow", "grp64")]
+
+
+@pytest.mark.parametrize("q,graph,emit", EMIT_CASES, ids=lambda x: x[0] if isinstance(x, tuple) else str(x))
 def test_rmat_parity_factorized_emission(rmat10, rmat10_raw, q, graph, emit, monkeypatch):
     """The factorized hop's rows written the other ways (the default — rows grouped by source, output
     tiles of k_femit_w — is covered by test_rmat_parity_factorized): binned = the generic unfiltered
