@@ -36,6 +36,13 @@ struct NonZeroU64 {
 struct CastU8U32 {
   __host__ __device__ uint32_t operator()(const uint8_t &x) const { return x; }
 };
+// a hub-annotated col entry (bit 31: the entry names a hub)
+struct HubFlag {
+  __host__ __device__ uint64_t operator()(const uint32_t &x) const { return x >> 31; }
+};
+struct HubFlag8 {
+  __host__ __device__ uint8_t operator()(const uint32_t &x) const { return (uint8_t)(x >> 31); }
+};
 
 class Timer {
  public:
@@ -143,6 +150,16 @@ class Timer {
   std::vector<hipEvent_t> *pool_;
   std::vector<Rec> recs_;
 };
+
+// out[i] = src[idx[i]] (u64 values at u64 positions: a CSR's row pointers mapped through a scan)
+__global__ void k_gather_u64_at(const uint64_t *src, const uint64_t *idx, uint64_t n, uint64_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = src[idx[i]];
+}
+static void launch_gather_u64_at(const uint64_t *src, const uint64_t *idx, uint64_t n, uint64_t *out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_gather_u64_at, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, idx, n, out);
+}
 
 // out[id[i]] = deg[i] (a fetched adjacency's degrees placed at their vertices)
 __global__ void k_scatter_deg(const uint32_t *id, const uint32_t *deg, uint64_t n, uint64_t *out) {
@@ -1118,37 +1135,92 @@ class Executor {
   // indices, regular tiles first (*nreg of them)
   const uint32_t *pullw_of(int eset, int dir, const uint64_t *rp, uint64_t E, const uint64_t **rb, uint64_t *nreg) {
     EdgeSet &es = g_.esets[eset];
-    if (!es.d_pullw_tiles[dir]) {  // built into local buffers, published once complete
-      const uint64_t nt = bfs_pull_w_tiles(E);
-      if (nt > 0xFFFFFFFFull) unsupported("a bottom-up level over 2^42 or more in-edges");
-      uint64_t *b = nullptr;
-      uint32_t *tl = nullptr;
-      HIP_CHECK(hipMalloc((void **)&b, std::max<uint64_t>(2 * nt, 1) * sizeof(uint64_t)));
-      if (hipMalloc((void **)&tl, std::max<uint64_t>(nt, 1) * sizeof(uint32_t)) != hipSuccess) {
-        (void)hipFree(b);
-        fail(OMX_E_OOM, "pull tiles");
-      }
-      uint64_t nr = 0;
-      try {
-        DBuf<uint8_t> reg(&pool_, std::max<uint64_t>(nt, 1));
-        DBuf<uint64_t> cnt(&pool_, 1);
-        launch_pull_w_bounds(rp, g_.V, E, b, reg.p, s_);
-        hipcub::CountingInputIterator<uint32_t> it(0);
-        cub([&](void *t, size_t &bytes) { return hipcub::DevicePartition::Flagged(t, bytes, it, reg.p, tl, cnt.p, (int64_t)nt, s_); });
-        nr = read1(cnt.p);
-      } catch (...) {
-        (void)hipFree(b);
-        (void)hipFree(tl);
-        throw;
-      }
-      es.d_pullw_rb[dir] = b;
-      es.pullw_nreg[dir] = nr;
-      es.d_pullw_tiles[dir] = tl;
-      g_.device_bytes += nt * 20;
-    }
+    if (!es.d_pullw_tiles[dir]) pullw_build(rp, E, es.d_pullw_rb[dir], es.d_pullw_tiles[dir], es.pullw_nreg[dir]);
     *rb = es.d_pullw_rb[dir];
     *nreg = es.pullw_nreg[dir];
     return es.d_pullw_tiles[dir];
+  }
+  // wave tiles of one CSR's in-edges: the tile bounds and the tile list, regular tiles first (built into
+  // local buffers, published once complete)
+  void pullw_build(const uint64_t *rp, uint64_t E, uint64_t *&rb_out, uint32_t *&tiles_out, uint64_t &nreg_out) {
+    const uint64_t nt = bfs_pull_w_tiles(E);
+    if (nt > 0xFFFFFFFFull) unsupported("a bottom-up level over 2^42 or more in-edges");
+    uint64_t *b = nullptr;
+    uint32_t *tl = nullptr;
+    HIP_CHECK(hipMalloc((void **)&b, std::max<uint64_t>(2 * nt, 1) * sizeof(uint64_t)));
+    if (hipMalloc((void **)&tl, std::max<uint64_t>(nt, 1) * sizeof(uint32_t)) != hipSuccess) {
+      (void)hipFree(b);
+      fail(OMX_E_OOM, "pull tiles");
+    }
+    uint64_t nr = 0;
+    try {
+      DBuf<uint8_t> reg(&pool_, std::max<uint64_t>(nt, 1));
+      DBuf<uint64_t> cnt(&pool_, 1);
+      launch_pull_w_bounds(rp, g_.V, E, b, reg.p, s_);
+      hipcub::CountingInputIterator<uint32_t> it(0);
+      cub([&](void *t, size_t &bytes) { return hipcub::DevicePartition::Flagged(t, bytes, it, reg.p, tl, cnt.p, (int64_t)nt, s_); });
+      nr = read1(cnt.p);
+    } catch (...) {
+      (void)hipFree(b);
+      (void)hipFree(tl);
+      throw;
+    }
+    rb_out = b;
+    nreg_out = nr;
+    tiles_out = tl;
+    g_.device_bytes += nt * 20;
+  }
+
+  // the hub entries of a pull col as their own CSR (EdgeSet::d_hub_rp / d_hub_col) and its wave tiles
+  struct HubCsr {
+    const uint64_t *rp = nullptr;
+    const uint32_t *col = nullptr;
+    uint64_t E = 0;
+    const uint32_t *tiles = nullptr;
+    const uint64_t *rb = nullptr;
+    uint64_t nreg = 0;
+  };
+  HubCsr hub_csr_of(int eset, int dir) {
+    EdgeSet &es = g_.esets[eset];
+    HubCsr h;
+    if (!es.d_pull_col[dir]) return h;
+    const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
+    if (!es.d_hub_col[dir]) {
+      uint64_t *hrp = nullptr;
+      uint32_t *hcol = nullptr;
+      uint64_t nh = 0;
+      try {
+        HIP_CHECK(hipMalloc((void **)&hrp, ((uint64_t)g_.V + 1) * 8));
+        // excl[e] = hub entries before e (u32 when E < 2^32), then hub_rp[v] = excl[rp[v]]
+        DBuf<uint64_t> ex(&pool_, E + 1);
+        HIP_CHECK(hipMemsetAsync(ex.p, 0, 8, s_));
+        hipcub::TransformInputIterator<uint64_t, HubFlag, const uint32_t *> fl(es.d_pull_col[dir], HubFlag());
+        if (E) cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, fl, ex.p + 1, (int64_t)E, s_); });
+        launch_gather_u64_at(ex.p, g_.rp(es, dir), (uint64_t)g_.V + 1, hrp, s_);
+        nh = read1(ex.p + E);
+        HIP_CHECK(hipMalloc((void **)&hcol, std::max<uint64_t>(nh, 1) * 4));
+        DBuf<uint64_t> nsel(&pool_, 1);
+        hipcub::TransformInputIterator<uint8_t, HubFlag8, const uint32_t *> f8(es.d_pull_col[dir], HubFlag8());
+        if (E) cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, es.d_pull_col[dir], f8, hcol, nsel.p, (int64_t)E, s_); });
+        HIP_CHECK(hipStreamSynchronize(s_));
+      } catch (...) {
+        if (hrp) (void)hipFree(hrp);
+        if (hcol) (void)hipFree(hcol);
+        throw;
+      }
+      es.d_hub_rp[dir] = hrp;
+      es.d_hub_col[dir] = hcol;
+      es.hub_entries[dir] = nh;
+      g_.device_bytes += ((uint64_t)g_.V + 1) * 8 + nh * 4;
+      pullw_build(hrp, nh, es.d_hubw_rb[dir], es.d_hubw_tiles[dir], es.hubw_nreg[dir]);
+    }
+    h.rp = es.d_hub_rp[dir];
+    h.col = es.d_hub_col[dir];
+    h.E = es.hub_entries[dir];
+    h.tiles = es.d_hubw_tiles[dir];
+    h.rb = es.d_hubw_rb[dir];
+    h.nreg = es.hubw_nreg[dir];
+    return h;
   }
 
   // the hub-annotated col of one CSR for the bottom-up BFS (built once per CSR, bfs.hip)
@@ -1166,9 +1238,15 @@ class Executor {
       (void)hipFree(es.d_pull_col[dir]);
       (void)hipFree(es.d_hubs[dir]);
       if (es.d_hub_bm[dir]) (void)hipFree(es.d_hub_bm[dir]);
+      for (void *x : {(void *)es.d_hub_rp[dir], (void *)es.d_hub_col[dir], (void *)es.d_hubw_rb[dir], (void *)es.d_hubw_tiles[dir]})
+        if (x) (void)hipFree(x);
       es.d_pull_col[dir] = nullptr;
       es.d_hubs[dir] = nullptr;
       es.d_hub_bm[dir] = nullptr;
+      es.d_hub_rp[dir] = nullptr;
+      es.d_hub_col[dir] = nullptr;
+      es.d_hubw_rb[dir] = nullptr;
+      es.d_hubw_tiles[dir] = nullptr;
     }
     if (!es.d_pull_col[dir]) {  // built into local buffers, published once complete
       const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
@@ -3186,8 +3264,13 @@ class Executor {
                 edges_iter_ += etot;
               }
             }
+            // (hubs-only: the tiles run over the hub entries' own CSR, EdgeSet::d_hub_rp / d_hub_col)
+            const HubCsr hc = hubs_only ? hub_csr_of(rspec.parts[p].first, rspec.parts[p].second) : HubCsr{};
             tm_.begin(probe ? "k_bfs_pull_sparse" : "k_bfs_pull");
-            if (pull_wave_) {  // wave tiles over the in-edges
+            if (hubs_only && hc.col) {
+              launch_bfs_pull_w(hc.rp, hc.col, hc.E, hc.tiles, hc.nreg, hc.rb, lanes & live, fr.p, hub_fr[p].p,
+                                pull_nh[p], nullptr, vis.p, nx.p, cus(), s_, true);
+            } else if (pull_wave_) {  // wave tiles over the in-edges
               const uint64_t *wrb = nullptr;
               uint64_t nreg = 0;
               const uint32_t *wt = pullw_of(rspec.parts[p].first, rspec.parts[p].second, radj.p[p].rp, pull_E[p], &wrb, &nreg);
@@ -3200,11 +3283,10 @@ class Executor {
             // per vertex: row_ptr pair + visited (+ next); per in-edge: col + the source's frontier mask.
             // HBM-necessary: the masks are shared by all the in-edges of a source, so each is needed once
             // (probe levels: the frontier's masks and the frontier bitmap; else every vertex's mask)
-            // (hubs-only: every col word is read, a mask gathered for the hub entries alone)
-            const uint64_t pg = hubs_only ? g_.esets[rspec.parts[p].first].hub_entries[rspec.parts[p].second] : pull_E[p];
-            tm_.end(16ull * V + 4ull * pull_E[p] + 8ull * pg,
-                    16ull * V + 4ull * pull_E[p] + (probe ? 8ull * h[2] + (hubs_only ? 0 : V / 8) : 8ull * V));
-            edges_iter_ += pull_E[p];
+            // (hubs-only over the hub CSR: its col words and a mask per entry)
+            const uint64_t pe = hubs_only && hc.col ? hc.E : pull_E[p];
+            tm_.end(16ull * V + 12ull * pe, 16ull * V + 4ull * pe + (probe ? 8ull * h[2] + (hubs_only ? 0 : V / 8) : 8ull * V));
+            edges_iter_ += pe;
           }
         } else {
           if (!list.p) list = DBuf<uint32_t>(&pool_, V);

@@ -112,6 +112,13 @@ struct EdgeSet {
   uint64_t *d_pullw_rb[2] = {nullptr, nullptr};
   uint32_t *d_pullw_tiles[2] = {nullptr, nullptr};
   uint64_t pullw_nreg[2] = {0, 0};
+  // the hub entries alone, as a CSR (row v: the entries of d_pull_col's row v that name a hub, in order)
+  // with its own wave tiles: what a hubs-only pull level reads (built with d_pull_col)
+  uint64_t *d_hub_rp[2] = {nullptr, nullptr};
+  uint32_t *d_hub_col[2] = {nullptr, nullptr};
+  uint64_t *d_hubw_rb[2] = {nullptr, nullptr};
+  uint32_t *d_hubw_tiles[2] = {nullptr, nullptr};
+  uint64_t hubw_nreg[2] = {0, 0};
   // partitioned snapshot: row pointers of every vertex's degree (V + 1 entries, the scan of all ranks'
   // degrees gathered once) — what out()/in()/both().size() in a WHERE reads (no col[] behind them)
   uint64_t *d_global_rp[2] = {nullptr, nullptr};
