@@ -1260,18 +1260,6 @@ class Executor {
         DBuf<unsigned long long> cnt(&pool_, 1);
         nh = build_pull_col(g_.rp(es, dir), g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, pull_hubs_, hub_idx.p, hist.p,
                             cnt.p, hubs, pcol, cus(), s_);
-        // the hubs' entries (a hubs-only pull reads these alone): Σ their degree in the opposite CSR
-        uint64_t he = 0;
-        if (nh) {
-          DAdj oa{};
-          oa.n = 1;
-          oa.p[0].rp = g_.rp(es, dir ^ 1);
-          DBuf<uint64_t> hd(&pool_, (uint64_t)nh + 1), hs(&pool_, 1);
-          launch_row_degree(hubs, nh, oa, hd.p, s_);
-          cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, hd.p, hs.p, (int64_t)nh + 1, s_); });
-          he = read1(hs.p);
-        }
-        es.hub_entries[dir] = he;
         HIP_CHECK(hipMemsetAsync(hbm, 0, std::max<size_t>(nwords_ * 8, 8), s_));
         if (nh) launch_mark_bitmap(hubs, nh, hbm, g_.V, s_);
         HIP_CHECK(hipStreamSynchronize(s_));

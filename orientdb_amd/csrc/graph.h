@@ -103,7 +103,7 @@ struct EdgeSet {
   uint32_t *d_hubs[2] = {nullptr, nullptr};
   uint64_t *d_hub_bm[2] = {nullptr, nullptr};  // the hubs as a V-bit set (built with d_pull_col)
   uint32_t n_hubs[2] = {0, 0};
-  uint64_t hub_entries[2] = {0, 0};     // entries of d_pull_col that name a hub (Σ their opposite degree)
+  uint64_t hub_entries[2] = {0, 0};     // entries of d_pull_col that name a hub (the hub CSR's size)
   uint32_t hubs_requested[2] = {0, 0};  // the hub budget d_pull_col was built with (rebuilt when it changes)
   // merge-path split of the CSR into pull tiles (bfs.hip k_pull_partition), built with d_pull_col
   uint64_t *d_pull_part[2] = {nullptr, nullptr};
