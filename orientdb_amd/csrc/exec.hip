@@ -36,6 +36,12 @@ struct NonZeroU64 {
 struct CastU8U32 {
   __host__ __device__ uint32_t operator()(const uint8_t &x) const { return x; }
 };
+// the degree of sorted row i's source: udeg[g[i]] (E_t summed over the distinct sources' degrees)
+struct RowSourceDeg {
+  const uint32_t *g;
+  const uint64_t *udeg;
+  __host__ __device__ uint64_t operator()(const uint64_t &i) const { return udeg[g[i]]; }
+};
 // a hub-annotated col entry (bit 31: the entry names a hub)
 struct HubFlag {
   __host__ __device__ uint64_t operator()(const uint32_t &x) const { return x >> 31; }
@@ -1980,11 +1986,7 @@ class Executor {
     const bool femit_ok = write && !semi_ && femit_ && cols.size() <= (size_t)kFemitCols && R > 0 && adj.n > 0;
     bool femit = false;
     if (femit_ok) {
-      DBuf<uint64_t> rdeg(&pool_, R + 1), et(&pool_, 1);
-      tm_.begin("k_row_degree");
-      launch_row_degree(src, R, adj, rdeg.p, s_);
-      tm_.end(R * (4ull + 8ull * adj.n + 8ull));
-      cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, rdeg.p, et.p, (int64_t)(R + 1), s_); });
+      DBuf<uint64_t> et(&pool_, 1);
       DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
       DBuf<uint8_t> head(&pool_, R);
       DBuf<uint64_t> nsel(&pool_, 1);
@@ -2009,6 +2011,12 @@ class Executor {
       launch_row_degree_dev(ub.p, nsel.p, R, adj, udeg.p, s_);
       tm_.end(R * 8ull);
       cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(R + 1), s_); });
+      // E_t = Σ_rows deg(source) = Σ over the sorted rows of their source's degree (no per-row row_ptr reads)
+      {
+        hipcub::CountingInputIterator<uint64_t> ci(0);
+        hipcub::TransformInputIterator<uint64_t, RowSourceDeg, hipcub::CountingInputIterator<uint64_t>> rd(ci, RowSourceDeg{g.p, udeg.p});
+        cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, rd, et.p, (int64_t)R, s_); });
+      }
       const uint64_t *words[3] = {et.p, nsel.p, doff.p + R};
       launch_post_ptrs(words, 3, mail(), s_);
       const uint64_t *m = wait_mail();
