@@ -1351,7 +1351,8 @@ class Executor {
                                            : std::max<uint64_t>(heavy_deg_sliced_, 128ull * P);
     if (ordered && member) fail(OMX_E_INVALID, "internal: an ordered expansion has no fused check");
     // per-tile sums → one-workgroup scan (posts the totals to the host) → per-tile offsets and chunks
-    DBuf<uint64_t> blk(&pool_, (uint64_t)(kBinKeys + P) * bin_tiles(R)), qb(&pool_, P + 1);
+    // (qb: the P + 1 chunk bounds, then the keys' totals of the per-key scan, launch_bin_scan)
+    DBuf<uint64_t> blk(&pool_, (uint64_t)(kBinKeys + P) * bin_tiles(R)), qb(&pool_, 2ull * P + 1 + kBinKeys);
     // a sliced hop that writes rows sizes its arenas from the target bitmap's density per slice
     // (posted with the binning totals); an arena found short re-runs the hop with the exact bound
     const bool estimate = sliced && write && arena_estimate_;

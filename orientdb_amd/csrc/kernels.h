@@ -214,6 +214,7 @@ inline unsigned bin_tiles(uint64_t R) { return (unsigned)((R + 1 + kBinBlock - 1
 void launch_bin_count(bool sliced, const uint32_t *src, uint64_t R, const DAdj &adj, const DCuts &cuts,
                       uint64_t heavy_deg, uint32_t P, uint64_t *blk, hipStream_t s, uint32_t chunk_shift = 10);
 // extra[0..nextra) (device words) are posted after the totals: mail[5 + P + i]
+// qb: 2·P + 1 + kBinKeys words (the P + 1 chunk bounds, then scratch for the per-key scan's totals)
 void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const Mail &mail, hipStream_t s,
                      const unsigned long long *extra = nullptr, uint32_t nextra = 0);
 // out[q] = set bits of slice q (2^shift vertices) of a V-bit bitmap, q < P

@@ -1259,6 +1259,64 @@ __global__ __launch_bounds__(1024) void k_bin_scan(uint64_t *blk, uint32_t nb, u
   }
 }
 
+// The same scan with one workgroup per key (nb ≤ 4096: four tiles a thread, in registers): the keys'
+// scans run side by side instead of one after another in a single workgroup (52 µs at M1's 3.6 K
+// tiles × 19 keys), and k_bin_scan_post turns the keys' totals into the slices' chunk bounds and the
+// same mail as k_bin_scan's.
+__global__ __launch_bounds__(1024) void k_bin_scan_key(uint64_t *blk, uint32_t nb, uint64_t *tot) {
+  constexpr int PER = 4;
+  __shared__ unsigned long long s_w[16];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t *a = blk + (uint64_t)blockIdx.x * nb;
+  const uint32_t i0 = threadIdx.x * PER;
+  uint64_t v[PER];
+  unsigned long long c = 0;
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const uint32_t i = i0 + p;
+    const uint64_t x = a[i < nb ? i : nb - 1];
+    v[p] = x & (0ull - (uint64_t)(i < nb));  // a mask, not a select: the load stays unconditional
+    c += v[p];
+  }
+  unsigned long long incl = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(incl, off, 64);
+    if (lane >= (uint32_t)off) incl += y;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  unsigned long long run = incl - c, all = 0;
+  for (uint32_t w = 0; w < 16; ++w) {
+    if (w < wave) run += s_w[w];
+    all += s_w[w];
+  }
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    if (i0 + p < nb) a[i0 + p] = run;
+    run += v[p];
+  }
+  if (threadIdx.x == 0) tot[blockIdx.x] = all;
+}
+__global__ void k_bin_scan_post(const uint64_t *tot, uint32_t P, uint64_t *qb, Mail mail,
+                                const unsigned long long *extra, uint32_t nextra) {
+  if (threadIdx.x != 0) return;
+  uint64_t q0 = 0;
+  mail.p[0] = tot[0];
+  mail.p[1] = tot[1];
+  mail.p[3] = tot[2];
+  for (uint32_t q = 0; q < P; ++q) {
+    qb[q] = q0;
+    mail.p[4 + q] = q0;
+    q0 += tot[kBinKeys + q];
+  }
+  qb[P] = q0;
+  mail.p[4 + P] = q0;
+  mail.p[2] = q0;
+  for (uint32_t i = 0; i < nextra; ++i) mail.p[5 + P + i] = extra[i];
+  mail_post(mail);
+}
+
 // Every tile redoes its rows' keys, adds the tile prefixes and writes the light offsets, the light
 // rows' first col index and the heavy rows' chunks. lr.row == nullptr: light data indexed by row
 // (loffs[R+1], lbase[R]: merge-path kernel); else compacted to the light rows in order (loffs[NL+1],
@@ -1365,6 +1423,14 @@ void launch_bin_scan(uint64_t *blk, uint64_t R, uint32_t P, uint64_t *qb, const 
                      const unsigned long long *extra, uint32_t nextra) {
   const unsigned nb = bin_tiles(R);
   if (5 + P + nextra >= (uint32_t)kMailSeq) fail(OMX_E_INVALID, "internal: bin-scan mail overflows");
+  if (nb <= 4096 && P > 4) {  // one workgroup per key, then the bounds and the mail
+    uint64_t *tot = qb + P + 1;  // (qb holds P + 1 + kBinKeys + P words, launch_bin_scan's contract)
+    hipLaunchKernelGGL(k_bin_scan_key, dim3(kBinKeys + P), dim3(1024), 0, s, blk, nb, tot);
+    KCHECK("k_bin_scan_key");
+    hipLaunchKernelGGL(k_bin_scan_post, dim3(1), dim3(64), 0, s, tot, P, qb, mail, extra, nextra);
+    KCHECK("k_bin_scan_post");
+    return;
+  }
   if (nb <= 4096 && P <= 4) {  // registers for (3 + P) keys × 4 tiles
 #define OMX_BS(M) hipLaunchKernelGGL((k_bin_scan<M, 4>), dim3(1), dim3(1024), 0, s, blk, nb, P, qb, mail, extra, nextra)
     if (P <= 1) OMX_BS(1);
