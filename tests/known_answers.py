@@ -178,7 +178,7 @@ KNOWN = [
      ("field_len", "foo"), (1, 2), True),
     ("testConditionInSquareBrackets", 1152,
      "match {class:TriangleV, as: friend1, where: (uid = 0)}return friend1.out('TriangleE')[uid = 2] as foo", None,
-     ("field_len", "foo"), (1, 1), True),
+     ("list_uids", "foo"), (1, [2]), True),  # :1168-1171: one vertex, uid == 2
     ("testIndexedEdge", 1175,
      "match {class:IndexedVertex, as: one, where: (uid = 0)}.out('IndexedEdge'){class:IndexedVertex, as: two, where: (uid = 1)}return one, two",
      None, None, (1, None), True),

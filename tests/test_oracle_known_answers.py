@@ -33,6 +33,8 @@ def check_outer(db, rows, outer, expect):
         assert all(isinstance(r[key], Record) and not r[key].is_edge for r in rows)
     elif kind == "field_len":
         assert all(len(r[key]) == values for r in rows)
+    elif kind == "list_uids":  # a list of vertices whose uids are `values`, in order
+        assert all([x.props["uid"] for x in r[key]] == values for r in rows)
     elif kind == "field_prefix":
         assert all(str(r[key]).startswith(values) for r in rows)
     else:
