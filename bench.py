@@ -204,6 +204,10 @@ def cpu_baseline(g, query, target_s=12.0, single_thread_too=False):
     nroots_total = int(np.count_nonzero(cg.columns[m.group(1)] < int(m.group(2)))) if m else g.V
     out = dfs_sample(dfs, cg, query, threads, target_s, nroots_total)
     out["cores_visible"] = visible
+    try:  # the same bindings set-at-a-time (the set-based CPU path beside the DFS)
+        out["set_based"] = set_sample(dfs, cg, query, threads, target_s, nroots_total)
+    except NotImplementedError:
+        pass
     if single_thread_too:  # configs[0]: the faithful one-thread DFS beside the port on the job's cores
         one = dfs_sample(dfs, cg, query, 1, target_s / 2, nroots_total)
         out["single_thread"] = {k: one[k] for k in ("value", "unit", "cores", "kind", "sample", "bindings_per_s")}
@@ -228,6 +232,30 @@ def dfs_sample(dfs, cg, query, threads, target_s, nroots_total):
             "sample": "%d of %d roots x %d repetitions (%.1f s, %d edges, %d bindings; oracle/dfs_ref.c DFS, %d "
                       "thread%s)" % (sample, nroots_total, reps, secs, edges, bindings, threads,
                                      "" if threads == 1 else "s = the job's host-core share (OMP_NUM_THREADS)"),
+            "bindings_per_s": bindings / secs}
+
+
+def set_sample(dfs, cg, query, threads, target_s, nroots_total):
+    """oracle/set_ref.c (the device's algebra on the host cores: per hop the distinct sources' filtered
+    lists once, then every row written) over the whole root set when it fits ≈ target_s / 3 per run, else a
+    bounded root sample; repeated until ≈ target_s is timed."""
+    probe = dfs.set_run(cg, query, nthreads=threads, root_sample=min(nroots_total, 4096))
+    per_root = max(probe["seconds"] / max(probe["nroots"], 1), 1e-9)
+    sample = int(min(nroots_total, max(4096, target_s / 3 / per_root)))
+    edges = bindings = 0
+    secs = 0.0
+    reps = 0
+    while secs < target_s and reps < 1000:
+        r = dfs.set_run(cg, query, nthreads=threads, root_sample=sample)
+        if reps:  # the first run pays the buffers' first touch
+            edges += r["edges"]
+            bindings += r["bindings"]
+            secs += r["seconds"]
+        reps += 1
+    return {"value": edges / secs / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
+            "sample": "%d of %d roots x %d timed repetitions (%.1f s, %d edges, %d rows written; oracle/set_ref.c "
+                      "set-at-a-time: distinct sources' filtered lists, then the rows, %d threads)" % (
+                          sample, nroots_total, reps - 1, secs, edges, bindings, threads),
             "bindings_per_s": bindings / secs}
 
 

@@ -30,6 +30,15 @@ class dfs_plan(C.Structure):
     _fields_ = [("nsteps", C.c_int32), ("naliases", C.c_int32), ("steps", dfs_step * MAXA)]
 
 
+class set_hop(C.Structure):
+    _fields_ = [("src", C.c_int32), ("set_valued", C.c_int32), ("rp", C.POINTER(C.c_uint64)),
+                ("col", C.POINTER(C.c_uint32)), ("where_bm", C.POINTER(C.c_uint64))]
+
+
+class set_plan(C.Structure):
+    _fields_ = [("nhops", C.c_int32), ("hops", set_hop * 8)]
+
+
 _lib = None
 
 
@@ -46,6 +55,13 @@ def lib():
         L.dfs_run_ex.argtypes = L.dfs_run.argtypes + [C.POINTER(C.c_int32), C.c_int32, C.c_uint64,
                                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.dfs_free.argtypes = [C.c_void_p]
+        L.set_run.restype = C.c_int64
+        L.set_run.argtypes = [C.POINTER(set_plan), C.c_uint32, C.POINTER(C.c_uint32), C.c_int64, C.c_int32,
+                              C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.set_digest.restype = C.c_uint64
+        L.set_digest.argtypes = [C.POINTER(C.c_int32), C.c_int32, C.c_uint64, C.c_int32]
+        L.set_rows.restype = C.POINTER(C.c_uint32)
+        L.set_rows.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
         L.bfs_varlen.restype = C.c_int64
         L.bfs_varlen.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32),
                                  C.c_int64, C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
@@ -165,87 +181,109 @@ def _bm_from_mask(mask):
     return words
 
 
+class _Steps:
+    """The oracle planner's fixed-length plan over a CsrGraph (shared by the DFS and the set-based runs):
+    sortEdges order, per step source/target alias, mode (0 free, 1 candidate, 2 bound), direction, CSR
+    parts, target WHERE / candidate masks."""
+
+    def __init__(self, g, query, params=None):
+        mo = MatchOracle(g.schema, query)
+        pmap = MatchOracle._param_map(params)
+        est = mo.estimate_root_entries(Ctx(pmap))
+        sorted_edges = mo.sort_edges(est)
+        self.mo = mo
+        self.aliases = aliases = list(mo.nodes)
+        self.aidx = aidx = {a: i for i, a in enumerate(aliases)}
+        prefetched = [a for a, v in est.items() if v < THRESHOLD] or [mo._next_alias(est, MatchContext())]
+        if sorted_edges:
+            e0, f0 = sorted_edges[0]
+            root = e0.out.alias if f0 else e0.in_.alias
+        else:
+            root = aliases[0]
+        self.root = root
+        cols = g.columns
+        if any(n.optional for n in mo.nodes.values()):
+            raise NotImplementedError("oracle C path: optional nodes")
+        if not all(e[0] == "field" and e[1] in aidx for e, _, _ in mo.st.return_items) and not any(
+                t.replace(" ", "").lower() in ("$matches", "$patterns", "$paths", "$elements", "$pathelements")
+                for _, _, t in mo.st.return_items):
+            raise NotImplementedError("oracle C path: RETURN expressions")
+
+        def where_mask(alias):
+            w = mo.where_of(alias)
+            if w is None:
+                return None
+            m = np_eval(w, cols, pmap)
+            return np.broadcast_to(np.asarray(m, bool), (g.V,))
+
+        def cand_mask(alias):
+            m = where_mask(alias)
+            return np.ones(g.V, bool) if m is None else m  # every vertex is a Person
+
+        self.cand_mask = cand_mask
+        self.steps = []
+        bound = {root}
+        for e, fwd in sorted_edges:
+            it = e.item
+            if it.multi is not None or it.filter.while_ is not None or it.filter.max_depth is not None:
+                raise NotImplementedError("oracle C path: variable-length / multi items")
+            s_alias, t_alias = (e.out.alias, e.in_.alias) if fwd else (e.in_.alias, e.out.alias)
+            if s_alias not in bound:
+                raise NotImplementedError("oracle C path: disconnected pattern")
+            m = it.method.lower()
+            if not fwd:
+                m = {"out": "in", "in": "out", "both": "both"}[m]
+            parts = {"out": lambda: [(g.rp, g.col)], "in": lambda: [(g.trp, g.tcol)],
+                     "both": lambda: [(g.rp, g.col), (g.trp, g.tcol)]}[m]()
+            if it.labels and not any(lab.lower() in ("knows", "e") for lab in it.labels):
+                parts = []
+            mode = 2 if t_alias in bound else (1 if t_alias in prefetched else 0)
+            self.steps.append({"src": aidx[s_alias], "dst": aidx[t_alias], "forward": bool(fwd), "mode": mode,
+                               "parts": parts, "where": where_mask(t_alias),
+                               "cand": cand_mask(t_alias) if mode == 1 else None,
+                               "need_dedup": len(parts) > 1 or not g.simple})
+            bound.add(t_alias)
+        if len(bound) != len(aliases):
+            raise NotImplementedError("oracle C path: cartesian product")
+
+    def roots(self, shard=None, root_sample=None):
+        roots = np.nonzero(self.cand_mask(self.root))[0].astype(np.uint32)
+        if shard is not None:  # the multi-GPU partition: root vertex v belongs to rank v % world
+            roots = roots[roots % shard[1] == shard[0]]
+        if root_sample is not None:
+            roots = roots[:root_sample]
+        return roots
+
+
 def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=None, digest=None, distinct=None):
     """Returns dict(rows=np.uint32[n, k] (distinct, sorted; None when emit=False), aliases, bindings,
     edges, seconds, nroots). digest = RETURN aliases: every binding's projection is hashed (row_digest of
     RIDs #11:v) into r["digest"] — the digest of the result when its rows are distinct by construction.
     distinct = one RETURN alias: r["distinct"] = its distinct vertex ids (sorted), via a V-bit set."""
-    mo = MatchOracle(g.schema, query)
-    pmap = MatchOracle._param_map(params)
-    est = mo.estimate_root_entries(Ctx(pmap))
-    sorted_edges = mo.sort_edges(est)
-    aliases = list(mo.nodes)
-    aidx = {a: i for i, a in enumerate(aliases)}
-    prefetched = [a for a, v in est.items() if v < THRESHOLD] or [mo._next_alias(est, MatchContext())]
-    if sorted_edges:
-        e0, f0 = sorted_edges[0]
-        root = e0.out.alias if f0 else e0.in_.alias
-    else:
-        root = aliases[0]
-    cols = g.columns
+    sp = _Steps(g, query, params)
+    aliases, aidx, root = sp.aliases, sp.aidx, sp.root
     keep = []
-    if any(n.optional for n in mo.nodes.values()):
-        raise NotImplementedError("oracle C path: optional nodes")
-    if not all(e[0] == "field" and e[1] in aidx for e, _, _ in mo.st.return_items) and not any(
-            t.replace(" ", "").lower() in ("$matches", "$patterns", "$paths", "$elements", "$pathelements")
-            for _, _, t in mo.st.return_items):
-        raise NotImplementedError("oracle C path: RETURN expressions")
-
-    def where_mask(alias):
-        w = mo.where_of(alias)
-        if w is None:
-            return None
-        m = np_eval(w, cols, pmap)
-        return np.broadcast_to(np.asarray(m, bool), (g.V,))
-
-    def cand_mask(alias):
-        m = where_mask(alias)
-        return np.ones(g.V, bool) if m is None else m  # every vertex is a Person
-
     plan = dfs_plan()
     plan.naliases = len(aliases)
-    bound = {root}
-    for i, (e, fwd) in enumerate(sorted_edges):
-        it = e.item
-        if it.multi is not None or it.filter.while_ is not None or it.filter.max_depth is not None:
-            raise NotImplementedError("oracle C path: variable-length / multi items")
-        s_alias, t_alias = (e.out.alias, e.in_.alias) if fwd else (e.in_.alias, e.out.alias)
-        if s_alias not in bound:
-            raise NotImplementedError("oracle C path: disconnected pattern")
+    for i, d in enumerate(sp.steps):
         st = plan.steps[i]
-        st.src, st.dst, st.forward = aidx[s_alias], aidx[t_alias], int(fwd)
-        st.mode = 2 if t_alias in bound else (1 if t_alias in prefetched else 0)
-        m = it.method.lower()
-        if not fwd:
-            m = {"out": "in", "in": "out", "both": "both"}[m]
-        parts = {"out": lambda: [(g.rp, g.col)], "in": lambda: [(g.trp, g.tcol)],
-                 "both": lambda: [(g.rp, g.col), (g.trp, g.tcol)]}[m]()
-        if it.labels and not any(lab.lower() in ("knows", "e") for lab in it.labels):
-            parts = []
-        st.nparts = len(parts)
-        for q, (rp, col) in enumerate(parts):
+        st.src, st.dst, st.forward, st.mode = d["src"], d["dst"], int(d["forward"]), d["mode"]
+        st.nparts = len(d["parts"])
+        for q, (rp, col) in enumerate(d["parts"]):
             st.rp[q] = rp.ctypes.data_as(C.POINTER(C.c_uint64))
             st.col[q] = col.ctypes.data_as(C.POINTER(C.c_uint32))
-        st.need_dedup = int(len(parts) > 1 or not g.simple)
+        st.need_dedup = int(d["need_dedup"])
         st.sorted = 1  # CsrGraph rows are sorted (the generator and the transpose sort them)
-        wm = where_mask(t_alias)
-        if wm is not None:
-            w = _bm_from_mask(wm)
+        if d["where"] is not None:
+            w = _bm_from_mask(d["where"])
             keep.append(w)
             st.where_bm = w.ctypes.data_as(C.POINTER(C.c_uint64))
-        if st.mode == 1:
-            cb = _bm_from_mask(cand_mask(t_alias))
+        if d["mode"] == 1:
+            cb = _bm_from_mask(d["cand"])
             keep.append(cb)
             st.cand_bm = cb.ctypes.data_as(C.POINTER(C.c_uint64))
-        bound.add(t_alias)
-    plan.nsteps = len(sorted_edges)
-    if len(bound) != len(aliases):
-        raise NotImplementedError("oracle C path: cartesian product")
-    roots = np.nonzero(cand_mask(root))[0].astype(np.uint32)
-    if shard is not None:  # the multi-GPU partition: root vertex v belongs to rank v % world
-        roots = roots[roots % shard[1] == shard[0]]
-    if root_sample is not None:
-        roots = roots[:root_sample]
+    plan.nsteps = len(sp.steps)
+    roots = sp.roots(shard, root_sample)
     out = C.POINTER(C.c_uint32)()
     nrows = C.c_uint64()
     edges = C.c_uint64()
@@ -270,6 +308,60 @@ def run(g, query, params=None, nthreads=1, emit=True, root_sample=None, shard=No
     if distinct:
         bits = np.unpackbits(seen.view(np.uint8), bitorder="little")[:g.V]
         res["distinct"] = np.nonzero(bits)[0].astype(np.uint32)
+    return res
+
+
+def set_run(g, query, params=None, nthreads=1, root_sample=None, digest=None, distinct=None, rows=False):
+    """oracle/set_ref.c: the same bindings as run() for a chain of free hops (every step binds a new alias
+    from a bound one: no closing check, no prefetched candidates), computed set-at-a-time — per hop the
+    distinct sources' filtered lists once, then the rows over them (the device's algebra, on the host
+    cores). Returns dict(bindings, edges, seconds, nroots, aliases[, digest][, distinct][, rows])."""
+    sp = _Steps(g, query, params)
+    keep = []
+    plan = set_plan()
+    if len(sp.steps) > 8:
+        raise NotImplementedError("oracle set path: more than 8 hops")
+    # column h + 1 of the row table is the h-th step's target
+    colof = {sp.aidx[sp.root]: 0}
+    for i, d in enumerate(sp.steps):
+        if d["mode"] != 0 or len(d["parts"]) != 1:
+            raise NotImplementedError("oracle set path: bound / candidate targets or several CSR parts")
+        h = plan.hops[i]
+        h.src = colof[d["src"]]
+        colof[d["dst"]] = i + 1
+        rp, col = d["parts"][0]
+        h.rp = rp.ctypes.data_as(C.POINTER(C.c_uint64))
+        h.col = col.ctypes.data_as(C.POINTER(C.c_uint32))
+        if d["where"] is not None:
+            w = _bm_from_mask(d["where"])
+            keep.append(w)
+            h.where_bm = w.ctypes.data_as(C.POINTER(C.c_uint64))
+            h.set_valued = int(d["forward"] and d["need_dedup"])
+    plan.nhops = len(sp.steps)
+    roots = np.ascontiguousarray(sp.roots(None, root_sample))
+    mark = None
+    if distinct is not None:
+        if colof[sp.aidx[distinct]] != len(sp.steps) or not sp.steps:
+            raise NotImplementedError("oracle set path: a distinct column other than the last hop's")
+        mark = np.zeros((g.V + 63) // 64, np.uint64)
+    edges = C.c_uint64()
+    t0 = time.perf_counter()
+    b = lib().set_run(C.byref(plan), g.V, roots.ctypes.data_as(C.POINTER(C.c_uint32)), len(roots), int(nthreads),
+                      mark.ctypes.data_as(C.POINTER(C.c_uint64)) if mark is not None else None, C.byref(edges))
+    dt = time.perf_counter() - t0
+    res = {"bindings": int(b), "edges": edges.value, "seconds": dt, "nroots": len(roots), "aliases": sp.aliases}
+    if digest:
+        proj = (C.c_int32 * len(digest))(*[colof[sp.aidx[a]] for a in digest])
+        res["digest"] = lib().set_digest(proj, len(digest), RID_BASE, int(nthreads))
+    if distinct is not None:
+        bits = np.unpackbits(mark.view(np.uint8), bitorder="little")[:g.V]
+        res["distinct"] = np.nonzero(bits)[0].astype(np.uint32)
+    if rows:
+        n, k = C.c_uint64(), C.c_int32()
+        p = lib().set_rows(C.byref(n), C.byref(k))
+        arr = np.ctypeslib.as_array(p, shape=(max(1, n.value * k.value),))[:n.value * k.value].reshape(-1, k.value)
+        order = [colof[sp.aidx[a]] for a in sp.aliases]
+        res["rows"] = arr[:, order].copy()
     return res
 
 

@@ -19,6 +19,9 @@ def main():
     if d.get("cpu_baseline"):
         c = d["cpu_baseline"]
         print("  cpu_baseline: %.3f %s on %s threads" % (c["value"], c["unit"], c["cores"]))
+        if c.get("set_based"):
+            print("  cpu_baseline set_based: %.3f %s on %s threads" % (c["set_based"]["value"], c["set_based"]["unit"],
+                                                                      c["set_based"]["cores"]))
     if len(sys.argv) > 2:
         f = glob.glob(os.path.join(sys.argv[2], "**", "*kernel_stats.csv"), recursive=True)
         if f:
