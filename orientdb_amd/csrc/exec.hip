@@ -167,24 +167,29 @@ static void launch_gather_u64_at(const uint64_t *src, const uint64_t *idx, uint6
   hipLaunchKernelGGL(k_gather_u64_at, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, idx, n, out);
 }
 
-// out[id[i]] = deg[i] (a fetched adjacency's degrees placed at their vertices)
-__global__ void k_scatter_deg(const uint32_t *id, const uint32_t *deg, uint64_t n, uint64_t *out) {
+// out[id[i]] = lo[i] | hi[i] << 32 (a fetched adjacency's degrees placed at their vertices)
+__global__ void k_scatter_deg(const uint32_t *id, const uint32_t *lo, const uint32_t *hi, uint64_t n, uint64_t *out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[id[i]] = deg[i];
+  if (i < n) out[id[i]] = (uint64_t)lo[i] | (uint64_t)hi[i] << 32;
 }
-static void launch_scatter_deg(const uint32_t *id, const uint32_t *deg, uint64_t n, uint64_t *out, hipStream_t s) {
+static void launch_scatter_deg(const uint32_t *id, const uint32_t *lo, const uint32_t *hi, uint64_t n, uint64_t *out,
+                               hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_scatter_deg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, id, deg, n, out);
+  hipLaunchKernelGGL(k_scatter_deg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, id, lo, hi, n, out);
 }
 
-// out[i] = (u32) in[i] (degrees of a partition's rows: below 2^32)
-__global__ void k_u64_to_u32(const uint64_t *in, uint64_t n, uint32_t *out) {
+// lo[i], hi[i] = the two words of in[i]: a u64 column as two u32 columns for a row exchange (a multigraph
+// row may hold 2^32 or more entries)
+__global__ void k_u64_split(const uint64_t *in, uint64_t n, uint32_t *lo, uint32_t *hi) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (uint32_t)in[i];
+  if (i < n) {
+    lo[i] = (uint32_t)in[i];
+    hi[i] = (uint32_t)(in[i] >> 32);
+  }
 }
-static void launch_u64_to_u32(const uint64_t *in, uint64_t n, uint32_t *out, hipStream_t s) {
+static void launch_u64_split(const uint64_t *in, uint64_t n, uint32_t *lo, uint32_t *hi, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_u64_to_u32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, n, out);
+  hipLaunchKernelGGL(k_u64_split, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, n, lo, hi);
 }
 
 // head[i] = 1 where a run of equal sorted keys starts
@@ -947,12 +952,12 @@ class Executor {
       if (n) launch_route_owner(ids.p, n, block_, (uint32_t)W, dest.p, hist.p, s_);
       n = exchange_cols({&ids}, n, dest, hist);
       // 3. the owners' degrees and lists, in id order
-      DBuf<uint32_t> deg32(&pool_, std::max<uint64_t>(n, 1)), lists;
+      DBuf<uint32_t> dlo(&pool_, std::max<uint64_t>(n, 1)), dhi(&pool_, std::max<uint64_t>(n, 1)), lists;
       uint64_t nl = 0;
       if (n) {
         DBuf<uint64_t> deg(&pool_, n + 1);
         launch_row_degree(ids.p, n, make_adj(as), deg.p, s_);
-        launch_u64_to_u32(deg.p, n, deg32.p, s_);
+        launch_u64_split(deg.p, n, dlo.p, dhi.p, s_);
         ExpandOut o = expand_core(ids.p, n, as, nullptr, {}, true, false, nullptr, nullptr, nullptr, nullptr, true);
         nl = o.n;
         lists = nl ? std::move(o.dst) : DBuf<uint32_t>(&pool_, 1);
@@ -960,19 +965,21 @@ class Executor {
         lists = DBuf<uint32_t>(&pool_, 1);
       }
       // 4. back to rank 0: (vertex, degree) rows, then the lists (both in rank order, then id order)
-      n = to_rank0({&ids, &deg32}, n);
+      n = to_rank0({&ids, &dlo, &dhi}, n);
       nl = to_rank0({&lists}, nl);
       if (tr_->rank() != 0 || n == 0) continue;
-      std::vector<uint32_t> hid(n), hdeg(n), hl(nl);
+      std::vector<uint32_t> hid(n), hlo(n), hhi(n), hl(nl);
       HIP_CHECK(hipMemcpyAsync(hid.data(), ids.p, n * 4, hipMemcpyDeviceToHost, s_));
-      HIP_CHECK(hipMemcpyAsync(hdeg.data(), deg32.p, n * 4, hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipMemcpyAsync(hlo.data(), dlo.p, n * 4, hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipMemcpyAsync(hhi.data(), dhi.p, n * 4, hipMemcpyDeviceToHost, s_));
       if (nl) HIP_CHECK(hipMemcpyAsync(hl.data(), lists.p, nl * 4, hipMemcpyDeviceToHost, s_));
       HIP_CHECK(hipStreamSynchronize(s_));
       uint64_t at = 0;
       for (uint64_t i = 0; i < n; ++i) {
-        if (at + hdeg[i] > nl) fail(OMX_E_INVALID, "internal: fetched adjacency lists are short");
-        out[{sa.first, hid[i]}] = std::vector<uint32_t>(hl.begin() + at, hl.begin() + at + hdeg[i]);
-        at += hdeg[i];
+        const uint64_t d = (uint64_t)hlo[i] | (uint64_t)hhi[i] << 32;
+        if (at + d > nl) fail(OMX_E_INVALID, "internal: fetched adjacency lists are short");
+        out[{sa.first, hid[i]}] = std::vector<uint32_t>(hl.begin() + at, hl.begin() + at + d);
+        at += d;
       }
     }
   }
@@ -1192,9 +1199,11 @@ class Executor {
     if (!es.d_pull_col[dir]) return h;
     const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
     if (!es.d_hub_col[dir]) {
-      uint64_t *hrp = nullptr;
-      uint32_t *hcol = nullptr;
-      uint64_t nh = 0;
+      // every field is built into locals and published only once all six exist (a throw in the tile
+      // build would otherwise leave d_hub_col set with no tiles for the next level to read)
+      uint64_t *hrp = nullptr, *wrb = nullptr;
+      uint32_t *hcol = nullptr, *wtiles = nullptr;
+      uint64_t nh = 0, wnreg = 0;
       try {
         HIP_CHECK(hipMalloc((void **)&hrp, ((uint64_t)g_.V + 1) * 8));
         // excl[e] = hub entries before e (u32 when E < 2^32), then hub_rp[v] = excl[rp[v]]
@@ -1209,6 +1218,7 @@ class Executor {
         hipcub::TransformInputIterator<uint8_t, HubFlag8, const uint32_t *> f8(es.d_pull_col[dir], HubFlag8());
         if (E) cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, es.d_pull_col[dir], f8, hcol, nsel.p, (int64_t)E, s_); });
         HIP_CHECK(hipStreamSynchronize(s_));
+        pullw_build(hrp, nh, wrb, wtiles, wnreg);
       } catch (...) {
         if (hrp) (void)hipFree(hrp);
         if (hcol) (void)hipFree(hcol);
@@ -1217,8 +1227,10 @@ class Executor {
       es.d_hub_rp[dir] = hrp;
       es.d_hub_col[dir] = hcol;
       es.hub_entries[dir] = nh;
+      es.d_hubw_rb[dir] = wrb;
+      es.d_hubw_tiles[dir] = wtiles;
+      es.hubw_nreg[dir] = wnreg;
       g_.device_bytes += ((uint64_t)g_.V + 1) * 8 + nh * 4;
-      pullw_build(hrp, nh, es.d_hubw_rb[dir], es.d_hubw_tiles[dir], es.hubw_nreg[dir]);
     }
     h.rp = es.d_hub_rp[dir];
     h.col = es.d_hub_col[dir];
@@ -2256,25 +2268,25 @@ class Executor {
     HIP_CHECK(hipMemsetAsync(hist.p, 0, W * sizeof(uint64_t), s_));
     if (m) launch_route_owner(ids.p, m, block_, (uint32_t)W, dest.p, hist.p, s_);
     m = exchange_cols({&ids}, m, dest, hist);
-    DBuf<uint32_t> deg32(&pool_, std::max<uint64_t>(m, 1)), lists;
+    DBuf<uint32_t> dlo(&pool_, std::max<uint64_t>(m, 1)), dhi(&pool_, std::max<uint64_t>(m, 1)), lists;
     uint64_t nl = 0;
     if (m) {
       DBuf<uint64_t> deg(&pool_, m + 1);
       launch_row_degree(ids.p, m, make_adj(as), deg.p, s_);
-      launch_u64_to_u32(deg.p, m, deg32.p, s_);
+      launch_u64_split(deg.p, m, dlo.p, dhi.p, s_);
       ExpandOut o = expand_core(ids.p, m, as, nullptr, {}, true, false, nullptr, nullptr, nullptr, nullptr, true);
       nl = o.n;
       lists = nl ? std::move(o.dst) : DBuf<uint32_t>(&pool_, 1);
     } else {
       lists = DBuf<uint32_t>(&pool_, 1);
     }
-    m = to_rank0({&ids, &deg32}, m);
+    m = to_rank0({&ids, &dlo, &dhi}, m);
     nl = to_rank0({&lists}, nl);
     if (!out) return;
     // rank 0: rp[v + 1] - rp[v] = the fetched degree of v (0 for the others), col = the lists in order
     DBuf<uint64_t> dv(&pool_, (uint64_t)g_.V + 1);
     HIP_CHECK(hipMemsetAsync(dv.p, 0, ((uint64_t)g_.V + 1) * 8, s_));
-    if (m) launch_scatter_deg(ids.p, deg32.p, m, dv.p, s_);
+    if (m) launch_scatter_deg(ids.p, dlo.p, dhi.p, m, dv.p, s_);
     out->rp = DBuf<uint64_t>(&pool_, (uint64_t)g_.V + 1);
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, dv.p, out->rp.p, (int64_t)g_.V + 1, s_); });
     out->col = std::move(lists);

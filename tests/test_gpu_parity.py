@@ -176,6 +176,10 @@ RMAT_QUERIES = [
      ["me", "f"]),
     ("matched_and_filter", "MATCH {class:Person,as:me,where:(age < 20)}<-Knows-{as:x}-Knows->{as:f, where:($matched.me <> $currentMatch and age < 50)} RETURN me, x, f",
      ["me", "x", "f"]),
+    # b's WHERE declared on another occurrence of the alias: rebindFilters (P/OMatchStatement.java:185-195)
+    # gives the forward hop into b the merged filter, so that hop is filtered and set-valued
+    ("where_other_occurrence", "MATCH {class:Person,as:a,where:(uid < 60)}-Knows->{as:b}, {as:b,where:(age < 50)} RETURN a,b",
+     ["a", "b"]),
     ("bound_candidate", "MATCH {class:Person,as:a,where:(uid = 1)}-Knows->{as:b},{class:Person,as:b,where:(uid < 600)} RETURN a,b",
      ["a", "b"]),
     # optional nodes (P/OMatchStatement.java:448-458): unmatched → the row continues with a null alias
@@ -579,7 +583,8 @@ def test_keep_device_segmented_result(rmat10):
 
 
 @pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in ("c2_both_ends", "c1_fof", "both_dir", "triangle",
-                                                                    "varlen_depth", "three_hop")],
+                                                                    "varlen_depth", "three_hop",
+                                                                    "where_other_occurrence")],
                          ids=lambda q: q[0])
 def test_rmat_parity_multigraph(rmat10_raw, q):
     g, ref = rmat10_raw

@@ -10,7 +10,7 @@ chosen by its length-ratio rule (merge), forced on every row that fits a tile (m
 import numpy as np
 import pytest
 
-from tests.test_gpu_parity import _parity, gpu_set, rmat10, rmat10_raw  # noqa: F401  (fixtures)
+from tests.test_gpu_parity import _parity, gpu_set, rmat10, rmat10_raw, rmat16  # noqa: F401  (fixtures)
 
 pytestmark = pytest.mark.gpu
 
@@ -90,6 +90,28 @@ def test_cycle_parity_heavy_and_multigraph(rmat10, rmat10_raw, q, merge, monkeyp
         monkeypatch.setenv("OMX_FUSE_CHECK", "1")
         for k in ("n_rows", "bindings", "edges_traversed"):
             assert rs.info[k] == un[k], k
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_fused_check_after_set_valued_hop_multigraph(rmat10_raw, mode, monkeypatch):
+    """On the multigraph the hop b → c into a node with a WHERE is set-valued (P/OMatchPathItem.java:61,
+    71-78: a c reached over parallel edges binds once, Step::distinct_nb), so the closing check c → a
+    cannot be fused into it per edge: every mode gives the oracle's rows and bindings."""
+    _mode(monkeypatch, mode)
+    g, ref = rmat10_raw
+    q = CYCLES[1][1]
+    _parity(g, ref, q, _cols(q))
+
+
+@pytest.mark.parametrize("merge", ["1", "force", "0"])
+def test_filtered_triangle_rmat16(rmat16, merge, monkeypatch):
+    """A filtered fused triangle at RMAT-16 (longer lists than RMAT-10: hubs of degree ~10^3) with the merge
+    chosen by its ratio rule, forced, and off; rows and bindings equal dfs_ref.c's."""
+    monkeypatch.setenv("OMX_MERGE", merge)
+    g, ref = rmat16
+    q = "MATCH {class:Person,as:a,where:(age < 10)}-Knows->{as:b}-Knows->{as:c,where:(age > 20)}-Knows->{as:a} RETURN a,b,c"
+    rs = _parity(g, ref, q, ["a", "b", "c"])
+    assert rs.info["n_rows"] > 0
 
 
 @pytest.mark.parametrize("k", [1, 7, 64, 100, 128, 200])
