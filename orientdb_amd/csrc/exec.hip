@@ -66,7 +66,7 @@ class Timer {
                                        "k_expand_light_sliced", "k_expand_light_check", "k_expand_heavy_check",
                                        "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit", "k_bfs_push",
                                        "k_bfs_emit", "k_trav_filter", "trav_select", "k_femit",
-                                       "k_isect_merge"};
+                                       "k_isect_merge", "k_flists", "k_flist_copy"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
     return false;
@@ -266,6 +266,7 @@ class Executor {
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
     if (const char *sj = std::getenv("OMX_SEMI")) semi_ok_ = std::strcmp(sj, "0") != 0;
     if (const char *gq = std::getenv("OMX_GRP32")) grp32_ = std::strcmp(gq, "0") != 0;
+    if (const char *fl = std::getenv("OMX_FLISTS")) flists_ = std::strcmp(fl, "0") != 0;  // "0": the sliced path
     if (const char *dp = std::getenv("OMX_DEVPROJ")) devproj_ = std::strcmp(dp, "0") != 0;
     if (const char *mf = std::getenv("OMX_MARK_FUSE")) mark_fuse_ = std::strcmp(mf, "0") != 0;
     if (const char *am = std::getenv("OMX_ARENA_MARGIN")) arena_margin_ = std::max(0.0, std::strtod(am, nullptr));
@@ -1301,6 +1302,101 @@ class Executor {
     return es.d_pull_col[dir];
   }
 
+  // the lists col of one CSR for the filtered lists (k_flists): the kFlistHubs vertices of highest degree
+  // in the opposite CSR are hubs, entered as vb + rank (built once per CSR, into locals, published when
+  // complete)
+  const uint32_t *list_col_of(int eset, int dir, uint32_t *nhubs, const uint32_t **hubs, uint32_t *vb) {
+    EdgeSet &es = g_.esets[eset];
+    if (!es.d_list_col[dir]) {
+      const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
+      uint32_t *lcol = nullptr, *lh = nullptr, nh = 0;
+      try {
+        HIP_CHECK(hipMalloc((void **)&lcol, (E + 4) * 4));  // padded: the lists kernel reads whole aligned 16-byte groups
+        HIP_CHECK(hipMalloc((void **)&lh, (size_t)kFlistHubs * 4));
+        DBuf<uint32_t> hub_idx(&pool_, g_.V), hist(&pool_, 4096);
+        DBuf<unsigned long long> cnt(&pool_, 1);
+        nh = build_pull_col(g_.rp(es, dir), g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, kFlistHubs, hub_idx.p,
+                            hist.p, cnt.p, lh, lcol, cus(), s_);
+        launch_list_col(lcol, E, (uint32_t)(nwords_ * 64), s_);
+        HIP_CHECK(hipStreamSynchronize(s_));
+      } catch (...) {
+        if (lcol) (void)hipFree(lcol);
+        if (lh) (void)hipFree(lh);
+        throw;
+      }
+      es.d_list_col[dir] = lcol;
+      es.d_list_hubs[dir] = lh;
+      es.n_list_hubs[dir] = nh;
+      es.list_vb[dir] = (uint32_t)(nwords_ * 64);
+      g_.device_bytes += E * 4 + (uint64_t)kFlistHubs * 4;
+    }
+    *vb = es.list_vb[dir];
+    *nhubs = es.n_list_hubs[dir];
+    *hubs = es.d_list_hubs[dir];
+    return es.d_list_col[dir];
+  }
+
+  // the filtered lists L(u) of the U distinct sources ub (doff: the scan of their degrees, EU = doff[U])
+  // as a CSR (loff[U+1], lcol) through k_flists; returns the list entries
+  uint64_t filtered_lists(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const AdjSpec &adjs,
+                          const uint64_t *filter, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol) {
+    const int es = adjs.parts[0].first, dir = adjs.parts[0].second;
+    uint32_t nh = 0;
+    const uint32_t *hubs = nullptr;
+    uint32_t vb = 0;
+    const uint32_t *acol = list_col_of(es, dir, &nh, &hubs, &vb);
+    if ((uint64_t)vb != nwords_ * 64) fail(OMX_E_INVALID, "internal: lists col built for another filter width");
+    const uint64_t *rp = g_.rp(g_.esets[es], dir);
+    // the chunk space: every source's row as aligned 4-entry chunks of the col, in source order
+    const uint64_t ntb = flist_tiles_bound(EU, U);
+    DBuf<uint32_t> nch(&pool_, U + 1);
+    DBuf<uint64_t> coff(&pool_, U + 1), rb(&pool_, 2 * ntb), base(&pool_, ntb + 1);
+    HIP_CHECK(hipMemsetAsync(nch.p + U, 0, 4, s_));
+    launch_flist_nch(ub, doff, U, rp, nch.p, s_);
+    {
+      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> it(nch.p, CastU64());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, it, coff.p, (int64_t)(U + 1), s_); });
+    }
+    DBuf<uint4> info(&pool_, std::max<uint64_t>(U, 1));
+    launch_flist_prep(ub, doff, coff.p, U, rp, coff.p + U, info.p, rb.p, ntb, s_);
+    const uint64_t nbits = vb / 32 + (nh + 31) / 32;
+    DBuf<uint32_t> bits(&pool_, nbits), ntot(&pool_, ntb + 1), loc(&pool_, std::max<uint64_t>(U, 1));
+    DBuf<uint32_t> scratch(&pool_, ntb * flist_tile_entries());
+    HIP_CHECK(hipMemsetAsync(ntot.p, 0, (ntb + 1) * 4, s_));
+    launch_probe_bits(hubs, nh, filter, vb, bits.p, s_);
+    FlistArgs a{};
+    a.ub = ub;
+    a.U = U;
+    a.info = info.p;
+    a.ec = coff.p + U;
+    a.acol = acol;
+    a.E = dir == 0 ? g_.esets[es].n_edges : g_.esets[es].n_in_edges;
+    a.hubs = hubs;
+    a.nh = nh;
+    a.vb = vb;
+    a.bits = bits.p;
+    a.bbytes = nbits * 4;
+    a.rb = rb.p;
+    a.scratch = scratch.p;
+    a.ntot = ntot.p;
+    a.loc = loc.p;
+    tm_.begin("k_flists");
+    launch_flist(a, ntb, cus(), s_);
+    tm_.end(4ull * EU + 16ull * U);
+    {
+      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> it(ntot.p, CastU64());
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, it, base.p, (int64_t)(ntb + 1), s_); });
+    }
+    const uint64_t n = read1(base.p + ntb);
+    lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(n, 1));
+    loff = DBuf<uint64_t>(&pool_, U + 1);
+    a.lcol = lcol.p;
+    tm_.begin("k_flist_copy");
+    launch_flist_finish(a, coff.p, base.p, loff.p, ntb, cus(), s_);
+    tm_.end(8ull * n + 16ull * U);
+    return n;
+  }
+
   // the slice-cut index of every part of an adjacency (built once per CSR and slice size)
   DCuts slice_cuts_of(const AdjSpec &adjs, uint32_t P) {
     DCuts c{};
@@ -1853,6 +1949,10 @@ class Executor {
   // OMX_SEMI=0: write the rows as any other hop.
   bool semi_ = false, semi_ok_ = true;
   bool grp32_ = true;  // OMX_GRP32=0: 64-bit counters in the factorized grouping
+  // the distinct sources' filtered lists through the hub-annotated col (factor.hip k_flists, round 5);
+  // OMX_FLISTS=0: the sliced expansion + grouping (still the path for multigraph set-valued hops, several
+  // CSR parts and partitioned snapshots)
+  bool flists_ = true;
   uint64_t semi_bindings_ = 0;
   bool semi_for(const Step &st) const {
     if (!semi_ok_ || p_.kind != Plan::MATCH || st.kind != S_EXPAND || st.optional || p_.optional[st.dst] ||
@@ -1989,7 +2089,7 @@ class Executor {
     const uint32_t *src = col_[st.src].p;
     uint64_t U = 0, Et = 0, EU = 0;
     DBuf<uint32_t> ub, g, perm_s;
-    DBuf<uint64_t> ubm;
+    DBuf<uint64_t> ubm, doffb;  // doffb: the scan of the distinct sources' degrees (doffb[U] = EU)
     const DAdj adj = make_adj(st.adj);
     // rows emitted by k_femit_w from the sources' lists: the rows are sorted by source here (the emission
     // wants them grouped), so the distinct sources are the sorted runs' heads and a row's source index
@@ -2019,18 +2119,20 @@ class Executor {
       cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, hc, g.p, (int64_t)R, s_); });
       launch_add_u32(g.p, R, -1, s_);
       // the distinct sources' degrees over the R-row bound (rows past U count 0), scanned
-      DBuf<uint64_t> udeg(&pool_, R + 1), doff(&pool_, R + 1);
+      DBuf<uint64_t> udeg(&pool_, R + 1);
+      doffb = DBuf<uint64_t>(&pool_, R + 1);
+      uint64_t *doff = doffb.p;
       tm_.begin("k_row_degree");
       launch_row_degree_dev(ub.p, nsel.p, R, adj, udeg.p, s_);
       tm_.end(R * 8ull);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(R + 1), s_); });
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff, (int64_t)(R + 1), s_); });
       // E_t = Σ_rows deg(source) = Σ over the sorted rows of their source's degree (no per-row row_ptr reads)
       {
         hipcub::CountingInputIterator<uint64_t> ci(0);
         hipcub::TransformInputIterator<uint64_t, RowSourceDeg, hipcub::CountingInputIterator<uint64_t>> rd(ci, RowSourceDeg{g.p, udeg.p});
         cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, rd, et.p, (int64_t)R, s_); });
       }
-      const uint64_t *words[3] = {et.p, nsel.p, doff.p + R};
+      const uint64_t *words[3] = {et.p, nsel.p, doff + R};
       launch_post_ptrs(words, 3, mail(), s_);
       const uint64_t *m = wait_mail();
       Et = m[0], U = m[1], EU = m[2];
@@ -2050,12 +2152,13 @@ class Executor {
       tm_.end(4ull * R + 8ull * nwords_);
       ub = bitmap_list(ubm.p, 0, 1, U);
       // the distinct sources' degrees, scanned
-      DBuf<uint64_t> udeg(&pool_, U + 1), doff(&pool_, U + 1);
+      DBuf<uint64_t> udeg(&pool_, U + 1);
+      doffb = DBuf<uint64_t>(&pool_, U + 1);
       tm_.begin("k_row_degree");
       launch_row_degree(ub.p, U, adj, udeg.p, s_);
       tm_.end(U * (4ull + 16ull * st.adj.parts.size()));
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff.p, (int64_t)(U + 1), s_); });
-      EU = read1(doff.p + U);
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doffb.p, (int64_t)(U + 1), s_); });
+      EU = read1(doffb.p + U);
     }
     if (Et < factor_min_ratio_ * EU) return false;
     edges_ += Et;
@@ -2073,60 +2176,75 @@ class Executor {
       launch_gather_u32(pos.p, src, R, g.p, s_);
       tm_.end(12ull * R);
     }
-    DBuf<unsigned long long> cnt(&pool_, U + 1);
-    DBuf<uint64_t> loff(&pool_, U + 1);
-    HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));
-    // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
-    // (the filtered lists stay in the expansion's per-worker segments: grouping reads them in place)
-    // (a set-valued hop over an adjacency that may repeat a neighbour: each list made distinct first)
+    // 2.-3. the filtered lists of the distinct sources, grouped by source (CSR loff / lcol)
     const bool nbset = st.distinct_nb && !st.adj.dup_free;
-    ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, !nbset);
-    edges_iter_ += l.E;
-    if (nbset && l.n) l.n = distinct_pairs(l.carry[0], l.dst, {}, l.n);
-    const uint64_t nlist = l.n;
-    // 3. grouped by source: offsets (U + 1) and the neighbours in group order (segmented lists under
-    // 2^32 entries: 32-bit counters and cursors, half the atomics' footprint)
-    const bool c32 = l.segmented && l.n < (1ull << 32) && grp32_;
-    DBuf<uint32_t> h32;
-    if (c32) {
-      h32 = DBuf<uint32_t>(&pool_, U + 1);
-      HIP_CHECK(hipMemsetAsync(h32.p, 0, (U + 1) * 4, s_));
-    }
-    if (l.n) {
-      tm_.begin("k_key_hist");
-      if (c32) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, h32.p, s_);
-      else if (l.segmented) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, s_);
-      else launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
-      tm_.end(4ull * l.n + (c32 ? 4ull : 8ull) * U);
-    }
-    if (c32) {
-      hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> hc(h32.p, CastU64());
-      cub([&](void *t, size_t &b) {
-        return hipcub::DeviceScan::ExclusiveSum(t, b, hc, loff.p, (int64_t)(U + 1), s_);
-      });
+    DBuf<uint64_t> loff;
+    DBuf<uint32_t> lcol;
+    uint64_t nlist = 0;
+    // (the chunk space's offsets are u32: EU / 4 + 2U chunks below 2^32)
+    if (flists_ && !nbset && st.adj.parts.size() == 1 && !g_.partitioned() && g_.V < 0x80000000u && EU > 0 &&
+        EU / 4 + 2 * U < 0xFFFFFF00ull) {
+      nlist = filtered_lists(ub.p, U, doffb.p, EU, st.adj, bitmap(st.filter_bm), loff, lcol);
+      edges_iter_ += EU;
+      if (write && semi_) {  // the new alias is never read again: the rows whose source has a list
+        semi_join(g, R, loff, cols);
+        return true;
+      }
     } else {
-      cub([&](void *t, size_t &b) {
-        return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
-      });
-    }
-    if (write && semi_) {  // the new alias is never read again: the rows whose source has a list
-      semi_join(g, R, loff, cols);
-      return true;
-    }
-    DBuf<uint32_t> lcol(&pool_, std::max<uint64_t>(l.n, 1));
-    if (l.n && c32) {
-      DBuf<uint32_t> cur(&pool_, U + 1);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, h32.p, cur.p, (int64_t)(U + 1), s_); });
-      tm_.begin("k_key_scatter");
-      launch_key_scatter_seg(l.carry[0].p, l.dst.p, l.seg_start.p, l.seg_count.p, l.nseg, cur.p, lcol.p, s_);
-      tm_.end(12ull * l.n + 4ull * U);
-    } else if (l.n) {
-      HIP_CHECK(hipMemcpyAsync(cnt.p, loff.p, (U + 1) * 8, hipMemcpyDeviceToDevice, s_));
-      tm_.begin("k_key_scatter");
-      if (l.segmented)
-        launch_key_scatter_seg(l.carry[0].p, l.dst.p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, lcol.p, s_);
-      else launch_key_scatter(l.carry[0].p, l.dst.p, l.n, cnt.p, lcol.p, s_);
-      tm_.end(12ull * l.n + 8ull * U);
+      DBuf<unsigned long long> cnt(&pool_, U + 1);
+      loff = DBuf<uint64_t>(&pool_, U + 1);
+      HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));
+      // 2. filtered lists of the distinct sources: (source index, neighbour) pairs
+      // (the filtered lists stay in the expansion's per-worker segments: grouping reads them in place)
+      // (a set-valued hop over an adjacency that may repeat a neighbour: each list made distinct first)
+      ExpandOut l = expand_core(ub.p, U, st.adj, bitmap(st.filter_bm), {iu.p}, true, !nbset);
+      edges_iter_ += l.E;
+      if (nbset && l.n) l.n = distinct_pairs(l.carry[0], l.dst, {}, l.n);
+      nlist = l.n;
+      // 3. grouped by source: offsets (U + 1) and the neighbours in group order (segmented lists under
+      // 2^32 entries: 32-bit counters and cursors, half the atomics' footprint)
+      const bool c32 = l.segmented && l.n < (1ull << 32) && grp32_;
+      DBuf<uint32_t> h32;
+      if (c32) {
+        h32 = DBuf<uint32_t>(&pool_, U + 1);
+        HIP_CHECK(hipMemsetAsync(h32.p, 0, (U + 1) * 4, s_));
+      }
+      if (l.n) {
+        tm_.begin("k_key_hist");
+        if (c32) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, h32.p, s_);
+        else if (l.segmented) launch_key_hist_seg(l.carry[0].p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, s_);
+        else launch_key_hist(l.carry[0].p, l.n, cnt.p, s_);
+        tm_.end(4ull * l.n + (c32 ? 4ull : 8ull) * U);
+      }
+      if (c32) {
+        hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> hc(h32.p, CastU64());
+        cub([&](void *t, size_t &b) {
+          return hipcub::DeviceScan::ExclusiveSum(t, b, hc, loff.p, (int64_t)(U + 1), s_);
+        });
+      } else {
+        cub([&](void *t, size_t &b) {
+          return hipcub::DeviceScan::ExclusiveSum(t, b, cnt.p, reinterpret_cast<unsigned long long *>(loff.p), (int64_t)(U + 1), s_);
+        });
+      }
+      if (write && semi_) {  // the new alias is never read again: the rows whose source has a list
+        semi_join(g, R, loff, cols);
+        return true;
+      }
+      lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(l.n, 1));
+      if (l.n && c32) {
+        DBuf<uint32_t> cur(&pool_, U + 1);
+        cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, h32.p, cur.p, (int64_t)(U + 1), s_); });
+        tm_.begin("k_key_scatter");
+        launch_key_scatter_seg(l.carry[0].p, l.dst.p, l.seg_start.p, l.seg_count.p, l.nseg, cur.p, lcol.p, s_);
+        tm_.end(12ull * l.n + 4ull * U);
+      } else if (l.n) {
+        HIP_CHECK(hipMemcpyAsync(cnt.p, loff.p, (U + 1) * 8, hipMemcpyDeviceToDevice, s_));
+        tm_.begin("k_key_scatter");
+        if (l.segmented)
+          launch_key_scatter_seg(l.carry[0].p, l.dst.p, l.seg_start.p, l.seg_count.p, l.nseg, cnt.p, lcol.p, s_);
+        else launch_key_scatter(l.carry[0].p, l.dst.p, l.n, cnt.p, lcol.p, s_);
+        tm_.end(12ull * l.n + 8ull * U);
+      }
     }
     // 4. the rows over their sources' lists
     if (femit) {

@@ -269,7 +269,526 @@ __global__ __launch_bounds__(256) void k_femit_slow(FemitArgs a, const uint32_t 
   }
 }
 
+// ---- the filtered lists of the distinct sources (round 5) -------------------------------------------
+// L(u) = {r in N(u) : filter(r)} for the U distinct sources of a factorized hop, grouped by source (CSR
+// loff / lcol), in one pass over their rows plus a copy.
+// The sources' rows are read as aligned 4-entry chunks of the CSR's hub-annotated col (one 16-byte load
+// per chunk; a row's first and last chunk mask the entries outside it): the chunks of all sources, in
+// source order, form the chunk space (coff = the scan of every source's chunk count), cut into tiles of
+// kFlChunks chunks, tile t → wave t mod W.
+// Filter: every entry probes one bit array with one buffer load per entry index of the lane: the filter's
+// words, then the hubs' bits by rank (a hub — one of the CSR's kFlistHubs vertices of highest in-degree,
+// bfs.hip build_pull_col — is entered in the lists col as vb + its rank, vb = the filter's bits: its bit
+// index is its entry, and the hubs' 64 KiB of bits stay cache-resident). No entry is checked before its
+// probe: a chunk's entries outside the source's row are other rows' entries (in range) or the col's
+// zeroed padding.
+// Output: a tile's survivors, in entry order — which is source order — are written to its own
+// kFlChunks·4-entry scratch slot (staged in LDS, 16-byte stores), with their count; the sources starting
+// strictly inside the tile get their offset inside the tile's survivors. A scan of the counts gives every
+// tile its base in lcol, k_flist_copy moves the survivors there (hub ranks back to vertices) and
+// k_flist_loff finishes the list offsets.
+// Measured (round 5, PMC): the pass is bound by instruction issue, not bytes — so no per-entry branch or
+// conditional LDS write: compactions write every lane, the ones that have nothing to write to a discard
+// slot of their own.
+// The pass is software-pipelined over a wave's tiles: step i requests tile i+4's bounds, tile i+3's
+// sources, tile i+2's chunks (after its LDS table is built), tile i+1's filter probes, and consumes tile i.
+// Every memory instruction of a step is unconditional (indices clamped, stores dropped by the buffer
+// range check), so the compiler's wait counts are exact, and every wait is for an instruction issued in
+// the previous step — never behind the stores that step ended with (vector memory completes in order).
+constexpr int kFlChunks = 128, kFlQ = kFlChunks / 64, kFlE = 4 * kFlQ;  // chunks per tile / per lane, entries per lane
+constexpr int kFlWaves = 8, kFlSlots = 128;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kFlDrop = 0x80000000u;     // a buffer offset past every range: the access is dropped
+constexpr uint32_t kFlDeferred = 0xFFFFFFFFu;  // a tile's count when k_flist_wide handles it
+
+// bits[i] = the filter's u32 word i (i < vb/32), then word vb/32 + w bit i = the filter bit of hubs[32w + i]
+// (no filter: every bit set)
+__global__ void k_probe_bits(const uint32_t *hubs, uint32_t nh, const uint64_t *filter, uint32_t vb, uint32_t *bits) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t fw = vb / 32, fwp = (fw + 63) & ~63u, lane = threadIdx.x & 63;
+  if (r < fwp) {  // (whole waves: threads [0, fwp) copy, the rest ballot 64 hubs a wave)
+    if (r < fw) bits[r] = filter ? reinterpret_cast<const uint32_t *>(filter)[r] : 0xFFFFFFFFu;
+    return;
+  }
+  const uint64_t h = r - fwp;
+  const bool b = h < nh && (!filter || bm_test(filter, hubs[h < nh ? h : 0]));
+  const uint64_t m = __builtin_amdgcn_ballot_w64(b);
+  const uint64_t w0 = (h - lane) / 32;
+  if (lane < 2 && (w0 + lane) * 32 < nh) bits[fw + w0 + lane] = (uint32_t)(m >> (32 * lane));
+}
+// a hub-annotated col entry (0x80000000 | rank) as vb + rank
+__global__ void k_list_col(uint32_t *col, uint64_t E, uint32_t vb) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < E) {
+    const uint32_t x = col[i];
+    if (x >> 31) col[i] = vb + (x & 0x7FFFFFFFu);
+  } else if (i < E + 4) {
+    col[i] = 0u;
+  }
+}
+
+// a source's row as chunks: the 4-entry groups of the col it touches
+__device__ __forceinline__ uint32_t fl_nch(uint64_t rs, uint64_t deg) {
+  return deg ? (uint32_t)(((rs + deg + 3) >> 2) - (rs >> 2)) : 0u;
+}
+__global__ void k_flist_nch(const uint32_t *ub, const uint64_t *doff, uint64_t U, const uint64_t *rp, uint32_t *nch) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < U) nch[i] = fl_nch(rp[ub[i]], doff[i + 1] - doff[i]);
+}
+// every source's chunk table entry {gbase, coff, pack}: chunk c of the space is col group gbase + c;
+// pack = first-chunk skip | (last-chunk entries − 1) << 2 | chunks << 4
+__global__ void k_flist_info(const uint32_t *ub, const uint64_t *doff, const uint64_t *coff, uint64_t U,
+                             const uint64_t *rp, uint4 *info) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= U) return;
+  const uint64_t rs = rp[ub[i]], deg = doff[i + 1] - doff[i], c = coff[i];
+  const uint64_t gb = (rs >> 2) - c;
+  const uint32_t n = fl_nch(rs, deg);
+  const uint32_t pack = (uint32_t)(rs & 3) | (deg ? (uint32_t)((rs + deg - 1) & 3) << 2 : 0u) | (n << 4);
+  info[i] = make_uint4((uint32_t)gb, (uint32_t)(gb >> 32), (uint32_t)c, pack);
+}
+// first / last source of every tile of the chunk space: the sources whose chunk ranges hold the tile's first
+// and last chunk (the last source with coff ≤ c: an empty source shares its coff with the next one, so
+// it is never the last) — one thread per tile, two binary searches
+__device__ __forceinline__ uint64_t fl_source_of(const uint64_t *coff, uint64_t U, uint64_t c) {
+  uint64_t lo = 0, hi = U;  // the first r with coff[r] > c, in (0, U]
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (coff[mid] <= c) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo - 1;
+}
+__global__ void k_flist_bounds(const uint64_t *coff, uint64_t U, const uint64_t *ec, uint64_t *rb) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, N = *ec;
+  if (t * kFlChunks >= N) return;
+  rb[2 * t] = fl_source_of(coff, U, t * kFlChunks);
+  rb[2 * t + 1] = fl_source_of(coff, U, min((t + 1) * (uint64_t)kFlChunks, N) - 1);
+}
+
+struct FlHdr {
+  uint64_t s0, ns;
+};
+struct FlSlot {  // a non-empty source of the tile being set up
+  uint64_t gbase;
+  uint32_t coff, pack;
+};
+struct FlWave {  // one wave's LDS
+  union {
+    struct {
+      FlSlot tbl[kFlSlots];            // setup: the tile's non-empty sources, in order
+      uint8_t st[kFlChunks];           // setup: st[c] = a non-empty source starts at chunk c of the tile
+    } s;
+    uint32_t surv[kFlE * 64];          // consume: the tile's survivors, in entry order
+  } u;
+  uint32_t coff[3][kFlSlots];          // the tiles' sources' first chunks (ring of 3)
+  FlHdr hdr[3];
+  uint16_t qs[kFlQ][64];               // consume: survivors before each chunk
+};
+
+__global__ __launch_bounds__(64 * kFlWaves) void k_flist(FlistArgs a) {
+  __shared__ uint32_t s_hub[kFlistHubs / 32];
+  __shared__ FlWave s_w[kFlWaves];
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  {  // the hubs' bits, 8 words a thread in flight
+    const uint32_t hw = (a.nh + 31) / 32, *hb = a.bits + a.vb / 32;
+    for (uint32_t b0 = 0; b0 < hw; b0 += 8 * blockDim.x) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t i = b0 + u * blockDim.x + threadIdx.x;
+        v[u] = hb[i < hw ? i : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t i = b0 + u * blockDim.x + threadIdx.x;
+        if (i < hw) s_hub[i] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  FlWave &w = s_w[wv];
+  const uint4 *const acol4 = reinterpret_cast<const uint4 *>(a.acol);
+  const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc((void *)a.bits, 0, (int32_t)a.bbytes, 0x00020000);
+  const uint64_t EC = *a.ec;
+  const uint64_t nt = (EC + kFlChunks - 1) / kFlChunks;
+  const uint64_t W = (uint64_t)gridDim.x * kFlWaves;
+  const uint64_t tw = (uint64_t)blockIdx.x * kFlWaves + wv;
+  if (tw >= nt) return;
+  const uint64_t ntw = (nt - tw + W - 1) / W;  // tiles of this wave
+  auto tile = [&](uint64_t i) { return tw + (i < ntw ? i : ntw - 1) * W; };
+  const uint64_t gmax = (a.E + 3) / 4 - 1;
+  // stage a: a tile's first / last source (lanes 0, 1)
+  auto ld_bounds = [&](uint64_t i) -> uint64_t { return a.rb[2 * tile(i) + (lane & 1)]; };
+  // stage b: its sources' chunk table entries
+  auto ld_src = [&](uint64_t bv, uint4 (&sv)[2], FlHdr &h) {
+    h.s0 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(bv >> 32), 0) << 32) | __builtin_amdgcn_readlane((uint32_t)bv, 0);
+    const uint64_t s1 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(bv >> 32), 1) << 32) | __builtin_amdgcn_readlane((uint32_t)bv, 1);
+    h.ns = s1 - h.s0 + 1;
+    const uint64_t smax = a.U - 1;
+    // (only the tile's sources: lanes past them are dropped by the range, no cache lines touched)
+    (void)smax;
+    const uint32_t nr = (uint32_t)min<uint64_t>(h.ns, (uint64_t)kFlSlots) * 16;
+    const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc((void *)(a.info + h.s0), 0, (int32_t)nr, 0x00020000);
+    const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(ir, 16 * lane, 0, 0);
+    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(ir, 16 * (64 + lane), 0, 0);
+    sv[0] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+    sv[1] = make_uint4(v1.x, v1.y, v1.z, v1.w);
+  };
+  // stage c: the tile's LDS table (non-empty sources in order, the chunks where they start), then its
+  // chunks requested; vm = the lane's valid entries (bit 4q + i: component i of its chunk q)
+  auto setup = [&](uint64_t i, const uint4 (&sv)[2], const FlHdr &h, int r, uint32_t (&x)[kFlE], uint32_t &vm) {
+    const uint64_t t = tile(i), c0 = t * kFlChunks;
+    const uint32_t nc = (uint32_t)min<uint64_t>((uint64_t)kFlChunks, EC - c0);
+    const bool reg = h.ns <= (uint64_t)kFlSlots;
+    if (lane < kFlChunks / 4) reinterpret_cast<uint32_t *>(w.u.s.st)[lane] = 0u;
+    if (lane == 0) w.hdr[r] = h;
+    uint32_t rank0 = 0;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const uint32_t k = 64 * c + lane;
+      const uint32_t cf = sv[c].z, nchk = sv[c].w >> 4;
+      w.coff[r][k] = cf;
+      const bool live = k < h.ns && nchk > 0;
+      const uint64_t bl = __builtin_amdgcn_ballot_w64(live);
+      FlSlot sl;
+      sl.gbase = ((uint64_t)sv[c].y << 32) | sv[c].x;
+      sl.coff = cf;
+      sl.pack = sv[c].w;
+      const uint32_t rk = rank0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+      if (live) w.u.s.tbl[rk] = sl;
+      rank0 += (uint32_t)__popcll(bl);
+      const uint32_t d = cf - (uint32_t)c0;  // (a start inside the tile: 0 < d < nc)
+      const bool in = live & (cf > (uint32_t)c0) & (d < nc);
+      if (in) w.u.s.st[d] = 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nval = reg ? nc : 0u;
+    uint32_t cs = 0;
+    vm = 0;
+#pragma unroll
+    for (int q = 0; q < kFlQ; ++q) {
+      const uint32_t cl = 64 * q + lane;
+      const uint64_t sb = __builtin_amdgcn_ballot_w64(w.u.s.st[cl] != 0);
+      const uint32_t k = cs + __builtin_amdgcn_mbcnt_hi((uint32_t)(sb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sb, 0u)) +
+                         (uint32_t)((sb >> lane) & 1u);
+      cs += (uint32_t)__popcll(sb);
+      const FlSlot sl = w.u.s.tbl[k];
+      const uint64_t c = c0 + cl;
+      const bool ok = cl < nval;
+      const uint32_t cc = (uint32_t)c - sl.coff, n = sl.pack >> 4;
+      const uint32_t from = cc == 0 ? (sl.pack & 3u) : 0u, to = cc + 1 == n ? ((sl.pack >> 2) & 3u) + 1u : 4u;
+      const uint32_t m4 = ok ? ((0xFu << from) & (0xFu >> (4u - to))) : 0u;
+      vm |= m4 << (4 * q);
+      const uint4 v = acol4[ok ? min(sl.gbase + c, gmax) : 0];
+      x[4 * q] = v.x;
+      x[4 * q + 1] = v.y;
+      x[4 * q + 2] = v.z;
+      x[4 * q + 3] = v.w;
+    }
+  };
+  // stage d: the filter words of the valid non-hub entries (one buffer load per entry index of the lane;
+  // the other lanes' offsets are dropped: no cache line touched)
+  auto probe = [&](const uint32_t (&x)[kFlE], uint32_t vm, uint32_t (&fw)[kFlE]) {
+#pragma unroll
+    for (int e = 0; e < kFlE; ++e) {
+      const bool p = ((vm >> e) & 1u) && x[e] < a.vb;
+      fw[e] = __builtin_amdgcn_raw_buffer_load_b32(fr, p ? (x[e] >> 3) & ~3u : kFlDrop, 0, 0);
+    }
+  };
+  // stage e: the tile's survivors staged in entry order and stored to its scratch slot, its count, and
+  // the offsets of the sources starting inside it
+  auto consume = [&](uint64_t i, const uint32_t (&x)[kFlE], uint32_t vm, const uint32_t (&fw)[kFlE], int r) {
+    const uint64_t t = tile(i), c0 = t * kFlChunks;
+    // (read off the LDS into SGPRs: a buffer descriptor built from a VGPR value becomes a waterfall loop)
+    FlHdr h;
+    h.s0 = wave_bcast64(w.hdr[r].s0);
+    h.ns = wave_bcast64(w.hdr[r].ns);
+    const bool deferred = h.ns > (uint64_t)kFlSlots;
+    // an entry's bit (a hub's from the LDS; vb is a multiple of 64: its bit index is x mod 32 too), kept
+    // where the entry is valid
+    uint32_t sv = 0;
+#pragma unroll
+    for (int e = 0; e < kFlE; ++e) {
+      const bool hub = x[e] >= a.vb;
+      const uint32_t lw = s_hub[hub && ((vm >> e) & 1u) ? (x[e] - a.vb) >> 5 : 0u];
+      sv |= (((hub ? lw : fw[e]) >> (x[e] & 31)) & 1u) << e;
+    }
+    sv &= vm;
+    // staging in entry order: row q of chunks (chunk 64q + lane) after rows < q; inside a row, the survivors
+    // of lower lanes (per component, a ballot) and of this chunk's earlier components
+    uint32_t qb = 0;
+#pragma unroll
+    for (int q = 0; q < kFlQ; ++q) {
+      const uint32_t sq = (sv >> (4 * q)) & 0xFu;
+      uint32_t before = 0, tq = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint64_t b = __builtin_amdgcn_ballot_w64((sq >> c) & 1u);
+        before += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        tq += (uint32_t)__popcll(b);
+      }
+      w.qs[q][lane] = (uint16_t)(qb + before);
+      uint32_t o = qb + before;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t b = (sq >> c) & 1u;
+        if (b) w.u.surv[o] = x[4 * q + c];
+        o += b;
+      }
+      qb += tq;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // 16-byte stores of the staged survivors, rounded up to whole 16 bytes (the slot has room)
+    const uint32_t tot = deferred ? 0u : qb;
+    const __amdgpu_buffer_rsrc_t sr =
+        __builtin_amdgcn_make_buffer_rsrc(a.scratch + t * (uint64_t)(kFlChunks * 4), 0, (int32_t)(((tot + 3) & ~3u) * 4), 0x00020000);
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(w.u.surv);
+#pragma unroll
+    for (int q = 0; q < kFlQ; ++q) {
+      const uint32_t k = 64 * q + lane;
+      const uint4 v = s4[k];
+      u32x4 vv;
+      vv.x = v.x;
+      vv.y = v.y;
+      vv.z = v.z;
+      vv.w = v.w;
+      __builtin_amdgcn_raw_buffer_store_b128(vv, sr, 4 * k < tot ? 16 * k : kFlDrop, 0, 0);
+    }
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(a.ntot + t, 0, 4, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(deferred ? kFlDeferred : qb, cr, lane == 0 ? 0u : kFlDrop, 0, 0);
+    // sources whose first chunk lies strictly inside the tile: survivors of the tile before it
+    const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc(a.loc + h.s0, 0, 4 * kFlSlots, 0x00020000);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const uint32_t k = 64 * c + lane;
+      const uint32_t cf = w.coff[r][k], d = cf - (uint32_t)c0;
+      const bool in = !deferred & (k < h.ns) & (cf > (uint32_t)c0) & (d < (uint32_t)kFlChunks);
+      const uint32_t cl = in ? d : 0u;
+      const uint32_t v = w.qs[cl >> 6][cl & 63];
+      __builtin_amdgcn_raw_buffer_store_b32(v, lr, in ? 4 * k : kFlDrop, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();  // the staging area is the next setup's table
+  };
+  // prologue: tiles 0 and 1 set up, tile 0 probed, tile 2's sources and tile 3's bounds loaded; drained
+  uint64_t P0, P1;
+  uint4 S0[2], S1[2];
+  FlHdr H0, H1;
+  uint32_t X0[kFlE], X1[kFlE], X2[kFlE], V0, V1, V2;
+  uint32_t F0[kFlE], F1[kFlE];
+  {
+    uint4 sv[2];
+    FlHdr hv;
+    ld_src(ld_bounds(0), sv, hv);
+    setup(0, sv, hv, 0, X0, V0);
+    probe(X0, V0, F0);
+    ld_src(ld_bounds(1), sv, hv);
+    setup(1, sv, hv, 1, X1, V1);
+    ld_src(ld_bounds(2), S0, H0);
+    P0 = ld_bounds(3);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+  // step i: a) tile i+4's bounds; b) tile i+3's sources; c) tile i+2 set up, its chunks requested;
+  // d) tile i+1 probed; e) tile i consumed. The register sets rotate over six unrolled steps (three
+  // chunk sets, two of everything else), so no set is copied while its loads are in flight.
+#define OMX_FL_STEP(PA, PB, SA, HA, SB, HB, XA, VA, XB, VB, XC, VC, FA, FB, RE, RC) \
+  {                                                                                \
+    PB = ld_bounds(i + 4);                                                         \
+    ld_src(PA, SB, HB);                                                            \
+    setup(i + 2, SA, HA, RC, XC, VC);                                              \
+    probe(XB, VB, FB);                                                             \
+    consume(i, XA, VA, FA, RE);                                                    \
+  }
+  for (uint64_t i = 0;;) {
+    OMX_FL_STEP(P0, P1, S0, H0, S1, H1, X0, V0, X1, V1, X2, V2, F0, F1, 0, 2)
+    if (++i >= ntw) break;
+    OMX_FL_STEP(P1, P0, S1, H1, S0, H0, X1, V1, X2, V2, X0, V0, F1, F0, 1, 0)
+    if (++i >= ntw) break;
+    OMX_FL_STEP(P0, P1, S0, H0, S1, H1, X2, V2, X0, V0, X1, V1, F0, F1, 2, 1)
+    if (++i >= ntw) break;
+    OMX_FL_STEP(P1, P0, S1, H1, S0, H0, X0, V0, X1, V1, X2, V2, F1, F0, 0, 2)
+    if (++i >= ntw) break;
+    OMX_FL_STEP(P0, P1, S0, H0, S1, H1, X1, V1, X2, V2, X0, V0, F0, F1, 1, 0)
+    if (++i >= ntw) break;
+    OMX_FL_STEP(P1, P0, S1, H1, S0, H0, X2, V2, X0, V0, X1, V1, F1, F0, 2, 1)
+    if (++i >= ntw) break;
+  }
+#undef OMX_FL_STEP
+}
+
+__device__ __forceinline__ uint32_t wave_excl_add(uint32_t v, uint32_t lane, uint32_t *total) {
+  uint32_t incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 64);
+    if (lane >= (uint32_t)off) incl += y;
+  }
+  *total = __builtin_amdgcn_readlane(incl, 63);
+  return incl - v;
+}
+
+// the deferred tiles (over more than kFlSlots sources): one wave per tile, every chunk's source by a binary search; the same outputs as k_flist
+__global__ __launch_bounds__(256) void k_flist_wide(FlistArgs a) {
+  __shared__ uint32_t s_q[4][kFlChunks + 1];  // survivors before every chunk of the tile
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t EC = *a.ec;
+  const uint64_t nt = (EC + kFlChunks - 1) / kFlChunks;
+  for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < nt; t += (uint64_t)gridDim.x * 4) {
+    if (a.ntot[t] != kFlDeferred) continue;
+    const uint64_t s0 = a.rb[2 * t], s1 = a.rb[2 * t + 1], c0 = t * kFlChunks;
+    const uint32_t nc = (uint32_t)min<uint64_t>((uint64_t)kFlChunks, EC - c0);
+    uint32_t qb = 0;
+    for (uint32_t q = 0; q < kFlQ; ++q) {
+      const uint32_t cl = 64 * q + lane;
+      uint32_t sq = 0;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (cl < nc) {
+        // the source of chunk c0 + cl: the last with coff ≤ c (its chunk table entry holds coff)
+        uint64_t lo = s0, hi = s1;
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi + 1) >> 1;
+          if ((uint64_t)a.info[mid].z <= c0 + cl) lo = mid;
+          else hi = mid - 1;
+        }
+        const uint4 in = a.info[lo];
+        const uint64_t gb = ((uint64_t)in.y << 32) | in.x;
+        const uint32_t cc = (uint32_t)(c0 + cl - in.z), n = in.w >> 4;
+        const uint32_t from = cc == 0 ? (in.w & 3u) : 0u, to = cc + 1 == n ? ((in.w >> 2) & 3u) + 1u : 4u;
+        v = reinterpret_cast<const uint4 *>(a.acol)[gb + c0 + cl];
+        const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+        for (uint32_t c = from; c < to; ++c) {
+          const uint32_t x = xs[c];
+          if ((a.bits[x >> 5] >> (x & 31)) & 1u) sq |= 1u << c;
+        }
+      }
+      uint32_t tq;
+      const uint32_t ex = wave_excl_add((uint32_t)__builtin_popcount(sq), lane, &tq);
+      s_q[wv][cl] = qb + ex;
+      uint32_t o = qb + ex;
+      const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+      for (int c = 0; c < 4; ++c)
+        if ((sq >> c) & 1u) a.scratch[t * (uint64_t)(kFlChunks * 4) + o++] = xs[c];
+      qb += tq;
+    }
+    if (lane == 0) s_q[wv][kFlChunks] = qb;
+    __builtin_amdgcn_wave_barrier();
+    for (uint64_t k = lane; k < s1 - s0 + 1; k += 64) {
+      const uint64_t cf = a.info[s0 + k].z;
+      if (cf > c0 && cf < c0 + kFlChunks) a.loc[s0 + k] = s_q[wv][cf - c0];
+    }
+    if (lane == 0) a.ntot[t] = qb;
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// the survivors of every tile moved to its base in lcol, hub ranks mapped back to vertices: a wave takes
+// kFlCopyT consecutive tiles at once (their first 64 survivors each: every load of the batch in flight
+// together), then any longer tile's rest
+constexpr int kFlCopyT = 8;
+__global__ __launch_bounds__(256) void k_flist_copy(FlistArgs a, const uint64_t *base) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nt = (*a.ec + kFlChunks - 1) / kFlChunks;
+  const uint64_t t0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kFlCopyT;
+  if (t0 >= nt) return;
+  const uint64_t tl = t0 + (lane & (kFlCopyT - 1));
+  const uint32_t nl = tl < nt ? a.ntot[tl] : 0u;
+  const uint64_t bl = base[tl < nt ? tl : nt - 1];
+  uint32_t n[kFlCopyT], x[kFlCopyT];
+  uint64_t b[kFlCopyT];
+#pragma unroll
+  for (int j = 0; j < kFlCopyT; ++j) {
+    n[j] = __builtin_amdgcn_readlane(nl, j);
+    b[j] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(bl >> 32), j) << 32) | __builtin_amdgcn_readlane((uint32_t)bl, j);
+  }
+#pragma unroll
+  for (int j = 0; j < kFlCopyT; ++j)
+    x[j] = a.scratch[min(t0 + j, nt - 1) * (uint64_t)(kFlChunks * 4) + (lane < n[j] ? lane : 0u)];  // (n = 0 past the end)
+#pragma unroll
+  for (int j = 0; j < kFlCopyT; ++j) {
+    const bool hub = x[j] >= a.vb;
+    const uint32_t v = a.hubs[hub ? x[j] - a.vb : 0u];
+    x[j] = hub ? v : x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < kFlCopyT; ++j)
+    if (lane < n[j]) a.lcol[b[j] + lane] = x[j];
+#pragma unroll
+  for (int j = 0; j < kFlCopyT; ++j) {
+    const uint32_t *src = a.scratch + (t0 + j) * (uint64_t)(kFlChunks * 4);
+    for (uint32_t k = 64 + lane; k < n[j]; k += 64) {
+      const uint32_t y = src[k];
+      a.lcol[b[j] + k] = y >= a.vb ? a.hubs[y - a.vb] : y;
+    }
+  }
+}
+
+// every list offset: a source whose first chunk opens a tile (or lies at the end) starts at that tile's
+// base, any other at its tile's base + its offset inside the tile (k_flist); loff[U] = the total
+__global__ void k_flist_loff(const uint64_t *coff, uint64_t U, const uint64_t *ec, const uint64_t *base, const uint32_t *loc,
+                             uint64_t *loff) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > U) return;
+  const uint64_t EC = *ec, nt = (EC + kFlChunks - 1) / kFlChunks;
+  const uint64_t c = s == U ? EC : coff[s];
+  if (c >= EC) loff[s] = base[nt];
+  else if (c % kFlChunks == 0) loff[s] = base[c / kFlChunks];
+  else loff[s] = base[c / kFlChunks] + loc[s];
+}
+
 }  // namespace
+
+// an upper bound of the chunk space's tiles: Σ ⌈(deg + 3) / 4⌉ + 1 chunks per source
+uint64_t flist_tiles_bound(uint64_t EU, uint64_t U) { return (EU / 4 + 2 * U + kFlChunks) / kFlChunks + 1; }
+uint64_t flist_tile_entries() { return 4ull * kFlChunks; }
+
+void launch_flist_nch(const uint32_t *ub, const uint64_t *doff, uint64_t U, const uint64_t *rp, uint32_t *nch,
+                      hipStream_t s) {
+  if (!U) return;
+  hipLaunchKernelGGL(k_flist_nch, dim3(nblocks(U, 256)), dim3(256), 0, s, ub, doff, U, rp, nch);
+  KCHECK("k_flist_nch");
+}
+
+void launch_flist_prep(const uint32_t *ub, const uint64_t *doff, const uint64_t *coff, uint64_t U, const uint64_t *rp,
+                       const uint64_t *ec, uint4 *info, uint64_t *rb, uint64_t nt_bound, hipStream_t s) {
+  if (!U) return;
+  hipLaunchKernelGGL(k_flist_info, dim3(nblocks(U, 256)), dim3(256), 0, s, ub, doff, coff, U, rp, info);
+  KCHECK("k_flist_info");
+  hipLaunchKernelGGL(k_flist_bounds, dim3(nblocks(nt_bound, 256)), dim3(256), 0, s, coff, U, ec, rb);
+  KCHECK("k_flist_bounds");
+}
+
+void launch_probe_bits(const uint32_t *hubs, uint32_t nh, const uint64_t *filter, uint32_t vb, uint32_t *bits,
+                       hipStream_t s) {
+  const uint64_t n = ((vb / 32 + 63) & ~63ull) + ((nh + 63) & ~63ull);
+  hipLaunchKernelGGL(k_probe_bits, dim3(nblocks(n, 256)), dim3(256), 0, s, hubs, nh, filter, vb, bits);
+  KCHECK("k_probe_bits");
+}
+
+void launch_list_col(uint32_t *col, uint64_t E, uint32_t vb, hipStream_t s) {
+  hipLaunchKernelGGL(k_list_col, dim3(nblocks(E + 4, 256)), dim3(256), 0, s, col, E, vb);
+  KCHECK("k_list_col");
+}
+
+void launch_flist(const FlistArgs &a, uint64_t nt_bound, int cus, hipStream_t s) {
+  if (a.nh > kFlistHubs) fail(OMX_E_INVALID, "internal: more hubs than the lists col holds");
+  // grids sized for the bound; waves past the real tile count exit at once
+  const dim3 grid((unsigned)std::min<uint64_t>((nt_bound + kFlWaves - 1) / kFlWaves, (uint64_t)cus)), blk(64 * kFlWaves);
+  hipLaunchKernelGGL(k_flist, grid, blk, 0, s, a);
+  KCHECK("k_flist");
+  const dim3 gw((unsigned)std::min<uint64_t>((nt_bound + 3) / 4, (uint64_t)cus * 4)), bw(256);
+  hipLaunchKernelGGL(k_flist_wide, gw, bw, 0, s, a);
+  KCHECK("k_flist_wide");
+}
+
+void launch_flist_finish(const FlistArgs &a, const uint64_t *coff, const uint64_t *base, uint64_t *loff, uint64_t nt_bound,
+                         int cus, hipStream_t s) {
+  hipLaunchKernelGGL(k_flist_copy, dim3((unsigned)((nt_bound + 4 * kFlCopyT - 1) / (4 * kFlCopyT))), dim3(256), 0, s, a,
+                     base);
+  KCHECK("k_flist_copy");
+  hipLaunchKernelGGL(k_flist_loff, dim3(nblocks(a.U + 1, 256)), dim3(256), 0, s, coff, a.U, a.ec, base, a.loc, loff);
+  KCHECK("k_flist_loff");
+}
 
 uint64_t femit_tiles(uint64_t N) { return (N + kEwTile - 1) / kEwTile; }
 

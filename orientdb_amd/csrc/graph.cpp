@@ -84,6 +84,7 @@ Graph::~Graph() {
       for (int d = 0; d < 2; ++d) {
         f(e.d_pull_col[d]); f(e.d_hubs[d]); f(e.d_hub_bm[d]); f(e.d_pull_part[d]); f(e.d_global_rp[d]);
         f(e.d_pullw_rb[d]); f(e.d_pullw_tiles[d]); f(e.d_hub_rp[d]); f(e.d_hub_col[d]); f(e.d_hubw_rb[d]); f(e.d_hubw_tiles[d]);
+        f(e.d_list_col[d]); f(e.d_list_hubs[d]);
       }
     }
     for (auto &p : props) { f(p.d_values); f(p.d_present); }

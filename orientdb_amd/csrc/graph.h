@@ -119,6 +119,14 @@ struct EdgeSet {
   uint64_t *d_hubw_rb[2] = {nullptr, nullptr};
   uint32_t *d_hubw_tiles[2] = {nullptr, nullptr};
   uint64_t hubw_nreg[2] = {0, 0};
+  // lists col of a CSR for the factorized hop's filtered lists (factor.hip k_flists): as d_pull_col, with
+  // the kFlistHubs vertices of highest degree in the opposite CSR as hubs, a hub's entry list_vb + its rank
+  // (its filter bit is read from a small, cache-resident array); built on the first factorized hop over
+  // the CSR
+  uint32_t *d_list_col[2] = {nullptr, nullptr};
+  uint32_t list_vb[2] = {0, 0};
+  uint32_t *d_list_hubs[2] = {nullptr, nullptr};
+  uint32_t n_list_hubs[2] = {0, 0};
   // partitioned snapshot: row pointers of every vertex's degree (V + 1 entries, the scan of all ranks'
   // degrees gathered once) — what out()/in()/both().size() in a WHERE reads (no col[] behind them)
   uint64_t *d_global_rp[2] = {nullptr, nullptr};

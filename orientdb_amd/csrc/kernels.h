@@ -301,6 +301,49 @@ void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, boo
 // nreg is a device count
 void launch_femit(const FemitArgs &a, const uint32_t *tiles, const uint64_t *nreg, uint64_t nt, int cus,
                   hipStream_t s);
+// factor.hip (round 5): the filtered lists of a factorized hop's distinct sources in one pass over their
+// rows (as aligned 4-entry chunks of the CSR's lists col: a hub — one of the kFlistHubs vertices of
+// highest in-degree — as vb + its rank, other vertices as themselves), every entry probing one bit array
+// (the filter's words, then the hubs' bits by rank: the hubs' bits stay cache-resident); each tile of the
+// chunk space writes its survivors to its own scratch slot with their count, a scan gives every tile its
+// base, and a copy moves them to lcol (grouped by source: the tiles are in source order) — CSR loff / lcol.
+constexpr uint32_t kFlistHubs = 1u << 20;  // (their bits: 128 KiB of a lists workgroup's LDS)
+struct FlistArgs {
+  const uint32_t *ub;        // [U] distinct sources
+  uint64_t U;
+  const uint4 *info;         // [U] per source: {chunk space → col group base (u64), first chunk, pack}
+  const uint64_t *ec;        // the chunk space's size (device)
+  const uint32_t *acol;      // the CSR's lists col (vb + hub rank, or the vertex), padded to 4
+  uint64_t E;                // its entries
+  const uint32_t *hubs;      // hub rank → vertex
+  uint32_t nh;               // hubs (≤ kFlistHubs)
+  uint32_t vb;               // a hub's first id in acol (the filter's words · 64 ≥ V)
+  const uint32_t *bits;      // [vb/32 + ⌈nh/32⌉] the target filter's bits, then the hubs' by rank
+  uint64_t bbytes;           // its bytes
+  const uint64_t *rb;        // [2·tiles] first / last source of every tile
+  uint32_t *scratch;         // [tiles · flist_tile_entries()] every tile's survivors
+  uint32_t *ntot;            // [tiles] their counts
+  uint32_t *loc;             // [U] a source's offset inside its first tile's survivors
+  uint32_t *lcol;            // the lists, grouped by source
+};
+uint64_t flist_tiles_bound(uint64_t EU, uint64_t U);
+uint64_t flist_tile_entries();
+// nch[i] = chunks of source i's row
+void launch_flist_nch(const uint32_t *ub, const uint64_t *doff, uint64_t U, const uint64_t *rp, uint32_t *nch,
+                      hipStream_t s);
+// info[U] and rb (tile bounds) from coff = the exclusive scan of nch (coff[U] = *ec)
+void launch_flist_prep(const uint32_t *ub, const uint64_t *doff, const uint64_t *coff, uint64_t U, const uint64_t *rp,
+                       const uint64_t *ec, uint4 *info, uint64_t *rb, uint64_t nt_bound, hipStream_t s);
+// bits = the filter's vb/32 words, then word w bit i = the filter bit of hubs[32w + i]
+void launch_probe_bits(const uint32_t *hubs, uint32_t nh, const uint64_t *filter, uint32_t vb, uint32_t *bits,
+                       hipStream_t s);
+// a hub-annotated col (0x80000000 | rank) as a lists col (vb + rank), its 4 padding entries zeroed
+void launch_list_col(uint32_t *col, uint64_t E, uint32_t vb, hipStream_t s);
+// the pass (scratch, ntot, loc)
+void launch_flist(const FlistArgs &a, uint64_t nt_bound, int cus, hipStream_t s);
+// base = exclusive scan of ntot: lcol and loff[U + 1]
+void launch_flist_finish(const FlistArgs &a, const uint64_t *coff, const uint64_t *base, uint64_t *loff, uint64_t nt_bound,
+                         int cus, hipStream_t s);
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
 // head[i] = 1 where a run of equal sorted keys starts
 void launch_run_heads(const uint32_t *sorted, uint64_t n, uint8_t *head, hipStream_t s);

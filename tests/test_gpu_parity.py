@@ -471,6 +471,44 @@ def test_factorized_emission_many_tiles_rmat16(rmat16, slow, monkeypatch):
     assert rs.info["edges_traversed"] == base.info["edges_traversed"]
 
 
+@pytest.mark.parametrize("lists", ["flists", "sliced"])
+@pytest.mark.parametrize("graph", ["simple", "multigraph"])
+@pytest.mark.parametrize("q", [q for q in RMAT_QUERIES if q[0] in FACTOR_IDS], ids=lambda q: q[0])
+def test_factorized_lists_paths(rmat10, rmat10_raw, q, graph, lists, monkeypatch):
+    """The distinct sources' filtered lists through the hub-annotated col (factor.hip k_flists: LDS table
+    per tile, or every tile's sources found by binary search) and through the sliced expansion + grouping
+    (OMX_FLISTS=0): the oracle's rows, bindings and E_t on every factorized hop, both emissions. (On the
+    multigraph a set-valued hop keeps the sliced path: its lists are made distinct there.)"""
+    import orientdb_amd as o
+    g, ref = rmat10 if graph == "simple" else rmat10_raw
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    monkeypatch.setenv("OMX_FLISTS", {"flists": "1", "sliced": "0"}[lists])
+    for emit in ("force", "0"):
+        monkeypatch.setenv("OMX_FEMIT", emit)
+        rs = _parity(g, ref, q[1], q[2])
+        if q[0] in ("c2_both_ends", "in_dir", "three_hop"):
+            assert rs.info["factorized_hops"] >= 1
+
+
+def test_factorized_lists_rmat16_digest(rmat16, monkeypatch):
+    """k_flists at RMAT-16 (thousands of tiles, hubs of degree ~10^3 spanning many tiles: the survivors of
+    a source continuing over tiles are placed through the tiles' last-source counts): rows, E_t, bindings
+    and digest equal the sliced path's and dfs_ref.c's."""
+    import orientdb_amd as o
+    from oracle import dfs
+    g, ref = rmat16
+    q = "MATCH {class:Person,as:a,where:(age < 3)}-Knows->{as:b}-Knows->{as:c,where:(age >= 80)} RETURN a,b,c"
+    want = dfs.run(ref.cg, q, nthreads=8, emit=False, digest=["a", "b", "c"])
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    out = {}
+    for lists in ("1", "0"):
+        monkeypatch.setenv("OMX_FLISTS", lists)
+        rs = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST, documents=False)
+        out[lists] = (rs.info["n_rows"], rs.info["edges_traversed"], rs.info["bindings"], rs.info["digest"])
+    assert out["1"] == out["0"]
+    assert out["1"][2] == want["bindings"] and out["1"][1] == want["edges"] and out["1"][3] == want["digest"]
+
+
 SEMI_QUERIES = [
     ("ab_of_abc", "MATCH {class:Person,as:a,where:(age < 5)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a, b",
      ["a", "b"]),
