@@ -1337,9 +1337,10 @@ class Executor {
   }
 
   // the filtered lists L(u) of the U distinct sources ub (doff: the scan of their degrees, EU = doff[U])
-  // as a CSR (loff[U+1], lcol) through k_flists; returns the list entries
-  uint64_t filtered_lists(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const AdjSpec &adjs,
-                          const uint64_t *filter, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol) {
+  // as a CSR (loff[U+1], lcol) through k_flists; the list entries stay on the device (loff[U]): lcol is
+  // sized for all EU, so no host round trip
+  void filtered_lists(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const AdjSpec &adjs,
+                      const uint64_t *filter, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol) {
     const int es = adjs.parts[0].first, dir = adjs.parts[0].second;
     uint32_t nh = 0;
     const uint32_t *hubs = nullptr;
@@ -1387,14 +1388,13 @@ class Executor {
       hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> it(ntot.p, CastU64());
       cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, it, base.p, (int64_t)(ntb + 1), s_); });
     }
-    const uint64_t n = read1(base.p + ntb);
-    lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(n, 1));
+    lcol = DBuf<uint32_t>(&pool_, std::max<uint64_t>(EU, 1));
     loff = DBuf<uint64_t>(&pool_, U + 1);
     a.lcol = lcol.p;
     tm_.begin("k_flist_copy");
     launch_flist_finish(a, coff.p, base.p, loff.p, ntb, cus(), s_);
-    tm_.end(8ull * n + 16ull * U);
-    return n;
+    tm_.end(16ull * U);  // (+ 8 bytes a list entry: amended when the count is read)
+    flist_copy_rec_ = tm_.last();
   }
 
   // the slice-cut index of every part of an adjacency (built once per CSR and slice size)
@@ -1937,6 +1937,8 @@ class Executor {
   // faster writes: C2 (RMAT-22, E_t 1.5e9) 1.21 ms against 1.15 binned; M1 (E_t 1.03e10) 4.2 against 5.2
   // (profiles/r03/femit/c2ab.txt)
   int femit_ = 1;
+  static constexpr uint64_t kOnDevice = UINT64_MAX;  // a count left on the device (emit_factorized's nlist)
+  size_t flist_copy_rec_ = SIZE_MAX;                  // the timing record of the last k_flist_copy
   uint64_t femit_min_et_ = 4000000000ull;
   bool femit_slow_ = false;  // OMX_FEMIT_SLOW=1: every output tile through k_femit_slow (tests)
 
@@ -1987,7 +1989,8 @@ class Executor {
   }
 
   // perm_sorted: the rows sorted by source (g in that order); perm_sorted[i] = the row at sorted
-  // position i. nlist: the entries of all U lists (each read from HBM once, then from L2 by its rows)
+  // position i. nlist: the entries of all U lists (each read from HBM once, then from L2 by its rows);
+  // kOnDevice: loff[U] holds them (read with the emission's own round trip)
   void emit_factorized(DBuf<uint32_t> &g, uint64_t R, uint64_t U, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol,
                        uint64_t nlist, const std::vector<int> &cols, const Step &st, const uint32_t *perm_sorted) {
     // 1. the rows whose list is not empty (the others write nothing), in row order or grouped by source.
@@ -2018,9 +2021,14 @@ class Executor {
     launch_femit_len(gs.p, R, loff.p, len.p, s_, rn);
     cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, len.p, roff.p, (int64_t)(R + 1), s_); });
     launch_femit_base(gs.p, R, loff.p, roff.p, rbase.p, s_, rn);
-    HIP_CHECK(hipMemcpyAsync(nsel.p + 1, roff.p + R, 8, hipMemcpyDeviceToDevice, s_));
-    const auto rn_n = read2(nsel.p);
-    const uint64_t Rn = rn_n.first, N = rn_n.second;
+    const uint64_t *words[3] = {nsel.p, roff.p + R, loff.p + U};
+    launch_post_ptrs(words, nlist == kOnDevice ? 3 : 2, mail(), s_);
+    const uint64_t *m = wait_mail();
+    const uint64_t Rn = m[0], N = m[1];
+    if (nlist == kOnDevice) {
+      nlist = m[2];
+      tm_.amend_at(flist_copy_rec_, 8ull * nlist + 16ull * U);
+    }
     edges_iter_ += N;
     alg_bytes_ += 8ull * R + 4ull * N * (cols.size() + 2);  // as expand_core's unfiltered written hop
     R_ = N;
@@ -2184,7 +2192,8 @@ class Executor {
     // (the chunk space's offsets are u32: EU / 4 + 2U chunks below 2^32)
     if (flists_ && !nbset && st.adj.parts.size() == 1 && !g_.partitioned() && g_.V < 0x80000000u && EU > 0 &&
         EU / 4 + 2 * U < 0xFFFFFF00ull) {
-      nlist = filtered_lists(ub.p, U, doffb.p, EU, st.adj, bitmap(st.filter_bm), loff, lcol);
+      filtered_lists(ub.p, U, doffb.p, EU, st.adj, bitmap(st.filter_bm), loff, lcol);
+      nlist = kOnDevice;
       edges_iter_ += EU;
       if (write && semi_) {  // the new alias is never read again: the rows whose source has a list
         semi_join(g, R, loff, cols);
