@@ -72,7 +72,7 @@ REPLICATED_ONLY = {"c1", "c4", "t1", "s1", "p1"}  # C4 LDBC replica; C1 all-root
 COUNT_MODE = {"c5"}   # the last hop counts its rows (count mode)
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # ≈7e4 Person, ≈2e6 Knows
 # kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)
-HOT_KERNELS = ("k_femit", "k_flists", "k_isect_merge", "k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light", "k_expand_light_sliced", "k_trav_filter",
+HOT_KERNELS = ("k_femit", "k_flists", "k_fof2_a", "k_fof2_b", "k_isect_merge", "k_expand_heavy", "k_expand_heavy_sliced", "k_expand_light", "k_expand_light_sliced", "k_trav_filter",
                "k_expand_light_check", "k_expand_heavy_check", "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit", "k_bfs_push", "k_bfs_prep", "k_bfs_emit",
                "k_gather_cols", "k_compact_segments")
 # timer records that are spans over other records or move no HBM bytes (not summed into a step)

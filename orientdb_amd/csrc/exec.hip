@@ -66,7 +66,7 @@ class Timer {
                                        "k_expand_light_sliced", "k_expand_light_check", "k_expand_heavy_check",
                                        "k_check", "k_bfs_pull", "k_bfs_pull_sparse", "k_bfs_pull_exit", "k_bfs_push",
                                        "k_bfs_emit", "k_trav_filter", "trav_select", "k_femit",
-                                       "k_isect_merge", "k_flists", "k_flist_copy"};
+                                       "k_isect_merge", "k_flists", "k_flist_copy", "k_fof2_a", "k_fof2_b"};
     for (const char *h : kHot)
       if (std::strcmp(name, h) == 0) return true;
     return false;
@@ -305,6 +305,8 @@ class Executor {
                           : p_.kind == Plan::SELECT ? select_expand()
                                                     : shortest_path());
       if (dist_) tr_->allgather_n({0, 0}, s_);  // the servers stop
+    } else if (!empty && fof2_ok()) {
+      fof2();
     } else if (!empty) {
       // a partitioned run keeps stepping with no local rows: every rank takes part in every exchange
       for (size_t i = 0; i < p_.steps.size() && (R_ > 0 || dist_); ++i) {
@@ -1865,6 +1867,78 @@ class Executor {
            p_.out_aliases[0] == st.dst && !p_.optional[st.dst] && p_.limit < 0 && o_.limit < 0 &&
            o_.mode == OMX_MODE_MATERIALIZE;
   }
+  // configs[0]'s shape — root, an unfiltered hop, the marked last hop — on a graph of ≤ kFof2Bits vertices:
+  // four launches (kernels.hip k_fof2_a / _b + the list) and one host round trip for the whole MATCH. The same
+  // distinct set and accounting as root() + expand_step() + expand_mark()'s factorized branch: E_t = E1
+  // + Σ over hop 1's rows of deg2, bindings = that sum, edges read = E1 + the distinct sources' entries
+  bool fof2_ok() {
+    if (!mark_fuse_ || !factor_ || dist_ || g_.partitioned() || p_.kind != Plan::MATCH || p_.steps.size() != 3 ||
+        g_.V > kFof2Bits || g_.V == 0)
+      return false;
+    const Step &r = p_.steps[0], &h1 = p_.steps[1], &h2 = p_.steps[2];
+    return r.kind == S_ROOT && r.cand_bm >= 0 && h1.kind == S_EXPAND && h2.kind == S_EXPAND && h1.src == r.dst && h2.src == h1.dst &&
+           h1.filter_bm < 0 && !h1.optional && !h1.distinct_nb && !h1.adj.parts.empty() && !h2.adj.parts.empty() &&
+           mark_ok(h2);
+  }
+  void fof2() {
+    const Step &r = p_.steps[0], &h1 = p_.steps[1], &h2 = p_.steps[2];
+    const uint64_t W = (g_.V + 63) / 64;
+    DBuf<uint64_t> z(&pool_, 2 * W + 4);  // ubm, bm, acc: one memset
+    DBuf<uint32_t> blk(&pool_, bitmap_list_blocks(W)), out(&pool_, g_.V);
+    HIP_CHECK(hipMemsetAsync(z.p, 0, (2 * W + 4) * 8, s_));
+    // ≥ 16 Ki edges a workgroup: its flush (W words, into the global set at agent scope) stays small beside
+    // its marking (measured at RMAT-16: 4 Ki edges a workgroup, 4× the flushes, took 0.085 ms against 0.046)
+    auto edges = [&](const AdjSpec &as) {
+      uint64_t E = 0;
+      for (auto &pt : as.parts) E += pt.second == 0 ? g_.esets[pt.first].n_edges : g_.esets[pt.first].n_in_edges;
+      return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus(), E / 16384));
+    };
+    Fof2Args a{};
+    a.a1 = make_adj(h1.adj);
+    a.a2 = make_adj(h2.adj);
+    a.roots = bitmap(r.cand_bm);
+    a.rank = o_.shard_world > 1 ? o_.shard_rank : 0;
+    a.world = std::max(1, o_.shard_world);
+    a.ubm = z.p;
+    a.bm = z.p + W;
+    a.acc = z.p + 2 * W;
+    a.V = g_.V;
+    a.W = W;
+    // (algorithmic bytes, amended once the counts are back: hop 1 reads the roots' words, its row pointers
+    // and entries and the targets' row pointers (E_t); hop 2 the distinct sources' words, row pointers and
+    // entries; the list the marked words and the vertices written)
+    tm_.begin("k_fof2_a");
+    launch_fof2(a, 0, edges(h1.adj), nullptr, nullptr, nullptr, s_);
+    tm_.end();
+    const size_t ra = tm_.last();
+    tm_.begin("k_fof2_b");
+    launch_fof2(a, 1, edges(h2.adj), nullptr, nullptr, nullptr, s_);
+    tm_.end();
+    const size_t rb = tm_.last();
+    const Mail ml = mail();
+    tm_.begin("k_bitmap_to_list");
+    launch_fof2(a, 2, 0, blk.p, out.p, &ml, s_);
+    tm_.end();
+    const size_t rl = tm_.last();
+    const uint64_t *m = wait_mail();
+    const uint64_t n = m[0], e1 = m[1], et = m[2], eu = m[3];
+    const uint64_t ba = W * 8 + 8ull * g_.V * a.a1.n + 4 * e1 + 16 * e1, bb = W * 16 + 8ull * g_.V * a.a2.n + 4 * eu,
+                   bl = W * 8 + 4 * n;
+    tm_.amend_at(ra, ba);
+    tm_.amend_at(rb, bb);
+    tm_.amend_at(rl, bl);
+    alg_bytes_ += ba + bb + bl;
+    edges_ += e1 + et;
+    edges_iter_ += e1 + eu;
+    marked_bindings_ = et;
+    marked_ = true;
+    factorized_hops_++;
+    bound_[r.dst] = bound_[h1.dst] = bound_[h2.dst] = 1;
+    col_[h2.dst] = std::move(out);
+    R_ = n;
+    segmented_ = false;
+  }
+
   void expand_mark(const Step &st) {
     route_owner(st.src);
     DBuf<uint64_t> bm(&pool_, std::max<uint64_t>(nwords_, 1));

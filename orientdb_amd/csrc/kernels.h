@@ -241,6 +241,21 @@ void launch_compact_segments(int ncols, uint32_t *const *in, uint32_t *const *ou
 // two launches: the bitmap's vertices in [lo, hi) (and v % world == rank), in order, and their count;
 // blk holds bitmap_list_blocks(nwords) words of scratch
 unsigned bitmap_list_blocks(uint64_t nwords);
+// configs[0] in four launches and one host round trip (kernels.hip k_fof2_a / k_fof2_b + the list):
+// roots → hop 1 → hop 2 marked → the marked set's ascending list in out; the mailbox gets {m, E1, E_t, EU}
+constexpr uint32_t kFof2Bits = 1u << 18;  // V bound: k_fof2_b stages two V-bit sets in LDS (64 KiB)
+struct Fof2Args {
+  DAdj a1, a2;            // hop 1 / hop 2 adjacency
+  const uint64_t *roots;  // V-bit root set (the rank's share: v % world == rank)
+  int32_t rank, world;
+  uint64_t *ubm, *bm;     // [W] zeroed: hop 1's targets (hop 2's distinct sources), hop 2's targets
+  uint32_t V;
+  uint64_t W;             // words of a V-bit set
+  uint64_t *acc;          // [3] zeroed: E1, E_t, EU
+};
+// phase 0: hop 1 (grid workgroups); 1: hop 2; 2: the list (blk: bitmap_list_blocks(W) words) and the mail
+void launch_fof2(const Fof2Args &a, int phase, unsigned grid, uint32_t *blk, uint32_t *out, const Mail *mail,
+                 hipStream_t s);
 void launch_bitmap_list_2k(const uint64_t *words, uint64_t nwords, uint32_t V, int rank, int world, uint32_t lo,
                            uint32_t hi, uint32_t *blk, uint32_t *out, const Mail &count, hipStream_t s);
 // one workgroup: soffs = inclusive prefix of cnt (soffs[0] = 0); mail = {soffs[nseg_h], soffs[nseg],

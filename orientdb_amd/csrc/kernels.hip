@@ -2252,7 +2252,7 @@ __global__ __launch_bounds__(kListB) void k_list_counts(const uint64_t *words, u
 }
 __global__ __launch_bounds__(kListB) void k_list_scatter(const uint64_t *words, uint64_t n, uint32_t V, int rank,
                                                          int world, uint32_t lo, uint32_t hi, const uint32_t *blk,
-                                                         uint32_t *out, Mail mail) {
+                                                         uint32_t *out, Mail mail, const uint64_t *extra, int nextra) {
   __shared__ uint32_t s_w[kListB / 64];
   __shared__ unsigned long long s_pre[kListB / 64];
   // prefix of the blocks before this one
@@ -2273,8 +2273,9 @@ __global__ __launch_bounds__(kListB) void k_list_scatter(const uint64_t *words, 
     out[o++] = (uint32_t)(i * 64 + __builtin_ctzll(w));
     w &= w - 1;
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the host only needs the count
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the host only needs the count (and extra's words)
     mail.p[0] = pre + tot;
+    for (int j = 0; j < nextra; ++j) mail.p[1 + j] = extra[j];
     mail_post(mail);
   }
 }
@@ -2283,10 +2284,135 @@ void launch_bitmap_list_2k(const uint64_t *words, uint64_t n, uint32_t V, int ra
   const unsigned g = nblocks(n, kListB);
   hipLaunchKernelGGL(k_list_counts, dim3(g), dim3(kListB), 0, s, words, n, V, rank, world, lo, hi, blk);
   KCHECK("k_list_counts");
-  hipLaunchKernelGGL(k_list_scatter, dim3(g), dim3(kListB), 0, s, words, n, V, rank, world, lo, hi, blk, out, mail);
+  hipLaunchKernelGGL(k_list_scatter, dim3(g), dim3(kListB), 0, s, words, n, V, rank, world, lo, hi, blk, out, mail,
+                     (const uint64_t *)nullptr, 0);
   KCHECK("k_list_scatter");
 }
 unsigned bitmap_list_blocks(uint64_t nwords) { return nblocks(nwords, kListB); }
+
+// ---- configs[0] in four launches (round 5) ----------------------------------------------------------
+// MATCH {class:Person}-Knows->{}-Knows->{as:fof} RETURN fof on a small graph (V ≤ kFof2Bits): the roots'
+// hop, the marked last hop (Executor::expand_mark's factorized branch: each distinct middle vertex's
+// adjacency read once) and the list of the marked set, queued back to back with one host round trip —
+// the general path's 15-odd launches and four round trips cost more than the work at RMAT-16.
+//   k_fof2_a: every edge (v, b) of hop 1 with v a root: b marked (LDS bitmap, flushed to ubm once per
+//             workgroup); E1 += 1; E_t += deg2(b)
+//   k_fof2_b: every edge (b, c) of hop 2 with b in ubm (staged in LDS): c marked (likewise, into bm);
+//             EU += 1
+//   then bm's ascending list (k_list_counts / k_list_scatter), whose last workgroup posts {m, E1, E_t,
+//   EU}. (A single cooperative launch with grid barriers measured 0.57 ms: the in-kernel cross-XCD
+//   bitmap traffic at agent scope costs more than the launches it saves.)
+// every edge of one part, a wave per contiguous range of 64-edge groups (balanced over edges, not
+// vertices): f(ok, v, x) for the lane's edge (v → x)
+template <class F>
+__device__ __forceinline__ void fof2_edges(const DAdjPart &p, uint32_t V, F &&f) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t E = p.rp[V];
+  const uint64_t chunk = ((E + nw - 1) / nw + 63) & ~63ull;
+  const uint64_t e0 = w * chunk, e1 = min(E, e0 + chunk);
+  if (e0 >= e1) return;
+  uint32_t lo = 0, hi = V;  // the source of e0: the last v with rp[v] ≤ e0 (rp[V] = E > e0)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (p.rp[mid] <= e0) lo = mid;
+    else hi = mid;
+  }
+  uint32_t v0 = lo;
+  for (uint64_t g = e0; g < e1; g += 64) {
+    const uint64_t e = g + lane;
+    const bool ok = e < e1;
+    uint32_t v = v0;
+    if (ok) {  // galloping from the group's first source
+      uint32_t a = v0, b = v0 + 1, step = 1;
+      while (b < V && p.rp[b] <= e) {
+        a = b;
+        step <<= 1;
+        b = a + step;
+      }
+      if (b > V) b = V;
+      while (b - a > 1) {
+        const uint32_t mid = (a + b) >> 1;
+        if (p.rp[mid] <= e) a = mid;
+        else b = mid;
+      }
+      v = a;
+    }
+    f(ok, v, ok ? p.col[e] : 0u);
+    v0 = __builtin_amdgcn_readlane(v, 63);
+  }
+}
+__device__ __forceinline__ void fof2_add(unsigned long long *acc, uint64_t x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  if ((threadIdx.x & 63) == 0 && x) atomicAdd(acc, (unsigned long long)x);
+}
+// a workgroup's LDS marks into the global set (only words with a new bit)
+__device__ __forceinline__ void fof2_flush(const unsigned long long *s_bm, uint64_t *bm, uint64_t W) {
+  __syncthreads();
+  for (uint64_t w = threadIdx.x; w < W; w += blockDim.x) {
+    const unsigned long long m = s_bm[w];
+    if (m && (__hip_atomic_load(&bm[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & m) != m)
+      atomicOr((unsigned long long *)&bm[w], m);
+  }
+}
+__global__ __launch_bounds__(1024) void k_fof2_a(Fof2Args a) {
+  extern __shared__ unsigned long long s_fof[];
+  for (uint64_t w = threadIdx.x; w < a.W; w += blockDim.x) s_fof[w] = 0;
+  __syncthreads();
+  uint64_t e1 = 0, et = 0;
+  for (int q = 0; q < a.a1.n; ++q)
+    fof2_edges(a.a1.p[q], a.V, [&](bool ok, uint32_t v, uint32_t b) {
+      if (ok && ((a.roots[v >> 6] >> (v & 63)) & 1ull) && (a.world <= 1 || v % (uint32_t)a.world == (uint32_t)a.rank)) {
+        e1 += 1;
+        et += adj_degree(a.a2, b);
+        atomicOr(&s_fof[b >> 6], 1ull << (b & 63));
+      }
+    });
+  unsigned long long *acc = reinterpret_cast<unsigned long long *>(a.acc);
+  fof2_add(acc + 0, e1);
+  fof2_add(acc + 1, et);
+  fof2_flush(s_fof, a.ubm, a.W);
+}
+__global__ __launch_bounds__(1024) void k_fof2_b(Fof2Args a) {
+  extern __shared__ unsigned long long s_fof[];
+  unsigned long long *s_ub = s_fof, *s_bm = s_fof + a.W;
+  for (uint64_t w = threadIdx.x; w < a.W; w += blockDim.x) {
+    s_ub[w] = a.ubm[w];
+    s_bm[w] = 0;
+  }
+  __syncthreads();
+  uint64_t eu = 0;
+  for (int q = 0; q < a.a2.n; ++q)
+    fof2_edges(a.a2.p[q], a.V, [&](bool ok, uint32_t b, uint32_t c) {
+      if (ok && ((s_ub[b >> 6] >> (b & 63)) & 1ull)) {
+        eu += 1;
+        atomicOr(&s_bm[c >> 6], 1ull << (c & 63));
+      }
+    });
+  fof2_add(reinterpret_cast<unsigned long long *>(a.acc) + 2, eu);
+  fof2_flush(s_bm, a.bm, a.W);
+}
+
+void launch_fof2(const Fof2Args &a, int phase, unsigned grid, uint32_t *blk, uint32_t *out, const Mail *mail,
+                 hipStream_t s) {
+  if (a.V > kFof2Bits || a.W != (a.V + 63) / 64) fail(OMX_E_INVALID, "internal: k_fof2 over a set its LDS cannot hold");
+  if (phase == 0) {
+    hipLaunchKernelGGL(k_fof2_a, dim3(std::max(1u, grid)), dim3(1024), a.W * 8, s, a);
+    KCHECK("k_fof2_a");
+  } else if (phase == 1) {
+    hipLaunchKernelGGL(k_fof2_b, dim3(std::max(1u, grid)), dim3(1024), a.W * 16, s, a);
+    KCHECK("k_fof2_b");
+  } else {
+    const unsigned g = nblocks(a.W, kListB);
+    hipLaunchKernelGGL(k_list_counts, dim3(g), dim3(kListB), 0, s, (const uint64_t *)a.bm, a.W, a.V, 0, 1, 0u, a.V, blk);
+    KCHECK("k_list_counts");
+    hipLaunchKernelGGL(k_list_scatter, dim3(g), dim3(kListB), 0, s, (const uint64_t *)a.bm, a.W, a.V, 0, 1, 0u, a.V,
+                       blk, out, *mail, (const uint64_t *)a.acc, 3);
+    KCHECK("k_list_scatter");
+  }
+}
 
 // inclusive prefix of the segments' row counts (soffs[0] = 0, soffs[i+1] = Σ_{j<=i}) and the four
 // words a filtered expansion reads back: rows of the first nseg_h segments, all rows, member words
