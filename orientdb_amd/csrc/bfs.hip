@@ -462,12 +462,8 @@ void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const 
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kPullB, 0) != hipSuccess || per < 1) per = 2;
   // resident workgroups per CU: 7 of the 8 that fit measured fastest at C3 (4.26 ms against 5.54 ms
-  // at 8 and 4.60 at 5: with a full CU the random gathers thrash L2); OMX_PULL_PER overrides
-  static const int cap = [] {
-    const char *e = std::getenv("OMX_PULL_PER");
-    return e ? std::atoi(e) : 7;
-  }();
-  if (cap > 0 && cap < per) per = cap;
+  // at 8 and 4.60 at 5: with a full CU the random gathers thrash L2)
+  per = std::min(per, 7);
   const unsigned g = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cus * per);
   hipLaunchKernelGGL(kern, dim3(g), dim3(kPullB), 0, s, V, rp, col, part, E, ntiles, lanes, frontier, hub_fr, fbm,
                      visited, next);
@@ -665,15 +661,8 @@ void launch_bfs_pull_w(const uint64_t *rp, const uint32_t *col, uint64_t E, cons
                        hipStream_t s, bool hubs_only) {
   const uint64_t nt = bfs_pull_w_tiles(E);
   if (!nt || !lanes) return;
-  static const int per = [] {  // workgroups per CU (4 waves each)
-    const char *e = std::getenv("OMX_PULLW_PER");
-    return e ? std::max(1, std::atoi(e)) : 1;
-  }();
-  static const uint32_t lds_cap = [] {  // OMX_PULLW_LDS_HUBS=n: at most n hub masks in LDS
-    const char *e = std::getenv("OMX_PULLW_LDS_HUBS");
-    return e ? (uint32_t)std::min<long>(kPwLdsHubs, std::max(0l, std::atol(e))) : (uint32_t)kPwLdsHubs;
-  }();
-  const uint32_t nlds = std::min(nhubs, lds_cap);
+  constexpr int per = 1;  // workgroups per CU (16 waves each: one LDS copy of the hub masks a CU)
+  const uint32_t nlds = std::min(nhubs, (uint32_t)kPwLdsHubs);
   static const bool slow_all = [] {  // OMX_PULLW_SLOW=1: every tile through k_bfs_pull_w_slow (tests)
     const char *e = std::getenv("OMX_PULLW_SLOW");
     return e && std::strcmp(e, "0") != 0;
@@ -1001,12 +990,8 @@ uint32_t build_pull_col(const uint64_t *rp_self, const uint64_t *rp_other, const
   hipLaunchKernelGGL(k_hub_mark, dim3(g), dim3(kB), 0, s, rp_other, V, (uint64_t)t, hub_idx, hubs, count);
   KCHECK("k_hub_mark");
   // hub index = rank by degree (descending): the masks gathered most often share the first lines of
-  // the packed array (OMX_PULL_HUB_ORDER=vertex keeps discovery order)
-  static const bool by_rank = [] {
-    const char *e = std::getenv("OMX_PULL_HUB_ORDER");
-    return !(e && std::strcmp(e, "vertex") == 0);
-  }();
-  if (by_rank && cum > 1) {
+  // the packed array
+  if (cum > 1) {
     const uint32_t n = (uint32_t)cum;
     uint32_t *deg = nullptr, *deg2 = nullptr, *h2 = nullptr;
     void *tmp = nullptr;
@@ -1032,11 +1017,7 @@ uint32_t build_pull_col(const uint64_t *rp_self, const uint64_t *rp_other, const
     const unsigned ge = (unsigned)std::min<uint64_t>(nblocks(E, kB), (uint64_t)cus * 16);
     hipLaunchKernelGGL(k_pull_annotate, dim3(ge), dim3(kB), 0, s, col, E, hub_idx, out);
     KCHECK("k_pull_annotate");
-    static const bool sort_rows = [] {
-      const char *e = std::getenv("OMX_PULL_SORT");
-      return !(e && std::strcmp(e, "0") == 0);
-    }();
-    if (sort_rows && cum > 0 && E < (1ull << 40)) {
+    if (cum > 0 && E < (1ull << 40)) {
       uint32_t *row = nullptr;
       uint64_t *k0 = nullptr, *k1 = nullptr;
       void *tmp = nullptr;

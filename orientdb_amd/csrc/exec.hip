@@ -241,9 +241,8 @@ class Executor {
     if (const char *de = std::getenv("OMX_DENSE_EXCHANGE")) dense_exchange_ = std::strcmp(de, "0") != 0;
     if (const char *hp = std::getenv("OMX_HUB_PUSH")) hub_push_ = std::strcmp(hp, "force") == 0 ? 2 : std::strcmp(hp, "0") != 0 ? 1 : 0;
     // OMX_MERGE: "0" keeps every closing check a binary-search probe; "force" merges every row whose two
-    // lists fit a tile (tests); OMX_MERGE_RATIO: merge when the longer list is ≤ ratio × the shorter
+    // lists fit a tile (tests); merge_ratio_: merge when the longer list is ≤ ratio × the shorter
     if (const char *mg = std::getenv("OMX_MERGE")) merge_ = std::strcmp(mg, "force") == 0 ? 2 : std::strcmp(mg, "0") != 0 ? 1 : 0;
-    if (const char *mr = std::getenv("OMX_MERGE_RATIO")) merge_ratio_ = std::max(1.0, std::strtod(mr, nullptr));
     if (const char *hb = std::getenv("OMX_PULL_HUBS")) pull_hubs_ = (uint32_t)std::strtoul(hb, nullptr, 10);
     if (const char *d = std::getenv("OMX_BFS_PULL_DIV")) pull_div_ = std::max(1e-9, std::strtod(d, nullptr));
     if (const char *lv = std::getenv("OMX_PULL_LIVE")) pull_live_ = std::strcmp(lv, "0") != 0;

@@ -431,7 +431,9 @@ __global__ __launch_bounds__(64 * kFlWaves) void k_flist(FlistArgs a) {
     const uint32_t nr = (uint32_t)min<uint64_t>(h.ns, (uint64_t)kFlSlots) * 16;
     const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc((void *)(a.info + h.s0), 0, (int32_t)nr, 0x00020000);
     const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(ir, 16 * lane, 0, 0);
-    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(ir, 16 * (64 + lane), 0, 0);
+    // (a tile over ≤ 64 sources — all of M1's — issues one load: the TA's cost is per instruction)
+    u32x4 v1 = {0u, 0u, 0u, 0u};
+    if (h.ns > 64) v1 = __builtin_amdgcn_raw_buffer_load_b128(ir, 16 * (64 + lane), 0, 0);
     sv[0] = make_uint4(v0.x, v0.y, v0.z, v0.w);
     sv[1] = make_uint4(v1.x, v1.y, v1.z, v1.w);
   };
@@ -548,6 +550,7 @@ __global__ __launch_bounds__(64 * kFlWaves) void k_flist(FlistArgs a) {
 #pragma unroll
     for (int q = 0; q < kFlQ; ++q) {
       const uint32_t k = 64 * q + lane;
+      if (q > 0 && tot <= 256u * q) break;  // (uniform: no store instruction for an empty row of lanes)
       const uint4 v = s4[k];
       u32x4 vv;
       vv.x = v.x;
@@ -563,6 +566,7 @@ __global__ __launch_bounds__(64 * kFlWaves) void k_flist(FlistArgs a) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const uint32_t k = 64 * c + lane;
+      if (c > 0 && h.ns <= 64) break;  // (uniform)
       const uint32_t cf = w.coff[r][k], d = cf - (uint32_t)c0;
       const bool in = !deferred & (k < h.ns) & (cf > (uint32_t)c0) & (d < (uint32_t)kFlChunks);
       const uint32_t cl = in ? d : 0u;

@@ -454,7 +454,7 @@ void launch_bfs_pull_exit(uint32_t V, const uint64_t *rp, const uint32_t *col, u
                           const uint64_t *frontier, const uint64_t *hub_fr, const uint64_t *visited, uint64_t *next,
                           uint32_t *rest, unsigned long long *counts, int cus, hipStream_t s, uint32_t vlo = 0);
 // hub-annotated col of a CSR for k_bfs_pull (returns the hub count; hub_idx u32[V], hist u32[4096] scratch)
-// rp_self: the CSR's own row pointers (its rows are re-ordered hub-first; OMX_PULL_SORT=0 keeps them)
+// rp_self: the CSR's own row pointers (its rows are re-ordered hub-first)
 uint32_t build_pull_col(const uint64_t *rp_self, const uint64_t *rp_other, const uint32_t *col, uint32_t V, uint64_t E,
                         uint32_t max_hubs,
                         uint32_t *hub_idx, uint32_t *hist, unsigned long long *count, uint32_t *hubs,

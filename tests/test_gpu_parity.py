@@ -101,6 +101,7 @@ class _Ref:
                                simple=simple)
         self._db = None
         self.bindings = None  # the C DFS's complete matches of the last expected() it answered
+        self._memo = {}  # (query, cols) → (rows, bindings): the same case is checked under several modes
 
     @property
     def db(self):
@@ -110,6 +111,14 @@ class _Ref:
         return self._db
 
     def expected(self, query, cols):
+        key = (query, tuple(cols) if cols is not None else None)
+        if key not in self._memo:
+            rows = self._expected(query, cols)
+            self._memo[key] = (rows, self.bindings)
+        rows, self.bindings = self._memo[key]
+        return rows
+
+    def _expected(self, query, cols):
         from oracle import dfs
         self.bindings = None
         if cols is not None:
