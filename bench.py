@@ -205,7 +205,9 @@ def cpu_baseline(g, query, target_s=12.0, single_thread_too=False):
     out = dfs_sample(dfs, cg, query, threads, target_s, nroots_total)
     out["cores_visible"] = visible
     try:  # the same bindings set-at-a-time (the set-based CPU path beside the DFS)
-        out["set_based"] = set_sample(dfs, cg, query, threads, target_s, nroots_total)
+        sb = set_sample(dfs, cg, query, threads, target_s, nroots_total, out.pop("bindings_per_root"))
+        if sb is not None:
+            out["set_based"] = sb
     except NotImplementedError:
         pass
     if single_thread_too:  # configs[0]: the faithful one-thread DFS beside the port on the job's cores
@@ -232,16 +234,25 @@ def dfs_sample(dfs, cg, query, threads, target_s, nroots_total):
             "sample": "%d of %d roots x %d repetitions (%.1f s, %d edges, %d bindings; oracle/dfs_ref.c DFS, %d "
                       "thread%s)" % (sample, nroots_total, reps, secs, edges, bindings, threads,
                                      "" if threads == 1 else "s = the job's host-core share (OMP_NUM_THREADS)"),
-            "bindings_per_s": bindings / secs}
+            "bindings_per_s": bindings / secs, "bindings_per_root": bindings / max(sample * reps, 1)}
 
 
-def set_sample(dfs, cg, query, threads, target_s, nroots_total):
+# rows the set-based CPU path may hold at once (it writes every hop's rows: ~16 B a row and column)
+SET_MAX_ROWS = 1.5e8
+
+
+def set_sample(dfs, cg, query, threads, target_s, nroots_total, bindings_per_root):
     """oracle/set_ref.c (the device's algebra on the host cores: per hop the distinct sources' filtered
     lists once, then every row written) over the whole root set when it fits ≈ target_s / 3 per run, else a
-    bounded root sample; repeated until ≈ target_s is timed."""
-    probe = dfs.set_run(cg, query, nthreads=threads, root_sample=min(nroots_total, 4096))
+    bounded root sample; repeated until ≈ target_s is timed. The sample is capped so that its rows
+    (bindings per root from the DFS sample) stay under SET_MAX_ROWS; None when one root alone exceeds it
+    (C5's 3-hop: 4e8 rows a root)."""
+    cap = int(SET_MAX_ROWS / max(bindings_per_root, 1e-9))
+    if cap < 1:
+        return None
+    probe = dfs.set_run(cg, query, nthreads=threads, root_sample=min(nroots_total, 4096, cap))
     per_root = max(probe["seconds"] / max(probe["nroots"], 1), 1e-9)
-    sample = int(min(nroots_total, max(4096, target_s / 3 / per_root)))
+    sample = int(min(nroots_total, cap, max(4096, target_s / 3 / per_root)))
     edges = bindings = 0
     secs = 0.0
     reps = 0
