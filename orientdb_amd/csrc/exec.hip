@@ -2080,14 +2080,23 @@ class Executor {
     }
     const uint64_t *rn = nsel.p;
     // (the rows are grouped by source already: the non-empty rows keep their sorted order)
-    DBuf<uint32_t> gs(&pool_, std::max<uint64_t>(R, 1)), perm(&pool_, std::max<uint64_t>(R, 1));
-    launch_gather_u32_dev(g.p, idx.p, rn, R, gs.p, s_);
-    launch_gather_u32_dev(perm_sorted, idx.p, rn, R, perm.p, s_);
+    // (the non-empty rows' source indices and carried columns in one pass)
+    DBuf<uint32_t> gs(&pool_, std::max<uint64_t>(R, 1));
     std::vector<DBuf<uint32_t>> sc;
-    for (int c : cols) {
+    FemitGather fg{};
+    fg.g = g.p;
+    fg.perm = perm_sorted;
+    fg.idx = idx.p;
+    fg.nd = rn;
+    fg.gs = gs.p;
+    fg.nc = (int32_t)cols.size();
+    if (cols.size() > (size_t)kFemitCols) fail(OMX_E_INVALID, "internal: emission over more carried columns than k_femit_w takes");
+    for (size_t c = 0; c < cols.size(); ++c) {
       sc.emplace_back(&pool_, std::max<uint64_t>(R, 1));
-      launch_gather_u32_dev(col_[c].p, perm.p, rn, R, sc.back().p, s_);
+      fg.in[c] = col_[cols[c]].p;
+      fg.out[c] = sc.back().p;
     }
+    launch_femit_gather(fg, R, s_);
     // 2. output rows of every binding row: the scan of its list length (rows ≥ Rn: 0, so roff[R] = N);
     // list position of output o
     DBuf<uint64_t> roff(&pool_, R + 1), rbase(&pool_, std::max<uint64_t>(R, 1));

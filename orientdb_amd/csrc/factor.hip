@@ -638,8 +638,13 @@ __global__ __launch_bounds__(256) void k_flist_wide(FlistArgs a) {
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t EC = *a.ec;
   const uint64_t nt = (EC + kFlChunks - 1) / kFlChunks;
-  for (uint64_t t = (uint64_t)blockIdx.x * 4 + wv; t < nt; t += (uint64_t)gridDim.x * 4) {
-    if (a.ntot[t] != kFlDeferred) continue;
+  // (a wave takes 64 consecutive tiles' counts at once and walks the deferred ones: one round trip per
+  // 64 tiles, not per tile — a scan one tile at a time took 36 µs at M1, which defers none)
+  for (uint64_t g0 = ((uint64_t)blockIdx.x * 4 + wv) * 64; g0 < nt; g0 += (uint64_t)gridDim.x * 4 * 64) {
+   const uint64_t tl = g0 + lane;
+   uint64_t dm = __builtin_amdgcn_ballot_w64(tl < nt && a.ntot[tl < nt ? tl : 0] == kFlDeferred);
+   for (; dm; dm &= dm - 1) {
+    const uint64_t t = g0 + __builtin_ctzll(dm);
     const uint64_t s0 = a.rb[2 * t], s1 = a.rb[2 * t + 1], c0 = t * kFlChunks;
     const uint32_t nc = (uint32_t)min<uint64_t>((uint64_t)kFlChunks, EC - c0);
     uint32_t qb = 0;
@@ -683,6 +688,7 @@ __global__ __launch_bounds__(256) void k_flist_wide(FlistArgs a) {
     }
     if (lane == 0) a.ntot[t] = qb;
     __builtin_amdgcn_wave_barrier();
+   }
   }
 }
 
@@ -780,7 +786,7 @@ void launch_flist(const FlistArgs &a, uint64_t nt_bound, int cus, hipStream_t s)
   const dim3 grid((unsigned)std::min<uint64_t>((nt_bound + kFlWaves - 1) / kFlWaves, (uint64_t)cus)), blk(64 * kFlWaves);
   hipLaunchKernelGGL(k_flist, grid, blk, 0, s, a);
   KCHECK("k_flist");
-  const dim3 gw((unsigned)std::min<uint64_t>((nt_bound + 3) / 4, (uint64_t)cus * 4)), bw(256);
+  const dim3 gw((unsigned)std::min<uint64_t>((nt_bound + 255) / 256, (uint64_t)cus * 4)), bw(256);
   hipLaunchKernelGGL(k_flist_wide, gw, bw, 0, s, a);
   KCHECK("k_flist_wide");
 }
@@ -792,6 +798,21 @@ void launch_flist_finish(const FlistArgs &a, const uint64_t *coff, const uint64_
   KCHECK("k_flist_copy");
   hipLaunchKernelGGL(k_flist_loff, dim3(nblocks(a.U + 1, 256)), dim3(256), 0, s, coff, a.U, a.ec, base, a.loc, loff);
   KCHECK("k_flist_loff");
+}
+
+__global__ void k_femit_gather(FemitGather a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *a.nd) return;
+  const uint32_t j = a.idx[i];
+  a.gs[i] = a.g[j];
+  const uint32_t p = a.perm[j];
+  for (int c = 0; c < a.nc; ++c) a.out[c][i] = a.in[c][p];
+}
+void launch_femit_gather(const FemitGather &a, uint64_t cap, hipStream_t s) {
+  if (!cap) return;
+  if (a.nc < 0 || a.nc > kFemitCols) fail(OMX_E_INVALID, "internal: k_femit_gather columns");
+  hipLaunchKernelGGL(k_femit_gather, dim3(nblocks(cap, 256)), dim3(256), 0, s, a);
+  KCHECK("k_femit_gather");
 }
 
 uint64_t femit_tiles(uint64_t N) { return (N + kEwTile - 1) / kEwTile; }

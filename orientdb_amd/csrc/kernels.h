@@ -307,6 +307,16 @@ uint64_t femit_tiles(uint64_t N);
 // nd: a device row count ≤ R (rows past it: length 0, no base); nullptr: all R rows
 void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s,
                       const uint64_t *nd = nullptr);
+// the non-empty rows (idx[0, *nd)) in one pass: gs[i] = g[idx[i]], p = perm[idx[i]], out[c][i] = in[c][p]
+struct FemitGather {
+  const uint32_t *g, *perm, *idx;
+  const uint64_t *nd;
+  uint32_t *gs;
+  int32_t nc;
+  const uint32_t *in[kFemitCols];
+  uint32_t *out[kFemitCols];
+};
+void launch_femit_gather(const FemitGather &a, uint64_t cap, hipStream_t s);
 void launch_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, const uint64_t *roff, uint64_t *rbase,
                        hipStream_t s, const uint64_t *nd = nullptr);
 // rb[2·femit_tiles(N)]: first / last binding row of every output tile; regular[t] = the tile is full and

@@ -518,6 +518,34 @@ def test_factorized_lists_rmat16_digest(rmat16, monkeypatch):
     assert out["1"][2] == want["bindings"] and out["1"][1] == want["edges"] and out["1"][3] == want["digest"]
 
 
+@pytest.mark.parametrize("every", [1, 7, 300])
+def test_factorized_lists_sparse_sources(every, monkeypatch):
+    """k_flists when most distinct sources have no out-edge: root 0 reaches b = 1 … 3000, and only every
+    `every`-th b has out-edges (to 3001 + (b mod 97) and 3001 + (b mod 89)). Sources without chunks still
+    count in a tile's source range, so a tile spans more than its 128 chunk slots' sources and goes to
+    k_flist_wide (every = 7, 300); rows equal the brute-force enumeration on both lists paths."""
+    import orientdb_amd as o
+    nb, V = 3000, 3200
+    out = {0: list(range(1, nb + 1))}
+    for b in range(1, nb + 1):
+        if b % every == 0:
+            out[b] = sorted({3001 + b % 97, 3001 + b % 89})
+    rp = np.zeros(V + 1, np.uint64)
+    rp[1:] = np.cumsum([len(out.get(v, [])) for v in range(V)])
+    col = np.array([t for v in range(V) for t in out.get(v, [])], np.uint32)
+    g = o.GraphSnapshot.person_knows(rp, col, seed=3, device=0, keep_csr=True)
+    q = "MATCH {class:Person,as:a,where:(uid = 0)}-Knows->{as:b}-Knows->{as:c,where:(age >= 0)} RETURN a,b,c"
+    want = sorted((0, b, c) for b in out[0] for c in out.get(b, []))
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    for lists in ("1", "0"):
+        monkeypatch.setenv("OMX_FLISTS", lists)
+        rs = o.OMatchStatement(q).execute(g, documents=False)
+        got = sorted(tuple(int(x) & ((1 << 48) - 1) for x in row) for row in rs.rows)
+        assert got == want, lists
+        assert rs.info["factorized_hops"] >= 1
+    g.close()
+
+
 SEMI_QUERIES = [
     ("ab_of_abc", "MATCH {class:Person,as:a,where:(age < 5)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a, b",
      ["a", "b"]),
