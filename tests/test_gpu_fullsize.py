@@ -162,7 +162,7 @@ def test_c5_shape_partitioned_rmat16():
 
 
 C5_QUERY = "MATCH {class:Person,as:a,where:(uid < 64)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d"
-C5_WINDOW = "MATCH {class:Person,as:a,where:(uid < 4)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d"
+C5_WINDOW = "MATCH {class:Person,as:a,where:(uid < 2)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d"
 
 
 @pytest.fixture(scope="module")
@@ -190,13 +190,13 @@ def test_c5_rmat26_count(rmat26, c5_ref):
 
 
 def test_c5_rmat26_window_materialized_digest(rmat26):
-    """configs[4]'s 3-hop on a root window that fits HBM when materialized (uid < 4): every row of the
+    """configs[4]'s 3-hop on a root window that fits HBM when materialized (uid < 2): every row of the
     last hop is expanded and written (no degree sum), and the digest of all (a, b, c, d) RID tuples
     equals the oracle's."""
     from oracle import dfs
     ref = dfs.run(_cg(rmat26), C5_WINDOW, nthreads=THREADS, emit=False, digest=["a", "b", "c", "d"])
     rs = _digest_run(rmat26, C5_WINDOW)
-    assert rs.info["n_rows"] == rs.info["bindings"] == ref["bindings"] > 1e7
+    assert rs.info["n_rows"] == rs.info["bindings"] == ref["bindings"] > 1e6
     assert rs.info["edges_traversed"] == ref["edges"]
     assert rs.info["digest"] == ref["digest"]
 
