@@ -711,25 +711,25 @@ __global__ __launch_bounds__(256) void k_flist_copy(FlistArgs a, const uint64_t 
     n[j] = __builtin_amdgcn_readlane(nl, j);
     b[j] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(bl >> 32), j) << 32) | __builtin_amdgcn_readlane((uint32_t)bl, j);
   }
+  // rounds of 64 entries of every tile at once (a tile of a hub's row holds up to 512 survivors: one
+  // tile at a time, its rounds were a chain of dependent round trips)
+  uint32_t nmax = 0;
 #pragma unroll
-  for (int j = 0; j < kFlCopyT; ++j)
-    x[j] = a.scratch[min(t0 + j, nt - 1) * (uint64_t)(kFlChunks * 4) + (lane < n[j] ? lane : 0u)];  // (n = 0 past the end)
+  for (int j = 0; j < kFlCopyT; ++j) nmax = max(nmax, n[j]);
+  for (uint32_t k0 = 0; k0 < nmax; k0 += 64) {
+    const uint32_t k = k0 + lane;
 #pragma unroll
-  for (int j = 0; j < kFlCopyT; ++j) {
-    const bool hub = x[j] >= a.vb;
-    const uint32_t v = a.hubs[hub ? x[j] - a.vb : 0u];
-    x[j] = hub ? v : x[j];
-  }
+    for (int j = 0; j < kFlCopyT; ++j)  // (n = 0 past the end: entry 0 of the last tile, never stored)
+      x[j] = a.scratch[min(t0 + j, nt - 1) * (uint64_t)(kFlChunks * 4) + (k < n[j] ? k : 0u)];
 #pragma unroll
-  for (int j = 0; j < kFlCopyT; ++j)
-    if (lane < n[j]) a.lcol[b[j] + lane] = x[j];
-#pragma unroll
-  for (int j = 0; j < kFlCopyT; ++j) {
-    const uint32_t *src = a.scratch + (t0 + j) * (uint64_t)(kFlChunks * 4);
-    for (uint32_t k = 64 + lane; k < n[j]; k += 64) {
-      const uint32_t y = src[k];
-      a.lcol[b[j] + k] = y >= a.vb ? a.hubs[y - a.vb] : y;
+    for (int j = 0; j < kFlCopyT; ++j) {  // (an unused lane's word may be a stale scratch word: never an index)
+      const bool hub = k < n[j] && x[j] >= a.vb && x[j] - a.vb < a.nh;
+      const uint32_t v = a.hubs[hub ? x[j] - a.vb : 0u];
+      x[j] = hub ? v : x[j];
     }
+#pragma unroll
+    for (int j = 0; j < kFlCopyT; ++j)
+      if (k < n[j]) a.lcol[b[j] + k] = x[j];
   }
 }
 
