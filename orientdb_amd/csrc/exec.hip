@@ -2007,12 +2007,13 @@ class Executor {
   // L2 by its rows (in row order they came from HBM / MALL: 4.35 against 5.2 ms per M1 step, round 3)
   // OMX_FEMIT: 0 = never, 1 = when the hop traverses at least femit_min_et_ edges (E_t), force = always
   // (tests). Below that its fixed costs (the row sort, selections, tile lists: ≈ 0.2 ms) outweigh the
-  // faster writes: C2 (RMAT-22, E_t 1.5e9) 1.21 ms against 1.15 binned; M1 (E_t 1.03e10) 4.2 against 5.2
-  // (profiles/r03/femit/c2ab.txt)
+  // faster writes. Round 3: C2 (RMAT-22, E_t 1.5e9) 1.21 ms against 1.15 binned (profiles/r03/femit/
+  // c2ab.txt), so 4e9; round 5, with the lists from k_flists: C2 1.02 against 1.16-1.27 binned, one box
+  // interleaved (gpurun_out/r5c2), so 1e9
   int femit_ = 1;
   static constexpr uint64_t kOnDevice = UINT64_MAX;  // a count left on the device (emit_factorized's nlist)
   size_t flist_copy_rec_ = SIZE_MAX;                  // the timing record of the last k_flist_copy
-  uint64_t femit_min_et_ = 4000000000ull;
+  uint64_t femit_min_et_ = 1000000000ull;
   bool femit_slow_ = false;  // OMX_FEMIT_SLOW=1: every output tile through k_femit_slow (tests)
 
   // step 4 of expand_factorized when the rows are written: the output space Σ_rows |L(g[r])| is laid out
