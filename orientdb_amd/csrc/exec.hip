@@ -1439,6 +1439,15 @@ class Executor {
       medges = DBuf<unsigned long long>(&pool_, 2);
       HIP_CHECK(hipMemsetAsync(medges.p, 0, 2 * sizeof(unsigned long long), s_));
     }
+    if (!write && filter == nullptr && !member && !mark && !ordered) {
+      // counting an unfiltered hop: its bindings are Σ degree — a degree reduction, no binning and no
+      // col[] reads (C5's last hop over 7 M rows: 0.33 ms of binning count + scan before, round 5;
+      // omx_result_info.edges_read excludes these edges)
+      o.E = o.n = degree_sum(src, R, adjs, raw_adj);
+      o.counted_from_degrees = true;
+      alg_bytes_ += 8 * R;
+      return o;
+    }
     // 1. degree binning + scans (light edges: merge path; heavy rows: chunks). A filtered hop over a
     // sorted adjacency cuts the heavy rows' chunks at bitmap-slice boundaries (LDS-sliced kernel).
     const bool sliced = filter != nullptr && !member && !raw_adj && !ordered && adj.sorted && sliced_ &&
@@ -3076,8 +3085,8 @@ class Executor {
     return true;
   }
 
-  uint64_t degree_sum(const uint32_t *src, uint64_t R, const AdjSpec &adjs) {
-    DAdj adj = make_adj(adjs);
+  uint64_t degree_sum(const uint32_t *src, uint64_t R, const AdjSpec &adjs, const DAdj *raw_adj = nullptr) {
+    DAdj adj = raw_adj ? *raw_adj : make_adj(adjs);
     if (adj.n == 0 || R == 0) return 0;
     DBuf<uint64_t> deg(&pool_, R + 1), sum(&pool_, 1);
     tm_.begin("k_row_degree");

@@ -339,32 +339,40 @@ __global__ __launch_bounds__(256) void k_eval_atoms4(DPred P, uint32_t V, uint64
 // vertices) a round with four 16-byte loads a lane in flight. The general kernel above holds 150 VGPRs
 // when compiled for four groups a wave (3 waves a SIMD: 55 µs for RMAT-24's 67 MB column); this one
 // holds few.
+// (T = int64_t: the same over an int64 column, C5's `uid < 64` — 8 bytes a vertex, two 16-byte loads a
+// group: 131 µs through the general kernel at RMAT-26, round 5)
 constexpr int kAtom1U = 4;
-__global__ __launch_bounds__(256) void k_eval_atom1_i32(const int32_t *col, int64_t lo, int64_t hi, int neg, uint32_t V,
-                                                        uint64_t *words, uint64_t nwords) {
+template <class T>
+__global__ __launch_bounds__(256) void k_eval_atom1(const T *col, int64_t lo, int64_t hi, int neg, uint32_t V,
+                                                    uint64_t *words, uint64_t nwords) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64, nwv = (uint64_t)gridDim.x * 4;
   const uint64_t nrounds = (nwords + 4 * kAtom1U - 1) / (4 * kAtom1U);
   for (uint64_t rd = wave; rd < nrounds; rd += nwv) {
     const uint64_t w0 = rd * 4 * kAtom1U;
     const bool full = (w0 + 4 * kAtom1U) * 64 <= (uint64_t)V;  // wave-uniform
-    int4 x[kAtom1U];
+    T x[kAtom1U][4];
 #pragma unroll
     for (int u = 0; u < kAtom1U; ++u) {
       const uint64_t v0 = (w0 + 4 * u) * 64 + 4 * lane;
       if (full) {
-        x[u] = *reinterpret_cast<const int4 *>(col + v0);
+        if (sizeof(T) == 4) {
+          const int4 q = *reinterpret_cast<const int4 *>(col + v0);
+          x[u][0] = (T)q.x, x[u][1] = (T)q.y, x[u][2] = (T)q.z, x[u][3] = (T)q.w;
+        } else {
+          const longlong2 *p = reinterpret_cast<const longlong2 *>(col + v0);
+          const longlong2 a = p[0], b = p[1];
+          x[u][0] = (T)a.x, x[u][1] = (T)a.y, x[u][2] = (T)b.x, x[u][3] = (T)b.y;
+        }
       } else {
-        x[u].x = col[v0 + 0 < V ? v0 + 0 : V - 1];
-        x[u].y = col[v0 + 1 < V ? v0 + 1 : V - 1];
-        x[u].z = col[v0 + 2 < V ? v0 + 2 : V - 1];
-        x[u].w = col[v0 + 3 < V ? v0 + 3 : V - 1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[u][j] = col[v0 + j < V ? v0 + j : V - 1];
       }
     }
 #pragma unroll
     for (int u = 0; u < kAtom1U; ++u) {
       const uint64_t v0 = (w0 + 4 * u) * 64 + 4 * lane;
-      const int32_t e[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+      const T *e = x[u];
       uint64_t nib = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -388,9 +396,11 @@ void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *
   for (int k = 0; four && k < pred.n_atoms; ++k)
     four = pred.atom_c[k].present == nullptr && pred.atom_c[k].type != OMX_PROP_INT64 &&
            pred.atom_c[k].type != OMX_PROP_DOUBLE;
-  // one int32 comparison with an integer constant, no class test: the range-test kernel
-  if (four && pred.n_atoms == 1 && !pred.use_class && pred.atom_c[0].type == OMX_PROP_INT32 && !pred.atom_dbl[0] &&
-      pred.atom_op[0] >= P_EQ && pred.atom_op[0] <= P_GE) {
+  // one int32 / int64 comparison with an integer constant, no class test: the range-test kernel
+  const bool one = pred.n > 0 && pred.n_atoms == 1 && !pred.use_class && pred.atom_c[0].present == nullptr &&
+                   (pred.atom_c[0].type == OMX_PROP_INT32 || pred.atom_c[0].type == OMX_PROP_INT64) &&
+                   !pred.atom_dbl[0] && pred.atom_op[0] >= P_EQ && pred.atom_op[0] <= P_GE;
+  if (one) {
     const int64_t b = pred.atom_i[0];
     int64_t lo = INT64_MIN, hi = INT64_MAX;
     int neg = 0;
@@ -411,9 +421,13 @@ void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *
     }
     const uint64_t rounds = (nwords + 4 * kAtom1U - 1) / (4 * kAtom1U);
     const uint64_t waves = std::min<uint64_t>(rounds, (uint64_t)std::max(cus, 1) * 32);
-    hipLaunchKernelGGL(k_eval_atom1_i32, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s,
-                       (const int32_t *)pred.atom_c[0].values, lo, hi, neg, V, words, nwords);
-    KCHECK("k_eval_atom1_i32");
+    if (pred.atom_c[0].type == OMX_PROP_INT32)
+      hipLaunchKernelGGL(k_eval_atom1<int32_t>, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s,
+                         (const int32_t *)pred.atom_c[0].values, lo, hi, neg, V, words, nwords);
+    else
+      hipLaunchKernelGGL(k_eval_atom1<int64_t>, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s,
+                         (const int64_t *)pred.atom_c[0].values, lo, hi, neg, V, words, nwords);
+    KCHECK("k_eval_atom1");
     return;
   }
   if (four) {
