@@ -2770,10 +2770,12 @@ class Executor {
     DBuf<uint64_t> nsel(&pool_, 1);
     hipcub::CountingInputIterator<uint32_t> cnt(0);
     cub([&](void *t, size_t &b) { return hipcub::DevicePartition::Flagged(t, b, cnt, fl.p, idx.p, nsel.p, (int64_t)R, s_); });
-    launch_post_words(sums.p, 2, mail(), s_);
+    const uint64_t *words[3] = {reinterpret_cast<const uint64_t *>(sums.p), reinterpret_cast<const uint64_t *>(sums.p) + 1,
+                                nsel.p};
+    launch_post_ptrs(words, 3, mail(), s_);  // (the sums and the swapped count in one round trip)
     const uint64_t *h = wait_mail();
     edges_ += h[0] + h[1];
-    const uint64_t nsw = read1(nsel.p);
+    const uint64_t nsw = h[2];
     ExpandOut og[2];
     const uint64_t gn[2] = {nsw, R - nsw};
     const uint32_t *gi[2] = {idx.p, idx.p + nsw};
@@ -2799,19 +2801,25 @@ class Executor {
     R_ = og[0].n + og[1].n;
     if (!write || R_ == 0) return;
     segmented_ = false;
-    auto cat = [&](DBuf<uint32_t> &a, uint64_t na, DBuf<uint32_t> &b, uint64_t nb) {
-      if (nb == 0) return std::move(a);
-      if (na == 0) return std::move(b);
-      DBuf<uint32_t> o(&pool_, na + nb);
-      HIP_CHECK(hipMemcpyAsync(o.p, a.p, na * 4, hipMemcpyDeviceToDevice, s_));
-      HIP_CHECK(hipMemcpyAsync(o.p + na, b.p, nb * 4, hipMemcpyDeviceToDevice, s_));
-      return o;
-    };
-    for (size_t i = 0; i < cols.size(); ++i) {
-      DBuf<uint32_t> e0, e1;
-      col_[cols[i]] = cat(og[0].n ? og[0].carry[i] : e0, og[0].n, og[1].n ? og[1].carry[i] : e1, og[1].n);
+    if (og[1].n == 0 || og[0].n == 0) {  // one group: its columns as they are
+      ExpandOut &o = og[0].n ? og[0] : og[1];
+      for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
+      col_[ex.dst] = std::move(o.dst);
+      return;
     }
-    col_[ex.dst] = cat(og[0].dst, og[0].n, og[1].dst, og[1].n);
+    // both groups: every column concatenated in one pass (six D2D copies at C4 were 50 µs of launches)
+    std::vector<DBuf<uint32_t>> cat;
+    std::vector<const uint32_t *> pa, pb;
+    std::vector<uint32_t *> po;
+    for (size_t i = 0; i <= cols.size(); ++i) {
+      cat.emplace_back(&pool_, og[0].n + og[1].n);
+      pa.push_back(i < cols.size() ? og[0].carry[i].p : og[0].dst.p);
+      pb.push_back(i < cols.size() ? og[1].carry[i].p : og[1].dst.p);
+      po.push_back(cat.back().p);
+    }
+    launch_concat_cols(og[0].n, og[1].n, (int)po.size(), pa.data(), pb.data(), po.data(), s_);
+    for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(cat[i]);
+    col_[ex.dst] = std::move(cat.back());
   }
 
   // The fused intersection N_x(x) ∩ N_y(y) with a merge path (isect.hip) for the rows whose lists have
