@@ -54,7 +54,8 @@ void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *front
 // hubs-only pull leaves to a push).
 __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t vlo, uint32_t V,
                                                  const uint64_t *while_bm, int expand, DAdj adj,
-                                                 unsigned long long *stats, uint64_t *fbm, const uint64_t *hub_bm) {
+                                                 unsigned long long *stats, uint64_t *fbm, const uint64_t *hub_bm,
+                                                 uint64_t *zero, int first) {
   __shared__ uint64_t s_r[6][kB / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint64_t te = 0, td = 0, tn = 0, tl = 0, hd = 0, hn = 0;
@@ -75,11 +76,13 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
       const uint64_t v0 = b0 + (uint64_t)u * kB;
       const uint64_t v = v0 + threadIdx.x;
       const uint64_t f = fu[u];
+      if (zero && v < V) zero[v] = 0;
+      if (first && v < V) visited[v] = f;  // (a batch's first level: visited is written, never read)
       uint64_t m = 0;
       if (f) {
-        const uint64_t vis = visited[v];
+        const uint64_t vis = first ? 0ull : visited[v];
         m = f & ~vis;
-        if (m) visited[v] = vis | m;
+        if (m && !first) visited[v] = vis | m;
         if (expand && while_bm && !bm_test(while_bm, (uint32_t)v)) m = 0;
         if (m != f) frontier[v] = m;
         if (m && expand) {
@@ -127,12 +130,12 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
 }
 void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
                      const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s, uint32_t vlo,
-                     const uint64_t *hub_bm) {
+                     const uint64_t *hub_bm, uint64_t *zero, bool first) {
   if (vlo && fbm) fail(OMX_E_INVALID, "internal: the frontier bitmap covers whole words from vertex 0");
   if (V <= vlo) return;
   const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V - vlo, kB * 4), (uint64_t)cus * 8);
   hipLaunchKernelGGL(k_bfs_prep, dim3(g), dim3(kB), 0, s, frontier, visited, vlo, V, while_bm, (int)expand, adj, stats,
-                     fbm, hub_bm);
+                     fbm, hub_bm, zero, (int)first);
   KCHECK("k_bfs_prep");
 }
 

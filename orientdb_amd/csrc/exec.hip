@@ -3348,8 +3348,10 @@ class Executor {
     for (uint64_t row0 = 0; row0 < R; row0 += 64) {
       const int nl = (int)std::min<uint64_t>(64, R - row0);
       const uint64_t lanes = nl == 64 ? ~0ull : ((1ull << nl) - 1);
+      // (one GPU: visited is zeroed by the first level's prologue, which covers every vertex)
+      const bool whole = !dist_ && vlo == 0 && vhi == V;
       HIP_CHECK(hipMemsetAsync(fr.p, 0, (size_t)V * 8, s_));
-      HIP_CHECK(hipMemsetAsync(vis.p, 0, (size_t)V * 8, s_));
+      if (!whole) HIP_CHECK(hipMemsetAsync(vis.p, 0, (size_t)V * 8, s_));
       launch_bfs_seed(srcc, row0, nl, fr.p, s_);
       for (int64_t d = 0;; ++d) {
         if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate");
@@ -3357,7 +3359,10 @@ class Executor {
         if (expand && depth_only_while) expand = !while_never && eval_pred_const(wconst, d);
         HIP_CHECK(hipMemsetAsync(stats.p, 0, 7 * sizeof(unsigned long long), s_));
         tm_.begin("k_bfs_prep");
-        launch_bfs_prep(fr.p, vis.p, vhi, while_bm, expand, adj, stats.p, dist_ ? nullptr : fbm.p, cus(), s_, vlo, hub_bm);
+        // (one GPU: the prologue zeroes the next level's masks as it streams the frontier, no memset)
+        const bool zero_nx = whole;
+        launch_bfs_prep(fr.p, vis.p, vhi, while_bm, expand, adj, stats.p, dist_ ? nullptr : fbm.p, cus(), s_, vlo, hub_bm,
+                        zero_nx ? nx.p : nullptr, whole && d == 0);
         tm_.end(8ull * (vhi - vlo));
         if (!expand) break;
         launch_post_words(stats.p, 6, mail(), s_);
@@ -3385,7 +3390,7 @@ class Executor {
         // level's kernels actually read (push: the frontier's out-edges once for all lanes; tiled pull:
         // every in-edge; early-exit pull: the in-edges walked, added when the traversal ends)
         edges_ += h[0];
-        HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
+        if (!zero_nx) HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
         if (debug_expand_)
           std::fprintf(stderr, "[omx bfs] batch %llu level %lld: %s active=%llu push_edges=%llu E_t=%llu\n",
                        (unsigned long long)row0, (long long)d, (double)h[1] * pull_div_ > (double)eadj ? "pull" : "push",
