@@ -1353,18 +1353,17 @@ class Executor {
     const uint64_t ntb = flist_tiles_bound(EU, U);
     DBuf<uint32_t> nch(&pool_, U + 1);
     DBuf<uint64_t> coff(&pool_, U + 1), rb(&pool_, 2 * ntb), base(&pool_, ntb + 1);
-    HIP_CHECK(hipMemsetAsync(nch.p + U, 0, 4, s_));
-    launch_flist_nch(ub, doff, U, rp, nch.p, s_);
+    launch_flist_nch(ub, doff, U, rp, nch.p, s_);  // (nch[U] = 0 included)
     {
       hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> it(nch.p, CastU64());
       cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, it, coff.p, (int64_t)(U + 1), s_); });
     }
     DBuf<uint4> info(&pool_, std::max<uint64_t>(U, 1));
-    launch_flist_prep(ub, doff, coff.p, U, rp, coff.p + U, info.p, rb.p, ntb, s_);
+    DBuf<uint32_t> ntot(&pool_, ntb + 1);
+    launch_flist_prep(ub, doff, coff.p, U, rp, coff.p + U, info.p, rb.p, ntot.p, ntb, s_);  // (ntot past the tiles zeroed)
     const uint64_t nbits = vb / 32 + (nh + 31) / 32;
-    DBuf<uint32_t> bits(&pool_, nbits), ntot(&pool_, ntb + 1), loc(&pool_, std::max<uint64_t>(U, 1));
+    DBuf<uint32_t> bits(&pool_, nbits), loc(&pool_, std::max<uint64_t>(U, 1));
     DBuf<uint32_t> scratch(&pool_, ntb * flist_tile_entries());
-    HIP_CHECK(hipMemsetAsync(ntot.p, 0, (ntb + 1) * 4, s_));
     launch_probe_bits(hubs, nh, filter, vb, bits.p, s_);
     FlistArgs a{};
     a.ub = ub;

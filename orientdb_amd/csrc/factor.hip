@@ -334,6 +334,7 @@ __device__ __forceinline__ uint32_t fl_nch(uint64_t rs, uint64_t deg) {
 __global__ void k_flist_nch(const uint32_t *ub, const uint64_t *doff, uint64_t U, const uint64_t *rp, uint32_t *nch) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < U) nch[i] = fl_nch(rp[ub[i]], doff[i + 1] - doff[i]);
+  else if (i == U) nch[U] = 0;  // (the scan's last entry)
 }
 // every source's chunk table entry {gbase, coff, pack}: chunk c of the space is col group gbase + c;
 // pack = first-chunk skip | (last-chunk entries − 1) << 2 | chunks << 4
@@ -359,9 +360,16 @@ __device__ __forceinline__ uint64_t fl_source_of(const uint64_t *coff, uint64_t 
   }
   return lo - 1;
 }
-__global__ void k_flist_bounds(const uint64_t *coff, uint64_t U, const uint64_t *ec, uint64_t *rb) {
+// (ntot: the tiles past the chunk space, up to the bound's ntb, get a zero count for the counts' scan —
+// every real tile's count is written by k_flist)
+__global__ void k_flist_bounds(const uint64_t *coff, uint64_t U, const uint64_t *ec, uint64_t *rb, uint32_t *ntot,
+                               uint64_t ntb) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, N = *ec;
-  if (t * kFlChunks >= N) return;
+  if (t > ntb) return;
+  if (t * kFlChunks >= N) {
+    ntot[t] = 0;
+    return;
+  }
   rb[2 * t] = fl_source_of(coff, U, t * kFlChunks);
   rb[2 * t + 1] = fl_source_of(coff, U, min((t + 1) * (uint64_t)kFlChunks, N) - 1);
 }
@@ -755,16 +763,16 @@ uint64_t flist_tile_entries() { return 4ull * kFlChunks; }
 void launch_flist_nch(const uint32_t *ub, const uint64_t *doff, uint64_t U, const uint64_t *rp, uint32_t *nch,
                       hipStream_t s) {
   if (!U) return;
-  hipLaunchKernelGGL(k_flist_nch, dim3(nblocks(U, 256)), dim3(256), 0, s, ub, doff, U, rp, nch);
+  hipLaunchKernelGGL(k_flist_nch, dim3(nblocks(U + 1, 256)), dim3(256), 0, s, ub, doff, U, rp, nch);
   KCHECK("k_flist_nch");
 }
 
 void launch_flist_prep(const uint32_t *ub, const uint64_t *doff, const uint64_t *coff, uint64_t U, const uint64_t *rp,
-                       const uint64_t *ec, uint4 *info, uint64_t *rb, uint64_t nt_bound, hipStream_t s) {
+                       const uint64_t *ec, uint4 *info, uint64_t *rb, uint32_t *ntot, uint64_t nt_bound, hipStream_t s) {
   if (!U) return;
   hipLaunchKernelGGL(k_flist_info, dim3(nblocks(U, 256)), dim3(256), 0, s, ub, doff, coff, U, rp, info);
   KCHECK("k_flist_info");
-  hipLaunchKernelGGL(k_flist_bounds, dim3(nblocks(nt_bound, 256)), dim3(256), 0, s, coff, U, ec, rb);
+  hipLaunchKernelGGL(k_flist_bounds, dim3(nblocks(nt_bound + 1, 256)), dim3(256), 0, s, coff, U, ec, rb, ntot, nt_bound);
   KCHECK("k_flist_bounds");
 }
 

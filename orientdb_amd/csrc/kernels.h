@@ -361,7 +361,7 @@ void launch_flist_nch(const uint32_t *ub, const uint64_t *doff, uint64_t U, cons
                       hipStream_t s);
 // info[U] and rb (tile bounds) from coff = the exclusive scan of nch (coff[U] = *ec)
 void launch_flist_prep(const uint32_t *ub, const uint64_t *doff, const uint64_t *coff, uint64_t U, const uint64_t *rp,
-                       const uint64_t *ec, uint4 *info, uint64_t *rb, uint64_t nt_bound, hipStream_t s);
+                       const uint64_t *ec, uint4 *info, uint64_t *rb, uint32_t *ntot, uint64_t nt_bound, hipStream_t s);
 // bits = the filter's vb/32 words, then word w bit i = the filter bit of hubs[32w + i]
 void launch_probe_bits(const uint32_t *hubs, uint32_t nh, const uint64_t *filter, uint32_t vb, uint32_t *bits,
                        hipStream_t s);
