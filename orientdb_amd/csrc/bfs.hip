@@ -55,7 +55,7 @@ void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *front
 __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t vlo, uint32_t V,
                                                  const uint64_t *while_bm, int expand, DAdj adj,
                                                  unsigned long long *stats, uint64_t *fbm, const uint64_t *hub_bm,
-                                                 uint64_t *zero, int first) {
+                                                 uint64_t *zero, int first, int zfull) {
   __shared__ uint64_t s_r[6][kB / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint64_t te = 0, td = 0, tn = 0, tl = 0, hd = 0, hn = 0;
@@ -64,19 +64,23 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
   // iteration's load came after the previous one's stores (vector memory completes in order)
   constexpr int kPrepU = 4;
   for (uint64_t b0 = vlo + (uint64_t)blockIdx.x * kB * kPrepU; b0 < V; b0 += (uint64_t)gridDim.x * kB * kPrepU) {
-    uint64_t fu[kPrepU];
+    uint64_t fu[kPrepU], ou[kPrepU];
 #pragma unroll
     for (int u = 0; u < kPrepU; ++u) {
       const uint64_t v = b0 + (uint64_t)u * kB + threadIdx.x;
       const uint64_t x = frontier[v < V ? v : V - 1];
       fu[u] = v < V ? x : 0;
+      // the previous level's frontier bits (before this level's ballot overwrites them): the next-mask
+      // array is the previous frontier array, non-zero only there
+      const uint64_t wi = (b0 + (uint64_t)u * kB) / 64 + wave;
+      ou[u] = (zero && !zfull && wi * 64 < V) ? fbm[wi] : ~0ull;
     }
 #pragma unroll
     for (int u = 0; u < kPrepU; ++u) {
       const uint64_t v0 = b0 + (uint64_t)u * kB;
       const uint64_t v = v0 + threadIdx.x;
       const uint64_t f = fu[u];
-      if (zero && v < V) zero[v] = 0;
+      if (zero && v < V && ((ou[u] >> lane) & 1ull)) zero[v] = 0;
       if (first && v < V) visited[v] = f;  // (a batch's first level: visited is written, never read)
       uint64_t m = 0;
       if (f) {
@@ -130,12 +134,12 @@ __global__ __launch_bounds__(kB) void k_bfs_prep(uint64_t *frontier, uint64_t *v
 }
 void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
                      const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s, uint32_t vlo,
-                     const uint64_t *hub_bm, uint64_t *zero, bool first) {
+                     const uint64_t *hub_bm, uint64_t *zero, bool first, bool zero_all) {
   if (vlo && fbm) fail(OMX_E_INVALID, "internal: the frontier bitmap covers whole words from vertex 0");
   if (V <= vlo) return;
   const unsigned g = (unsigned)std::min<uint64_t>(nblocks(V - vlo, kB * 4), (uint64_t)cus * 8);
   hipLaunchKernelGGL(k_bfs_prep, dim3(g), dim3(kB), 0, s, frontier, visited, vlo, V, while_bm, (int)expand, adj, stats,
-                     fbm, hub_bm, zero, (int)first);
+                     fbm, hub_bm, zero, (int)first, (int)(zero_all || !fbm));
   KCHECK("k_bfs_prep");
 }
 

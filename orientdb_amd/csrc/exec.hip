@@ -3361,7 +3361,7 @@ class Executor {
         // (one GPU: the prologue zeroes the next level's masks as it streams the frontier, no memset)
         const bool zero_nx = whole;
         launch_bfs_prep(fr.p, vis.p, vhi, while_bm, expand, adj, stats.p, dist_ ? nullptr : fbm.p, cus(), s_, vlo, hub_bm,
-                        zero_nx ? nx.p : nullptr, whole && d == 0);
+                        zero_nx ? nx.p : nullptr, whole && d == 0, d == 0);
         tm_.end(8ull * (vhi - vlo));
         if (!expand) break;
         launch_post_words(stats.p, 6, mail(), s_);

@@ -429,11 +429,13 @@ bool eval_pred_const(const DPred &pred, int64_t depth);
 // multi-source BFS (bfs.hip): u64 lane mask per vertex, 64 binding rows per batch
 void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, hipStream_t s);
 // vertices [vlo, V) (a partition's own rows: vlo = part_lo, V = part_hi; fbm only from vertex 0);
-// zero: the next level's mask array, zeroed over the same vertices (no separate memset); first: a batch's
-// first level — visited is not read but written (= the frontier) over the same vertices
+// zero: the next level's mask array — the previous level's frontier array — zeroed where the previous
+// level's frontier bits (fbm, read before this level's overwrite) are set, or everywhere with zero_all (no
+// separate memset); first: a batch's first level — visited is not read but written (= the frontier)
 void launch_bfs_prep(uint64_t *frontier, uint64_t *visited, uint32_t V, const uint64_t *while_bm, bool expand,
                      const DAdj &adj, unsigned long long *stats, uint64_t *fbm, int cus, hipStream_t s,
-                     uint32_t vlo = 0, const uint64_t *hub_bm = nullptr, uint64_t *zero = nullptr, bool first = false);
+                     uint32_t vlo = 0, const uint64_t *hub_bm = nullptr, uint64_t *zero = nullptr, bool first = false,
+                     bool zero_all = true);
 void launch_bfs_list(const uint64_t *frontier, uint32_t V, uint32_t *list, unsigned long long *count, int cus,
                      hipStream_t s);
 void launch_bfs_list_deg(const uint32_t *list, uint64_t nl, const uint64_t *rp, uint64_t *deg, hipStream_t s);
