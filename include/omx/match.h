@@ -197,6 +197,12 @@ typedef struct omx_result_info {
                              /* expressions, $elements, LIMIT): rows this rank received when the     */
                              /* rows met on rank 0 — distinct tuples only, each rank de-duplicates   */
                              /* its hash share first; 0 elsewhere (diagnostic)                       */
+  uint64_t host_rows_bytes;  /* bytes of the library-owned host block holding omx_result_rows (0 with  */
+                             /* KEEP_DEVICE or for documents); released to a pooled cache by         */
+                             /* omx_result_free and reused by the next result of a similar size      */
+  int32_t host_rows_pinned;  /* 1: that block is pinned (page-locked) host memory, so the rows came   */
+                             /* over PCIe by DMA; 0: pageable (pinning failed) or no block            */
+  int32_t reserved0;
 } omx_result_info;
 
 /* A null binding (an unmatched optional node, P/OMatchStatement.java:448-458) in omx_result_rows. */
@@ -205,7 +211,8 @@ typedef struct omx_result_info {
 int omx_result_info_get(const omx_result *r, omx_result_info *info);
 const char *omx_result_column_name(const omx_result *r, int32_t col);
 /* Row-major n_rows × n_cols RIDs ((cluster << 48) | position), or dense ids with NO_RID_MAP.
- * Library-owned; valid until omx_result_free. NULL with KEEP_DEVICE. */
+ * Library-owned pinned host memory (info.host_rows_bytes / host_rows_pinned); valid until omx_result_free,
+ * which returns the block to the library's pool. NULL with KEEP_DEVICE. */
 const uint64_t *omx_result_rows(const omx_result *r);
 /* Per-kernel device timing (OMX_FLAG_KERNEL_TIMING): i-th kernel name, launches, total ms, and the
  * algorithmic bytes the launches of that kernel moved. Returns OMX_E_INVALID past the end. */

@@ -60,6 +60,8 @@ def lib():
                               C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.set_digest.restype = C.c_uint64
         L.set_digest.argtypes = [C.POINTER(C.c_int32), C.c_int32, C.c_uint64, C.c_int32]
+        L.set_max_rows.restype = C.c_uint64
+        L.set_max_rows.argtypes = []
         L.set_rows.restype = C.POINTER(C.c_uint32)
         L.set_rows.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
         L.bfs_varlen.restype = C.c_int64
@@ -349,7 +351,10 @@ def set_run(g, query, params=None, nthreads=1, root_sample=None, digest=None, di
     b = lib().set_run(C.byref(plan), g.V, roots.ctypes.data_as(C.POINTER(C.c_uint32)), len(roots), int(nthreads),
                       mark.ctypes.data_as(C.POINTER(C.c_uint64)) if mark is not None else None, C.byref(edges))
     dt = time.perf_counter() - t0
-    res = {"bindings": int(b), "edges": edges.value, "seconds": dt, "nroots": len(roots), "aliases": sp.aliases}
+    if b < 0:
+        raise MemoryError("oracle/set_ref.c: a host allocation failed (the rows of %d roots)" % len(roots))
+    res = {"bindings": int(b), "edges": edges.value, "seconds": dt, "nroots": len(roots), "aliases": sp.aliases,
+           "max_rows": int(lib().set_max_rows())}
     if digest:
         proj = (C.c_int32 * len(digest))(*[colof[sp.aidx[a]] for a in digest])
         res["digest"] = lib().set_digest(proj, len(digest), RID_BASE, int(nthreads))

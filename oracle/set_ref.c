@@ -53,6 +53,7 @@ typedef struct {
   uint64_t ucap, lcap;
   uint64_t *roff;
   uint64_t rcap;
+  uint64_t max_rows;         /* the most rows any hop of the last run wrote (set_max_rows) */
   /* the last result */
   const uint32_t *rows;
   uint64_t nrows;
@@ -61,14 +62,25 @@ typedef struct {
 
 static set_ctx C;
 
-static void *grow(void *p, uint64_t *cap, uint64_t need, size_t elem) {
-  if (need <= *cap) return p;
+/* set when a host allocation failed: the run stops and set_run returns -1 (the bench then skips the
+   set-based baseline instead of crashing) */
+static int set_oom;
+
+/* grows *pp to hold `need` elements; 0 (and set_oom) when realloc fails, *pp and *cap unchanged */
+static int grow(void **pp, uint64_t *cap, uint64_t need, size_t elem) {
+  if (need <= *cap) return 1;
   uint64_t c = *cap ? *cap : 1024;
   while (c < need) c *= 2;
-  p = realloc(p, c * elem);
+  void *q = realloc(*pp, c * elem);
+  if (!q) {
+    set_oom = 1;
+    return 0;
+  }
+  *pp = q;
   *cap = c;
-  return p;
+  return 1;
 }
+#define GROW(p, cap, need, elem) grow((void **)&(p), (cap), (need), (elem))
 
 static inline int bm(const uint64_t *b, uint32_t v) { return (int)((b[v >> 6] >> (v & 63)) & 1ull); }
 
@@ -113,6 +125,15 @@ static uint64_t hop(const set_hop *h, uint32_t V, const uint32_t *in, uint64_t R
       C.flag = (uint8_t *)calloc(V, 1);
       C.idx = (uint32_t *)malloc((size_t)V * 4);
       C.V = V;
+      if (!C.flag || !C.idx) {
+        free(C.flag);
+        free(C.idx);
+        C.flag = NULL;
+        C.idx = NULL;
+        C.V = 0;
+        set_oom = 1;
+        return 0;
+      }
     }
 #pragma omp parallel for num_threads(T) schedule(static)
     for (uint64_t i = 0; i < R; ++i) C.flag[in[i * k + s]] = 1;
@@ -131,17 +152,23 @@ static uint64_t hop(const set_hop *h, uint32_t V, const uint32_t *in, uint64_t R
       {
         for (int j = 1; j <= n; ++j) cnt[j] += cnt[j - 1];
         U = cnt[n];
-        C.ulist = (uint32_t *)grow(C.ulist, &C.ucap, U + 1, 4);
-        C.loff = (uint64_t *)realloc(C.loff, (C.ucap + 1) * 8);
+        if (GROW(C.ulist, &C.ucap, U + 1, 4)) {
+          uint64_t *lo2 = (uint64_t *)realloc(C.loff, (C.ucap + 1) * 8);
+          if (lo2) C.loff = lo2;
+          else set_oom = 1;
+        }
       }
+      /* (the single's implicit barrier: every thread sees set_oom) */
       uint64_t p = cnt[t];
       for (uint64_t v = lo; v < hi; ++v)
         if (C.flag[v]) {
           C.flag[v] = 0;
+          if (set_oom) continue;
           C.idx[v] = (uint32_t)p;
           C.ulist[p++] = (uint32_t)v;
         }
     }
+    if (set_oom) return 0;
     /* 2. filtered lists: count, scan, fill */
     uint64_t *len = C.loff;  /* counts in place, then scanned into roff scratch and copied back */
 #pragma omp parallel for num_threads(T) schedule(dynamic, 256)
@@ -158,11 +185,11 @@ static uint64_t hop(const set_hop *h, uint32_t V, const uint32_t *in, uint64_t R
       }
       len[u] = c;
     }
-    C.roff = (uint64_t *)grow(C.roff, &C.rcap, U + 1 > R + 1 ? U + 1 : R + 1, 8);
+    if (!GROW(C.roff, &C.rcap, U + 1 > R + 1 ? U + 1 : R + 1, 8)) return 0;
     scan_u64(len, U, C.roff, T);
     memcpy(C.loff, C.roff, (U + 1) * 8);
     const uint64_t NL = C.loff[U];
-    C.lcol = (uint32_t *)grow(C.lcol, &C.lcap, NL + 1, 4);
+    if (!GROW(C.lcol, &C.lcap, NL + 1, 4)) return 0;
 #pragma omp parallel for num_threads(T) schedule(dynamic, 256)
     for (uint64_t u = 0; u < U; ++u) {
       const uint32_t v = C.ulist[u];
@@ -179,6 +206,10 @@ static uint64_t hop(const set_hop *h, uint32_t V, const uint32_t *in, uint64_t R
   }
   /* 3. rows: per row its list length (and its source's degree, E_t), scanned */
   uint64_t *rl = (uint64_t *)malloc((R + 1) * 8);
+  if (!rl) {
+    set_oom = 1;
+    return 0;
+  }
   uint64_t et = 0;
 #pragma omp parallel for num_threads(T) schedule(static) reduction(+ : et)
   for (uint64_t i = 0; i < R; ++i) {
@@ -207,6 +238,11 @@ static uint64_t hop(const set_hop *h, uint32_t V, const uint32_t *in, uint64_t R
     } else {
       /* unfiltered: the distinct sources' adjacency rows (each source once) */
       uint8_t *seen_src = (uint8_t *)calloc(V, 1);
+      if (!seen_src) {
+        set_oom = 1;
+        free(rl);
+        return 0;
+      }
 #pragma omp parallel for num_threads(T) schedule(dynamic, 1024)
       for (uint64_t i = 0; i < R; ++i) {
         const uint32_t v = in[i * k + s];
@@ -221,12 +257,16 @@ static uint64_t hop(const set_hop *h, uint32_t V, const uint32_t *in, uint64_t R
     free(rl);
     return tot;
   }
-  C.roff = (uint64_t *)grow(C.roff, &C.rcap, R + 1, 8);
+  if (!GROW(C.roff, &C.rcap, R + 1, 8)) {
+    free(rl);
+    return 0;
+  }
   scan_u64(rl, R, C.roff, T);
   free(rl);
   const uint64_t N = C.roff[R];
   const int k2 = k + 1;
-  C.tab[slot] = (uint32_t *)grow(C.tab[slot], &C.cap[slot], N * k2 + 1, 4);
+  if (N > C.max_rows) C.max_rows = N;
+  if (!GROW(C.tab[slot], &C.cap[slot], N * k2 + 1, 4)) return 0;
   uint32_t *out = C.tab[slot];
 #pragma omp parallel for num_threads(T) schedule(dynamic, 1024)
   for (uint64_t i = 0; i < R; ++i) {
@@ -258,7 +298,12 @@ int64_t set_run(const set_plan *p, uint32_t V, const uint32_t *roots, int64_t nr
                 uint64_t *edges) {
   const int T = nthreads < 1 ? 1 : nthreads;
   *edges = 0;
-  C.tab[0] = (uint32_t *)grow(C.tab[0], &C.cap[0], (uint64_t)nroots + 1, 4);
+  set_oom = 0;
+  C.max_rows = 0;
+  C.rows = NULL;
+  C.nrows = 0;
+  C.k = 0;
+  if (!GROW(C.tab[0], &C.cap[0], (uint64_t)nroots + 1, 4)) return -1;
   memcpy(C.tab[0], roots, (size_t)nroots * 4);
   const uint32_t *in = C.tab[0];
   uint64_t R = (uint64_t)nroots;
@@ -267,12 +312,10 @@ int64_t set_run(const set_plan *p, uint32_t V, const uint32_t *roots, int64_t nr
     const int last = h == p->nhops - 1;
     if (last && mark) {
       const uint64_t b = hop(&p->hops[h], V, in, R, k, slot, mark, edges, T);
-      C.rows = NULL;
-      C.nrows = 0;
-      C.k = 0;
-      return (int64_t)b;
+      return set_oom ? -1 : (int64_t)b;
     }
     R = hop(&p->hops[h], V, in, R, k, slot, NULL, edges, T);
+    if (set_oom) return -1;
     in = C.tab[slot];
     slot ^= 1;
     ++k;
@@ -304,6 +347,9 @@ uint64_t set_digest(const int32_t *proj, int32_t nproj, uint64_t rid_base, int32
 }
 
 /* the last result: rows (row-major, *k u32 each), valid until the next set_run */
+/* the most rows one hop of the last set_run wrote (the run's peak table, rows of width ≤ 9) */
+uint64_t set_max_rows(void) { return C.max_rows; }
+
 const uint32_t *set_rows(uint64_t *n, int32_t *k) {
   *n = C.nrows;
   *k = C.k;

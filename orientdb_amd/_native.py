@@ -62,7 +62,8 @@ class omx_result_info(C.Structure):
                 ("edges_traversed", C.c_uint64), ("bindings", C.c_uint64), ("alg_bytes", C.c_uint64),
                 ("device_ms", C.c_double), ("total_ms", C.c_double), ("edges_read", C.c_uint64),
                 ("digest", C.c_uint64), ("documents", C.c_int32), ("factorized_hops", C.c_int32),
-                ("rows_gathered", C.c_uint64)]
+                ("rows_gathered", C.c_uint64), ("host_rows_bytes", C.c_uint64), ("host_rows_pinned", C.c_int32),
+                ("reserved0", C.c_int32)]
 
 
 OMX_NULL_RID = (1 << 64) - 1  # a null binding (unmatched optional node)

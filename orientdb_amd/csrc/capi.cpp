@@ -415,8 +415,8 @@ const char *omx_result_column_name(const omx_result *r, int32_t col) {
 }
 
 const uint64_t *omx_result_rows(const omx_result *r) {
-  if (!r || r->rows.empty()) return nullptr;
-  return r->rows.data();
+  if (!r || !r->rows || !r->info.n_rows) return nullptr;
+  return r->rows;
 }
 
 int omx_result_kernel_stat(const omx_result *r, int32_t i, const char **name, int64_t *launches, double *total_ms,

@@ -11,7 +11,15 @@
 struct omx_result {
   omx_result_info info{};
   std::vector<std::string> names;
-  std::vector<uint64_t> rows;  // row-major n_rows × n_cols
+  // row-major n_rows × n_cols RIDs in a library-owned host block (graph.h host_rows_acquire: pinned,
+  // pooled, never value-initialised), returned to the pool by omx_result_free
+  uint64_t *rows = nullptr;
+  size_t rows_capacity = 0;  // bytes of the block
+  bool rows_pinned = false;
+  omx_result() = default;
+  omx_result(const omx_result &) = delete;
+  omx_result &operator=(const omx_result &) = delete;
+  ~omx_result() { omx::host_rows_release(rows); }
   std::vector<omx::Document> docs;  // RETURN expressions / JSON: one document per row (info.documents)
   struct KStat {
     std::string name;

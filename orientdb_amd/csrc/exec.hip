@@ -107,6 +107,7 @@ class Timer {
   }
   // index of the region just closed (SIZE_MAX when it was not recorded)
   size_t last() const { return last_; }
+  bool on() const { return on_; }
   void amend_at(size_t i, uint64_t bytes, uint64_t hbm = UINT64_MAX) {
     if (i < recs_.size()) {
       recs_[i].bytes = bytes;
@@ -444,18 +445,7 @@ class Executor {
       launch_digest(ncols, cp.data(), n, (o_.flags & OMX_FLAG_NO_RID_MAP) ? nullptr : g_.d_rids, g_.V, d.p, cus(), s_);
       digest_ = read1(reinterpret_cast<const uint64_t *>(d.p));
     }
-    if (n > 0 && !counted_only && !docs && !(o_.flags & OMX_FLAG_KEEP_DEVICE)) {
-      DBuf<uint64_t> rids(&pool_, n * ncols);
-      std::vector<const uint32_t *> cp;
-      for (auto &c : out) cp.push_back(c.p);
-      tm_.begin("k_map_rids");
-      launch_map_rids(ncols, cp.data(), n, (o_.flags & OMX_FLAG_NO_RID_MAP) ? nullptr : g_.d_rids, rids.p, g_.V, s_);
-      tm_.end(n * ncols * 12);
-      res->rows.resize(n * ncols);
-      tm_.begin("deliver_d2h");  // the rows' hand-over to the host (reported apart from the step)
-      HIP_CHECK(hipMemcpyAsync(res->rows.data(), rids.p, n * ncols * sizeof(uint64_t), hipMemcpyDeviceToHost, s_));
-      tm_.end(n * ncols * sizeof(uint64_t));
-    }
+    if (n > 0 && !counted_only && !docs && !(o_.flags & OMX_FLAG_KEEP_DEVICE)) deliver_rows(out, n, ncols, *res);
     mark("launched");
     HIP_CHECK(hipEventRecord(eb, s_));
     // spin on the end event (the stream is usually idle by now: the last mailbox read waited for the
@@ -500,6 +490,56 @@ class Executor {
   }
 
  private:
+  // The rows' hand-over to the host (SURVEY §8(b) Ownership, §8(d): reported apart from the step): the
+  // dense ids are mapped to RIDs chunk by chunk into a ring of two device staging slots (k_map_rids on the
+  // executor's stream) and each chunk is copied by DMA into the result's pinned host block on the side
+  // stream, so chunk i+1's map runs under chunk i's copy and the device never holds the whole RID table.
+  // The block comes from the process-wide pool (host_rows_acquire): no pinning, no zeroing once warm.
+  void deliver_rows(const std::vector<DBuf<uint32_t>> &out, uint64_t n, int ncols, omx_result &res) {
+    const uint64_t row_bytes = 8ull * (uint64_t)ncols, total = n * row_bytes;
+    res.rows = static_cast<uint64_t *>(host_rows_acquire(total, &res.rows_capacity, &res.rows_pinned));
+    res.info.host_rows_bytes = res.rows_capacity;
+    res.info.host_rows_pinned = res.rows_pinned ? 1 : 0;
+    // chunks of 1/8 of the table, between 256 KiB and 256 MiB: a mid-size result still overlaps
+    const uint64_t chunk_bytes = std::min<uint64_t>(256ull << 20, std::max<uint64_t>(256ull << 10, total / 8));
+    const uint64_t chunk_rows = std::max<uint64_t>(1, chunk_bytes / row_bytes);
+    const uint64_t nslot = std::min<uint64_t>(n, chunk_rows);
+    DBuf<uint64_t> stage(&pool_, 2 * nslot * ncols);
+    const uint64_t *rid_map = (o_.flags & OMX_FLAG_NO_RID_MAP) ? nullptr : g_.d_rids;
+    hipStream_t cs = g_.stream2;
+    hipEvent_t mapped[2], copied[2], fin;
+    for (int j = 0; j < 2; ++j) {
+      HIP_CHECK(hipEventCreateWithFlags(&mapped[j], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&copied[j], hipEventDisableTiming));
+    }
+    HIP_CHECK(hipEventCreateWithFlags(&fin, hipEventDisableTiming));
+    tm_.begin("deliver_d2h");
+    std::vector<const uint32_t *> cp(ncols);
+    uint64_t c = 0;
+    for (uint64_t r0 = 0; r0 < n; r0 += chunk_rows, ++c) {
+      const int slot = (int)(c & 1);
+      const uint64_t nr = std::min(chunk_rows, n - r0);
+      uint64_t *dst = stage.p + (uint64_t)slot * nslot * ncols;
+      if (c >= 2) HIP_CHECK(hipStreamWaitEvent(s_, copied[slot], 0));  // the slot's previous copy is done
+      for (int k = 0; k < ncols; ++k) cp[k] = out[k].p + r0;
+      tm_.begin("k_map_rids");
+      launch_map_rids(ncols, cp.data(), nr, rid_map, dst, g_.V, s_);
+      tm_.end(nr * (uint64_t)ncols * 12);
+      HIP_CHECK(hipEventRecord(mapped[slot], s_));
+      HIP_CHECK(hipStreamWaitEvent(cs, mapped[slot], 0));
+      HIP_CHECK(hipMemcpyAsync(res.rows + r0 * ncols, dst, nr * row_bytes, hipMemcpyDeviceToHost, cs));
+      HIP_CHECK(hipEventRecord(copied[slot], cs));
+    }
+    HIP_CHECK(hipEventRecord(fin, cs));
+    HIP_CHECK(hipStreamWaitEvent(s_, fin, 0));  // the executor's end event waits for the last copy
+    tm_.end(total);
+    for (int j = 0; j < 2; ++j) {
+      (void)hipEventDestroy(mapped[j]);
+      (void)hipEventDestroy(copied[j]);
+    }
+    (void)hipEventDestroy(fin);
+  }
+
   Graph &g_;
   const Plan &p_;
   omx_exec_options o_;
@@ -1311,9 +1351,19 @@ class Executor {
     if (!es.d_list_col[dir]) {
       const uint64_t E = dir == 0 ? es.n_edges : es.n_in_edges;
       uint32_t *lcol = nullptr, *lh = nullptr, nh = 0;
+      // the cached col stays for the snapshot's lifetime: built only when it and a pass's scratch over
+      // every entry (lcol + survivors, 8 B an entry) leave 1 GiB of the device free (OMX_E_OOM otherwise:
+      // the caller takes the binned lists)
+      size_t free_b = 0, total_b = 0;
+      HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+      if ((uint64_t)free_b + pool_.cached_bytes() < (E + 4) * 4 + 8 * E + (1ull << 30))
+        fail(OMX_E_OOM, "no room for the lists col of a " + std::to_string(E) + "-entry CSR");
       try {
-        HIP_CHECK(hipMalloc((void **)&lcol, (E + 4) * 4));  // padded: the lists kernel reads whole aligned 16-byte groups
-        HIP_CHECK(hipMalloc((void **)&lh, (size_t)kFlistHubs * 4));
+        // padded: the lists kernel reads whole aligned 16-byte groups
+        if (hipMalloc((void **)&lcol, (E + 4) * 4) != hipSuccess || hipMalloc((void **)&lh, (size_t)kFlistHubs * 4) != hipSuccess) {
+          (void)hipGetLastError();
+          fail(OMX_E_OOM, "device allocation of the lists col failed");
+        }
         DBuf<uint32_t> hub_idx(&pool_, g_.V), hist(&pool_, 4096);
         DBuf<unsigned long long> cnt(&pool_, 1);
         nh = build_pull_col(g_.rp(es, dir), g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, kFlistHubs, hub_idx.p,
@@ -1877,7 +1927,10 @@ class Executor {
   // configs[0]'s shape — root, an unfiltered hop, the marked last hop — on a graph of ≤ kFof2Bits vertices:
   // four launches (kernels.hip k_fof2_a / _b + the list) and one host round trip for the whole MATCH. The same
   // distinct set and accounting as root() + expand_step() + expand_mark()'s factorized branch: E_t = E1
-  // + Σ over hop 1's rows of deg2, bindings = that sum, edges read = E1 + the distinct sources' entries
+  // + Σ over hop 1's rows of deg2, bindings = that sum, edges read = E1 + the distinct sources' entries.
+  // (edges_read and factorized_hops are diagnostics of what ran: this path always reads the distinct
+  // sources' entries only, so they say so even where the general path's thresholds — factor_min_rows_,
+  // factor_min_ratio_ — would have read Σ deg2 one row at a time; E_t and bindings are path-independent)
   bool fof2_ok() {
     if (!mark_fuse_ || !factor_ || dist_ || g_.partitioned() || p_.kind != Plan::MATCH || p_.steps.size() != 3 ||
         g_.V > kFof2Bits || g_.V == 0)
@@ -2283,12 +2336,26 @@ class Executor {
     // (the chunk space's offsets are u32: EU / 4 + 2U chunks below 2^32; a semi-join needs the lists'
     // lengths only, which the binned path counts without grouping them: R1 1.66 against 1.81 ms through
     // the tiled pass without its copy, one box, `r05pmc2`)
-    if (flists_ && !(write && semi_) && !nbset && st.adj.parts.size() == 1 && !g_.partitioned() && g_.V < 0x80000000u && EU > 0 &&
-        EU / 4 + 2 * U < 0xFFFFFF00ull) {
-      filtered_lists(ub.p, U, doffb.p, EU, st.adj, bitmap(st.filter_bm), loff, lcol);
-      nlist = kOnDevice;
-      edges_iter_ += EU;
-    } else {
+    // (k_flist_info packs a source's chunk count in 28 bits: rows under 2^30 entries)
+    bool use_fl = flists_ && !(write && semi_) && !nbset && st.adj.parts.size() == 1 && !g_.partitioned() &&
+                  g_.V < 0x80000000u && EU > 0 && EU / 4 + 2 * U < 0xFFFFFF00ull &&
+                  g_.esets[st.adj.parts[0].first].max_deg[st.adj.parts[0].second] < (1ull << 30);
+    if (use_fl) {
+      try {
+        filtered_lists(ub.p, U, doffb.p, EU, st.adj, bitmap(st.filter_bm), loff, lcol);
+        nlist = kOnDevice;
+        edges_iter_ += EU;
+      } catch (const OmxError &e) {
+        // the lists col (E entries) or the pass's scratch (≈ 2 EU entries) did not fit: the binned lists
+        // below size their buffers by the filtered count instead
+        if (e.code != OMX_E_OOM) throw;
+        (void)hipGetLastError();
+        use_fl = false;
+        loff = DBuf<uint64_t>();
+        lcol = DBuf<uint32_t>();
+      }
+    }
+    if (!use_fl) {
       DBuf<unsigned long long> cnt(&pool_, U + 1);
       loff = DBuf<uint64_t>(&pool_, U + 1);
       HIP_CHECK(hipMemsetAsync(cnt.p, 0, (U + 1) * 8, s_));
@@ -2348,6 +2415,10 @@ class Executor {
     if (femit) {
       emit_factorized(g, R, U, loff, lcol, nlist, cols, st, perm_s.p);
       return true;
+    }
+    if (nlist == kOnDevice && (debug_expand_ || tm_.on())) {  // (diagnostics only: one more host read)
+      nlist = read1(loff.p + U);
+      tm_.amend_at(flist_copy_rec_, 8ull * nlist + 16ull * U);
     }
     DAdj ladj{};
     ladj.n = 1;

@@ -3,8 +3,10 @@
 // A filtered hop whose rows repeat their source vertices is expanded once per distinct source u: L(u) =
 // the neighbours of u passing the target's WHERE bitmap (OMatchPathItem.executeTraversal with the
 // filter, P/OMatchPathItem.java:63-78), grouped by source so that the rows are written over the lists.
-// The lists come from the generic filtered expansion and a key histogram / scatter (exec.hip); this file
-// writes the rows over them (the factorized emission below).
+// This file builds the lists in one tiled pass over the sources' rows (k_flist + k_flist_copy, round 5;
+// exec.hip falls back to the binned filtered expansion + key histogram / scatter for multigraph
+// set-valued hops, several CSR parts, partitions, semi-joins and when the lists col does not fit) and
+// writes the rows over them (the factorized emission, k_femit_w).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(256) void k_femit_slow(FemitArgs a, const uint32_t 
 // Filter: every entry probes one bit array with one buffer load per entry index of the lane: the filter's
 // words, then the hubs' bits by rank (a hub — one of the CSR's kFlistHubs vertices of highest in-degree,
 // bfs.hip build_pull_col — is entered in the lists col as vb + its rank, vb = the filter's bits: its bit
-// index is its entry, and the hubs' 64 KiB of bits stay cache-resident). No entry is checked before its
+// index is its entry; the hubs' 128 KiB of bits sit in the workgroup's LDS). No entry is checked before its
 // probe: a chunk's entries outside the source's row are other rows' entries (in range) or the col's
 // zeroed padding.
 // Output: a tile's survivors, in entry order — which is source order — are written to its own

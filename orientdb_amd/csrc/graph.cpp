@@ -4,7 +4,9 @@
 #include <algorithm>
 #include <atomic>
 #include <memory>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "kernels.h"
@@ -25,6 +27,19 @@ static size_t round_size(size_t b) {
   return (b + g - 1) / g * g;
 }
 
+bool pool_poison() {  // read on every allocation, so a test can switch it within one process
+  const char *e = std::getenv("OMX_POOL_POISON");
+  return e && std::strcmp(e, "0") != 0;
+}
+
+// the whole device is drained first: a reused buffer may still be read by a kernel queued on any stream
+static void poison_fill(void *p, size_t bytes) {
+  if (!pool_poison()) return;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemset(p, 0xFF, bytes) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess)
+    fail(OMX_E_DEVICE, std::string("OMX_POOL_POISON fill failed: ") + hipGetErrorString(hipGetLastError()));
+}
+
 void *DevicePool::alloc(size_t bytes) {
   size_t sz = round_size(bytes);
   auto it = free_.lower_bound(sz);
@@ -33,6 +48,7 @@ void *DevicePool::alloc(size_t bytes) {
     live_[p] = it->first;
     cached_ -= it->first;
     free_.erase(it);
+    poison_fill(p, live_[p]);
     return p;
   }
   void *p = nullptr;
@@ -45,6 +61,7 @@ void *DevicePool::alloc(size_t bytes) {
     }
   }
   live_[p] = sz;
+  poison_fill(p, sz);
   return p;
 }
 
@@ -65,6 +82,113 @@ void DevicePool::trim() {
 DevicePool::~DevicePool() {
   trim();
   for (auto &kv : live_) (void)hipFree(kv.first);
+}
+
+// ---- host blocks for result rows -------------------------------------------------------------------
+
+namespace {
+struct HostRows {
+  std::mutex mu;
+  std::multimap<size_t, void *> free_;                         // capacity → block
+  std::unordered_map<void *, std::pair<size_t, bool>> live_;  // block → (capacity, pinned)
+  std::unordered_map<void *, bool> pinned_free_;               // cached block → pinned
+  size_t cached = 0;
+  size_t limit = [] {
+    const char *e = std::getenv("OMX_PINNED_CACHE_GB");
+    return (size_t)(e ? std::strtod(e, nullptr) : 64.0) << 30;
+  }();
+  static void drop(void *p, bool pinned) {
+    if (pinned) (void)hipHostFree(p);
+    else std::free(p);
+  }
+  ~HostRows() {
+    for (auto &kv : free_) drop(kv.second, pinned_free_[kv.second]);
+  }
+};
+HostRows &host_rows() {
+  static HostRows *h = new HostRows;  // never destroyed: results may be freed during static teardown
+  return *h;
+}
+}  // namespace
+
+void *host_rows_acquire(size_t bytes, size_t *capacity, bool *pinned) {
+  HostRows &h = host_rows();
+  const size_t g = 2u << 20;
+  const size_t sz = std::max<size_t>(g, (bytes + g - 1) / g * g);
+  {
+    std::lock_guard<std::mutex> lk(h.mu);
+    // a cached block of at least sz and at most 2·sz (+64 MiB) bytes
+    auto it = h.free_.lower_bound(sz);
+    if (it != h.free_.end() && it->first <= 2 * sz + (64u << 20)) {
+      void *p = it->second;
+      const size_t cap = it->first;
+      const bool pin = h.pinned_free_[p];
+      h.pinned_free_.erase(p);
+      h.live_[p] = {cap, pin};
+      h.cached -= cap;
+      h.free_.erase(it);
+      *capacity = cap;
+      *pinned = pin;
+      return p;
+    }
+  }
+  void *p = nullptr;
+  bool pin = true;
+  if (hipHostMalloc(&p, sz, hipHostMallocDefault) != hipSuccess || !p) {
+    (void)hipGetLastError();
+    // trim the cache and try again, then fall back to pageable memory
+    {
+      std::lock_guard<std::mutex> lk(h.mu);
+      for (auto &kv : h.free_) HostRows::drop(kv.second, h.pinned_free_[kv.second]);
+      h.free_.clear();
+      h.pinned_free_.clear();
+      h.cached = 0;
+    }
+    p = nullptr;
+    if (hipHostMalloc(&p, sz, hipHostMallocDefault) != hipSuccess || !p) {
+      (void)hipGetLastError();
+      pin = false;
+      p = std::malloc(sz);
+      if (!p) fail(OMX_E_OOM, "host allocation of " + std::to_string(sz) + " result bytes failed");
+    }
+  }
+  std::lock_guard<std::mutex> lk(h.mu);
+  h.live_[p] = {sz, pin};
+  *capacity = sz;
+  *pinned = pin;
+  return p;
+}
+
+void host_rows_release(void *p) {
+  if (!p) return;
+  HostRows &h = host_rows();
+  std::lock_guard<std::mutex> lk(h.mu);
+  auto it = h.live_.find(p);
+  if (it == h.live_.end()) return;
+  const size_t cap = it->second.first;
+  const bool pin = it->second.second;
+  h.live_.erase(it);
+  if (cap > h.limit) {
+    HostRows::drop(p, pin);
+    return;
+  }
+  // evict the largest cached blocks until this one fits under the limit
+  while (h.cached + cap > h.limit && !h.free_.empty()) {
+    auto last = std::prev(h.free_.end());
+    HostRows::drop(last->second, h.pinned_free_[last->second]);
+    h.pinned_free_.erase(last->second);
+    h.cached -= last->first;
+    h.free_.erase(last);
+  }
+  h.free_.emplace(cap, p);
+  h.pinned_free_[p] = pin;
+  h.cached += cap;
+}
+
+size_t host_rows_cached_bytes() {
+  HostRows &h = host_rows();
+  std::lock_guard<std::mutex> lk(h.mu);
+  return h.cached;
 }
 
 // ---- graph -----------------------------------------------------------------------------------------
@@ -183,6 +307,19 @@ static std::pair<bool, bool> scan_rows(uint32_t V, const uint64_t *rp, const uin
     if (!si) simple = false;
   });
   return {sorted.load(), simple.load()};
+}
+
+// the longest row of a CSR (EdgeSet::max_deg)
+static uint64_t max_row(uint32_t V, const uint64_t *rp) {
+  std::atomic<uint64_t> m{0};
+  parallel_for(V, [&](uint64_t lo, uint64_t hi) {
+    uint64_t x = 0;
+    for (uint64_t v = lo; v < hi; ++v) x = std::max(x, rp[v + 1] - rp[v]);
+    uint64_t cur = m.load();
+    while (x > cur && !m.compare_exchange_weak(cur, x)) {
+    }
+  });
+  return m.load();
 }
 
 static void sort_rows(uint32_t V, const uint64_t *rp, uint32_t *col) {
@@ -330,6 +467,8 @@ Graph *graph_create(const omx_graph_desc *d) {
       es.in_sorted = si.first;
       es.in_simple = si.second;
     }
+    es.max_deg[0] = max_row(VL, t.orp);
+    es.max_deg[1] = max_row(VL, t.irp);
     g->esets.push_back(es);
   }
 

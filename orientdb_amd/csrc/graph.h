@@ -46,6 +46,20 @@ class DevicePool {
   size_t cached_ = 0;
 };
 
+// Process-wide pool of pinned host blocks that back result rows (omx_result_rows, SURVEY §8(b) Ownership:
+// a library-owned pinned buffer released by omx_result_free). A block is never value-initialised; a freed
+// one goes back to the pool (up to OMX_PINNED_CACHE_GB, default 64 GiB, cached) and the next result of
+// a similar size reuses it, so a steady-state hand-over neither pins nor zeroes host pages. Process-wide
+// rather than per graph: a result may outlive its snapshot. If pinning fails the block is pageable
+// (malloc, also uninitialised); *pinned says which.
+void *host_rows_acquire(size_t bytes, size_t *capacity, bool *pinned);
+void host_rows_release(void *p);
+size_t host_rows_cached_bytes();
+
+// OMX_POOL_POISON=1 (debug): every buffer DevicePool::alloc hands out, fresh or reused, is filled with 0xFF
+// bytes first, so a kernel that reads a scratch word it never wrote sees 0xFFFFFFFF, not a lucky zero
+bool pool_poison();
+
 template <class T>
 struct DBuf {
   DevicePool *pool = nullptr;
@@ -89,6 +103,7 @@ struct EdgeSet {
   uint64_t n_in_edges = 0;  // in CSR edges (of the owned rows)
   bool out_sorted = true, in_sorted = true;  // rows ascending
   bool out_simple = true, in_simple = true;  // rows strictly ascending (no parallel edges)
+  uint64_t max_deg[2] = {0, 0};               // the longest row of the out / in CSR (of the owned rows)
   uint64_t *d_out_rp = nullptr, *d_in_rp = nullptr;
   uint32_t *d_out_col = nullptr, *d_in_col = nullptr;
   // slice-cut index of a CSR (0 = out, 1 = in), per slice shift: for every vertex, the offsets inside

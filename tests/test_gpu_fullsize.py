@@ -65,6 +65,17 @@ def test_c2_rmat22_digest():
     assert rs.info["n_rows"] == rs.info["bindings"] == ref["bindings"] > 1e8
     assert rs.info["edges_traversed"] == ref["edges"]
     assert rs.info["digest"] == ref["digest"]
+    # the 155 M RID rows handed to the host (3.7 GB: 15 chunks through the two staging slots into the
+    # pooled pinned block), twice: the second execution reuses the first one's block
+    import orientdb_amd as o
+    st = o.OMatchStatement(C2_QUERY)
+    for _ in range(2):
+        d = st.execute(g, documents=False)
+        assert d.info["n_rows"] == ref["bindings"]
+        assert d.info["host_rows_pinned"] == 1
+        assert d.info["host_rows_bytes"] >= d.rows.nbytes == ref["bindings"] * 3 * 8
+        assert dfs.row_digest(d.rows) == ref["digest"]
+        del d
 
 
 @pytest.fixture(scope="module")

@@ -546,6 +546,51 @@ def test_factorized_lists_sparse_sources(every, monkeypatch):
     g.close()
 
 
+@pytest.mark.parametrize("case", ["m1_shape_rmat16", "deferred_tiles", "multigraph_set_valued"])
+def test_factorized_lists_poisoned_pool(rmat16, rmat10_raw, case, monkeypatch):
+    """The factorized hop's scratch under OMX_POOL_POISON=1: every device buffer the pool hands out is
+    0xFF-filled first, so a kernel that reads a word it never wrote (a zero-survivor tile's scratch slot
+    used as a hub index — the illegal access of round 5's uncommitted k_flist_copy variant, DESIGN.md
+    "Round 5: the k_flist_copy fault") reads 0xFFFFFFFF instead of a lucky zero and faults or differs.
+    Cases: M1's query shape at RMAT-16 (k_flists + k_femit_w), tiles spanning more sources than their
+    slots (k_flist_wide, the deferred tiles), and the multigraph's set-valued hop (lists made distinct)."""
+    import orientdb_amd as o
+    from oracle import dfs
+    monkeypatch.setenv("OMX_POOL_POISON", "1")
+    monkeypatch.setenv("OMX_FACTOR", "force")
+    monkeypatch.setenv("OMX_FEMIT", "force")
+    if case == "m1_shape_rmat16":
+        g, ref = rmat16
+        q = "MATCH {class:Person,as:a,where:(age < 3)}-Knows->{as:b}-Knows->{as:c,where:(age >= 80)} RETURN a,b,c"
+        want = dfs.run(ref.cg, q, nthreads=8, emit=False, digest=["a", "b", "c"])
+        rs = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST, documents=False)
+        assert rs.info["factorized_hops"] >= 1
+        assert (rs.info["n_rows"], rs.info["edges_traversed"], rs.info["digest"]) == \
+            (want["bindings"], want["edges"], want["digest"])
+        d = o.OMatchStatement(q).execute(g, documents=False)  # the rows handed to the host, poisoned staging
+        assert dfs.row_digest(d.rows) == want["digest"]
+    elif case == "deferred_tiles":
+        nb, V = 3000, 3200
+        out = {0: list(range(1, nb + 1))}
+        for b in range(7, nb + 1, 7):
+            out[b] = sorted({3001 + b % 97, 3001 + b % 89})
+        rp = np.zeros(V + 1, np.uint64)
+        rp[1:] = np.cumsum([len(out.get(v, [])) for v in range(V)])
+        col = np.array([t for v in range(V) for t in out.get(v, [])], np.uint32)
+        g = o.GraphSnapshot.person_knows(rp, col, seed=3, device=0, keep_csr=True)
+        q = "MATCH {class:Person,as:a,where:(uid = 0)}-Knows->{as:b}-Knows->{as:c,where:(age >= 0)} RETURN a,b,c"
+        rs = o.OMatchStatement(q).execute(g, documents=False)
+        got = sorted(tuple(int(x) & ((1 << 48) - 1) for x in row) for row in rs.rows)
+        assert got == sorted((0, b, c) for b in out[0] for c in out.get(b, []))
+        g.close()
+    else:
+        g, ref = rmat10_raw
+        q = next(x for x in RMAT_QUERIES if x[0] == "c2_both_ends")
+        for lists in ("1", "0"):
+            monkeypatch.setenv("OMX_FLISTS", lists)
+            _parity(g, ref, q[1], q[2])
+
+
 SEMI_QUERIES = [
     ("ab_of_abc", "MATCH {class:Person,as:a,where:(age < 5)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a, b",
      ["a", "b"]),
@@ -700,6 +745,23 @@ def test_root_shards_partition_the_result(rmat10):
     parts = [gpu_set(o.OMatchStatement(q).execute(g, shard=(r, 4))) for r in range(4)]
     assert set().union(*parts) == full
     assert sum(len(p) for p in parts) == len(full)
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"], ids=["fof2", "general"])
+def test_root_shards_fof(rmat10, fuse, monkeypatch):
+    """configs[0]'s shape under root shards (the replicated multi-GPU bench's C1): k_fof2_a's shard filter
+    (a.rank / a.world), or the general root → hop → marked hop path (OMX_MARK_FUSE=0). A fof may be reached
+    from roots of several shards, so the shards' sets overlap: their union is the full set, and their
+    bindings and E_t add up to the full run's."""
+    import orientdb_amd as o
+    monkeypatch.setenv("OMX_MARK_FUSE", fuse)
+    g, ref = rmat10
+    q = next(x for x in RMAT_QUERIES if x[0] == "c1_fof")
+    full = _parity(g, ref, q[1], q[2])
+    parts = [o.OMatchStatement(q[1]).execute(g, shard=(r, 3), documents=False) for r in range(3)]
+    assert set().union(*(gpu_set(p, q[2]) for p in parts)) == gpu_set(full, q[2])
+    assert sum(p.info["bindings"] for p in parts) == full.info["bindings"]
+    assert sum(p.info["edges_traversed"] for p in parts) == full.info["edges_traversed"]
 
 
 def test_count_mode_matches_materialize(rmat10):
