@@ -36,12 +36,6 @@ struct NonZeroU64 {
 struct CastU8U32 {
   __host__ __device__ uint32_t operator()(const uint8_t &x) const { return x; }
 };
-// the degree of sorted row i's source: udeg[g[i]] (E_t summed over the distinct sources' degrees)
-struct RowSourceDeg {
-  const uint32_t *g;
-  const uint64_t *udeg;
-  __host__ __device__ uint64_t operator()(const uint64_t &i) const { return udeg[g[i]]; }
-};
 // a hub-annotated col entry (bit 31: the entry names a hub)
 struct HubFlag {
   __host__ __device__ uint64_t operator()(const uint32_t &x) const { return x >> 31; }
@@ -193,6 +187,19 @@ static void launch_u64_split(const uint64_t *in, uint64_t n, uint32_t *lo, uint3
   hipLaunchKernelGGL(k_u64_split, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, n, lo, hi);
 }
 
+// a partition's CSR as V + 1 global row pointers (rows outside [lo, hi) empty): what the lists col's
+// hub-first row reordering (build_pull_col) walks
+__global__ void k_full_rp(const uint64_t *rp_local, uint32_t lo, uint32_t hi, uint32_t V, uint64_t *out) {
+  const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v <= V) out[v] = v < lo ? 0 : v <= hi ? rp_local[v - lo] : rp_local[hi - lo];
+}
+// occurrences of every vertex in a col (a partition's stand-in for the opposite CSR's degrees: the hubs of
+// its lists col are the targets its own rows name most)
+__global__ void k_col_occurrences(const uint32_t *col, uint64_t E, uint32_t *cnt) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (uint64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[col[e]], 1u);
+}
+
 // head[i] = 1 where a run of equal sorted keys starts
 __global__ void k_u64_heads(const uint64_t *k, uint64_t n, uint8_t *head) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -284,6 +291,8 @@ class Executor {
       if (host_trace) marks.emplace_back(n, std::chrono::steady_clock::now());
     };
     mark("run");
+    trace_waits_ = host_trace;
+    last_wait_end_ = t0;
     auto res = std::make_unique<omx_result>();
     hipEvent_t ea, eb;
     HIP_CHECK(hipEventCreate(&ea));
@@ -483,6 +492,8 @@ class Executor {
       };
       std::fprintf(stderr, "[omx host] gap %.1f", last_exit.time_since_epoch().count() ? us(last_exit, t0) : 0.0);
       for (size_t i = 1; i < marks.size(); ++i) std::fprintf(stderr, " %s %.1f", marks[i].first, us(marks[i - 1].second, marks[i].second));
+      std::fprintf(stderr, " | waits %zu:", waits_.size());
+      for (auto &w : waits_) std::fprintf(stderr, " +%.0f/%.0f", w.first, w.second);
       std::fprintf(stderr, "\n");
       last_exit = std::chrono::steady_clock::now();
     }
@@ -607,6 +618,9 @@ class Executor {
   uint64_t factorized_hops_ = 0;
   uint64_t semi_hops_ = 0;  // last hops written as a semi-join (Executor::semi_join)
   uint64_t arena_retries_ = 0;
+  bool trace_waits_ = false;  // OMX_HOST_TRACE
+  std::vector<std::pair<double, double>> waits_;
+  std::chrono::steady_clock::time_point last_wait_end_;
 
   // ---- helpers -----------------------------------------------------------------------------------
   template <class F>
@@ -623,6 +637,19 @@ class Executor {
   const uint64_t *wait_mail() {
     volatile uint64_t *f = g_.h_mail + kMailSeq;
     const uint64_t seq = g_.mail_seq;
+    // OMX_HOST_TRACE: each host wait's (µs since the previous wait ended, µs waited)
+    struct WaitMark {
+      std::vector<std::pair<double, double>> *w;
+      std::chrono::steady_clock::time_point t0;
+      std::chrono::steady_clock::time_point *last;
+      ~WaitMark() {
+        if (!w) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        w->emplace_back(std::chrono::duration<double, std::micro>(t0 - *last).count(),
+                        std::chrono::duration<double, std::micro>(t1 - t0).count());
+        *last = t1;
+      }
+    } wm{trace_waits_ ? &waits_ : nullptr, std::chrono::steady_clock::now(), &last_wait_end_};
     for (uint32_t spins = 1; *f != seq; ++spins) {
       if (spins % 4096 == 0) {
         const hipError_t e = hipStreamQuery(s_);
@@ -1366,8 +1393,28 @@ class Executor {
         }
         DBuf<uint32_t> hub_idx(&pool_, g_.V), hist(&pool_, 4096);
         DBuf<unsigned long long> cnt(&pool_, 1);
-        nh = build_pull_col(g_.rp(es, dir), g_.rp(es, dir ^ 1), g_.col(es, dir), g_.V, E, kFlistHubs, hub_idx.p,
-                            hist.p, cnt.p, lh, lcol, cus(), s_);
+        const uint64_t *rp_self = g_.rp(es, dir), *rp_other = g_.rp(es, dir ^ 1);
+        DBuf<uint64_t> full, occ_rp;
+        if (g_.partitioned()) {
+          // a partition holds its own rows only: the rows as V + 1 global row pointers, and hubs ranked
+          // by how often the rank's own col names them (the opposite CSR's rows of other ranks are absent)
+          const uint64_t V1 = (uint64_t)g_.V + 1;
+          full = DBuf<uint64_t>(&pool_, V1);
+          occ_rp = DBuf<uint64_t>(&pool_, V1);
+          DBuf<uint32_t> occ(&pool_, V1);
+          hipLaunchKernelGGL(k_full_rp, dim3((unsigned)((V1 + 255) / 256)), dim3(256), 0, s_,
+                             dir == 0 ? es.d_out_rp : es.d_in_rp, g_.part_lo, g_.part_hi, g_.V, full.p);
+          HIP_CHECK(hipMemsetAsync(occ.p, 0, V1 * 4, s_));
+          if (E) hipLaunchKernelGGL(k_col_occurrences, dim3((unsigned)std::min<uint64_t>((E + 255) / 256, 16ull * cus())), dim3(256), 0, s_,
+                                    g_.col(es, dir), E, occ.p);
+          hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> it(occ.p, CastU64());
+          cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, it, occ_rp.p, (int64_t)V1, s_); });
+          HIP_CHECK(hipStreamSynchronize(s_));
+          rp_self = full.p;
+          rp_other = occ_rp.p;
+        }
+        nh = build_pull_col(rp_self, rp_other, g_.col(es, dir), g_.V, E, kFlistHubs, hub_idx.p, hist.p, cnt.p, lh,
+                            lcol, cus(), s_);
         launch_list_col(lcol, E, (uint32_t)(nwords_ * 64), s_);
         HIP_CHECK(hipStreamSynchronize(s_));
       } catch (...) {
@@ -2131,42 +2178,33 @@ class Executor {
     // 1. the rows whose list is not empty (the others write nothing), in row order or grouped by source.
     // Their count Rn stays on the device until the output size N is known: the kernels in between run
     // over R rows and read Rn, so one host round trip returns both
-    DBuf<uint64_t> len(&pool_, R + 1);
-    launch_femit_len(g.p, R, loff.p, len.p, s_);
-    DBuf<uint32_t> idx(&pool_, R);
-    DBuf<uint64_t> nsel(&pool_, 2);
-    {
-      hipcub::CountingInputIterator<uint32_t> cnt(0);
-      hipcub::TransformInputIterator<uint8_t, NonZeroU64, const uint64_t *> fl(len.p, NonZeroU64());
-      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, cnt, fl, idx.p, nsel.p, (int64_t)R, s_); });
-    }
-    const uint64_t *rn = nsel.p;
-    // (the rows are grouped by source already: the non-empty rows keep their sorted order)
-    // (the non-empty rows' source indices and carried columns in one pass)
+    // (the rows are grouped by source already: the non-empty rows keep their sorted order; their source
+    // indices and carried columns, first output rows and list bases in three launches, one mail:
+    // factor.hip k_emitrows_*, round 6)
     DBuf<uint32_t> gs(&pool_, std::max<uint64_t>(R, 1));
     std::vector<DBuf<uint32_t>> sc;
-    FemitGather fg{};
-    fg.g = g.p;
-    fg.perm = perm_sorted;
-    fg.idx = idx.p;
-    fg.nd = rn;
-    fg.gs = gs.p;
-    fg.nc = (int32_t)cols.size();
     if (cols.size() > (size_t)kFemitCols) fail(OMX_E_INVALID, "internal: emission over more carried columns than k_femit_w takes");
+    // 2. output rows of every binding row: the scan of its list length (roff[Rn] = N); list position of
+    // output o
+    DBuf<uint64_t> roff(&pool_, R + 1), rbase(&pool_, std::max<uint64_t>(R, 1));
+    FemitRows fr{};
+    fr.g = g.p;
+    fr.perm = perm_sorted;
+    fr.loff = loff.p;
+    fr.R = R;
+    fr.gs = gs.p;
+    fr.roff = roff.p;
+    fr.rbase = rbase.p;
+    fr.nc = (int32_t)cols.size();
     for (size_t c = 0; c < cols.size(); ++c) {
       sc.emplace_back(&pool_, std::max<uint64_t>(R, 1));
-      fg.in[c] = col_[cols[c]].p;
-      fg.out[c] = sc.back().p;
+      fr.in[c] = col_[cols[c]].p;
+      fr.out[c] = sc.back().p;
     }
-    launch_femit_gather(fg, R, s_);
-    // 2. output rows of every binding row: the scan of its list length (rows ≥ Rn: 0, so roff[R] = N);
-    // list position of output o
-    DBuf<uint64_t> roff(&pool_, R + 1), rbase(&pool_, std::max<uint64_t>(R, 1));
-    launch_femit_len(gs.p, R, loff.p, len.p, s_, rn);
-    cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, len.p, roff.p, (int64_t)(R + 1), s_); });
-    launch_femit_base(gs.p, R, loff.p, roff.p, rbase.p, s_, rn);
-    const uint64_t *words[3] = {nsel.p, roff.p + R, loff.p + U};
-    launch_post_ptrs(words, nlist == kOnDevice ? 3 : 2, mail(), s_);
+    DBuf<uint64_t> tt(&pool_, 2 * emitrows_tiles(R)), tot(&pool_, 2);
+    tm_.begin("k_emitrows");
+    launch_emitrows(fr, tt.p, tot.p, mail(), s_, nlist == kOnDevice ? loff.p + U : nullptr);
+    tm_.end(28ull * R);
     const uint64_t *m = wait_mail();
     const uint64_t Rn = m[0], N = m[1];
     if (nlist == kOnDevice) {
@@ -2251,41 +2289,26 @@ class Executor {
     const bool femit_ok = write && !semi_ && femit_ && cols.size() <= (size_t)kFemitCols && R > 0 && adj.n > 0;
     bool femit = false;
     if (femit_ok) {
-      DBuf<uint64_t> et(&pool_, 1);
       DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
-      DBuf<uint8_t> head(&pool_, R);
-      DBuf<uint64_t> nsel(&pool_, 1);
       perm_s = DBuf<uint32_t>(&pool_, R);
       ub = DBuf<uint32_t>(&pool_, R);
       g = DBuf<uint32_t>(&pool_, R);
       launch_iota(iota.p, R, s_);
+      // the key bits of the largest source id: V − 1, or V for a null (optional) binding — at RMAT-24 24
+      // bits, three 8-bit onesweep passes instead of four for bits_for(V) = 25 (round 6)
+      const int kbits = std::max(1, bits_for(p_.optional[st.src] ? (uint64_t)g_.V : (uint64_t)g_.V - 1));
       tm_.begin("femit_row_sort");
       cub([&](void *t, size_t &b) {
-        return hipcub::DeviceRadixSort::SortPairs(t, b, src, ss.p, iota.p, perm_s.p, (int64_t)R, 0,
-                                                  std::max(1, bits_for(g_.V)), s_);
+        return hipcub::DeviceRadixSort::SortPairs(t, b, src, ss.p, iota.p, perm_s.p, (int64_t)R, 0, kbits, s_);
       });
-      tm_.end(16ull * R * ((bits_for(g_.V) + 7) / 8));
-      launch_run_heads(ss.p, R, head.p, s_);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Flagged(t, b, ss.p, head.p, ub.p, nsel.p, (int64_t)R, s_); });
-      hipcub::TransformInputIterator<uint32_t, CastU8U32, const uint8_t *> hc(head.p, CastU8U32());
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, hc, g.p, (int64_t)R, s_); });
-      launch_add_u32(g.p, R, -1, s_);
-      // the distinct sources' degrees over the R-row bound (rows past U count 0), scanned
-      DBuf<uint64_t> udeg(&pool_, R + 1);
+      tm_.end(16ull * R * ((kbits + 7) / 8));
+      // the sorted rows' distinct sources (run heads), each row's source index, the sources' degree scan
+      // and E_t = Σ_rows deg(source): three launches, one mail {E_t, U, EU} (factor.hip k_srcrows_*)
       doffb = DBuf<uint64_t>(&pool_, R + 1);
-      uint64_t *doff = doffb.p;
-      tm_.begin("k_row_degree");
-      launch_row_degree_dev(ub.p, nsel.p, R, adj, udeg.p, s_);
-      tm_.end(R * 8ull);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, udeg.p, doff, (int64_t)(R + 1), s_); });
-      // E_t = Σ_rows deg(source) = Σ over the sorted rows of their source's degree (no per-row row_ptr reads)
-      {
-        hipcub::CountingInputIterator<uint64_t> ci(0);
-        hipcub::TransformInputIterator<uint64_t, RowSourceDeg, hipcub::CountingInputIterator<uint64_t>> rd(ci, RowSourceDeg{g.p, udeg.p});
-        cub([&](void *t, size_t &b) { return hipcub::DeviceReduce::Sum(t, b, rd, et.p, (int64_t)R, s_); });
-      }
-      const uint64_t *words[3] = {et.p, nsel.p, doff + R};
-      launch_post_ptrs(words, 3, mail(), s_);
+      DBuf<uint64_t> tt(&pool_, 3 * prologue_tiles(R)), tot(&pool_, 3);
+      tm_.begin("k_srcrows");
+      launch_srcrows(ss.p, R, adj, tt.p, tot.p, ub.p, g.p, doffb.p, mail(), s_);
+      tm_.end(12ull * R + 16ull * R);
       const uint64_t *m = wait_mail();
       Et = m[0], U = m[1], EU = m[2];
       femit = femit_ == 2 || Et >= femit_min_et_;
@@ -2337,8 +2360,7 @@ class Executor {
     // lengths only, which the binned path counts without grouping them: R1 1.66 against 1.81 ms through
     // the tiled pass without its copy, one box, `r05pmc2`)
     // (k_flist_info packs a source's chunk count in 28 bits: rows under 2^30 entries)
-    bool use_fl = flists_ && !(write && semi_) && !nbset && st.adj.parts.size() == 1 && !g_.partitioned() &&
-                  g_.V < 0x80000000u && EU > 0 && EU / 4 + 2 * U < 0xFFFFFF00ull &&
+    bool use_fl = flists_ && !(write && semi_) && !nbset && st.adj.parts.size() == 1 && g_.V < 0x80000000u && EU > 0 && EU / 4 + 2 * U < 0xFFFFFF00ull &&
                   g_.esets[st.adj.parts[0].first].max_deg[st.adj.parts[0].second] < (1ull << 30);
     if (use_fl) {
       try {

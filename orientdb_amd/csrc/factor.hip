@@ -71,12 +71,6 @@ __global__ void k_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff,
   len[r] = loff[u + 1] - loff[u];
 }
 
-__global__ void k_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, const uint64_t *roff, uint64_t *rbase,
-                             const uint64_t *nd) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < (nd ? *nd : R)) rbase[r] = loff[g[r]] - roff[r];
-}
-
 // first and last binding row of every output tile (the rows holding its first and last output): one
 // thread per binding row writes the tiles whose first / last output row falls in it (rows are non-empty,
 // so every tile gets exactly one of each); then whether the tile is regular (full, ≤ 64 rows; slow_all:
@@ -810,19 +804,339 @@ void launch_flist_finish(const FlistArgs &a, const uint64_t *coff, const uint64_
   KCHECK("k_flist_loff");
 }
 
-__global__ void k_femit_gather(FemitGather a) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *a.nd) return;
-  const uint32_t j = a.idx[i];
-  a.gs[i] = a.g[j];
-  const uint32_t p = a.perm[j];
-  for (int c = 0; c < a.nc; ++c) a.out[c][i] = a.in[c][p];
+// ---- the factorized hop's prologues in three launches each (round 6) ---------------------------------
+// Both walk the hop's R rows (sorted by source) in tiles of kPtT rows, 8 consecutive rows a thread: a
+// count pass writes per-tile totals, one workgroup scans them and posts the hop's totals to the host
+// mailbox, a fill pass writes the per-row / per-source arrays at the scanned offsets. They replace chains
+// of ~10-12 small kernels (run heads, flagged selects, scans, degree gathers, reduces: each a launch, most
+// of them rocPRIM's lookback-state init + scan pair), which at M1 cost more in launch gaps than in work.
+constexpr int kPtB = 256, kPtI = 8, kPtT = kPtB * kPtI;
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
 }
-void launch_femit_gather(const FemitGather &a, uint64_t cap, hipStream_t s) {
-  if (!cap) return;
-  if (a.nc < 0 || a.nc > kFemitCols) fail(OMX_E_INVALID, "internal: k_femit_gather columns");
-  hipLaunchKernelGGL(k_femit_gather, dim3(nblocks(cap, 256)), dim3(256), 0, s, a);
-  KCHECK("k_femit_gather");
+// block-wide exclusive scan of one u64 per thread (kPtB threads); *total = the block's sum
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t x, uint64_t *s_w, uint64_t *total) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t incl = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off, 64);
+    if (lane >= (uint32_t)off) incl += y;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint64_t woff = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kPtB / 64; ++w) {
+    const uint64_t t = s_w[w];
+    woff += w < (int)wave ? t : 0;
+    tot += t;
+  }
+  __syncthreads();  // (s_w is reused by the next scan)
+  *total = tot;
+  return woff + incl - x;
+}
+
+// (a) the sorted rows' sources. ss[R]: the rows' source vertices, ascending. Per tile: the run heads (a
+// distinct source starts), Σ deg over the heads (EU), Σ deg over the rows (E_t).
+// a thread's 8 consecutive rows (i0 a multiple of 8: two aligned 16-byte loads when all are in range)
+__device__ __forceinline__ void load8(const uint32_t *a, uint64_t i0, uint64_t R, uint32_t (&v)[kPtI]) {
+  if (i0 + kPtI <= R) {
+    const uint4 x = *reinterpret_cast<const uint4 *>(a + i0), y = *reinterpret_cast<const uint4 *>(a + i0 + 4);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < kPtI; ++k) v[k] = i0 + k < R ? a[i0 + k] : 0u;
+  }
+}
+
+__global__ __launch_bounds__(kPtB) void k_srcrows_count(const uint32_t *ss, uint64_t R, DAdj adj, uint64_t *tt) {
+  __shared__ uint64_t s_w[3][kPtB / 64];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kPtT + (uint64_t)threadIdx.x * kPtI;
+  uint32_t v[kPtI];
+  load8(ss, i0, R, v);
+  const uint32_t prev0 = (i0 > 0 && i0 <= R) ? ss[i0 - 1] : 0u;
+  // the degree of every run's first row in the thread (a head, or the thread's first row): independent
+  // loads, issued together
+  uint64_t dg[kPtI];
+  uint64_t h = 0;
+#pragma unroll
+  for (int k = 0; k < kPtI; ++k) {
+    const uint64_t i = i0 + k;
+    const uint32_t pv = k ? v[k - 1] : prev0;
+    const bool head = i < R && (i == 0 || v[k] != pv);
+    h += head;
+    dg[k] = (i < R && (head || k == 0)) ? adj_degree(adj, v[k]) : UINT64_MAX;
+  }
+  uint64_t eu = 0, et = 0, d = 0;
+#pragma unroll
+  for (int k = 0; k < kPtI; ++k) {
+    const uint64_t i = i0 + k;
+    if (i >= R) break;
+    const uint32_t pv = k ? v[k - 1] : prev0;
+    const bool head = i == 0 || v[k] != pv;
+    if (dg[k] != UINT64_MAX) d = dg[k];
+    eu += head ? d : 0;
+    et += d;
+  }
+  h = wave_sum_u64(h);
+  eu = wave_sum_u64(eu);
+  et = wave_sum_u64(et);
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_w[0][wave] = h;
+    s_w[1][wave] = eu;
+    s_w[2][wave] = et;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    uint64_t t = 0;
+    for (int w = 0; w < kPtB / 64; ++w) t += s_w[threadIdx.x][w];
+    tt[3 * (uint64_t)blockIdx.x + threadIdx.x] = t;
+  }
+}
+
+// one workgroup: exclusive scans of the tiles' K counters (in place, all K side by side), the totals to
+// tot[0..K) and the mailbox (words in the order `order` lists them)
+// (extra: one more word appended to the mail, e.g. a count another kernel left on the device)
+constexpr int kScanB = 1024;
+template <int K>
+__global__ __launch_bounds__(kScanB) void k_tiles_scan(uint64_t *tt, uint64_t nt, uint64_t *tot, Mail mail, int4 order,
+                                                        const uint64_t *extra) {
+  __shared__ uint64_t s_w[K][kScanB / 64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t carry[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) carry[j] = 0;
+  for (uint64_t t0 = 0; t0 < nt; t0 += kScanB) {
+    const uint64_t t = t0 + threadIdx.x;
+    uint64_t x[K], incl[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) incl[j] = x[j] = t < nt ? tt[K * t + j] : 0;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint64_t y = __shfl_up(incl[j], off, 64);
+        if (lane >= (uint32_t)off) incl[j] += y;
+      }
+    if (lane == 63)
+#pragma unroll
+      for (int j = 0; j < K; ++j) s_w[j][wave] = incl[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      uint64_t woff = 0, tsum = 0;
+      for (int w = 0; w < kScanB / 64; ++w) {
+        const uint64_t v = s_w[j][w];
+        woff += w < (int)wave ? v : 0;
+        tsum += v;
+      }
+      if (t < nt) tt[K * t + j] = carry[j] + woff + incl[j] - x[j];
+      carry[j] += tsum;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) tot[j] = carry[j];
+    const int ord[4] = {order.x, order.y, order.z, order.w};
+    for (int j = 0; j < K; ++j) mail.p[j] = carry[ord[j]];
+    if (extra) mail.p[K] = *extra;
+    mail_post(mail);
+  }
+}
+
+// ub[u] = the u-th distinct source, g[i] = row i's source index, doff[u] = Σ deg of sources before u
+// (doff[U] = EU); tt: the scanned tile counters (heads, EU, E_t), tot = {U, EU, E_t}
+__global__ __launch_bounds__(kPtB) void k_srcrows_fill(const uint32_t *ss, uint64_t R, DAdj adj, const uint64_t *tt,
+                                                        const uint64_t *tot, uint32_t *ub, uint32_t *g, uint64_t *doff) {
+  __shared__ uint64_t s_w[kPtB / 64];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kPtT + (uint64_t)threadIdx.x * kPtI;
+  uint32_t v[kPtI];
+  load8(ss, i0, R, v);
+  const uint32_t prev0 = (i0 > 0 && i0 <= R) ? ss[i0 - 1] : 0u;
+  uint64_t dg[kPtI];
+  uint32_t hm = 0;  // head bits
+  uint64_t h = 0, eu = 0;
+#pragma unroll
+  for (int k = 0; k < kPtI; ++k) {
+    const uint64_t i = i0 + k;
+    const uint32_t pv = k ? v[k - 1] : prev0;
+    const bool head = i < R && (i == 0 || v[k] != pv);
+    dg[k] = head ? adj_degree(adj, v[k]) : 0;
+    hm |= head ? 1u << k : 0u;
+    h += head;
+  }
+#pragma unroll
+  for (int k = 0; k < kPtI; ++k) eu += dg[k];
+  uint64_t th, te;
+  uint64_t hb = block_excl_scan_u64(h, s_w, &th) + tt[3 * (uint64_t)blockIdx.x];
+  uint64_t eb = block_excl_scan_u64(eu, s_w, &te) + tt[3 * (uint64_t)blockIdx.x + 1];
+  // the run a thread's first row continues (when it is not a head) is the last one before: index hb − 1
+  uint64_t u = hb - 1;
+  uint32_t gv[kPtI];
+#pragma unroll
+  for (int k = 0; k < kPtI; ++k) {
+    if ((hm >> k) & 1u) {
+      u = hb++;
+      ub[u] = v[k];
+      doff[u] = eb;
+      eb += dg[k];
+    }
+    gv[k] = (uint32_t)u;
+  }
+  if (i0 + kPtI <= R) {
+    *reinterpret_cast<uint4 *>(g + i0) = make_uint4(gv[0], gv[1], gv[2], gv[3]);
+    *reinterpret_cast<uint4 *>(g + i0 + 4) = make_uint4(gv[4], gv[5], gv[6], gv[7]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kPtI; ++k)
+      if (i0 + k < R) g[i0 + k] = gv[k];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) doff[tot[0]] = tot[1];
+}
+
+// (b) the emission's rows: row r (sorted by source) writes |L(g[r])| output rows; the non-empty rows,
+// compacted (their source index, carried values through perm, first output row and list base)
+// (b uses tiles of kErT rows, 4 a thread: its fill stages a tile's compacted rows in LDS)
+constexpr int kErI = 4, kErT = kPtB * kErI;
+__global__ __launch_bounds__(kPtB) void k_emitrows_count(const uint32_t *g, uint64_t R, const uint64_t *loff,
+                                                          uint64_t *tt) {
+  __shared__ uint64_t s_w[2][kPtB / 64];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kErT + (uint64_t)threadIdx.x * kErI;
+  uint32_t uu[kErI];
+  if (i0 + kErI <= R) {
+    const uint4 x = *reinterpret_cast<const uint4 *>(g + i0);
+    uu[0] = x.x; uu[1] = x.y; uu[2] = x.z; uu[3] = x.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < kErI; ++k) uu[k] = i0 + k < R ? g[i0 + k] : 0u;
+  }
+  uint64_t ln[kErI];
+#pragma unroll
+  for (int k = 0; k < kErI; ++k) ln[k] = i0 + k < R ? loff[uu[k] + 1] - loff[uu[k]] : 0;  // (independent loads)
+  uint64_t c = 0, n = 0;
+#pragma unroll
+  for (int k = 0; k < kErI; ++k) {
+    c += ln[k] != 0;
+    n += ln[k];
+  }
+  c = wave_sum_u64(c);
+  n = wave_sum_u64(n);
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_w[0][wave] = c;
+    s_w[1][wave] = n;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint64_t t = 0;
+    for (int w = 0; w < kPtB / 64; ++w) t += s_w[threadIdx.x][w];
+    tt[2 * (uint64_t)blockIdx.x + threadIdx.x] = t;
+  }
+}
+
+// tot = {Rn, N}: gs[j], out[c][j] = in[c][perm[r]], roff[j] (roff[Rn] = N), rbase[j] = loff[g[r]] − roff[j].
+// A tile's non-empty rows are compacted into LDS, then written as block-wide runs (a thread writing its own
+// rows' consecutive slots scattered every store over the wave: 158 against ≈30 µs at M1)
+__global__ __launch_bounds__(kPtB) void k_emitrows_fill(FemitRows a, const uint64_t *tt, const uint64_t *tot) {
+  __shared__ uint64_t s_w[kPtB / 64];
+  __shared__ uint32_t s_gs[kErT];
+  __shared__ uint64_t s_ro[kErT], s_lo[kErT];
+  __shared__ uint32_t s_cv[kFemitCols][kErT];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kErT + (uint64_t)threadIdx.x * kErI;
+  uint32_t uu[kErI];
+  if (i0 + kErI <= a.R) {
+    const uint4 x = *reinterpret_cast<const uint4 *>(a.g + i0);
+    uu[0] = x.x; uu[1] = x.y; uu[2] = x.z; uu[3] = x.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < kErI; ++k) uu[k] = i0 + k < a.R ? a.g[i0 + k] : 0u;
+  }
+  uint64_t ln[kErI], lo[kErI];
+  uint64_t c = 0, n = 0;
+#pragma unroll
+  for (int k = 0; k < kErI; ++k) {
+    lo[k] = i0 + k < a.R ? a.loff[uu[k]] : 0;
+    ln[k] = i0 + k < a.R ? a.loff[uu[k] + 1] - lo[k] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kErI; ++k) {
+    c += ln[k] != 0;
+    n += ln[k];
+  }
+  // the carried values of the non-empty rows: every load issued before the LDS writes
+  uint32_t cv[kFemitCols][kErI];
+  uint32_t pr[kErI];
+#pragma unroll
+  for (int k = 0; k < kErI; ++k) pr[k] = ln[k] ? a.perm[i0 + k] : 0u;
+#pragma unroll
+  for (int cc = 0; cc < kFemitCols; ++cc)
+#pragma unroll
+    for (int k = 0; k < kErI; ++k) cv[cc][k] = (cc < a.nc && ln[k]) ? a.in[cc][pr[k]] : 0u;
+  uint64_t tc, tn;
+  uint64_t jl = block_excl_scan_u64(c, s_w, &tc);
+  uint64_t o = block_excl_scan_u64(n, s_w, &tn) + tt[2 * (uint64_t)blockIdx.x + 1];
+#pragma unroll
+  for (int k = 0; k < kErI; ++k) {
+    if (!ln[k]) continue;
+    s_gs[jl] = uu[k];
+    s_ro[jl] = o;
+    s_lo[jl] = lo[k];
+#pragma unroll
+    for (int cc = 0; cc < kFemitCols; ++cc)
+      if (cc < a.nc) s_cv[cc][jl] = cv[cc][k];
+    ++jl;
+    o += ln[k];
+  }
+  __syncthreads();
+  const uint64_t jb = tt[2 * (uint64_t)blockIdx.x];
+  for (uint32_t t = threadIdx.x; t < (uint32_t)tc; t += kPtB) {
+    a.gs[jb + t] = s_gs[t];
+    a.roff[jb + t] = s_ro[t];
+    a.rbase[jb + t] = s_lo[t] - s_ro[t];
+#pragma unroll
+    for (int cc = 0; cc < kFemitCols; ++cc)
+      if (cc < a.nc) a.out[cc][jb + t] = s_cv[cc][t];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.roff[tot[0]] = tot[1];
+}
+
+uint64_t prologue_tiles(uint64_t R) { return (R + kPtT - 1) / kPtT; }
+uint64_t emitrows_tiles(uint64_t R) { return (R + kErT - 1) / kErT; }
+
+void launch_srcrows(const uint32_t *ss, uint64_t R, const DAdj &adj, uint64_t *tt, uint64_t *tot, uint32_t *ub,
+                    uint32_t *g, uint64_t *doff, const Mail &mail, hipStream_t s) {
+  const uint64_t nt = prologue_tiles(R);
+  if (!nt) fail(OMX_E_INVALID, "internal: launch_srcrows without rows");
+  if (nt > 0xFFFFFFFFull) unsupported("a factorized hop over 2^43 or more rows");
+  hipLaunchKernelGGL(k_srcrows_count, dim3((unsigned)nt), dim3(kPtB), 0, s, ss, R, adj, tt);
+  KCHECK("k_srcrows_count");
+  // tiles' counters (heads, EU, E_t) → tot = {U, EU, E_t}; mail = {E_t, U, EU}
+  hipLaunchKernelGGL(k_tiles_scan<3>, dim3(1), dim3(kScanB), 0, s, tt, nt, tot, mail, make_int4(2, 0, 1, 0),
+                     (const uint64_t *)nullptr);
+  KCHECK("k_tiles_scan");
+  hipLaunchKernelGGL(k_srcrows_fill, dim3((unsigned)nt), dim3(kPtB), 0, s, ss, R, adj, tt, tot, ub, g, doff);
+  KCHECK("k_srcrows_fill");
+}
+
+void launch_emitrows(const FemitRows &a, uint64_t *tt, uint64_t *tot, const Mail &mail, hipStream_t s,
+                     const uint64_t *extra) {
+  const uint64_t nt = emitrows_tiles(a.R);
+  if (!nt) fail(OMX_E_INVALID, "internal: launch_emitrows without rows");
+  if (nt > 0xFFFFFFFFull) unsupported("a factorized emission over 2^43 or more rows");
+  if (a.nc < 0 || a.nc > kFemitCols) fail(OMX_E_INVALID, "internal: k_emitrows_fill columns");
+  hipLaunchKernelGGL(k_emitrows_count, dim3((unsigned)nt), dim3(kPtB), 0, s, a.g, a.R, a.loff, tt);
+  KCHECK("k_emitrows_count");
+  // tiles' counters (non-empty rows, output rows) → tot = {Rn, N}; mail = {Rn, N}
+  hipLaunchKernelGGL(k_tiles_scan<2>, dim3(1), dim3(kScanB), 0, s, tt, nt, tot, mail, make_int4(0, 1, 0, 0), extra);
+  KCHECK("k_tiles_scan");
+  hipLaunchKernelGGL(k_emitrows_fill, dim3((unsigned)nt), dim3(kPtB), 0, s, a, tt, tot);
+  KCHECK("k_emitrows_fill");
 }
 
 uint64_t femit_tiles(uint64_t N) { return (N + kEwTile - 1) / kEwTile; }
@@ -834,13 +1148,6 @@ void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint6
                       const uint64_t *nd) {
   hipLaunchKernelGGL(k_femit_len, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, g, R, loff, len, nd);
   KCHECK("k_femit_len");
-}
-
-void launch_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, const uint64_t *roff, uint64_t *rbase,
-                       hipStream_t s, const uint64_t *nd) {
-  if (!R) return;
-  hipLaunchKernelGGL(k_femit_base, dim3(nblocks(R, 256)), dim3(256), 0, s, g, R, loff, roff, rbase, nd);
-  KCHECK("k_femit_base");
 }
 
 void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, bool slow_all, hipStream_t s) {

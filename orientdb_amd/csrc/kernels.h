@@ -179,9 +179,6 @@ void launch_route_bounds(const uint32_t *id, uint64_t R, const uint64_t *bounds,
 void launch_add_u32(uint32_t *x, uint64_t n, int64_t delta, hipStream_t s);
 
 void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_t *deg, hipStream_t s);
-// deg[r] = degree of src[r] for r < *n (a device count ≤ R), 0 for *n ≤ r ≤ R
-void launch_row_degree_dev(const uint32_t *src, const uint64_t *n, uint64_t R, const DAdj &adj, uint64_t *deg,
-                           hipStream_t s);
 // deg[v - lo] = degree of row v (u64: a multigraph row may hold 2^32 or more entries)
 void launch_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint64_t *deg, hipStream_t s);
 void launch_mp_partition(const uint64_t *offs, uint64_t R, uint64_t E, uint64_t ntiles, uint64_t *part,
@@ -310,18 +307,29 @@ uint64_t femit_tiles(uint64_t N);
 // nd: a device row count ≤ R (rows past it: length 0, no base); nullptr: all R rows
 void launch_femit_len(const uint32_t *g, uint64_t R, const uint64_t *loff, uint64_t *len, hipStream_t s,
                       const uint64_t *nd = nullptr);
-// the non-empty rows (idx[0, *nd)) in one pass: gs[i] = g[idx[i]], p = perm[idx[i]], out[c][i] = in[c][p]
-struct FemitGather {
-  const uint32_t *g, *perm, *idx;
-  const uint64_t *nd;
+// The factorized hop's prologues in three launches each (factor.hip, round 6); tt: 3 (srcrows) or 2
+// (emitrows) u64 counters per prologue_tiles(R) tile, tot: 3 / 2 u64 totals.
+uint64_t prologue_tiles(uint64_t R);  // launch_srcrows' tiles
+uint64_t emitrows_tiles(uint64_t R);  // launch_emitrows' tiles
+// ss[R]: the rows' sources, sorted → ub[U] (distinct sources), g[R] (row → source index), doff[U + 1] (scan
+// of the sources' degrees); tot = {U, EU, E_t}; mail = {E_t, U, EU}
+void launch_srcrows(const uint32_t *ss, uint64_t R, const DAdj &adj, uint64_t *tt, uint64_t *tot, uint32_t *ub,
+                    uint32_t *g, uint64_t *doff, const Mail &mail, hipStream_t s);
+// rows r < R grouped by source g[r]: the non-empty ones (|L(g[r])| > 0) compacted to j < Rn: gs[j] = g[r],
+// out[c][j] = in[c][perm[r]], roff[j] = their first output row (roff[Rn] = N), rbase[j] = loff[g[r]] − roff[j];
+// tot = {Rn, N}; mail = {Rn, N[, *extra]}
+struct FemitRows {
+  const uint32_t *g, *perm;
+  const uint64_t *loff;
+  uint64_t R;
   uint32_t *gs;
+  uint64_t *roff, *rbase;
   int32_t nc;
   const uint32_t *in[kFemitCols];
   uint32_t *out[kFemitCols];
 };
-void launch_femit_gather(const FemitGather &a, uint64_t cap, hipStream_t s);
-void launch_femit_base(const uint32_t *g, uint64_t R, const uint64_t *loff, const uint64_t *roff, uint64_t *rbase,
-                       hipStream_t s, const uint64_t *nd = nullptr);
+void launch_emitrows(const FemitRows &a, uint64_t *tt, uint64_t *tot, const Mail &mail, hipStream_t s,
+                     const uint64_t *extra = nullptr);
 // rb[2·femit_tiles(N)]: first / last binding row of every output tile; regular[t] = the tile is full and
 // spans at most 64 binding rows (slow_all: none is)
 void launch_femit_bounds(const FemitArgs &a, uint64_t *rb, uint8_t *regular, bool slow_all, hipStream_t s);
@@ -373,8 +381,6 @@ void launch_flist(const FlistArgs &a, uint64_t nt_bound, int cus, hipStream_t s)
 void launch_flist_finish(const FlistArgs &a, const uint64_t *coff, const uint64_t *base, uint64_t *loff, uint64_t nt_bound,
                          int cus, hipStream_t s);
 void launch_key_hist(const uint32_t *key, uint64_t n, unsigned long long *counts, hipStream_t s);
-// head[i] = 1 where a run of equal sorted keys starts
-void launch_run_heads(const uint32_t *sorted, uint64_t n, uint8_t *head, hipStream_t s);
 // the same over a block-segmented table (segment s: entries [seg_start[s], + seg_count[s]))
 void launch_key_hist_seg(const uint32_t *key, const uint64_t *seg_start, const uint32_t *seg_count, uint32_t nseg,
                          unsigned long long *counts, hipStream_t s);

@@ -523,17 +523,6 @@ void launch_row_degree(const uint32_t *src, uint64_t R, const DAdj &adj, uint64_
   KCHECK("k_row_degree");
 }
 
-__global__ void k_row_degree_dev(const uint32_t *src, const uint64_t *nd, uint64_t R, DAdj adj, uint64_t *deg) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > R) return;
-  deg[r] = r < *nd ? adj_degree(adj, src[r]) : 0;
-}
-void launch_row_degree_dev(const uint32_t *src, const uint64_t *n, uint64_t R, const DAdj &adj, uint64_t *deg,
-                           hipStream_t s) {
-  hipLaunchKernelGGL(k_row_degree_dev, dim3(nblocks(R + 1, 256)), dim3(256), 0, s, src, n, R, adj, deg);
-  KCHECK("k_row_degree_dev");
-}
-
 // degrees of the rows [lo, hi) of one CSR (u32: a row of 2^32 or more entries does not occur in a
 // partition's snapshot)
 __global__ void k_row_degree_range(const uint64_t *rp, uint32_t lo, uint32_t hi, uint64_t *deg) {
@@ -2730,16 +2719,6 @@ void launch_key_scatter(const uint32_t *key, const uint32_t *val, uint64_t n, un
 }
 
 // head[i] = 1 where a sorted key run starts
-__global__ void k_run_heads(const uint32_t *s, uint64_t n, uint8_t *head) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) head[i] = i == 0 || s[i] != s[i - 1];
-}
-void launch_run_heads(const uint32_t *sorted, uint64_t n, uint8_t *head, hipStream_t s) {
-  if (!n) return;
-  hipLaunchKernelGGL(k_run_heads, dim3(nblocks(n, 256)), dim3(256), 0, s, sorted, n, head);
-  KCHECK("k_run_heads");
-}
-
 // the same over a block-segmented table (an expansion's per-worker arenas, ExpandArgs::seg_start /
 // seg_count) without compacting it first: one wave per segment, kSegU × 64 entries a round. A round
 // issues all its loads, then all its atomics, then its stores: vector memory completes in order, so

@@ -103,12 +103,20 @@ def test_partitioned_sliced_kernel(rmat10_full, monkeypatch):
 def test_partitioned_factorized(rmat10_full, world, monkeypatch):
     """The factorized expansion (distinct sources, grouped lists, rows over the lists) on every filtered
     hop of every rank: each rank decides on its own rows, which sit with the owner of their source."""
+    import orientdb_amd as o
     monkeypatch.setenv("OMX_FACTOR", "force")
     _, ref = rmat10_full
-    for qn in ("c2_both_ends", "three_hop", "triangle_filtered"):
-        name, query, cols = [q for q in RMAT_QUERIES if q[0] == qn][0]
-        res = run_ranks(_parts(world), query)
-        assert set().union(*[gpu_set(r, cols) for r in res]) == ref.expected(query, cols), qn
+    for lists in ("1", "0"):  # the lists through k_flists over each rank's own lists col, or binned
+        monkeypatch.setenv("OMX_FLISTS", lists)
+        for emit in ("force", "0"):
+            monkeypatch.setenv("OMX_FEMIT", emit)
+            for qn in ("c2_both_ends", "three_hop", "triangle_filtered", "in_dir"):
+                name, query, cols = [q for q in RMAT_QUERIES if q[0] == qn][0]
+                res = run_ranks(_parts(world), query, flags=o.OMX_FLAG_KERNEL_TIMING)
+                assert set().union(*[gpu_set(r, cols) for r in res]) == ref.expected(query, cols), (qn, lists, emit)
+                if qn == "c2_both_ends":
+                    ran = {k["name"] for r in res for k in r.kernel_stats}
+                    assert ("k_flists" in ran) == (lists == "1"), (lists, sorted(ran))
 
 
 def test_rccl_one_rank_routes_through_itself(rmat10_full, monkeypatch):

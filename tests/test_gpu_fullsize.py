@@ -112,7 +112,10 @@ def test_m1_partitioned_rmat24(m1_ref, world):
     from tests.test_gpu_dist import run_ranks
     parts = [o.GraphSnapshot.rmat(24, device=0, partition=(r, world)) for r in range(world)]
     try:
-        mat = run_ranks(parts, C2_QUERY, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST, documents=False)
+        mat = run_ranks(parts, C2_QUERY, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST | o.OMX_FLAG_KERNEL_TIMING |
+                        o.OMX_FLAG_TIME_HOT, documents=False)
+        # every rank's second hop builds its lists through k_flists over its own lists col (round 6)
+        assert all("k_flists" in {k["name"] for k in r.kernel_stats} for r in mat)
         assert sum(r.info["n_rows"] for r in mat) == m1_ref["bindings"] > 5e8
         assert sum(r.info["edges_traversed"] for r in mat) == m1_ref["edges"]
         assert sum(r.info["digest"] for r in mat) % (1 << 64) == m1_ref["digest"]
