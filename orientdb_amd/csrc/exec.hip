@@ -823,7 +823,26 @@ class Executor {
     if (id < 0) return nullptr;
     if (!bms_[id].p) {
       bms_[id] = DBuf<uint64_t>(&pool_, padded_words());
-      eval_bitmap(p_.bitmaps[id].prog, p_.bitmaps[id].class_id, 0, bms_[id].p, padded_words());
+      // another bitmap of the plan that is one comparison over the same column (M1: the root's `age < 1`
+      // and the last hop's `age >= 90`) is evaluated in the same pass over the column (round 6)
+      const BitmapSpec &b = p_.bitmaps[id];
+      const bool cf = b.prog >= 0 && p_.progs[b.prog].const_false;
+      for (size_t j = 0; j < bms_.size() && !cf && b.prog >= 0; ++j) {
+        const BitmapSpec &c = p_.bitmaps[j];
+        if ((int)j == id || bms_[j].p || c.prog < 0 || p_.progs[c.prog].const_false) continue;
+        const DPred pa = make_pred(b.prog, b.class_id), pb = make_pred(c.prog, c.class_id);
+        DBuf<uint64_t> other(&pool_, padded_words());
+        tm_.begin("k_eval_bitmap");
+        if (!launch_eval_bitmap_pair(pa, pb, g_.V, bms_[id].p, other.p, s_, padded_words())) {
+          tm_.end();
+          continue;
+        }
+        tm_.end((uint64_t)g_.V * 4 + 2 * nwords_ * 8);
+        alg_bytes_ += (uint64_t)g_.V * 4;
+        bms_[j] = std::move(other);
+        return bms_[id].p;
+      }
+      eval_bitmap(b.prog, b.class_id, 0, bms_[id].p, padded_words());
     }
     return bms_[id].p;
   }
@@ -1437,8 +1456,10 @@ class Executor {
   // the filtered lists L(u) of the U distinct sources ub (doff: the scan of their degrees, EU = doff[U])
   // as a CSR (loff[U+1], lcol) through k_flists; the list entries stay on the device (loff[U]): lcol is
   // sized for all EU, so no host round trip
+  // (pre_coff / pre_info: the sources' chunk offsets and chunk table entries from launch_srcrows)
   void filtered_lists(const uint32_t *ub, uint64_t U, const uint64_t *doff, uint64_t EU, const AdjSpec &adjs,
-                      const uint64_t *filter, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol) {
+                      const uint64_t *filter, DBuf<uint64_t> &loff, DBuf<uint32_t> &lcol,
+                      const uint64_t *pre_coff = nullptr, const uint4 *pre_info = nullptr) {
     const int es = adjs.parts[0].first, dir = adjs.parts[0].second;
     uint32_t nh = 0;
     const uint32_t *hubs = nullptr;
@@ -1448,16 +1469,23 @@ class Executor {
     const uint64_t *rp = g_.rp(g_.esets[es], dir);
     // the chunk space: every source's row as aligned 4-entry chunks of the col, in source order
     const uint64_t ntb = flist_tiles_bound(EU, U);
-    DBuf<uint32_t> nch(&pool_, U + 1);
-    DBuf<uint64_t> coff(&pool_, U + 1), rb(&pool_, 2 * ntb), base(&pool_, ntb + 1);
-    launch_flist_nch(ub, doff, U, rp, nch.p, s_);  // (nch[U] = 0 included)
-    {
+    DBuf<uint64_t> coffb, rb(&pool_, 2 * ntb), base(&pool_, ntb + 1);
+    DBuf<uint4> infob;
+    const uint64_t *coff = pre_coff;
+    const uint4 *info = pre_info;
+    if (!pre_coff) {
+      DBuf<uint32_t> nch(&pool_, U + 1);
+      coffb = DBuf<uint64_t>(&pool_, U + 1);
+      launch_flist_nch(ub, doff, U, rp, nch.p, s_);  // (nch[U] = 0 included)
       hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> it(nch.p, CastU64());
-      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, it, coff.p, (int64_t)(U + 1), s_); });
+      cub([&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, it, coffb.p, (int64_t)(U + 1), s_); });
+      infob = DBuf<uint4>(&pool_, std::max<uint64_t>(U, 1));
+      coff = coffb.p;
+      info = infob.p;
     }
-    DBuf<uint4> info(&pool_, std::max<uint64_t>(U, 1));
     DBuf<uint32_t> ntot(&pool_, ntb + 1);
-    launch_flist_prep(ub, doff, coff.p, U, rp, coff.p + U, info.p, rb.p, ntot.p, ntb, s_);  // (ntot past the tiles zeroed)
+    // (ntot past the tiles zeroed)
+    launch_flist_prep(ub, doff, coff, U, rp, coff + U, pre_coff ? nullptr : infob.p, rb.p, ntot.p, ntb, s_);
     const uint64_t nbits = vb / 32 + (nh + 31) / 32;
     DBuf<uint32_t> bits(&pool_, nbits), loc(&pool_, std::max<uint64_t>(U, 1));
     DBuf<uint32_t> scratch(&pool_, ntb * flist_tile_entries());
@@ -1465,8 +1493,8 @@ class Executor {
     FlistArgs a{};
     a.ub = ub;
     a.U = U;
-    a.info = info.p;
-    a.ec = coff.p + U;
+    a.info = info;
+    a.ec = coff + U;
     a.acol = acol;
     a.E = dir == 0 ? g_.esets[es].n_edges : g_.esets[es].n_in_edges;
     a.hubs = hubs;
@@ -1489,7 +1517,7 @@ class Executor {
     loff = DBuf<uint64_t>(&pool_, U + 1);
     a.lcol = lcol.p;
     tm_.begin("k_flist_copy");
-    launch_flist_finish(a, coff.p, base.p, loff.p, ntb, cus(), s_);
+    launch_flist_finish(a, coff, base.p, loff.p, ntb, cus(), s_);
     tm_.end(16ull * U);  // (+ 8 bytes a list entry: amended when the count is read)
     flist_copy_rec_ = tm_.last();
   }
@@ -2288,6 +2316,13 @@ class Executor {
     // adjacency total EU come back in one host round trip (three before: 0.06-0.09 ms of idle device)
     const bool femit_ok = write && !semi_ && femit_ && cols.size() <= (size_t)kFemitCols && R > 0 && adj.n > 0;
     bool femit = false;
+    const bool nbset = st.distinct_nb && !st.adj.dup_free;
+    // the lists pass's conditions known before the sources are (its EU bounds are checked after)
+    // (k_flist_info packs a source's chunk count in 28 bits: rows under 2^30 entries)
+    const bool fl_ok = flists_ && !(write && semi_) && !nbset && st.adj.parts.size() == 1 && g_.V < 0x80000000u &&
+                       g_.esets[st.adj.parts[0].first].max_deg[st.adj.parts[0].second] < (1ull << 30);
+    DBuf<uint64_t> ccoff;  // the sources' chunk offsets and chunk table (launch_srcrows, for k_flist)
+    DBuf<uint4> cinfo;
     if (femit_ok) {
       DBuf<uint32_t> iota(&pool_, R), ss(&pool_, R);
       perm_s = DBuf<uint32_t>(&pool_, R);
@@ -2305,9 +2340,13 @@ class Executor {
       // the sorted rows' distinct sources (run heads), each row's source index, the sources' degree scan
       // and E_t = Σ_rows deg(source): three launches, one mail {E_t, U, EU} (factor.hip k_srcrows_*)
       doffb = DBuf<uint64_t>(&pool_, R + 1);
-      DBuf<uint64_t> tt(&pool_, 3 * prologue_tiles(R)), tot(&pool_, 3);
+      DBuf<uint64_t> tt(&pool_, 4 * prologue_tiles(R)), tot(&pool_, 4);
+      if (fl_ok) {
+        ccoff = DBuf<uint64_t>(&pool_, R + 1);
+        cinfo = DBuf<uint4>(&pool_, R);
+      }
       tm_.begin("k_srcrows");
-      launch_srcrows(ss.p, R, adj, tt.p, tot.p, ub.p, g.p, doffb.p, mail(), s_);
+      launch_srcrows(ss.p, R, adj, tt.p, tot.p, ub.p, g.p, doffb.p, mail(), s_, ccoff.p, cinfo.p);
       tm_.end(12ull * R + 16ull * R);
       const uint64_t *m = wait_mail();
       Et = m[0], U = m[1], EU = m[2];
@@ -2352,19 +2391,16 @@ class Executor {
       tm_.end(12ull * R);
     }
     // 2.-3. the filtered lists of the distinct sources, grouped by source (CSR loff / lcol)
-    const bool nbset = st.distinct_nb && !st.adj.dup_free;
     DBuf<uint64_t> loff;
     DBuf<uint32_t> lcol;
     uint64_t nlist = 0;
     // (the chunk space's offsets are u32: EU / 4 + 2U chunks below 2^32; a semi-join needs the lists'
     // lengths only, which the binned path counts without grouping them: R1 1.66 against 1.81 ms through
     // the tiled pass without its copy, one box, `r05pmc2`)
-    // (k_flist_info packs a source's chunk count in 28 bits: rows under 2^30 entries)
-    bool use_fl = flists_ && !(write && semi_) && !nbset && st.adj.parts.size() == 1 && g_.V < 0x80000000u && EU > 0 && EU / 4 + 2 * U < 0xFFFFFF00ull &&
-                  g_.esets[st.adj.parts[0].first].max_deg[st.adj.parts[0].second] < (1ull << 30);
+    bool use_fl = fl_ok && EU > 0 && EU / 4 + 2 * U < 0xFFFFFF00ull;
     if (use_fl) {
       try {
-        filtered_lists(ub.p, U, doffb.p, EU, st.adj, bitmap(st.filter_bm), loff, lcol);
+        filtered_lists(ub.p, U, doffb.p, EU, st.adj, bitmap(st.filter_bm), loff, lcol, ccoff.p, cinfo.p);
         nlist = kOnDevice;
         edges_iter_ += EU;
       } catch (const OmxError &e) {

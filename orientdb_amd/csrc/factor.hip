@@ -766,8 +766,10 @@ void launch_flist_nch(const uint32_t *ub, const uint64_t *doff, uint64_t U, cons
 void launch_flist_prep(const uint32_t *ub, const uint64_t *doff, const uint64_t *coff, uint64_t U, const uint64_t *rp,
                        const uint64_t *ec, uint4 *info, uint64_t *rb, uint32_t *ntot, uint64_t nt_bound, hipStream_t s) {
   if (!U) return;
-  hipLaunchKernelGGL(k_flist_info, dim3(nblocks(U, 256)), dim3(256), 0, s, ub, doff, coff, U, rp, info);
-  KCHECK("k_flist_info");
+  if (info) {  // (nullptr: the chunk table came with the sources, launch_srcrows)
+    hipLaunchKernelGGL(k_flist_info, dim3(nblocks(U, 256)), dim3(256), 0, s, ub, doff, coff, U, rp, info);
+    KCHECK("k_flist_info");
+  }
   hipLaunchKernelGGL(k_flist_bounds, dim3(nblocks(nt_bound + 1, 256)), dim3(256), 0, s, coff, U, ec, rb, ntot, nt_bound);
   KCHECK("k_flist_bounds");
 }
@@ -853,15 +855,19 @@ __device__ __forceinline__ void load8(const uint32_t *a, uint64_t i0, uint64_t R
   }
 }
 
+// CH (a one-part adjacency, the lists pass's input): also Σ over the heads of their row's 4-entry chunks
+// (k_flist's chunk space), so the fill writes the sources' chunk offsets and chunk table entries too
+template <bool CH>
 __global__ __launch_bounds__(kPtB) void k_srcrows_count(const uint32_t *ss, uint64_t R, DAdj adj, uint64_t *tt) {
-  __shared__ uint64_t s_w[3][kPtB / 64];
+  constexpr int K = CH ? 4 : 3;
+  __shared__ uint64_t s_w[K][kPtB / 64];
   const uint64_t i0 = (uint64_t)blockIdx.x * kPtT + (uint64_t)threadIdx.x * kPtI;
   uint32_t v[kPtI];
   load8(ss, i0, R, v);
   const uint32_t prev0 = (i0 > 0 && i0 <= R) ? ss[i0 - 1] : 0u;
   // the degree of every run's first row in the thread (a head, or the thread's first row): independent
   // loads, issued together
-  uint64_t dg[kPtI];
+  uint64_t dg[kPtI], rs[kPtI];
   uint64_t h = 0;
 #pragma unroll
   for (int k = 0; k < kPtI; ++k) {
@@ -869,9 +875,15 @@ __global__ __launch_bounds__(kPtB) void k_srcrows_count(const uint32_t *ss, uint
     const uint32_t pv = k ? v[k - 1] : prev0;
     const bool head = i < R && (i == 0 || v[k] != pv);
     h += head;
-    dg[k] = (i < R && (head || k == 0)) ? adj_degree(adj, v[k]) : UINT64_MAX;
+    const bool need = i < R && (head || k == 0);
+    if (CH) {
+      rs[k] = need ? adj.p[0].rp[v[k]] : 0;
+      dg[k] = need ? adj.p[0].rp[v[k] + 1] - rs[k] : UINT64_MAX;
+    } else {
+      dg[k] = need ? adj_degree(adj, v[k]) : UINT64_MAX;
+    }
   }
-  uint64_t eu = 0, et = 0, d = 0;
+  uint64_t eu = 0, et = 0, d = 0, ec = 0;
 #pragma unroll
   for (int k = 0; k < kPtI; ++k) {
     const uint64_t i = i0 + k;
@@ -881,21 +893,20 @@ __global__ __launch_bounds__(kPtB) void k_srcrows_count(const uint32_t *ss, uint
     if (dg[k] != UINT64_MAX) d = dg[k];
     eu += head ? d : 0;
     et += d;
+    if (CH && head) ec += fl_nch(rs[k], d);
   }
-  h = wave_sum_u64(h);
-  eu = wave_sum_u64(eu);
-  et = wave_sum_u64(et);
+  uint64_t x[4] = {h, eu, et, ec};
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    s_w[0][wave] = h;
-    s_w[1][wave] = eu;
-    s_w[2][wave] = et;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    x[j] = wave_sum_u64(x[j]);
+    if (lane == 0) s_w[j][wave] = x[j];
   }
   __syncthreads();
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < K) {
     uint64_t t = 0;
     for (int w = 0; w < kPtB / 64; ++w) t += s_w[threadIdx.x][w];
-    tt[3 * (uint64_t)blockIdx.x + threadIdx.x] = t;
+    tt[K * (uint64_t)blockIdx.x + threadIdx.x] = t;
   }
 }
 
@@ -944,38 +955,53 @@ __global__ __launch_bounds__(kScanB) void k_tiles_scan(uint64_t *tt, uint64_t nt
 #pragma unroll
     for (int j = 0; j < K; ++j) tot[j] = carry[j];
     const int ord[4] = {order.x, order.y, order.z, order.w};
-    for (int j = 0; j < K; ++j) mail.p[j] = carry[ord[j]];
-    if (extra) mail.p[K] = *extra;
+    const int nm = K < 3 ? K : 3;  // (a fourth counter is not posted)
+    for (int j = 0; j < nm; ++j) mail.p[j] = carry[ord[j]];
+    if (extra) mail.p[nm] = *extra;
     mail_post(mail);
   }
 }
 
 // ub[u] = the u-th distinct source, g[i] = row i's source index, doff[u] = Σ deg of sources before u
 // (doff[U] = EU); tt: the scanned tile counters (heads, EU, E_t), tot = {U, EU, E_t}
+// CH: coff[u] = the chunks of the sources before u (coff[U] = all), info[u] = k_flist's chunk table entry
+template <bool CH>
 __global__ __launch_bounds__(kPtB) void k_srcrows_fill(const uint32_t *ss, uint64_t R, DAdj adj, const uint64_t *tt,
-                                                        const uint64_t *tot, uint32_t *ub, uint32_t *g, uint64_t *doff) {
+                                                        const uint64_t *tot, uint32_t *ub, uint32_t *g, uint64_t *doff,
+                                                        uint64_t *coff, uint4 *info) {
+  constexpr int K = CH ? 4 : 3;
   __shared__ uint64_t s_w[kPtB / 64];
   const uint64_t i0 = (uint64_t)blockIdx.x * kPtT + (uint64_t)threadIdx.x * kPtI;
   uint32_t v[kPtI];
   load8(ss, i0, R, v);
   const uint32_t prev0 = (i0 > 0 && i0 <= R) ? ss[i0 - 1] : 0u;
-  uint64_t dg[kPtI];
+  uint64_t dg[kPtI], rs[kPtI];
   uint32_t hm = 0;  // head bits
-  uint64_t h = 0, eu = 0;
+  uint64_t h = 0, eu = 0, ec = 0;
 #pragma unroll
   for (int k = 0; k < kPtI; ++k) {
     const uint64_t i = i0 + k;
     const uint32_t pv = k ? v[k - 1] : prev0;
     const bool head = i < R && (i == 0 || v[k] != pv);
-    dg[k] = head ? adj_degree(adj, v[k]) : 0;
+    if (CH) {
+      rs[k] = head ? adj.p[0].rp[v[k]] : 0;
+      dg[k] = head ? adj.p[0].rp[v[k] + 1] - rs[k] : 0;
+    } else {
+      dg[k] = head ? adj_degree(adj, v[k]) : 0;
+    }
     hm |= head ? 1u << k : 0u;
     h += head;
   }
 #pragma unroll
-  for (int k = 0; k < kPtI; ++k) eu += dg[k];
-  uint64_t th, te;
-  uint64_t hb = block_excl_scan_u64(h, s_w, &th) + tt[3 * (uint64_t)blockIdx.x];
-  uint64_t eb = block_excl_scan_u64(eu, s_w, &te) + tt[3 * (uint64_t)blockIdx.x + 1];
+  for (int k = 0; k < kPtI; ++k) {
+    eu += dg[k];
+    if (CH && ((hm >> k) & 1u)) ec += fl_nch(rs[k], dg[k]);
+  }
+  const uint64_t *tb = tt + K * (uint64_t)blockIdx.x;
+  uint64_t th, te, tc;
+  uint64_t hb = block_excl_scan_u64(h, s_w, &th) + tb[0];
+  uint64_t eb = block_excl_scan_u64(eu, s_w, &te) + tb[1];
+  uint64_t cb = CH ? block_excl_scan_u64(ec, s_w, &tc) + tb[3] : 0;
   // the run a thread's first row continues (when it is not a head) is the last one before: index hb − 1
   uint64_t u = hb - 1;
   uint32_t gv[kPtI];
@@ -986,6 +1012,14 @@ __global__ __launch_bounds__(kPtB) void k_srcrows_fill(const uint32_t *ss, uint6
       ub[u] = v[k];
       doff[u] = eb;
       eb += dg[k];
+      if (CH) {
+        const uint32_t n = fl_nch(rs[k], dg[k]);
+        const uint64_t gb = (rs[k] >> 2) - cb;
+        const uint32_t pack = (uint32_t)(rs[k] & 3) | (dg[k] ? (uint32_t)((rs[k] + dg[k] - 1) & 3) << 2 : 0u) | (n << 4);
+        coff[u] = cb;
+        info[u] = make_uint4((uint32_t)gb, (uint32_t)(gb >> 32), (uint32_t)cb, pack);
+        cb += n;
+      }
     }
     gv[k] = (uint32_t)u;
   }
@@ -997,7 +1031,10 @@ __global__ __launch_bounds__(kPtB) void k_srcrows_fill(const uint32_t *ss, uint6
     for (int k = 0; k < kPtI; ++k)
       if (i0 + k < R) g[i0 + k] = gv[k];
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) doff[tot[0]] = tot[1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    doff[tot[0]] = tot[1];
+    if (CH) coff[tot[0]] = tot[3];
+  }
 }
 
 // (b) the emission's rows: row r (sorted by source) writes |L(g[r])| output rows; the non-empty rows,
@@ -1110,18 +1147,31 @@ uint64_t prologue_tiles(uint64_t R) { return (R + kPtT - 1) / kPtT; }
 uint64_t emitrows_tiles(uint64_t R) { return (R + kErT - 1) / kErT; }
 
 void launch_srcrows(const uint32_t *ss, uint64_t R, const DAdj &adj, uint64_t *tt, uint64_t *tot, uint32_t *ub,
-                    uint32_t *g, uint64_t *doff, const Mail &mail, hipStream_t s) {
+                    uint32_t *g, uint64_t *doff, const Mail &mail, hipStream_t s, uint64_t *coff, uint4 *info) {
   const uint64_t nt = prologue_tiles(R);
   if (!nt) fail(OMX_E_INVALID, "internal: launch_srcrows without rows");
   if (nt > 0xFFFFFFFFull) unsupported("a factorized hop over 2^43 or more rows");
-  hipLaunchKernelGGL(k_srcrows_count, dim3((unsigned)nt), dim3(kPtB), 0, s, ss, R, adj, tt);
-  KCHECK("k_srcrows_count");
-  // tiles' counters (heads, EU, E_t) → tot = {U, EU, E_t}; mail = {E_t, U, EU}
-  hipLaunchKernelGGL(k_tiles_scan<3>, dim3(1), dim3(kScanB), 0, s, tt, nt, tot, mail, make_int4(2, 0, 1, 0),
-                     (const uint64_t *)nullptr);
-  KCHECK("k_tiles_scan");
-  hipLaunchKernelGGL(k_srcrows_fill, dim3((unsigned)nt), dim3(kPtB), 0, s, ss, R, adj, tt, tot, ub, g, doff);
-  KCHECK("k_srcrows_fill");
+  if (coff && adj.n != 1) fail(OMX_E_INVALID, "internal: the lists' chunk space over several adjacency parts");
+  // tiles' counters (heads, EU, E_t[, chunks]) → tot = {U, EU, E_t[, EC]}; mail = {E_t, U, EU}
+  if (coff) {
+    hipLaunchKernelGGL(k_srcrows_count<true>, dim3((unsigned)nt), dim3(kPtB), 0, s, ss, R, adj, tt);
+    KCHECK("k_srcrows_count");
+    hipLaunchKernelGGL(k_tiles_scan<4>, dim3(1), dim3(kScanB), 0, s, tt, nt, tot, mail, make_int4(2, 0, 1, 0),
+                       (const uint64_t *)nullptr);
+    KCHECK("k_tiles_scan");
+    hipLaunchKernelGGL(k_srcrows_fill<true>, dim3((unsigned)nt), dim3(kPtB), 0, s, ss, R, adj, tt, tot, ub, g, doff,
+                       coff, info);
+    KCHECK("k_srcrows_fill");
+  } else {
+    hipLaunchKernelGGL(k_srcrows_count<false>, dim3((unsigned)nt), dim3(kPtB), 0, s, ss, R, adj, tt);
+    KCHECK("k_srcrows_count");
+    hipLaunchKernelGGL(k_tiles_scan<3>, dim3(1), dim3(kScanB), 0, s, tt, nt, tot, mail, make_int4(2, 0, 1, 0),
+                       (const uint64_t *)nullptr);
+    KCHECK("k_tiles_scan");
+    hipLaunchKernelGGL(k_srcrows_fill<false>, dim3((unsigned)nt), dim3(kPtB), 0, s, ss, R, adj, tt, tot, ub, g, doff,
+                       (uint64_t *)nullptr, (uint4 *)nullptr);
+    KCHECK("k_srcrows_fill");
+  }
 }
 
 void launch_emitrows(const FemitRows &a, uint64_t *tt, uint64_t *tot, const Mail &mail, hipStream_t s,

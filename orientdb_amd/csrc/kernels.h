@@ -158,6 +158,10 @@ void launch_isect_merge(const IsectArgs &a, bool write, int cus, hipStream_t s);
 // nwords > ⌈V/64⌉ zero-fills the padding words (0: no padding)
 void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s,
                         uint64_t nwords = 0);
+// two single-comparison predicates over the same int32 / int64 column (no class test), evaluated in one
+// pass into their two bitmaps; false (nothing launched) when they are not of that form
+bool launch_eval_bitmap_pair(const DPred &a, const DPred &b, uint32_t V, uint64_t *wa, uint64_t *wb, hipStream_t s,
+                             uint64_t nwords = 0);
 // filter bitmaps (Executor::bitmap) are padded to a multiple of the largest slice, so the sliced
 // kernels stage whole slices with unchecked 16-byte loads
 constexpr uint64_t kBitmapPadWords = kSliceBits / 64;
@@ -313,8 +317,11 @@ uint64_t prologue_tiles(uint64_t R);  // launch_srcrows' tiles
 uint64_t emitrows_tiles(uint64_t R);  // launch_emitrows' tiles
 // ss[R]: the rows' sources, sorted → ub[U] (distinct sources), g[R] (row → source index), doff[U + 1] (scan
 // of the sources' degrees); tot = {U, EU, E_t}; mail = {E_t, U, EU}
+// coff / info (a one-part adjacency; tt then 4 counters a tile, tot 4): the sources' chunk offsets in
+// k_flist's chunk space (coff[U + 1], coff[U] = all chunks) and their chunk table entries
 void launch_srcrows(const uint32_t *ss, uint64_t R, const DAdj &adj, uint64_t *tt, uint64_t *tot, uint32_t *ub,
-                    uint32_t *g, uint64_t *doff, const Mail &mail, hipStream_t s);
+                    uint32_t *g, uint64_t *doff, const Mail &mail, hipStream_t s, uint64_t *coff = nullptr,
+                    uint4 *info = nullptr);
 // rows r < R grouped by source g[r]: the non-empty ones (|L(g[r])| > 0) compacted to j < Rn: gs[j] = g[r],
 // out[c][j] = in[c][perm[r]], roff[j] = their first output row (roff[Rn] = N), rbase[j] = loff[g[r]] − roff[j];
 // tot = {Rn, N}; mail = {Rn, N[, *extra]}

@@ -342,9 +342,12 @@ __global__ __launch_bounds__(256) void k_eval_atoms4(DPred P, uint32_t V, uint64
 // (T = int64_t: the same over an int64 column, C5's `uid < 64` — 8 bytes a vertex, two 16-byte loads a
 // group: 131 µs through the general kernel at RMAT-26, round 5)
 constexpr int kAtom1U = 4;
+// (words2: a second range test lo2…hi2 over the same column into its own bitmap — two predicates of a
+// plan on one column, M1's root `age < 1` and last-hop `age >= 90`, in one pass over it)
 template <class T>
 __global__ __launch_bounds__(256) void k_eval_atom1(const T *col, int64_t lo, int64_t hi, int neg, uint32_t V,
-                                                    uint64_t *words, uint64_t nwords) {
+                                                    uint64_t *words, uint64_t nwords, int64_t lo2, int64_t hi2, int neg2,
+                                                    uint64_t *words2) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64, nwv = (uint64_t)gridDim.x * 4;
   const uint64_t nrounds = (nwords + 4 * kAtom1U - 1) / (4 * kAtom1U);
@@ -373,19 +376,80 @@ __global__ __launch_bounds__(256) void k_eval_atom1(const T *col, int64_t lo, in
     for (int u = 0; u < kAtom1U; ++u) {
       const uint64_t v0 = (w0 + 4 * u) * 64 + 4 * lane;
       const T *e = x[u];
-      uint64_t nib = 0;
+      uint64_t nib = 0, nib2 = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bool r = ((int64_t)e[j] >= lo && (int64_t)e[j] <= hi) != (neg != 0);
         nib |= (uint64_t)(r && v0 + j < V) << j;
+        const bool r2 = ((int64_t)e[j] >= lo2 && (int64_t)e[j] <= hi2) != (neg2 != 0);
+        nib2 |= (uint64_t)(r2 && v0 + j < V) << j;
       }
-      uint64_t w = nib << (4 * (lane & 15));
+      uint64_t w = nib << (4 * (lane & 15)), w2 = nib2 << (4 * (lane & 15));
 #pragma unroll
       for (int off = 1; off < 16; off <<= 1) w |= __shfl_xor(w, off, 64);
       const uint64_t wi = w0 + 4 * u + lane / 16;
       if ((lane & 15) == 0 && wi < nwords) words[wi] = w;
+      if (words2) {  // (wave-uniform)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) w2 |= __shfl_xor(w2, off, 64);
+        if ((lane & 15) == 0 && wi < nwords) words2[wi] = w2;
+      }
     }
   }
+}
+
+// pred is one int32 / int64 comparison with an integer constant, no class test: its range lo…hi (negated
+// for !=)
+static bool atom1_range(const DPred &pred, int64_t *plo, int64_t *phi, int *pneg) {
+  const bool one = pred.n > 0 && pred.n_atoms == 1 && !pred.use_class && pred.atom_c[0].present == nullptr &&
+                   (pred.atom_c[0].type == OMX_PROP_INT32 || pred.atom_c[0].type == OMX_PROP_INT64) &&
+                   !pred.atom_dbl[0] && pred.atom_op[0] >= P_EQ && pred.atom_op[0] <= P_GE;
+  if (!one) return false;
+  const int64_t b = pred.atom_i[0];
+  int64_t lo = INT64_MIN, hi = INT64_MAX;
+  int neg = 0;
+  switch (pred.atom_op[0]) {
+    case P_EQ: lo = hi = b; break;
+    case P_NE: lo = hi = b; neg = 1; break;
+    case P_LT: if (b == INT64_MIN) lo = 1, hi = 0; else hi = b - 1; break;  // (lo > hi: nothing)
+    case P_LE: hi = b; break;
+    case P_GT: if (b == INT64_MAX) lo = 1, hi = 0; else lo = b + 1; break;
+    default: lo = b; break;  // P_GE
+  }
+  *plo = lo, *phi = hi, *pneg = neg;
+  return true;
+}
+
+static void launch_atom1(const DPred &pred, int64_t lo, int64_t hi, int neg, uint64_t *words, uint64_t *words2,
+                         int64_t lo2, int64_t hi2, int neg2, uint32_t V, uint64_t nwords, hipStream_t s) {
+  static int cus_of[64] = {};  // CUs of each device (queried once)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+    if (!cus_of[dev] && hipDeviceGetAttribute(&cus_of[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus_of[dev] = 256;
+    cus = cus_of[dev];
+  }
+  const uint64_t rounds = (nwords + 4 * kAtom1U - 1) / (4 * kAtom1U);
+  const uint64_t waves = std::min<uint64_t>(rounds, (uint64_t)std::max(cus, 1) * 32);
+  if (pred.atom_c[0].type == OMX_PROP_INT32)
+    hipLaunchKernelGGL(k_eval_atom1<int32_t>, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s,
+                       (const int32_t *)pred.atom_c[0].values, lo, hi, neg, V, words, nwords, lo2, hi2, neg2, words2);
+  else
+    hipLaunchKernelGGL(k_eval_atom1<int64_t>, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s,
+                       (const int64_t *)pred.atom_c[0].values, lo, hi, neg, V, words, nwords, lo2, hi2, neg2, words2);
+  KCHECK("k_eval_atom1");
+}
+
+bool launch_eval_bitmap_pair(const DPred &a, const DPred &b, uint32_t V, uint64_t *wa, uint64_t *wb, hipStream_t s,
+                             uint64_t nwords) {
+  int64_t la, ha, lb, hb;
+  int na, nb;
+  if (!V || !atom1_range(a, &la, &ha, &na) || !atom1_range(b, &lb, &hb, &nb) ||
+      a.atom_c[0].values != b.atom_c[0].values || a.atom_c[0].type != b.atom_c[0].type)
+    return false;
+  if (!nwords) nwords = ((uint64_t)V + 63) / 64;
+  launch_atom1(a, la, ha, na, wa, wb, lb, hb, nb, V, nwords, s);
+  return true;
 }
 
 void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s,
@@ -397,37 +461,10 @@ void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *
     four = pred.atom_c[k].present == nullptr && pred.atom_c[k].type != OMX_PROP_INT64 &&
            pred.atom_c[k].type != OMX_PROP_DOUBLE;
   // one int32 / int64 comparison with an integer constant, no class test: the range-test kernel
-  const bool one = pred.n > 0 && pred.n_atoms == 1 && !pred.use_class && pred.atom_c[0].present == nullptr &&
-                   (pred.atom_c[0].type == OMX_PROP_INT32 || pred.atom_c[0].type == OMX_PROP_INT64) &&
-                   !pred.atom_dbl[0] && pred.atom_op[0] >= P_EQ && pred.atom_op[0] <= P_GE;
-  if (one) {
-    const int64_t b = pred.atom_i[0];
-    int64_t lo = INT64_MIN, hi = INT64_MAX;
-    int neg = 0;
-    switch (pred.atom_op[0]) {
-      case P_EQ: lo = hi = b; break;
-      case P_NE: lo = hi = b; neg = 1; break;
-      case P_LT: if (b == INT64_MIN) lo = 1, hi = 0; else hi = b - 1; break;  // (lo > hi: nothing)
-      case P_LE: hi = b; break;
-      case P_GT: if (b == INT64_MAX) lo = 1, hi = 0; else lo = b + 1; break;
-      default: lo = b; break;  // P_GE
-    }
-    static int cus_of[64] = {};  // CUs of each device (queried once)
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-      if (!cus_of[dev] && hipDeviceGetAttribute(&cus_of[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus_of[dev] = 256;
-      cus = cus_of[dev];
-    }
-    const uint64_t rounds = (nwords + 4 * kAtom1U - 1) / (4 * kAtom1U);
-    const uint64_t waves = std::min<uint64_t>(rounds, (uint64_t)std::max(cus, 1) * 32);
-    if (pred.atom_c[0].type == OMX_PROP_INT32)
-      hipLaunchKernelGGL(k_eval_atom1<int32_t>, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s,
-                         (const int32_t *)pred.atom_c[0].values, lo, hi, neg, V, words, nwords);
-    else
-      hipLaunchKernelGGL(k_eval_atom1<int64_t>, dim3(nblocks(waves * 64, 256)), dim3(256), 0, s,
-                         (const int64_t *)pred.atom_c[0].values, lo, hi, neg, V, words, nwords);
-    KCHECK("k_eval_atom1");
+  int64_t lo, hi;
+  int neg;
+  if (atom1_range(pred, &lo, &hi, &neg)) {
+    launch_atom1(pred, lo, hi, neg, words, nullptr, 0, 0, 0, V, nwords, s);
     return;
   }
   if (four) {
