@@ -910,60 +910,54 @@ __global__ __launch_bounds__(kPtB) void k_srcrows_count(const uint32_t *ss, uint
   }
 }
 
-// one workgroup: exclusive scans of the tiles' K counters (in place, all K side by side), the totals to
-// tot[0..K) and the mailbox (words in the order `order` lists them)
+// one workgroup: exclusive scans of the tiles' K counters (in place), the totals to tot[0..K) and the
+// mailbox (words in the order `order` lists them)
 // (extra: one more word appended to the mail, e.g. a count another kernel left on the device)
-constexpr int kScanB = 1024;
+constexpr int kScanB = kPtB, kScanI = 4;  // a thread scans 4 consecutive tiles a round
 template <int K>
 __global__ __launch_bounds__(kScanB) void k_tiles_scan(uint64_t *tt, uint64_t nt, uint64_t *tot, Mail mail, int4 order,
                                                         const uint64_t *extra) {
-  __shared__ uint64_t s_w[K][kScanB / 64];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ uint64_t s_w[kScanB / 64];
   uint64_t carry[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) carry[j] = 0;
-  for (uint64_t t0 = 0; t0 < nt; t0 += kScanB) {
-    const uint64_t t = t0 + threadIdx.x;
-    uint64_t x[K], incl[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) incl[j] = x[j] = t < nt ? tt[K * t + j] : 0;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1)
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const uint64_t y = __shfl_up(incl[j], off, 64);
-        if (lane >= (uint32_t)off) incl[j] += y;
-      }
-    if (lane == 63)
-#pragma unroll
-      for (int j = 0; j < K; ++j) s_w[j][wave] = incl[j];
-    __syncthreads();
+  for (uint64_t t0 = 0; t0 < nt; t0 += (uint64_t)kScanB * kScanI) {
+    const uint64_t tb = t0 + (uint64_t)threadIdx.x * kScanI;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      uint64_t woff = 0, tsum = 0;
-      for (int w = 0; w < kScanB / 64; ++w) {
-        const uint64_t v = s_w[j][w];
-        woff += w < (int)wave ? v : 0;
-        tsum += v;
+      uint64_t x[kScanI], sum = 0;
+#pragma unroll
+      for (int q = 0; q < kScanI; ++q) {
+        x[q] = tb + q < nt ? tt[K * (tb + q) + j] : 0;
+        sum += x[q];
       }
-      if (t < nt) tt[K * t + j] = carry[j] + woff + incl[j] - x[j];
-      carry[j] += tsum;
+      uint64_t total;
+      uint64_t ex = carry[j] + block_excl_scan_u64(sum, s_w, &total);
+#pragma unroll
+      for (int q = 0; q < kScanI; ++q) {
+        if (tb + q < nt) tt[K * (tb + q) + j] = ex;
+        ex += x[q];
+      }
+      carry[j] += total;
     }
-    __syncthreads();
   }
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int j = 0; j < K; ++j) tot[j] = carry[j];
     const int ord[4] = {order.x, order.y, order.z, order.w};
     const int nm = K < 3 ? K : 3;  // (a fourth counter is not posted)
-    for (int j = 0; j < nm; ++j) mail.p[j] = carry[ord[j]];
+#pragma unroll
+    for (int j = 0; j < nm; ++j) {
+      uint64_t w = 0;  // carry[ord[j]] with static indices (a dynamic one would put carry in scratch)
+#pragma unroll
+      for (int q = 0; q < K; ++q) w = ord[j] == q ? carry[q] : w;
+      mail.p[j] = w;
+    }
     if (extra) mail.p[nm] = *extra;
     mail_post(mail);
   }
 }
 
-// ub[u] = the u-th distinct source, g[i] = row i's source index, doff[u] = Σ deg of sources before u
-// (doff[U] = EU); tt: the scanned tile counters (heads, EU, E_t), tot = {U, EU, E_t}
 // CH: coff[u] = the chunks of the sources before u (coff[U] = all), info[u] = k_flist's chunk table entry
 template <bool CH>
 __global__ __launch_bounds__(kPtB) void k_srcrows_fill(const uint32_t *ss, uint64_t R, DAdj adj, const uint64_t *tt,
