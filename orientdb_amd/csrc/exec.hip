@@ -1201,6 +1201,7 @@ class Executor {
     bool segmented = false;
     DBuf<uint64_t> seg_start;
     DBuf<uint32_t> seg_count;
+    DBuf<uint64_t> seg_offs;  // the segments' dense offsets (their counts' scan)
     uint32_t nseg = 0;
   };
 
@@ -1885,6 +1886,7 @@ class Executor {
       o.segmented = true;
       o.dst = std::move(odst);
       o.carry = std::move(outc);
+      o.seg_offs = std::move(soffs);
       return o;
     }
     o.dst = DBuf<uint32_t>(&pool_, n);
@@ -2922,32 +2924,34 @@ class Executor {
       }
       launch_gather_cols(gi[g], gn[g], (int)cols.size(), in.data(), out.data(), s_);
       for (auto &b : gc) carry.push_back(b.p);
+      // (left block-segmented: both groups are compacted straight into one table below)
       if (g == 0)  // |N_x(x)| > |N_y(y)|: iterate N_y(y), probe N_x(x)
-        og[g] = expand_core(gc[iy].p, gn[g], ck.adj, nullptr, carry, write, false, gc[ix].p, &ex.adj, cfilter);
+        og[g] = expand_core(gc[iy].p, gn[g], ck.adj, nullptr, carry, write, write, gc[ix].p, &ex.adj, cfilter);
       else
-        og[g] = expand_core(gc[ix].p, gn[g], ex.adj, nullptr, carry, write, false, gc[iy].p, &ck.adj, cfilter);
+        og[g] = expand_core(gc[ix].p, gn[g], ex.adj, nullptr, carry, write, write, gc[iy].p, &ck.adj, cfilter);
     }
     edges_iter_ += og[0].E + og[1].E;  // the iterated lists (the probed ones are binary-searched)
     R_ = og[0].n + og[1].n;
     if (!write || R_ == 0) return;
     segmented_ = false;
-    if (og[1].n == 0 || og[0].n == 0) {  // one group: its columns as they are
-      ExpandOut &o = og[0].n ? og[0] : og[1];
-      for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(o.carry[i]);
-      col_[ex.dst] = std::move(o.dst);
-      return;
-    }
-    // both groups: every column concatenated in one pass (six D2D copies at C4 were 50 µs of launches)
+    // each group's segments compacted into its part of one table (round 6: the groups' compactions into
+    // their own buffers and a concatenation of every column cost 47 µs more at C4)
     std::vector<DBuf<uint32_t>> cat;
-    std::vector<const uint32_t *> pa, pb;
-    std::vector<uint32_t *> po;
-    for (size_t i = 0; i <= cols.size(); ++i) {
-      cat.emplace_back(&pool_, og[0].n + og[1].n);
-      pa.push_back(i < cols.size() ? og[0].carry[i].p : og[0].dst.p);
-      pb.push_back(i < cols.size() ? og[1].carry[i].p : og[1].dst.p);
-      po.push_back(cat.back().p);
+    for (size_t i = 0; i <= cols.size(); ++i) cat.emplace_back(&pool_, R_);
+    uint64_t base = 0;
+    for (int g = 0; g < 2; ++g) {
+      ExpandOut &o = og[g];
+      if (!o.n) continue;
+      std::vector<uint32_t *> ins, outs;
+      for (size_t i = 0; i <= cols.size(); ++i) {
+        ins.push_back(i < cols.size() ? o.carry[i].p : o.dst.p);
+        outs.push_back(cat[i].p + base);
+      }
+      tm_.begin("k_compact_segments");
+      launch_compact_segments((int)ins.size(), ins.data(), outs.data(), o.seg_start.p, o.seg_count.p, o.seg_offs.p, o.nseg, s_);
+      tm_.end(8ull * ins.size() * o.n);
+      base += o.n;
     }
-    launch_concat_cols(og[0].n, og[1].n, (int)po.size(), pa.data(), pb.data(), po.data(), s_);
     for (size_t i = 0; i < cols.size(); ++i) col_[cols[i]] = std::move(cat[i]);
     col_[ex.dst] = std::move(cat.back());
   }

@@ -274,9 +274,6 @@ void launch_check(const uint32_t *src, const uint32_t *dst, uint64_t R, const DA
                   uint8_t *flags, hipStream_t s);
 void launch_gather_cols(const uint32_t *idx, uint64_t n, int ncols, const uint32_t *const *in, uint32_t *const *out,
                         hipStream_t s);
-// out[c] = a[c][0, na) followed by b[c][0, nb) (ncols ≤ kMaxCols)
-void launch_concat_cols(uint64_t na, uint64_t nb, int ncols, const uint32_t *const *a, const uint32_t *const *b,
-                        uint32_t *const *out, hipStream_t s);
 void launch_cross(uint64_t R, int ncols, const uint32_t *const *in, uint32_t *const *out, const uint32_t *cand,
                   uint64_t ncand, uint32_t *out_dst, hipStream_t s);
 void launch_flag_bitmap(const uint32_t *v, uint64_t n, const uint64_t *bm, uint8_t *flags, hipStream_t s);

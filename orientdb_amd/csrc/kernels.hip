@@ -2580,30 +2580,6 @@ void launch_gather_cols(const uint32_t *idx, uint64_t n, int ncols, const uint32
   KCHECK("k_gather_cols");
 }
 
-// out[c] = a[c][0, na) then b[c][0, nb), every column in one pass
-struct ConcatPtrs {
-  const uint32_t *a[kMaxCols], *b[kMaxCols];
-  uint32_t *out[kMaxCols];
-};
-__global__ void k_concat_cols(uint64_t na, uint64_t nb, int ncols, ConcatPtrs cp) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= na + nb) return;
-  for (int c = 0; c < ncols; ++c) cp.out[c][i] = i < na ? cp.a[c][i] : cp.b[c][i - na];
-}
-void launch_concat_cols(uint64_t na, uint64_t nb, int ncols, const uint32_t *const *a, const uint32_t *const *b,
-                        uint32_t *const *out, hipStream_t s) {
-  if (!(na + nb) || !ncols) return;
-  if (ncols > kMaxCols) fail(OMX_E_INVALID, "internal: k_concat_cols columns");
-  ConcatPtrs cp;
-  for (int c = 0; c < ncols; ++c) {
-    cp.a[c] = a[c];
-    cp.b[c] = b[c];
-    cp.out[c] = out[c];
-  }
-  hipLaunchKernelGGL(k_concat_cols, dim3(nblocks(na + nb, 256)), dim3(256), 0, s, na, nb, ncols, cp);
-  KCHECK("k_concat_cols");
-}
-
 __global__ void k_cross(uint64_t R, int ncols, ColPtrs cp, const uint32_t *cand, uint64_t ncand, uint32_t *out_dst) {
   uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= R * ncand) return;
