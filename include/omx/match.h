@@ -71,6 +71,12 @@ typedef struct omx_edge_set_desc {
                                 /* a partition: the in-rows of the owned vertices)                 */
   const uint32_t *in_col;       /* [n_in_edges]                                                    */
   uint64_t n_in_edges;          /* edges of the in CSR; 0 = n_edges (always equal when unpartitioned) */
+  /* Regular (heavyweight) edges: the edge records behind the CSR entries, which MATCH binds to edge   */
+  /* nodes (outE('L'){as: e, where: (...)}.inV(), OSQLFunctionMove.java:109-144). NULL: lightweight     */
+  /* edges (no records: such patterns are OMX_E_UNSUPPORTED). Not on a partitioned snapshot.            */
+  const uint64_t *edge_rids;    /* [n_edges] RID of the edge record of out_col entry i               */
+  const uint64_t *in_edge_index;/* [n_in_edges] the out_col entry of the same edge record, for every  */
+                                /* in_col entry; required with edge_rids when in_row_ptr is given      */
 } omx_edge_set_desc;
 
 typedef struct omx_property_desc {
@@ -107,6 +113,10 @@ typedef struct omx_graph_desc {
    * [part_lo, part_hi) only; classes, RIDs and properties stay replicated for all V vertices. Rank r of
    * a world of N owns [r·B, min(V, (r+1)·B)) with B = ⌈V/N⌉. part_lo = part_hi = 0: every row. */
   uint32_t part_lo, part_hi;
+  /* Properties of the edge records (edge sets with edge_rids): values indexed by edge id = the edge   */
+  /* sets' out_col entries one after the other (set 0's entries, then set 1's, ...), as given.         */
+  int32_t n_edge_properties;
+  const omx_property_desc *edge_properties;
 } omx_graph_desc;
 
 typedef struct omx_graph omx_graph;

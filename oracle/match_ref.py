@@ -123,10 +123,10 @@ class RefDB:
         self.by_class[cls].append(r)
         return r
 
-    def add_edge(self, cls, out_v, in_v):
+    def add_edge(self, cls, out_v, in_v, props=None):
         """Regular (heavyweight) edge: an edge record linked from out_<cls> of out_v and in_<cls> of in_v
-        (B/OrientVertex.java:109-180, createLink)."""
-        e = Record((self.classes[cls]["cluster"], len(self.by_class[cls])), cls, {}, is_edge=True)
+        (B/OrientVertex.java:109-180, createLink), with its own fields."""
+        e = Record((self.classes[cls]["cluster"], len(self.by_class[cls])), cls, dict(props or {}), is_edge=True)
         e.out_v, e.in_v = out_v, in_v
         self.records.append(e)
         self.by_class[cls].append(e)
@@ -145,7 +145,7 @@ class RefDB:
         for v in obj["vertices"]:
             db.add_vertex(v["class"], v["props"])
         for e in obj["edges"]:
-            db.add_edge(e["class"], db.vertices[e["out"]], db.vertices[e["in"]])
+            db.add_edge(e["class"], db.vertices[e["out"]], db.vertices[e["in"]], e.get("props"))
         for ix in obj.get("indexes", []):
             db.indexes.append((ix["class"], ix["property"], bool(ix["unique"])))
         return db

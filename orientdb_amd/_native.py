@@ -25,7 +25,8 @@ class omx_class_desc(C.Structure):
 class omx_edge_set_desc(C.Structure):
     _fields_ = [("edge_class", C.c_int32), ("n_edges", C.c_uint64),
                 ("out_row_ptr", C.POINTER(C.c_uint64)), ("out_col", C.POINTER(C.c_uint32)),
-                ("in_row_ptr", C.POINTER(C.c_uint64)), ("in_col", C.POINTER(C.c_uint32)), ("n_in_edges", C.c_uint64)]
+                ("in_row_ptr", C.POINTER(C.c_uint64)), ("in_col", C.POINTER(C.c_uint32)), ("n_in_edges", C.c_uint64),
+                ("edge_rids", C.POINTER(C.c_uint64)), ("in_edge_index", C.POINTER(C.c_uint64))]
 
 
 class omx_property_desc(C.Structure):
@@ -43,7 +44,8 @@ class omx_graph_desc(C.Structure):
                 ("n_edge_sets", C.c_int32), ("edge_sets", C.POINTER(omx_edge_set_desc)),
                 ("n_properties", C.c_int32), ("properties", C.POINTER(omx_property_desc)),
                 ("n_indexes", C.c_int32), ("indexes", C.POINTER(omx_index_desc)), ("device", C.c_int32),
-                ("part_lo", C.c_uint32), ("part_hi", C.c_uint32)]
+                ("part_lo", C.c_uint32), ("part_hi", C.c_uint32),
+                ("n_edge_properties", C.c_int32), ("edge_properties", C.POINTER(omx_property_desc))]
 
 
 class omx_value(C.Structure):

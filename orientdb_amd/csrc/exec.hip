@@ -1996,7 +1996,7 @@ class Executor {
   uint64_t marked_bindings_ = 0;
   bool mark_fuse_ = true;  // OMX_MARK_FUSE=0: write the rows and mark them in the projection
   bool mark_ok(const Step &st) const {
-    return mark_fuse_ && !dist_ && st.filter_bm < 0 && !st.optional && p_.kind == Plan::MATCH &&
+    return mark_fuse_ && !dist_ && st.filter_bm < 0 && !st.optional && p_.kind == Plan::MATCH && !g_.edge_records &&
            p_.proj == Plan::PROJ_ALIASES && !p_.unique_by_construction && p_.out_aliases.size() == 1 &&
            p_.out_aliases[0] == st.dst && !p_.optional[st.dst] && p_.limit < 0 && o_.limit < 0 &&
            o_.mode == OMX_MODE_MATERIALIZE;
@@ -2010,7 +2010,7 @@ class Executor {
   // factor_min_ratio_ — would have read Σ deg2 one row at a time; E_t and bindings are path-independent)
   bool fof2_ok() {
     if (!mark_fuse_ || !factor_ || dist_ || g_.partitioned() || p_.kind != Plan::MATCH || p_.steps.size() != 3 ||
-        g_.V > kFof2Bits || g_.V == 0)
+        g_.V > kFof2Bits || g_.V == 0 || g_.edge_records)
       return false;
     const Step &r = p_.steps[0], &h1 = p_.steps[1], &h2 = p_.steps[2];
     return r.kind == S_ROOT && r.cand_bm >= 0 && h1.kind == S_EXPAND && h2.kind == S_EXPAND && h1.src == r.dst && h2.src == h1.dst &&
@@ -2304,7 +2304,14 @@ class Executor {
                                            : alg);
   }
 
+  // an adjacency over edge records (the snapshot's record or endpoint sets, Graph::edge_records)
+  bool records_adj(const AdjSpec &a) const {
+    for (auto &p : a.parts)
+      if (g_.esets[p.first].pseudo) return true;
+    return false;
+  }
   bool expand_factorized(const Step &st, bool write, const std::vector<int> &cols) {
+    if (records_adj(st.adj)) return false;  // edge-record hops: the direct expansion
     const uint64_t R = R_;
     const uint32_t *src = col_[st.src].p;
     uint64_t U = 0, Et = 0, EU = 0;

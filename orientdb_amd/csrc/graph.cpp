@@ -1,6 +1,8 @@
 // graph.cpp — snapshot validation, host-side statistics and upload to HBM.
 #include "graph.h"
 
+#include <set>
+
 #include <algorithm>
 #include <atomic>
 #include <memory>
@@ -341,7 +343,7 @@ static T *upload(const T *h, size_t n, uint64_t &acc) {
 
 extern "C" int omx_csr_transpose(uint32_t, const uint64_t *, const uint32_t *, uint64_t **, uint32_t **);
 
-Graph *graph_create(const omx_graph_desc *d) {
+static Graph *create_snapshot(const omx_graph_desc *d) {
   if (!d) fail(OMX_E_INVALID, "null graph descriptor");
   if (d->n_classes <= 0 || d->n_classes > 256) fail(OMX_E_INVALID, "n_classes must be in [1, 256]");
   if (d->n_vertices > 0 && (!d->vertex_class || !d->rids)) fail(OMX_E_INVALID, "vertex_class and rids required");
@@ -509,6 +511,219 @@ Graph *graph_create(const omx_graph_desc *d) {
     omx_host_free(t.own_col);
   }
   return g.release();
+}
+
+namespace {
+// property values of one record kind, widened to the merged column (codes of a string remapped)
+void merge_prop(const omx_property_desc *pd, uint64_t n, uint64_t at, size_t w, const std::vector<std::string> &dict,
+                std::vector<uint8_t> &vals, std::vector<uint8_t> &pres) {
+  if (!pd) return;
+  std::vector<int32_t> remap;
+  if (pd->type == OMX_PROP_STRING)
+    for (int k = 0; k < pd->dict_size; ++k)
+      remap.push_back((int32_t)(std::lower_bound(dict.begin(), dict.end(), std::string(pd->dict[k])) - dict.begin()));
+  for (uint64_t i = 0; i < n; ++i) {
+    pres[at + i] = pd->present ? pd->present[i] : 1;
+    if (!remap.empty()) {
+      int32_t c = ((const int32_t *)pd->values)[i];
+      if (pres[at + i] && (c < 0 || c >= (int32_t)remap.size())) fail(OMX_E_INVALID, std::string("string code out of range in ") + pd->name);
+      c = pres[at + i] ? remap[c] : 0;
+      std::memcpy(vals.data() + (at + i) * w, &c, 4);
+    } else {
+      std::memcpy(vals.data() + (at + i) * w, (const uint8_t *)pd->values + i * w, w);
+    }
+  }
+}
+}  // namespace
+
+// Edge records (every edge set given with edge_rids): one id space of records — the vertices [0, V), then
+// the edge records [V, V + E) (set 0's out entries in the given order, then set 1's, ...) — so a MATCH
+// edge node binds a record id like any alias (classes, RIDs and fields are per record, as ODocument's).
+// Per edge class a second set holds its records' ids (outE()/inE() as CSRs), and one set the records'
+// endpoints (outV()/inV()); vertex rows of those are the records' ridbags, edge rows of the vertex sets
+// are empty (out()/in() of an edge record yields nothing, GF/OSQLFunctionMove.java:66-91).
+Graph *graph_create(const omx_graph_desc *d) {
+  if (!d) fail(OMX_E_INVALID, "null graph descriptor");
+  bool erec = d->n_edge_sets > 0;
+  for (int i = 0; i < d->n_edge_sets; ++i) erec = erec && d->edge_sets[i].edge_rids != nullptr;
+  if (!erec) {
+    Graph *g = create_snapshot(d);
+    g->vertices = g->V;
+    for (auto &p : g->props) p.nulls_v = p.has_nulls;
+    return g;
+  }
+  if (!(d->part_lo == 0 && (d->part_hi == 0 || d->part_hi == d->n_vertices)))
+    fail(OMX_E_INVALID, "edge records (edge_rids) on a partitioned snapshot");
+  if (d->n_vertices > 0 && (!d->vertex_class || !d->rids)) fail(OMX_E_INVALID, "vertex_class and rids required");
+  const uint64_t V = d->n_vertices;
+  const int ns = d->n_edge_sets;
+  std::vector<uint64_t> base(ns + 1, 0);
+  for (int i = 0; i < ns; ++i) {
+    const omx_edge_set_desc &ed = d->edge_sets[i];
+    if (!ed.out_row_ptr || (ed.n_edges && !ed.out_col)) fail(OMX_E_INVALID, "edge set without an out CSR");
+    if (ed.out_row_ptr[0] != 0 || ed.out_row_ptr[V] != ed.n_edges) fail(OMX_E_INVALID, "out_row_ptr inconsistent");
+    if (ed.edge_class < 0 || ed.edge_class >= d->n_classes) fail(OMX_E_INVALID, "bad edge class index");
+    base[i + 1] = base[i] + ed.n_edges;
+  }
+  const uint64_t E = base[ns], N = V + E;
+  if (N >= 0xFFFFFFFFull) fail(OMX_E_INVALID, "2^32 - 1 or more vertex and edge records");
+  // records: class and RID
+  std::vector<uint16_t> vclass(N);
+  std::vector<uint64_t> rids(N);
+  std::copy(d->vertex_class, d->vertex_class + V, vclass.begin());
+  std::copy(d->rids, d->rids + V, rids.begin());
+  std::vector<uint32_t> head(E), tail(E);
+  for (int i = 0; i < ns; ++i) {
+    const omx_edge_set_desc &ed = d->edge_sets[i];
+    for (uint64_t o = 0; o < ed.n_edges; ++o) {
+      vclass[V + base[i] + o] = (uint16_t)ed.edge_class;
+      rids[V + base[i] + o] = ed.edge_rids[o];
+    }
+    for (uint64_t u = 0; u < V; ++u)
+      for (uint64_t o = ed.out_row_ptr[u]; o < ed.out_row_ptr[u + 1]; ++o) {
+        if (ed.out_col[o] >= V) fail(OMX_E_INVALID, "out_col entry out of range");
+        tail[base[i] + o] = (uint32_t)u;
+        head[base[i] + o] = ed.out_col[o];
+      }
+  }
+  // fields: one column per name over every record (absent where the record kind lacks it)
+  struct MP {
+    std::string name;
+    int type;
+    const omx_property_desc *v = nullptr, *e = nullptr;
+    std::vector<std::string> dict;
+    std::vector<uint8_t> vals, pres;
+    std::vector<const char *> dict_p;
+  };
+  std::vector<MP> mps;
+  auto find = [&](const std::string &n) -> MP * {
+    for (auto &m : mps)
+      if (m.name == n) return &m;
+    return nullptr;
+  };
+  for (int k = 0; k < d->n_properties; ++k) {
+    const omx_property_desc &pd = d->properties[k];
+    mps.push_back(MP{pd.name ? pd.name : "", pd.type});
+    mps.back().v = &pd;
+  }
+  for (int k = 0; k < d->n_edge_properties; ++k) {
+    const omx_property_desc &pd = d->edge_properties[k];
+    const std::string n = pd.name ? pd.name : "";
+    MP *m = find(n);
+    if (!m) {
+      mps.push_back(MP{n, pd.type});
+      m = &mps.back();
+    } else if (m->type != pd.type) {
+      fail(OMX_E_INVALID, "field " + n + " has different types on vertices and edges");
+    }
+    m->e = &pd;
+  }
+  for (auto &m : mps) {
+    if (m.type < OMX_PROP_INT32 || m.type > OMX_PROP_BOOL) fail(OMX_E_INVALID, "bad property type for " + m.name);
+    const size_t w = (m.type == OMX_PROP_INT64 || m.type == OMX_PROP_DOUBLE) ? 8 : 4;
+    if (m.type == OMX_PROP_STRING) {
+      std::set<std::string> all;
+      for (const omx_property_desc *pd : {m.v, m.e})
+        if (pd)
+          for (int k = 0; k < pd->dict_size; ++k) all.insert(pd->dict[k]);
+      m.dict.assign(all.begin(), all.end());
+      for (auto &x : m.dict) m.dict_p.push_back(x.c_str());
+    }
+    m.vals.assign(std::max<size_t>(1, N * w), 0);
+    m.pres.assign(N, 0);
+    merge_prop(m.v, V, 0, w, m.dict, m.vals, m.pres);
+    if (m.e) {
+      merge_prop(m.e, E, V, w, m.dict, m.vals, m.pres);
+    }
+  }
+  std::vector<omx_property_desc> props;
+  for (auto &m : mps)
+    props.push_back(omx_property_desc{m.name.c_str(), m.type, m.vals.data(), m.pres.data(), (int32_t)m.dict.size(),
+                                      m.dict_p.empty() ? nullptr : m.dict_p.data()});
+  // edge sets: the classes' adjacency over N rows, their records, the endpoints
+  std::vector<std::vector<uint64_t>> rps;
+  std::vector<std::vector<uint32_t>> cols;
+  auto ext = [&](const uint64_t *rp) {  // V + 1 row pointers → N + 1 (edge rows empty)
+    rps.emplace_back(N + 1);
+    std::copy(rp, rp + V + 1, rps.back().begin());
+    std::fill(rps.back().begin() + V + 1, rps.back().end(), rp[V]);
+    return rps.back().data();
+  };
+  std::vector<omx_edge_set_desc> sets(2 * ns + 1);
+  for (int i = 0; i < ns; ++i) {
+    const omx_edge_set_desc &ed = d->edge_sets[i];
+    omx_edge_set_desc &a = sets[i], &r = sets[ns + i];
+    a = omx_edge_set_desc{};
+    a.edge_class = r.edge_class = ed.edge_class;
+    a.n_edges = r.n_edges = ed.n_edges;
+    a.out_row_ptr = r.out_row_ptr = ext(ed.out_row_ptr);
+    a.out_col = ed.out_col;
+    cols.emplace_back(ed.n_edges);
+    for (uint64_t o = 0; o < ed.n_edges; ++o) cols.back()[o] = (uint32_t)(V + base[i] + o);
+    r.out_col = cols.back().data();
+    if (ed.in_row_ptr && ed.in_col) {
+      if (!ed.in_edge_index) fail(OMX_E_INVALID, "in_edge_index is required with edge_rids and an in CSR");
+      const uint64_t ni = ed.n_in_edges ? ed.n_in_edges : ed.n_edges;
+      if (ni != ed.n_edges || ed.in_row_ptr[0] != 0 || ed.in_row_ptr[V] != ni) fail(OMX_E_INVALID, "in_row_ptr inconsistent");
+      a.in_row_ptr = r.in_row_ptr = ext(ed.in_row_ptr);
+      a.in_col = ed.in_col;
+      a.n_in_edges = r.n_in_edges = ni;
+      cols.emplace_back(ni);
+      for (uint64_t q = 0; q < ni; ++q) {
+        const uint64_t o = ed.in_edge_index[q];
+        if (o >= ed.n_edges) fail(OMX_E_INVALID, "in_edge_index out of range");
+        cols.back()[q] = (uint32_t)(V + base[i] + o);
+      }
+      r.in_col = cols.back().data();
+    } else {
+      // the transpose of the records: an in row lists its edges in out order
+      rps.emplace_back(N + 1, 0);
+      std::vector<uint64_t> &irp = rps.back();
+      for (uint64_t o = 0; o < ed.n_edges; ++o) irp[ed.out_col[o] + 1]++;
+      for (uint64_t v = 0; v < N; ++v) irp[v + 1] += irp[v];
+      std::vector<uint64_t> cur(irp.begin(), irp.end() - 1);
+      cols.emplace_back(ed.n_edges);
+      std::vector<uint32_t> &ic = cols.back();
+      for (uint64_t o = 0; o < ed.n_edges; ++o) ic[cur[ed.out_col[o]]++] = (uint32_t)(V + base[i] + o);
+      r.in_row_ptr = irp.data();
+      r.in_col = ic.data();
+      r.n_in_edges = ed.n_edges;
+    }
+  }
+  {
+    omx_edge_set_desc &q = sets[2 * ns];
+    q = omx_edge_set_desc{};
+    q.edge_class = d->edge_sets[0].edge_class;
+    q.n_edges = q.n_in_edges = E;
+    rps.emplace_back(N + 1, 0);
+    for (uint64_t k = 0; k < E; ++k) rps.back()[V + k + 1] = k + 1;
+    q.out_row_ptr = q.in_row_ptr = rps.back().data();
+    q.out_col = tail.data();
+    q.in_col = head.data();
+  }
+  omx_graph_desc nd = *d;
+  nd.n_vertices = (uint32_t)N;
+  nd.vertex_class = vclass.data();
+  nd.rids = rids.data();
+  nd.n_edge_sets = (int32_t)sets.size();
+  nd.edge_sets = sets.data();
+  nd.n_properties = (int32_t)props.size();
+  nd.properties = props.data();
+  nd.part_lo = nd.part_hi = 0;
+  nd.n_edge_properties = 0;
+  nd.edge_properties = nullptr;
+  Graph *g = create_snapshot(&nd);
+  g->vertices = (uint32_t)V;
+  g->edge_records = true;
+  for (size_t k = 0; k < mps.size(); ++k) {
+    const std::vector<uint8_t> &pr = mps[k].pres;
+    Property &p = g->props[k];
+    p.nulls_v = std::find(pr.begin(), pr.begin() + V, 0) != pr.begin() + V;
+    p.nulls_e = std::find(pr.begin() + V, pr.end(), 0) != pr.end();
+  }
+  for (int i = 0; i < ns; ++i) g->esets[ns + i].pseudo = 1;
+  g->esets[2 * ns].pseudo = 2;
+  return g;
 }
 
 }  // namespace omx

@@ -99,6 +99,10 @@ struct ClassInfo {
 
 struct EdgeSet {
   int cls = -1;
+  // 0: an edge class's adjacency (vertex → vertex). Snapshots with edge records (Graph::edge_records) add
+  // 1: that class's edge records (out: vertex → the ids of its out-edges, in: vertex → its in-edges) and
+  // 2 (one set): every record's endpoints (out: edge → its out-vertex, outV(); in: edge → its in-vertex, inV())
+  int pseudo = 0;
   uint64_t n_edges = 0;     // out CSR edges (of the owned rows)
   uint64_t n_in_edges = 0;  // in CSR edges (of the owned rows)
   bool out_sorted = true, in_sorted = true;  // rows ascending
@@ -152,6 +156,8 @@ struct Property {
   int type = 0;
   std::vector<std::string> dict;        // strings, sorted
   bool has_nulls = false;
+  // absent on some vertex / some edge record (edge_records: a vertex field is absent on every edge)
+  bool nulls_v = false, nulls_e = false;
   void *d_values = nullptr;
   uint8_t *d_present = nullptr;
   // host copy kept only for indexed properties (root estimation, OWhereClause.estimate)
@@ -168,7 +174,9 @@ struct IndexInfo {
 
 struct Graph {
   uint64_t uid = 0;  // process-unique id (plan caches key on it, not on the address)
-  uint32_t V = 0;
+  uint32_t V = 0;  // records: vertices, then (edge_records) the edge records, ids [vertices, V)
+  uint32_t vertices = 0;
+  bool edge_records = false;
   int device = -1;
   // 1-D partition: the CSR rows held are those of [part_lo, part_hi) (local row pointers); the
   // device row-pointer arrays are addressed with a global vertex id through rp(): base − part_lo

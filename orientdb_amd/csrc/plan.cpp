@@ -79,13 +79,15 @@ class Planner {
     exprs_ = st_.expressions;  // private copy: default aliases / rebound filters are assigned here
     assign_default_aliases();
     // the logical plan (explain) keeps the reference's edge nodes; the device plan fuses them
-    if (!logical_only) fuse_edge_items();
+    // (with edge records, $paths / $pathElements read the edge nodes: those are kept)
+    if (!logical_only && !(g_.edge_records && (returns_has("$paths") || returns_has("$pathElements")))) fuse_edge_items();
     for (auto &e : exprs_) add_expression(e);
     for (auto &e : exprs_) {
       add_aliases(e.origin);
       for (auto &it : e.items) add_aliases(it.filter);
     }
     validate();
+    if (!logical_only) type_nodes();
     for (auto &n : nodes_) {
       plan_->aliases.push_back(n.alias);
       plan_->explicit_alias.push_back(n.alias.rfind(kDefaultPrefix, 0) != 0);
@@ -322,6 +324,55 @@ class Planner {
         items.push_back(a);
       }
       e.items.swap(items);
+    }
+  }
+  bool returns_has(const char *name) const {
+    for (auto &r : st_.returns)
+      if (ieq(r.text, name)) return true;
+    return false;
+  }
+  // the record kind each pattern node binds (OSQLFunctionMove: out/in/both and outE/inE/bothE start at a
+  // vertex, outV/inV/bothV at an edge record; GF/OSQLFunctionMove.java:66-144): a node reached both ways,
+  // or whose class is of the other kind, matches no record in the reference; the device leaves it to the
+  // reference engine
+  std::vector<char> edge_node_;  // per node: 1 = binds edge records
+  void type_nodes() {
+    std::vector<int> kind(nodes_.size(), 0);  // 0 unknown, 1 vertex, 2 edge
+    auto set = [&](int n, int k) {
+      if (kind[n] && kind[n] != k)
+        unsupported("pattern node " + nodes_[n].alias + " reached both as a vertex and as an edge record");
+      kind[n] = k;
+    };
+    for (auto &e : edges_) {
+      const PathItem &it = *e.item;
+      const std::string m = it.is_multi ? std::string() : lower(it.method);
+      if (m == "oute" || m == "ine" || m == "bothe") {
+        set(e.out, 1);
+        set(e.in, 2);
+      } else if (m == "outv" || m == "inv" || m == "bothv") {
+        set(e.out, 2);
+        set(e.in, 1);
+      } else {
+        set(e.out, 1);
+        set(e.in, 1);
+      }
+    }
+    edge_node_.assign(nodes_.size(), 0);
+    for (size_t n = 0; n < nodes_.size(); ++n) {
+      auto c = alias_class_.find(nodes_[n].alias);
+      if (c != alias_class_.end()) {
+        const int ci = g_.class_id(c->second);
+        if (ci >= 0) {
+          const int k = g_.classes[ci].is_edge ? 2 : 1;
+          if (kind[n] && kind[n] != k)
+            unsupported("pattern node " + nodes_[n].alias + " of class " + c->second + " reached as a" +
+                        (kind[n] == 2 ? "n edge record" : " vertex"));
+          kind[n] = k;
+        }
+      }
+      edge_node_[n] = kind[n] == 2;
+      if (edge_node_[n] && !g_.edge_records)
+        unsupported("edge node " + nodes_[n].alias + " on a snapshot without edge records (lightweight edges)");
     }
   }
   int node(const MatchFilter &f) {
@@ -692,8 +743,23 @@ class Planner {
     return C_NUL;
   }
 
-  AdjSpec adjacency(const std::string &method_in, const std::vector<std::string> &labels_in) const {
+  // records: the edge methods bind edge records (outE/inE/bothE → the record sets, outV/inV/bothV → the
+  // endpoints set; Graph::edge_records); otherwise outE/inE/bothE stand for their vertices' adjacency (a
+  // fused pair, a degree)
+  AdjSpec adjacency(const std::string &method_in, const std::vector<std::string> &labels_in, bool records = false) const {
     std::string m = lower(method_in);
+    if (records && (m == "outv" || m == "inv" || m == "bothv")) {
+      AdjSpec a;
+      for (size_t i = 0; i < g_.esets.size(); ++i)
+        if (g_.esets[i].pseudo == 2) {
+          if (m != "inv") a.parts.emplace_back((int)i, 0);
+          if (m != "outv") a.parts.emplace_back((int)i, 1);
+        }
+      a.sorted = true;
+      a.dup_free = a.parts.size() == 1;
+      return a;
+    }
+    const int want = records && (m == "oute" || m == "ine" || m == "bothe") ? 1 : 0;
     if (m == "oute") m = "out";
     else if (m == "ine") m = "in";
     else if (m == "bothe") m = "both";
@@ -704,7 +770,7 @@ class Planner {
     std::vector<int> classes;
     if (labels.empty()) {
       for (auto &es : g_.esets)
-        if (std::find(classes.begin(), classes.end(), es.cls) == classes.end()) classes.push_back(es.cls);
+        if (!es.pseudo && std::find(classes.begin(), classes.end(), es.cls) == classes.end()) classes.push_back(es.cls);
     } else {
       for (auto &l : labels) {
         int c = g_.class_id(l);
@@ -716,7 +782,7 @@ class Planner {
     AdjSpec a;
     for (int c : classes)
       for (size_t i = 0; i < g_.esets.size(); ++i) {
-        if (g_.esets[i].cls != c) continue;
+        if (g_.esets[i].cls != c || g_.esets[i].pseudo != want) continue;
         if (m == "out" || m == "both") a.parts.emplace_back((int)i, 0);
         if (m == "in" || m == "both") a.parts.emplace_back((int)i, 1);
       }
@@ -784,6 +850,9 @@ class Planner {
     }
   }
 
+  // the records a predicate is compiled for: edge records (an edge node's WHERE) or vertices
+  bool pred_edges_ = false;
+  bool prop_nulls(int p) const { return pred_edges_ ? g_.props[p].nulls_e : g_.props[p].nulls_v; }
   // can the value be null for some vertex of the snapshot (a property with absent values, a field no
   // vertex has, arithmetic over either)
   bool may_be_null(const ExprP &e) const {
@@ -791,7 +860,7 @@ class Planner {
     switch (e->kind) {
       case Expr::FIELD: {
         const int p = g_.prop_id(e->name);
-        return p < 0 || g_.props[p].has_nulls;
+        return p < 0 || prop_nulls(p);
       }
       case Expr::MATH: return may_be_null(e->kids[0]) || may_be_null(e->kids[1]);
       default: return false;  // $depth, out()/in()/both().size()
@@ -808,7 +877,7 @@ class Planner {
 
   bool string_may_be_null(const ExprP &e) const {
     int p;
-    return string_field(e, &p) && g_.props[p].has_nulls;
+    return string_field(e, &p) && prop_nulls(p);
   }
 
   bool string_field(const ExprP &e, int *prop) const {
@@ -896,14 +965,14 @@ class Planner {
           return;
         }
         if (string_field(L, &prop) && fr && fr->kind == Value::STR) {
-          if ((op == ">" || op == ">=" || op == "<=") && g_.props[prop].has_nulls)
+          if ((op == ">" || op == ">=" || op == "<=") && prop_nulls(prop))
             unsupported("a possibly-null left operand of " + op + " (NullPointerException in the reference): " + expr_text(L));
           return emit_string_cmp(b, prop, op, fr->s);
         }
         const bool ordering = op == "<" || op == "<=" || op == ">" || op == ">=";
         if (string_field(R, &prop) && fl && fl->kind == Value::STR) {
           // a constant left operand: a null right one is the reference's NPE for every ordering operator
-          if (ordering && g_.props[prop].has_nulls)
+          if (ordering && prop_nulls(prop))
             unsupported("a possibly-null right operand of " + op + " (NullPointerException in the reference): " + expr_text(R));
           return emit_string_cmp(b, prop, flip(op), fl->s);
         }
@@ -971,7 +1040,10 @@ class Planner {
     BitmapSpec s;
     if (kind == 1 && has_row_conds(alias))
       unsupported("$matched in the WHERE of a root, prefetched or cartesian alias (" + alias + ")");
+    auto ai = alias_idx_.find(alias);
+    pred_edges_ = ai != alias_idx_.end() && (size_t)ai->second < edge_node_.size() && edge_node_[ai->second];
     s.prog = add_prog(vertex_where_of(alias), false);
+    pred_edges_ = false;
     if (kind == 1) {
       auto c = alias_class_.find(alias);
       if (c == alias_class_.end()) fail(OMX_E_EXECUTION, "Cannot execute MATCH statement on alias " + alias + ": class not defined");
@@ -1037,8 +1109,10 @@ class Planner {
         st.where_bm = bitmap(nodes_[t].alias, 0);
       }
       std::string m = lower(it.method);
-      if (!it.is_multi && m != "out" && m != "in" && m != "both")
+      const bool erec = m == "oute" || m == "ine" || m == "bothe" || m == "outv" || m == "inv" || m == "bothv";
+      if (!it.is_multi && m != "out" && m != "in" && m != "both" && !(erec && g_.edge_records))
         unsupported("traversal method " + it.method + "() on the device");
+      if (erec && varlen) unsupported("a variable-length item over edge records (" + it.method + "())");
       std::vector<std::pair<std::string, bool>> rconds;
       vertex_where_of(nodes_[t].alias, &rconds);
       if (!rconds.empty()) {
@@ -1070,8 +1144,17 @@ class Planner {
         st.max_depth = it.filter.max_depth;
         if (st.mode == T_CAND) st.cand_bm = bitmap(nodes_[t].alias, 1);
       } else {
-        std::string rm = fwd ? m : (m == "out" ? "in" : m == "in" ? "out" : "both");  // executeReverse
-        st.adj = adjacency(rm, it.labels);
+        // executeReverse (P/OMethodCall.java:92-126): outE ↔ outV, inE ↔ inV
+        static const std::map<std::string, std::string> kRev = {{"out", "in"}, {"in", "out"}, {"both", "both"},
+                                                                {"oute", "outv"}, {"outv", "oute"},
+                                                                {"ine", "inv"}, {"inv", "ine"}};
+        std::string rm = m;
+        if (!fwd) {
+          auto r = kRev.find(m);
+          if (r == kRev.end()) unsupported("a reversed " + it.method + "() item");
+          rm = r->second;
+        }
+        st.adj = adjacency(rm, it.labels, erec);
         if (st.mode == T_BOUND) {
           st.kind = S_CHECK;
           st.filter_bm = fwd ? bitmap(nodes_[t].alias, 0) : -1;
@@ -1184,6 +1267,12 @@ class Planner {
       case Expr::CALL: unsupported("function call " + e->name + "() in a RETURN expression");
       case Expr::CHAIN:
         check_return(e->kids[0], refs);
+        if (e->kids[0]->kind == Expr::FIELD && !e->suffixes.empty() && e->suffixes[0].kind == Suffix::FIELD &&
+            (e->suffixes[0].name == "out" || e->suffixes[0].name == "in")) {
+          auto ai = alias_idx_.find(e->kids[0]->name);
+          if (ai != alias_idx_.end() && edge_node_.size() > (size_t)ai->second && edge_node_[ai->second])
+            unsupported("the " + e->suffixes[0].name + " link of an edge record in a RETURN expression");
+        }
         for (size_t si = 0; si < e->suffixes.size(); ++si) {
           const Suffix &s = e->suffixes[si];
           if (s.kind == Suffix::METHOD) {

@@ -30,12 +30,15 @@ def _ptr(a, ctype):
 
 class GraphSnapshot:
     """One omx_graph. `classes` = list of (name, superclass index or -1, is_edge, cluster id);
-    `edge_sets` = list of dicts {cls, out_rp, out_col[, in_rp, in_col]} (numpy u64/u32);
+    `edge_sets` = list of dicts {cls, out_rp, out_col[, in_rp, in_col][, edge_rids[, in_edge_index]]} (numpy
+    u64/u32; edge_rids: the edge records behind the out entries, on every set or none);
     `properties` = list of dicts {name, type, values[, present][, dict]};
-    `indexes` = list of (class index, property name, unique)."""
+    `indexes` = list of (class index, property name, unique);
+    `edge_properties` = fields of the edge records (as `properties`, indexed by the sets' out entries one
+    after another)."""
 
     def __init__(self, n_vertices, classes, vertex_class, rids, edge_sets, properties=(), indexes=(), device=0,
-                 part=None):
+                 part=None, edge_properties=()):
         """part = (lo, hi): a 1-D partition holding the CSR rows of vertices [lo, hi) only (local row
         pointers of hi − lo + 1 entries; the in CSR is required); see include/omx/match.h."""
         L = N.lib()
@@ -59,24 +62,17 @@ class GraphSnapshot:
             icol = es.get("in_col")
             irp = None if irp is None else np.ascontiguousarray(irp, dtype=np.uint64)
             icol = None if icol is None else np.ascontiguousarray(icol, dtype=np.uint32)
-            keep += [orp, ocol, irp, icol]
+            erid = es.get("edge_rids")
+            erid = None if erid is None else np.ascontiguousarray(erid, dtype=np.uint64)
+            eix = es.get("in_edge_index")
+            eix = None if eix is None else np.ascontiguousarray(eix, dtype=np.uint64)
+            keep += [orp, ocol, irp, icol, erid, eix]
             es_arr[i] = N.omx_edge_set_desc(es["cls"], int(orp[-1]), _ptr(orp, C.c_uint64), _ptr(ocol, C.c_uint32),
                                             _ptr(irp, C.c_uint64), _ptr(icol, C.c_uint32),
-                                            int(irp[-1]) if irp is not None else 0)
-        pr_arr = (N.omx_property_desc * max(1, len(properties)))()
-        for i, p in enumerate(properties):
-            t = p["type"]
-            dt = {N.OMX_PROP_INT32: np.int32, N.OMX_PROP_INT64: np.int64, N.OMX_PROP_DOUBLE: np.float64,
-                  N.OMX_PROP_STRING: np.int32, N.OMX_PROP_BOOL: np.int32}[t]
-            vals = np.ascontiguousarray(p["values"], dtype=dt)
-            pres = p.get("present")
-            pres = None if pres is None else np.ascontiguousarray(pres, dtype=np.uint8)
-            d = p.get("dict") or []
-            dict_arr = (C.c_char_p * max(1, len(d)))(*[s.encode() for s in d]) if d else None
-            nb = p["name"].encode()
-            keep += [vals, pres, dict_arr, nb]
-            pr_arr[i] = N.omx_property_desc(nb, t, vals.ctypes.data_as(C.c_void_p), _ptr(pres, C.c_uint8),
-                                            len(d), C.cast(dict_arr, C.POINTER(C.c_char_p)) if dict_arr else None)
+                                            int(irp[-1]) if irp is not None else 0, _ptr(erid, C.c_uint64),
+                                            _ptr(eix, C.c_uint64))
+        pr_arr = _property_array(properties, keep)
+        epr_arr = _property_array(edge_properties, keep)
         ix_arr = (N.omx_index_desc * max(1, len(indexes)))()
         for i, (ci, prop, unique) in enumerate(indexes):
             b = prop.encode()
@@ -85,7 +81,8 @@ class GraphSnapshot:
         self.part = (0, self.V) if part is None else (int(part[0]), int(part[1]))
         desc = N.omx_graph_desc(self.V, len(self.classes), cls_arr, _ptr(self.vertex_class, C.c_uint16),
                                 _ptr(self.rids, C.c_uint64), len(edge_sets), es_arr, len(properties), pr_arr,
-                                len(indexes), ix_arr, device, *((0, 0) if part is None else self.part))
+                                len(indexes), ix_arr, device, *((0, 0) if part is None else self.part),
+                                len(edge_properties), epr_arr)
         h = C.c_void_p()
         N.check(L.omx_graph_create(C.byref(desc), C.byref(h)))
         self._h = h
@@ -131,10 +128,13 @@ class GraphSnapshot:
         return g
 
     @classmethod
-    def from_records(cls, db, device=0):
+    def from_records(cls, db, device=0, edge_records=False):
         """Snapshot of a record-level description (the JSON of tests/golden/make_match_test_db.py):
-        classes in creation order, one cluster per class (ids from 11), vertices in insertion order."""
-        g = cls(*records_arrays(db), device)
+        classes in creation order, one cluster per class (ids from 11), vertices in insertion order.
+        edge_records: the edges as records (RID #cluster:rank within the class, fields from each edge's
+        "props"), so MATCH can bind edge nodes; otherwise lightweight adjacency."""
+        a = records_arrays(db, edge_records)
+        g = cls(*a[:7], device, None, a[7] if edge_records else ())
         g.records = db
         return g
 
@@ -195,9 +195,57 @@ class GraphSnapshot:
 
 
 
-def records_arrays(db):
+def _property_array(properties, keep):
+    arr = (N.omx_property_desc * max(1, len(properties)))()
+    for i, p in enumerate(properties):
+        t = p["type"]
+        dt = {N.OMX_PROP_INT32: np.int32, N.OMX_PROP_INT64: np.int64, N.OMX_PROP_DOUBLE: np.float64,
+              N.OMX_PROP_STRING: np.int32, N.OMX_PROP_BOOL: np.int32}[t]
+        vals = np.ascontiguousarray(p["values"], dtype=dt)
+        pres = p.get("present")
+        pres = None if pres is None else np.ascontiguousarray(pres, dtype=np.uint8)
+        d = p.get("dict") or []
+        dict_arr = (C.c_char_p * max(1, len(d)))(*[s.encode() for s in d]) if d else None
+        nb = p["name"].encode()
+        keep += [vals, pres, dict_arr, nb]
+        arr[i] = N.omx_property_desc(nb, t, vals.ctypes.data_as(C.c_void_p), _ptr(pres, C.c_uint8),
+                                     len(d), C.cast(dict_arr, C.POINTER(C.c_char_p)) if dict_arr else None)
+    return arr
+
+
+def _columns(recs):
+    """One property column per field name over the records' "props" dicts (absent → not present)."""
+    fields = []
+    for rec in recs:
+        for k in rec.get("props", {}):
+            if k not in fields:
+                fields.append(k)
+    props = []
+    for f in fields:
+        vals = [rec.get("props", {}).get(f) for rec in recs]
+        present = np.array([x is not None for x in vals], np.uint8)
+        nonnull = [x for x in vals if x is not None]
+        if all(isinstance(x, str) for x in nonnull):
+            d = sorted(set(nonnull), key=lambda s: s.encode())
+            code = {s: i for i, s in enumerate(d)}
+            col = np.array([code[x] if x is not None else -1 for x in vals], np.int32)
+            props.append({"name": f, "type": N.OMX_PROP_STRING, "values": col, "present": present, "dict": d})
+        elif all(isinstance(x, bool) for x in nonnull):
+            col = np.array([int(x) if x is not None else 0 for x in vals], np.int32)
+            props.append({"name": f, "type": N.OMX_PROP_BOOL, "values": col, "present": present})
+        elif all(isinstance(x, int) and not isinstance(x, bool) for x in nonnull):
+            col = np.array([x if x is not None else 0 for x in vals], np.int64)
+            props.append({"name": f, "type": N.OMX_PROP_INT64, "values": col, "present": present})
+        else:
+            col = np.array([float(x) if x is not None else 0.0 for x in vals], np.float64)
+            props.append({"name": f, "type": N.OMX_PROP_DOUBLE, "values": col, "present": present})
+    return props
+
+
+def records_arrays(db, edge_records=False):
     """(V, classes, vertex_class, rids, edge_sets, properties, indexes) of a record-level description
-    (GraphSnapshot.from_records)."""
+    (GraphSnapshot.from_records); edge_records: + the edge records (edge_rids per set) and an 8th item,
+    the edge records' property columns."""
     if isinstance(db, str):
         with open(db) as f:
             db = json.load(f)
@@ -218,45 +266,28 @@ def records_arrays(db):
         rids[v] = pack_rid(classes[ci][3], pos)
     # adjacency: one CSR per edge class, rows in insertion order (ridbag order)
     edge_sets = []
-    for ci, (name, _, is_edge, _) in enumerate(classes):
+    edge_recs = []  # the edge records in edge-id order (the sets' out entries one after another)
+    for ci, (name, _, is_edge, cluster) in enumerate(classes):
         if not is_edge:
             continue
-        es = [(e["out"], e["in"]) for e in db["edges"] if e["class"] == name]
-        if not es:
+        recs = [e for e in db["edges"] if e["class"] == name]  # rank within the class = RID position
+        if not recs:
             continue
-        src = np.array([a for a, _ in es], np.int64)
-        dst = np.array([b for _, b in es], np.uint32)
+        src = np.array([e["out"] for e in recs], np.int64)
+        dst = np.array([e["in"] for e in recs], np.uint32)
         order = np.argsort(src, kind="stable")
         rp = np.zeros(V + 1, np.uint64)
         np.add.at(rp, src + 1, 1)
         rp = np.cumsum(rp).astype(np.uint64)
-        edge_sets.append({"cls": ci, "out_rp": rp, "out_col": dst[order]})
-    # properties: one column per field name over all vertices
-    fields = []
-    for rec in db["vertices"]:
-        for k in rec["props"]:
-            if k not in fields:
-                fields.append(k)
-    props = []
-    for f in fields:
-        vals = [rec["props"].get(f) for rec in db["vertices"]]
-        present = np.array([x is not None for x in vals], np.uint8)
-        nonnull = [x for x in vals if x is not None]
-        if all(isinstance(x, str) for x in nonnull):
-            d = sorted(set(nonnull), key=lambda s: s.encode())
-            code = {s: i for i, s in enumerate(d)}
-            col = np.array([code[x] if x is not None else -1 for x in vals], np.int32)
-            props.append({"name": f, "type": N.OMX_PROP_STRING, "values": col, "present": present, "dict": d})
-        elif all(isinstance(x, bool) for x in nonnull):
-            col = np.array([int(x) if x is not None else 0 for x in vals], np.int32)
-            props.append({"name": f, "type": N.OMX_PROP_BOOL, "values": col, "present": present})
-        elif all(isinstance(x, int) and not isinstance(x, bool) for x in nonnull):
-            col = np.array([x if x is not None else 0 for x in vals], np.int64)
-            props.append({"name": f, "type": N.OMX_PROP_INT64, "values": col, "present": present})
-        else:
-            col = np.array([float(x) if x is not None else 0.0 for x in vals], np.float64)
-            props.append({"name": f, "type": N.OMX_PROP_DOUBLE, "values": col, "present": present})
+        es = {"cls": ci, "out_rp": rp, "out_col": dst[order]}
+        if edge_records:
+            es["edge_rids"] = (np.uint64(cluster) << np.uint64(RID_POS_BITS)) | order.astype(np.uint64)
+            edge_recs += [recs[k] for k in order]
+        edge_sets.append(es)
+    props = _columns(db["vertices"])
     indexes = [(names.index(ix["class"]), ix["property"], bool(ix["unique"])) for ix in db.get("indexes", [])]
+    if edge_records:
+        return V, classes, vclass, rids, edge_sets, props, indexes, _columns(edge_recs)
     return V, classes, vclass, rids, edge_sets, props, indexes
 
 
