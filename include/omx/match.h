@@ -272,7 +272,7 @@ const char *omx_version(void);
  * start of the buffer (0 = none). Arrays are naturally aligned; strings are NUL-terminated UTF-8. omx
  * validates every offset and length against `size` (OMX_E_INVALID otherwise) and copies what it keeps. */
 #define OMX_BLOB_MAGIC   0x47584D4Fu /* "OMXG" */
-#define OMX_BLOB_VERSION 1u
+#define OMX_BLOB_VERSION 2u          /* version 1 buffers (the header up to indexes_off) are accepted too */
 typedef struct omx_graph_blob {       /* at offset 0 of the buffer                                       */
   uint32_t magic, version;
   uint32_t n_vertices;
@@ -285,7 +285,15 @@ typedef struct omx_graph_blob {       /* at offset 0 of the buffer              
   uint64_t edge_sets_off;    /* omx_edge_set_rec[n_edge_sets]                                          */
   uint64_t properties_off;   /* omx_property_rec[n_properties]                                         */
   uint64_t indexes_off;      /* omx_index_rec[n_indexes]                                               */
+  /* version 2: edge records (omx_edge_set_desc.edge_rids / in_edge_index, omx_graph_desc.edge_properties) */
+  uint64_t edge_records_off; /* omx_edge_records_rec[n_edge_sets], 0 = lightweight edges             */
+  int32_t n_edge_properties, reserved;
+  uint64_t edge_properties_off; /* omx_property_rec[n_edge_properties], values over the edge records  */
 } omx_graph_blob;
+typedef struct omx_edge_records_rec {
+  uint64_t edge_rids_off;      /* uint64_t[n_edges]                                                   */
+  uint64_t in_edge_index_off;  /* uint64_t[n_in_edges]; 0 when the set has no in CSR                  */
+} omx_edge_records_rec;
 typedef struct omx_class_rec {
   uint64_t name_off;
   int32_t superclass, is_edge_class, cluster_id, reserved;

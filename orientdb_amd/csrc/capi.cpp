@@ -1,6 +1,7 @@
 // capi.cpp — the extern "C" boundary (include/omx/match.h).
 #include <algorithm>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -100,10 +101,11 @@ std::string params_key(const omx_value *vals, int32_t n) {
   return k;
 }
 // ---- pointer-free buffers (omx_graph_create_blob / omx_execute_packed) ------------------------------
-static_assert(sizeof(omx_graph_blob) == 88, "omx_graph_blob layout");
+static_assert(sizeof(omx_graph_blob) == 112 && offsetof(omx_graph_blob, edge_records_off) == 88, "omx_graph_blob layout");
 static_assert(sizeof(omx_class_rec) == 24 && sizeof(omx_edge_set_rec) == 56 && sizeof(omx_property_rec) == 40 &&
-                  sizeof(omx_index_rec) == 16 && sizeof(omx_param_rec) == 40,
+                  sizeof(omx_index_rec) == 16 && sizeof(omx_param_rec) == 40 && sizeof(omx_edge_records_rec) == 16,
               "blob record layouts");
+constexpr uint64_t kBlobV1Header = 88;  // a version-1 header ends at indexes_off
 
 class Blob {
  public:
@@ -174,10 +176,13 @@ int omx_graph_create_blob(const void *blob, uint64_t size, omx_graph **out) {
   return guard([&] {
     if (!out) omx::fail(OMX_E_INVALID, "null out pointer");
     const Blob b(blob, size);
-    if (size < sizeof(omx_graph_blob)) omx::fail(OMX_E_INVALID, "buffer smaller than its header");
+    if (size < kBlobV1Header) omx::fail(OMX_E_INVALID, "buffer smaller than its header");
     if (reinterpret_cast<uintptr_t>(blob) % 8) omx::fail(OMX_E_INVALID, "buffer not 8-byte aligned");
     const omx_graph_blob *h = static_cast<const omx_graph_blob *>(blob);
-    if (h->magic != OMX_BLOB_MAGIC || h->version != OMX_BLOB_VERSION) omx::fail(OMX_E_INVALID, "buffer: bad magic/version");
+    if (h->magic != OMX_BLOB_MAGIC || (h->version != 1 && h->version != OMX_BLOB_VERSION))
+      omx::fail(OMX_E_INVALID, "buffer: bad magic/version");
+    const bool v2 = h->version >= 2;
+    if (v2 && size < sizeof(omx_graph_blob)) omx::fail(OMX_E_INVALID, "buffer smaller than its header");
     if (h->n_classes < 0 || h->n_edge_sets < 0 || h->n_properties < 0 || h->n_indexes < 0)
       omx::fail(OMX_E_INVALID, "buffer: negative count");
     const uint64_t V = h->n_vertices;
@@ -215,27 +220,47 @@ int omx_graph_create_blob(const void *blob, uint64_t size, omx_graph **out) {
     }
     d.n_edge_sets = h->n_edge_sets;
     d.edge_sets = es.data();
-    std::vector<omx_property_desc> pr(h->n_properties);
-    std::vector<std::vector<const char *>> dicts(h->n_properties);
-    const omx_property_rec *prr = b.array<omx_property_rec>(h->properties_off, h->n_properties, "properties");
-    for (int i = 0; i < h->n_properties; ++i) {
-      const omx_property_rec &r = prr[i];
-      pr[i].name = b.str(r.name_off, "property name");
-      pr[i].type = r.type;
-      const size_t w = r.type == OMX_PROP_INT64 || r.type == OMX_PROP_DOUBLE ? 8 : 4;
-      pr[i].values = w == 8 ? (const void *)b.array<uint64_t>(r.values_off, V, "property values")
-                            : (const void *)b.array<uint32_t>(r.values_off, V, "property values");
-      pr[i].present = b.array<uint8_t>(r.present_off, V, "present", true);
-      if (r.dict_size < 0) omx::fail(OMX_E_INVALID, "buffer: negative dictionary size");
-      if (r.type == OMX_PROP_STRING) {
-        const uint64_t *doff = b.array<uint64_t>(r.dict_off, (uint64_t)r.dict_size, "dictionary");
-        for (int k = 0; k < r.dict_size; ++k) dicts[i].push_back(b.str(doff[k], "dictionary string"));
+    uint64_t n_erec = 0;
+    if (v2 && h->edge_records_off) {
+      const omx_edge_records_rec *xr = b.array<omx_edge_records_rec>(h->edge_records_off, h->n_edge_sets, "edge records");
+      for (int i = 0; i < h->n_edge_sets; ++i) {
+        es[i].edge_rids = b.array<uint64_t>(xr[i].edge_rids_off, es[i].n_edges, "edge_rids");
+        es[i].in_edge_index = es[i].in_row_ptr ? b.array<uint64_t>(xr[i].in_edge_index_off, es[i].n_in_edges ? es[i].n_in_edges : es[i].n_edges, "in_edge_index")
+                                               : nullptr;
+        n_erec += es[i].n_edges;
       }
-      pr[i].dict_size = r.dict_size;
-      pr[i].dict = dicts[i].empty() ? nullptr : dicts[i].data();
     }
+    if (v2 && (h->n_edge_properties < 0 || (h->n_edge_properties > 0 && !h->edge_records_off)))
+      omx::fail(OMX_E_INVALID, "buffer: edge properties without edge records");
+    const int n_eprops = v2 ? h->n_edge_properties : 0;
+    std::vector<std::vector<const char *>> dicts(h->n_properties + n_eprops);
+    auto props = [&](uint64_t off, int n, uint64_t rows, int d0) {
+      std::vector<omx_property_desc> pr(n);
+      const omx_property_rec *prr = b.array<omx_property_rec>(off, n, "properties");
+      for (int i = 0; i < n; ++i) {
+        const omx_property_rec &r = prr[i];
+        pr[i].name = b.str(r.name_off, "property name");
+        pr[i].type = r.type;
+        const size_t w = r.type == OMX_PROP_INT64 || r.type == OMX_PROP_DOUBLE ? 8 : 4;
+        pr[i].values = w == 8 ? (const void *)b.array<uint64_t>(r.values_off, rows, "property values")
+                              : (const void *)b.array<uint32_t>(r.values_off, rows, "property values");
+        pr[i].present = b.array<uint8_t>(r.present_off, rows, "present", true);
+        if (r.dict_size < 0) omx::fail(OMX_E_INVALID, "buffer: negative dictionary size");
+        if (r.type == OMX_PROP_STRING) {
+          const uint64_t *doff = b.array<uint64_t>(r.dict_off, (uint64_t)r.dict_size, "dictionary");
+          for (int k = 0; k < r.dict_size; ++k) dicts[d0 + i].push_back(b.str(doff[k], "dictionary string"));
+        }
+        pr[i].dict_size = r.dict_size;
+        pr[i].dict = dicts[d0 + i].empty() ? nullptr : dicts[d0 + i].data();
+      }
+      return pr;
+    };
+    std::vector<omx_property_desc> pr = props(h->properties_off, h->n_properties, V, 0);
+    std::vector<omx_property_desc> epr = props(v2 ? h->edge_properties_off : 0, n_eprops, n_erec, h->n_properties);
     d.n_properties = h->n_properties;
     d.properties = pr.data();
+    d.n_edge_properties = n_eprops;
+    d.edge_properties = epr.data();
     std::vector<omx_index_desc> ix(h->n_indexes);
     const omx_index_rec *ir = b.array<omx_index_rec>(h->indexes_off, h->n_indexes, "indexes");
     for (int i = 0; i < h->n_indexes; ++i) ix[i] = omx_index_desc{ir[i].class_id, b.str(ir[i].property_off, "index property"), ir[i].unique};

@@ -7,7 +7,7 @@ import struct
 
 import numpy as np
 
-MAGIC, VERSION = 0x47584D4F, 1
+MAGIC, VERSION = 0x47584D4F, 2
 
 
 class _Buf:
@@ -29,9 +29,25 @@ class _Buf:
         return self.put(a.tobytes(), a.dtype.itemsize) if a.size else 0
 
 
-def graph_blob(n_vertices, classes, vertex_class, rids, edge_sets, properties=(), indexes=(), device=0, part=None):
-    """Arguments as GraphSnapshot(...) takes them; returns (bytes, numpy u64 buffer keeping it 8-aligned)."""
-    B = _Buf(88)
+def _props(B, properties):
+    prec = b""
+    for p in properties:
+        t = p["type"]
+        dt = {1: np.int32, 2: np.int64, 3: np.float64, 4: np.int32, 5: np.int32}[t]
+        v_off = B.put_array(p["values"], dt)
+        pres = p.get("present")
+        pr_off = B.put_array(pres, np.uint8) if pres is not None else 0
+        d = p.get("dict") or []
+        d_off = B.put(struct.pack("<%dQ" % len(d), *[B.put_str(s) for s in d])) if d else 0
+        prec += struct.pack("<QiiQQQ", B.put_str(p["name"]), t, len(d), v_off, pr_off, d_off)
+    return B.put(prec) if prec else 0
+
+
+def graph_blob(n_vertices, classes, vertex_class, rids, edge_sets, properties=(), indexes=(), device=0, part=None,
+               edge_properties=(), version=VERSION):
+    """Arguments as GraphSnapshot(...) takes them; returns (bytes, numpy u64 buffer keeping it 8-aligned).
+    version 1: the 88-byte header without edge records."""
+    B = _Buf(112 if version >= 2 else 88)
     crec = b""
     for name, sup, is_edge, cluster in classes:
         crec += struct.pack("<Qiiii", B.put_str(name), sup, int(is_edge), cluster, 0)
@@ -48,22 +64,23 @@ def graph_blob(n_vertices, classes, vertex_class, rids, edge_sets, properties=()
         n_in = int(np.asarray(irp)[-1]) if irp is not None else 0
         erec += struct.pack("<iiQQQQQQ", es["cls"], 0, int(orp[-1]), o_rp, o_col, i_rp, i_col, n_in)
     es_off = B.put(erec) if erec else 0
-    prec = b""
-    for p in properties:
-        t = p["type"]
-        dt = {1: np.int32, 2: np.int64, 3: np.float64, 4: np.int32, 5: np.int32}[t]
-        v_off = B.put_array(p["values"], dt)
-        pres = p.get("present")
-        pr_off = B.put_array(pres, np.uint8) if pres is not None else 0
-        d = p.get("dict") or []
-        d_off = B.put(struct.pack("<%dQ" % len(d), *[B.put_str(s) for s in d])) if d else 0
-        prec += struct.pack("<QiiQQQ", B.put_str(p["name"]), t, len(d), v_off, pr_off, d_off)
-    pr_off = B.put(prec) if prec else 0
+    xr_off = 0
+    if edge_sets and all(es.get("edge_rids") is not None for es in edge_sets):
+        xrec = b""
+        for es in edge_sets:
+            eix = es.get("in_edge_index")
+            xrec += struct.pack("<QQ", B.put_array(es["edge_rids"], np.uint64),
+                                B.put_array(eix, np.uint64) if eix is not None else 0)
+        xr_off = B.put(xrec)
+    pr_off = _props(B, properties)
+    epr_off = _props(B, edge_properties)
     irec = b"".join(struct.pack("<Qii", B.put_str(prop), ci, int(u)) for ci, prop, u in indexes)
     ix_off = B.put(irec) if irec else 0
     lo, hi = part if part is not None else (0, 0)
-    struct.pack_into("<IIIiiiiiIIQQQQQQ", B.b, 0, MAGIC, VERSION, n_vertices, len(classes), len(edge_sets),
+    struct.pack_into("<IIIiiiiiIIQQQQQQ", B.b, 0, MAGIC, version, n_vertices, len(classes), len(edge_sets),
                      len(properties), len(indexes), device, lo, hi, classes_off, vc_off, rid_off, es_off, pr_off, ix_off)
+    if version >= 2:
+        struct.pack_into("<QiiQ", B.b, 88, xr_off, len(edge_properties), 0, epr_off)
     while len(B.b) % 8:
         B.b.append(0)
     return np.frombuffer(bytes(B.b), np.uint64).copy()

@@ -120,3 +120,75 @@ def test_packed_execute_on_device(match_test_db_json):
         L.omx_result_free(r)
     assert len(got) == len(want) == 2
     assert {d["person"] for d in got} == {d["person"] for d in want}
+
+
+def test_blob_version1_header_accepted(match_test_db_json):
+    """Buffers of the 88-byte version-1 header (no edge records) still describe the same snapshot."""
+    import orientdb_amd as o
+    from orientdb_amd.graph import records_arrays
+    arrays = records_arrays(match_test_db_json)
+    g = o.GraphSnapshot.from_blob(graph_blob(*arrays, device=-1, version=1))
+    ref = o.GraphSnapshot(*arrays, device=-1)
+    for cls in ("V", "E", "Person", "TriangleE"):
+        assert g.class_count(cls) == ref.class_count(cls)
+
+
+EDGE_Q = "MATCH {class: TriangleV, as: a}.outE('TriangleE'){as: e}.inV(){as: b, where: (uid < 3)} RETURN a, e, b"
+
+
+@pytest.fixture(scope="module")
+def blob_edge_arrays():
+    from orientdb_amd.graph import records_arrays
+    from tests.test_gpu_edges import edge_db
+    db = edge_db(n=60, n_knows=200, n_likes=50)
+    a = records_arrays(db, edge_records=True)
+    # one set given with its in CSR (+ in_edge_index), as a Java builder reading in_ ridbags would
+    es = a[4][0]
+    rp, col = np.asarray(es["out_rp"], np.int64), np.asarray(es["out_col"], np.int64)
+    src = np.repeat(np.arange(len(rp) - 1), np.diff(rp))
+    order = np.argsort(col, kind="stable")
+    irp = np.zeros(len(rp), np.uint64)
+    np.add.at(irp, col + 1, 1)
+    es["in_rp"], es["in_col"], es["in_edge_index"] = np.cumsum(irp).astype(np.uint64), src[order], order
+    return a
+
+
+def test_blob_edge_records_equal_pointer_snapshot(blob_edge_arrays):
+    import orientdb_amd as o
+    a = blob_edge_arrays
+    ref = o.GraphSnapshot(*a[:7], device=-1, edge_properties=a[7])
+    g = o.GraphSnapshot.from_blob(graph_blob(*a[:7], device=-1, edge_properties=a[7]))
+    for cls in ("V", "E", "Person", "Knows", "Likes"):
+        assert g.class_count(cls) == ref.class_count(cls)
+    assert ref.class_count("Knows") == 200 and ref.class_count("E") == 250
+    for q in ("MATCH {class: Person, as: a}.outE('Knows'){as: e, where: (since > 2012)}.inV(){as: b} RETURN e",
+              "MATCH {class: Knows, as: e, where: (since = 2015)}.outV(){as: a} RETURN e, a"):
+        st = o.OMatchStatement(q)
+        assert st.explain(g) == st.explain(ref)
+        assert st.explain(g)["supported"]
+
+
+def test_blob_edge_properties_need_records(blob_edge_arrays):
+    import orientdb_amd as o
+    a = blob_edge_arrays
+    sets = [{k: v for k, v in es.items() if k not in ("edge_rids", "in_edge_index")} for es in a[4]]
+    buf = graph_blob(*a[:4], sets, *a[5:7], device=-1, edge_properties=a[7])
+    assert _create(buf) == o._native.OMX_E_INVALID
+
+
+@pytest.mark.gpu
+def test_blob_edge_records_on_device(blob_edge_arrays):
+    """An edge-node MATCH on the blob snapshot (one set with a given in CSR) against the oracle."""
+    import orientdb_amd as o
+    from oracle.match_ref import MatchOracle, RefDB
+    from tests.test_gpu_edges import edge_db
+    from tests.test_gpu_parity import gpu_set, oracle_set
+    a = blob_edge_arrays
+    g = o.GraphSnapshot.from_blob(graph_blob(*a[:7], device=0, edge_properties=a[7]))
+    ref = RefDB.from_json(edge_db(n=60, n_knows=200, n_likes=50))
+    for q in ("MATCH {class: Person, as: b, where: (uid < 30)}.inE('Knows'){as: e, where: (since > 2010)}.outV(){as: a} RETURN a, e, b",
+              "MATCH {class: Person, as: a}.outE('Knows'){as: e, where: (w < 0.5)}.inV(){as: b} RETURN $pathElements"):
+        rs = o.OMatchStatement(q).execute(g)
+        want = MatchOracle(ref, q).execute()
+        cols = rs.columns if rs.columns[0] != "$pathElements" else None
+        assert len(want) > 0 and gpu_set(rs) == oracle_set(want, cols)
