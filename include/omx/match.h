@@ -357,6 +357,15 @@ int omx_ridbag_decode_csr_ex(int32_t device, const uint8_t *streams, uint64_t st
                              int32_t n_files, uint32_t page_size, uint64_t *row_ptr, uint32_t *col,
                              uint64_t *n_entries);
 
+/* omx_ridbag_decode_csr_ex for bags of edge records (edge_rids / edge_targets required) that also returns
+ * entry_rids[*n_entries] (may be NULL), the edge record RID of every CSR entry — the edge_rids of an
+ * omx_edge_set_desc built from the same out_ bags, so edge nodes can bind those records. */
+int omx_ridbag_decode_edges(int32_t device, const uint8_t *streams, uint64_t stream_bytes, const uint64_t *offsets,
+                            uint32_t n_vertices, const uint64_t *vertex_rids, const uint64_t *edge_rids,
+                            const uint64_t *edge_targets, uint64_t n_edge_records, const omx_bonsai_file *files,
+                            int32_t n_files, uint32_t page_size, uint64_t *row_ptr, uint32_t *col,
+                            uint64_t *entry_rids, uint64_t *n_entries);
+
 /* Parameters as one buffer: uint32_t n, uint32_t reserved, omx_param_rec[n], then the strings. */
 typedef struct omx_param_rec {
   int32_t type, index;       /* OMX_VAL_*, positional index (when name_off == 0)                       */

@@ -141,6 +141,10 @@ SIGNATURES = {
                                            C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                            C.c_uint64, C.c_void_p, C.c_int32, C.c_uint32, C.POINTER(C.c_uint64),
                                            C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+    "omx_ridbag_decode_edges": (C.c_int, [C.c_int32, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32,
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                          C.c_uint64, C.c_void_p, C.c_int32, C.c_uint32, C.POINTER(C.c_uint64),
+                                          C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 }
 
 

@@ -564,6 +564,20 @@ int omx_ridbag_decode_csr_ex(int32_t device, const uint8_t *streams, uint64_t st
   });
 }
 
+int omx_ridbag_decode_edges(int32_t device, const uint8_t *streams, uint64_t stream_bytes, const uint64_t *offsets,
+                            uint32_t n_vertices, const uint64_t *vertex_rids, const uint64_t *edge_rids,
+                            const uint64_t *edge_targets, uint64_t n_edge_records, const omx_bonsai_file *files,
+                            int32_t n_files, uint32_t page_size, uint64_t *row_ptr, uint32_t *col,
+                            uint64_t *entry_rids, uint64_t *n_entries) {
+  return guard([&] {
+    if (!edge_rids || !edge_targets) omx::fail(OMX_E_INVALID, "omx_ridbag_decode_edges decodes bags of edge records");
+    omx::ridbag_decode_csr(device, streams, stream_bytes, offsets, n_vertices, vertex_rids, edge_rids, edge_targets,
+                           n_edge_records, files, files ? n_files : 0,
+                           page_size ? page_size : OMX_BONSAI_PAGE_SIZE, row_ptr, col, n_entries,
+                           col ? entry_rids : nullptr);
+  });
+}
+
 const char *omx_last_error(void) { return g_last_error.c_str(); }
 
 const char *omx_version(void) { return "omx 0.1 (gfx950)"; }

@@ -221,6 +221,6 @@ Graph *graph_create(const omx_graph_desc *d);
 void ridbag_decode_csr(int device, const uint8_t *streams, uint64_t nbytes, const uint64_t *offsets, uint32_t V,
                        const uint64_t *vertex_rids, const uint64_t *edge_rids, const uint64_t *edge_targets,
                        uint64_t nedges, const omx_bonsai_file *files, int32_t nfiles, uint32_t page_size,
-                       uint64_t *row_ptr, uint32_t *col, uint64_t *n_entries);
+                       uint64_t *row_ptr, uint32_t *col, uint64_t *n_entries, uint64_t *entry_rids = nullptr);
 
 }  // namespace omx

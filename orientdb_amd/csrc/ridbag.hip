@@ -232,7 +232,8 @@ __global__ void k_index_fill(const uint64_t *rids, const T *vals, uint64_t n, co
 constexpr int kDecB = 256, kDecIPT = 8, kDecTile = kDecB * kDecIPT, kDecRows = 1024;
 __global__ __launch_bounds__(kDecB) void k_bag_decode(const uint8_t *s, const uint64_t *pay, uint32_t V,
                                                       const uint64_t *rp, uint64_t E, RidIndex<uint32_t> vix,
-                                                      RidIndex<uint64_t> eix, int edges, uint32_t *col, uint32_t *err) {
+                                                      RidIndex<uint64_t> eix, int edges, uint32_t *col, uint32_t *err,
+                                                      uint64_t *erid) {
   __shared__ uint64_t s_r[2];
   __shared__ uint64_t s_rp[kDecRows + 1];
   __shared__ uint64_t s_pay[kDecRows];
@@ -295,6 +296,11 @@ __global__ __launch_bounds__(kDecB) void k_bag_decode(const uint8_t *s, const ui
       const uint64_t pos = __builtin_bswap64((b07 >> 16) | (b89 << 48));
       if (cl < 0 || (pos >> 48)) atomicOr(err, (uint32_t)kBagPosition);
       else rid[k] = ((uint64_t)(uint16_t)cl << 48) | pos;
+    }
+    if (erid) {  // the entries themselves: the edge records' RIDs
+#pragma unroll
+      for (int k = 0; k < kDecIPT; ++k)
+        if (off[k] != ~0ull) erid[t0 + (uint64_t)k * kDecB + threadIdx.x] = rid[k];
     }
     if (edges) {  // edge records: their opposite vertices
 #pragma unroll
@@ -678,13 +684,16 @@ __global__ void k_tree_row_counts(const uint32_t *tv, uint32_t nt, const uint64_
 // one thread per run: its RID → dense vertex id, written `count` times at the row's place
 __global__ void k_runs_write(const uint64_t *rrid, const uint64_t *rcnt, uint64_t R, const uint64_t *ro,
                              const uint64_t *roff, uint32_t nt, const uint32_t *tv, const uint64_t *rp,
-                             RidIndex<uint32_t> vix, RidIndex<uint64_t> eix, int edges, uint32_t *col, uint32_t *err) {
+                             RidIndex<uint32_t> vix, RidIndex<uint64_t> eix, int edges, uint32_t *col, uint32_t *err,
+                             uint64_t *erid) {
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t c = rcnt[r];
     if (!c) continue;
     const uint64_t t = last_le(roff, nt, r);
     const uint64_t out = rp[tv[t]] + (ro[r] - ro[roff[t]]);
     uint64_t id = rrid[r];
+    if (erid)
+      for (uint64_t k = 0; k < c; ++k) erid[out + k] = id;
     uint32_t x = 0xFFFFFFFFu;
     if (id != ~0ull && edges && !eix.find(id, &id)) {
       atomicOr(err, (uint32_t)kBagUnknownEdge);
@@ -875,8 +884,9 @@ void decode_trees(hipStream_t s, const uint8_t *ds, uint32_t V, const TreeHdr &t
 void ridbag_decode_csr(int device, const uint8_t *streams, uint64_t nbytes, const uint64_t *offsets, uint32_t V,
                        const uint64_t *vertex_rids, const uint64_t *edge_rids, const uint64_t *edge_targets,
                        uint64_t nedges, const omx_bonsai_file *files, int32_t nfiles, uint32_t page_size,
-                       uint64_t *row_ptr, uint32_t *col, uint64_t *n_entries) {
+                       uint64_t *row_ptr, uint32_t *col, uint64_t *n_entries, uint64_t *entry_rids) {
   if (device < 0) fail(OMX_E_INVALID, "ridbag decoding runs on a device");
+  if (entry_rids && !edge_rids) fail(OMX_E_INVALID, "entry_rids needs the edge records (edge_rids, edge_targets)");
   if (!offsets || !n_entries || (V && !vertex_rids) || (nbytes && !streams)) fail(OMX_E_INVALID, "null argument");
   if ((edge_rids == nullptr) != (edge_targets == nullptr)) fail(OMX_E_INVALID, "edge_rids and edge_targets go together");
   if (offsets[0] > offsets[V] || offsets[V] > nbytes) fail(OMX_E_INVALID, "stream offsets out of range");
@@ -974,10 +984,13 @@ void ridbag_decode_csr(int device, const uint8_t *streams, uint64_t nbytes, cons
   HostIndex<uint64_t> eix;
   if (edge_rids) build_index<uint64_t>(eix, edge_rids, edge_targets, nedges, s);
   DevArr<uint32_t> dcol(E);
+  std::unique_ptr<DevArr<uint64_t>> derid;
+  if (entry_rids) derid.reset(new DevArr<uint64_t>(E));
+  uint64_t *erp = entry_rids ? derid->p : nullptr;
   if (E) {
     const unsigned grid = (unsigned)std::min<uint64_t>((E + kDecTile - 1) / kDecTile, 65536);
     hipLaunchKernelGGL(k_bag_decode, dim3(grid), dim3(kDecB), 0, s, ds.p, pay.p, V, rp.p, E, vix.dev, eix.dev,
-                       edge_rids ? 1 : 0, dcol.p, err.p);
+                       edge_rids ? 1 : 0, dcol.p, err.p, erp);
     KCHECK("k_bag_decode");
   }
   if (tr.R) {  // the SBTree rows: every run's RID `count` times at its place in the row
@@ -985,10 +998,11 @@ void ridbag_decode_csr(int device, const uint8_t *streams, uint64_t nbytes, cons
     cub_call(s, [&](void *t, size_t &b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tr.rcnt->p, ro.p, (int64_t)tr.R, s); });
     hipLaunchKernelGGL(k_runs_write, dim3((unsigned)std::min<uint64_t>(nblocks(tr.R, 256), 65536)), dim3(256), 0, s,
                        tr.rrid->p, tr.rcnt->p, tr.R, ro.p, tr.roff->p, tr.nt, tr.tv->p, rp.p, vix.dev, eix.dev,
-                       edge_rids ? 1 : 0, dcol.p, err.p);
+                       edge_rids ? 1 : 0, dcol.p, err.p, erp);
     KCHECK("k_runs_write");
   }
   if (E) HIP_CHECK(hipMemcpyAsync(col, dcol.p, E * 4, hipMemcpyDeviceToHost, s));
+  if (E && entry_rids) HIP_CHECK(hipMemcpyAsync(entry_rids, erp, E * 8, hipMemcpyDeviceToHost, s));
   herr = read_err(err.p, s);
   if (herr) fail(OMX_E_INVALID, "ridbag streams:" + bag_error_text(herr));
 }

@@ -242,3 +242,54 @@ def test_sbtree_refused(bad):
     streams = [stream] + [b""] * (V - 1)
     with pytest.raises(o.OmxError):
         decode_ridbags(streams, vr, files=None if bad == "no_files" else files)
+
+
+@pytest.mark.parametrize("trees", [False, True], ids=["embedded", "sbtree"])
+def test_edge_record_bags_to_edge_nodes(trees):
+    """Bags of edge records decoded with their entries' RIDs (omx_ridbag_decode_edges) make an
+    edge-records snapshot whose edge-node MATCH rows equal the record-level snapshot's. Each bag is written
+    reversed (embedded: the decoded entry order differs from the original, so the RIDs must travel with
+    their entries) or, from two entries on, as an SBTree (entries in RID order, k_runs_write's path)."""
+    import random
+
+    import orientdb_amd as o
+    from orientdb_amd.graph import records_arrays
+    from orientdb_amd.ridbag import decode_ridbags
+    from tests.test_gpu_edges import edge_db
+    db = edge_db(n=80, n_knows=400, n_likes=100, seed=9)
+    V, classes, vclass, rids, sets, props, indexes, eprops = records_arrays(db, edge_records=True)
+    f = R.BonsaiFile(7, rng=random.Random(2)) if trees else None
+    new_sets, where = [], []
+    base = 0
+    orig = {}
+    for es in sets:
+        rp, col, er = es["out_rp"], es["out_col"], es["edge_rids"]
+        for i, x in enumerate(er):
+            orig[int(x)] = base + i
+        base += len(er)
+        streams = []
+        for v in range(V):
+            row = [(int(x) >> 48, int(x) & ((1 << 48) - 1)) for x in er[int(rp[v]):int(rp[v + 1])]]
+            if trees and len(row) >= 2:
+                root = f.build_tree([(r, 1) for r in sorted(row)], rng=random.Random(v))
+                streams.append(R.encode_sbtree_pointer(f.file_id, *root))
+            else:
+                streams.append(R.encode_embedded(row[::-1]))
+        files = {7: f.data()} if trees else None
+        grp, gcol, ent = decode_ridbags(streams, rids, er, rids[col], files=files, entry_rids=True)
+        assert len(ent) == len(er) and set(ent.tolist()) == set(er.tolist())
+        if not trees:
+            assert not np.array_equal(ent, er)  # the entries came back in another order
+        new_sets.append({"cls": es["cls"], "out_rp": grp, "out_col": gcol, "edge_rids": ent})
+        where += [orig[int(x)] for x in ent]
+    idx = np.array(where, np.int64)
+    eprops2 = [dict(p, values=np.asarray(p["values"])[idx], present=np.asarray(p["present"])[idx]) for p in eprops]
+    g1 = o.GraphSnapshot.from_records(db, device=0, edge_records=True)
+    g2 = o.GraphSnapshot(V, classes, vclass, rids, new_sets, props, indexes, 0, None, eprops2)
+    for q in ("MATCH {class: Person, as: a}.outE('Knows'){as: e, where: (since > 2012)}.inV(){as: b} RETURN a, e, b",
+              "MATCH {class: Person, as: b, where: (uid < 40)}.inE(){as: e}.outV(){as: a} RETURN $pathElements",
+              "MATCH {class: Likes, as: e}.inV(){as: b, where: (age < 50)} RETURN e, b"):
+        r1 = o.OMatchStatement(q).execute(g1, flags=o.OMX_FLAG_DIGEST)
+        r2 = o.OMatchStatement(q).execute(g2, flags=o.OMX_FLAG_DIGEST)
+        assert r1.info["n_rows"] == r2.info["n_rows"] > 0
+        assert r1.info["digest"] == r2.info["digest"]
