@@ -670,10 +670,8 @@ void launch_bfs_pull_w(const uint64_t *rp, const uint32_t *col, uint64_t E, cons
   if (!nt || !lanes) return;
   constexpr int per = 1;  // workgroups per CU (16 waves each: one LDS copy of the hub masks a CU)
   const uint32_t nlds = std::min(nhubs, (uint32_t)kPwLdsHubs);
-  static const bool slow_all = [] {  // OMX_PULLW_SLOW=1: every tile through k_bfs_pull_w_slow (tests)
-    const char *e = std::getenv("OMX_PULLW_SLOW");
-    return e && std::strcmp(e, "0") != 0;
-  }();
+  const char *slow_env = std::getenv("OMX_PULLW_SLOW");  // 1: every tile through k_bfs_pull_w_slow (tests)
+  const bool slow_all = slow_env && std::strcmp(slow_env, "0") != 0;
   if (slow_all) nreg = 0;
   if (nreg) {
     const dim3 g((unsigned)std::min<uint64_t>((nreg + kPwWaves - 1) / kPwWaves, (uint64_t)cus * per));

@@ -261,15 +261,13 @@ class Executor {
     col_.resize(p.aliases.size());
     bound_.assign(p.aliases.size(), 0);
     if (const char *r = std::getenv("OMX_ROUTE_SELF")) route_self_ = std::strcmp(r, "0") != 0;
-    debug_expand_ = std::getenv("OMX_DEBUG_EXPAND") != nullptr;  // one stderr line per expansion
+    debug_expand_ = std::getenv("OMX_HOST_TRACE") != nullptr;  // + one stderr line per expansion
     if (const char *ls = std::getenv("OMX_LIGHT_SLICED")) light_sliced_ = std::strcmp(ls, "0") != 0;
-    if (const char *ae = std::getenv("OMX_ARENA_ESTIMATE")) arena_estimate_ = std::strcmp(ae, "0") != 0;
     if (const char *fz = std::getenv("OMX_FACTOR")) {  // "0": never; "force": every filtered hop (tests)
       factor_ = std::strcmp(fz, "0") != 0;
       if (std::strcmp(fz, "force") == 0) factor_min_rows_ = 1, factor_min_ratio_ = 0;
     }
     if (const char *fe = std::getenv("OMX_FEMIT")) femit_ = std::strcmp(fe, "force") == 0 ? 2 : std::strcmp(fe, "0") != 0 ? 1 : 0;
-    if (const char *fm = std::getenv("OMX_FEMIT_MIN_ET")) femit_min_et_ = std::strtoull(fm, nullptr, 10);
     if (const char *fl = std::getenv("OMX_FEMIT_SLOW")) femit_slow_ = std::strcmp(fl, "0") != 0;
     if (const char *sj = std::getenv("OMX_SEMI")) semi_ok_ = std::strcmp(sj, "0") != 0;
     if (const char *gq = std::getenv("OMX_GRP32")) grp32_ = std::strcmp(gq, "0") != 0;
@@ -610,9 +608,8 @@ class Executor {
   // instead of the frontier blocks (OMX_DENSE_EXCHANGE=1: always the blocks)
   bool dense_exchange_ = false;
   bool segmented_ = false;  // the final table is block-segmented (see expand_core)
-  // sliced hops size their arenas from the target bitmap's density (OMX_ARENA_ESTIMATE=0: exact bound;
-  // OMX_ARENA_MARGIN scales the estimate, 0 forces the short-arena re-run in tests)
-  bool arena_estimate_ = true;
+  // sliced hops size their arenas from the target bitmap's density (OMX_ARENA_MARGIN scales the
+  // estimate, 0 forces the short-arena re-run in tests)
   double arena_margin_ = 1.25;
   bool factor_ = true;           // factorized expansion of filtered hops (OMX_FACTOR=0: direct)
   uint64_t factorized_hops_ = 0;
@@ -1598,7 +1595,7 @@ class Executor {
     DBuf<uint64_t> blk(&pool_, (uint64_t)(kBinKeys + P) * bin_tiles(R)), qb(&pool_, 2ull * P + 1 + kBinKeys);
     // a sliced hop that writes rows sizes its arenas from the target bitmap's density per slice
     // (posted with the binning totals); an arena found short re-runs the hop with the exact bound
-    const bool estimate = sliced && write && arena_estimate_;
+    const bool estimate = sliced && write;
     DBuf<unsigned long long> spop;
     if (estimate) {
       spop = DBuf<unsigned long long>(&pool_, P);
@@ -2151,7 +2148,7 @@ class Executor {
   int femit_ = 1;
   static constexpr uint64_t kOnDevice = UINT64_MAX;  // a count left on the device (emit_factorized's nlist)
   size_t flist_copy_rec_ = SIZE_MAX;                  // the timing record of the last k_flist_copy
-  uint64_t femit_min_et_ = 1000000000ull;
+  static constexpr uint64_t femit_min_et_ = 1000000000ull;
   bool femit_slow_ = false;  // OMX_FEMIT_SLOW=1: every output tile through k_femit_slow (tests)
 
   // step 4 of expand_factorized when the rows are written: the output space Σ_rows |L(g[r])| is laid out

@@ -1115,8 +1115,13 @@ class Planner {
       if (erec && varlen) unsupported("a variable-length item over edge records (" + it.method + "())");
       std::vector<std::pair<std::string, bool>> rconds;
       vertex_where_of(nodes_[t].alias, &rconds);
+      // a reversed traversal into a bound or prefetched target applies no WHERE (executeReverse's
+      // branches :468-490 test existence / candidates only); a forward one into a bound target filters
+      // the traversal with the WHERE, $matched included (:468-477 after executeTraversal), so the
+      // row-level conjuncts follow the check
+      if (!fwd && st.mode != T_FREE) rconds.clear();
       if (!rconds.empty()) {
-        if (varlen || it.is_multi || st.mode != T_FREE || st.optional)
+        if (varlen || it.is_multi || st.mode == T_CAND || st.optional)
           unsupported("$matched in the WHERE of a variable-length, multi-step, bound or prefetched target (" +
                       nodes_[t].alias + ")");
         for (auto &rc : rconds) {

@@ -185,6 +185,12 @@ RMAT_QUERIES = [
      ["me", "f"]),
     ("matched_and_filter", "MATCH {class:Person,as:me,where:(age < 20)}<-Knows-{as:x}-Knows->{as:f, where:($matched.me <> $currentMatch and age < 50)} RETURN me, x, f",
      ["me", "x", "f"]),
+    # a bound (cycle-closing) target with a row-level conjunct: the forward check filters with it (:468-477)
+    ("matched_bound", "MATCH {class:Person,as:a,where:(uid < 100)}-Knows->{as:b}-Knows->{as:c},"
+                      "{as:a}-Knows->{as:c, where:($matched.b != $currentMatch and age < 70)} RETURN a, b, c",
+     ["a", "b", "c"]),
+    ("matched_bound_eq", "MATCH {class:Person,as:a,where:(uid < 200)}-Knows->{as:b}-Knows->{as:c},"
+                         "{as:b}-Knows->{as:c, where:($currentMatch = $matched.a)} RETURN a, b, c", ["a", "b", "c"]),
     # b's WHERE declared on another occurrence of the alias: rebindFilters (P/OMatchStatement.java:185-195)
     # gives the forward hop into b the merged filter, so that hop is filtered and set-valued
     ("where_other_occurrence", "MATCH {class:Person,as:a,where:(uid < 60)}-Knows->{as:b}, {as:b,where:(age < 50)} RETURN a,b",
