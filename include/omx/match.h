@@ -394,6 +394,21 @@ int omx_comm_create_rccl(int32_t rank, int32_t world, int32_t device, const uint
 /* Ranks that are threads of this process (any devices, one GPU included): out[0..world-1]. The exchange
  * is device-to-device copies behind a barrier; each rank's omx_execute runs on its own thread. */
 int omx_comm_create_threads(int32_t world, omx_comm **out);
+/* Ranks that are processes joined by the caller's own host collectives (e.g. torch.distributed over gloo,
+ * MPI): the exchange is staged through host memory — counts and rows copied to the host, exchanged by the
+ * callbacks, copied back. For hosts without RCCL between the ranks' GPUs (or one GPU shared by several
+ * processes); the routing code is the one the RCCL transport runs. Callbacks return 0 on success. */
+typedef struct omx_host_collectives {
+  void *ctx;
+  /* every rank's `nbytes` bytes of `send`, rank-major, into recv (world × nbytes bytes) */
+  int (*allgather)(void *ctx, const void *send, uint64_t nbytes, void *recv);
+  /* byte all-to-all-v: send[sdispl[p], +scount[p]) goes to rank p; what rank p sends lands at
+   * recv[rdispl[p], +rcount[p]) (counts and displacements in bytes, world entries each) */
+  int (*alltoallv)(void *ctx, const void *send, const uint64_t *scount, const uint64_t *sdispl, void *recv,
+                   const uint64_t *rcount, const uint64_t *rdispl);
+  void (*abort)(void *ctx); /* may be NULL */
+} omx_host_collectives;
+int omx_comm_create_host(int32_t rank, int32_t world, const omx_host_collectives *c, omx_comm **out);
 int32_t omx_comm_rank(const omx_comm *c);
 int32_t omx_comm_world(const omx_comm *c);
 void omx_comm_destroy(omx_comm *c);

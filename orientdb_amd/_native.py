@@ -130,6 +130,7 @@ SIGNATURES = {
     "omx_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "omx_comm_create_rccl": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]),
     "omx_comm_create_threads": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "omx_comm_create_host": (C.c_int, [C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]),
     "omx_comm_rank": (C.c_int32, [C.c_void_p]),
     "omx_comm_world": (C.c_int32, [C.c_void_p]),
     "omx_comm_destroy": (None, [C.c_void_p]),

@@ -423,6 +423,15 @@ int omx_comm_create_threads(int32_t world, omx_comm **out) {
   });
 }
 
+int omx_comm_create_host(int32_t rank, int32_t world, const omx_host_collectives *hc, omx_comm **out) {
+  return guard([&] {
+    if (!hc || !out) omx::fail(OMX_E_INVALID, "null argument");
+    auto c = std::make_unique<omx_comm>();
+    c->t = omx::make_host_transport(rank, world, omx::HostCollectives{hc->ctx, hc->allgather, hc->alltoallv, hc->abort});
+    *out = c.release();
+  });
+}
+
 int32_t omx_comm_rank(const omx_comm *c) { return c ? c->t->rank() : -1; }
 int32_t omx_comm_world(const omx_comm *c) { return c ? c->t->world() : 0; }
 void omx_comm_destroy(omx_comm *c) { delete c; }

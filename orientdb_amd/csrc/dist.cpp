@@ -199,7 +199,95 @@ class RcclTransport : public Transport {
   uint64_t *d_one_ = nullptr, *d_all_ = nullptr;  // allgather staging
 };
 
+// ---- host collectives ------------------------------------------------------------------------------
+
+class HostTransport : public Transport {
+ public:
+  HostTransport(int rank, int world, const HostCollectives &c) : rank_(rank), world_(world), c_(c) {}
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  void abort() override {
+    aborted_ = true;
+    if (c_.abort) c_.abort(c_.ctx);
+  }
+
+  std::vector<uint64_t> allgather_n(const std::vector<uint64_t> &x, hipStream_t) override {
+    ++exchanges;
+    live();
+    std::vector<uint64_t> out(x.size() * world_);
+    if (x.empty()) return out;
+    call(c_.allgather(c_.ctx, x.data(), x.size() * 8, out.data()), "allgather");
+    return out;
+  }
+
+  void counts(const uint64_t *d_send, std::vector<uint64_t> &send, std::vector<uint64_t> &recv,
+              hipStream_t s) override {
+    ++exchanges;
+    live();
+    const int W = world_;
+    send.assign(W, 0);
+    HIP_OK(hipMemcpyAsync(send.data(), d_send, W * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    std::vector<uint64_t> all((size_t)W * W);
+    call(c_.allgather(c_.ctx, send.data(), W * 8ull, all.data()), "allgather");
+    recv.assign(W, 0);
+    for (int p = 0; p < W; ++p) recv[p] = all[(size_t)p * W + rank_];
+  }
+
+  // every column's rows through one host exchange: the columns' send buckets side by side per peer
+  // (peer p's part = its rows of column 0, then of column 1, ...), so one callback moves them all
+  void alltoallv(const std::vector<const uint32_t *> &sbuf, const std::vector<uint64_t> &send,
+                 const std::vector<uint64_t> &sdispl, const std::vector<uint32_t *> &rbuf,
+                 const std::vector<uint64_t> &recv, const std::vector<uint64_t> &rdispl, hipStream_t s) override {
+    ++exchanges;
+    live();
+    const int W = world_;
+    const size_t C = sbuf.size();
+    uint64_t ns = 0, nr = 0;
+    for (int p = 0; p < W; ++p) ns += send[p], nr += recv[p];
+    std::vector<uint32_t> hs(std::max<uint64_t>(ns * C, 1)), hr(std::max<uint64_t>(nr * C, 1));
+    std::vector<uint64_t> sc(W), sd(W), rc(W), rd(W);
+    uint64_t o = 0;
+    for (int p = 0; p < W; ++p) {
+      sd[p] = o * 4;
+      sc[p] = send[p] * C * 4;
+      for (size_t c = 0; c < C; ++c, o += send[p])
+        if (send[p]) HIP_OK(hipMemcpyAsync(hs.data() + o, sbuf[c] + sdispl[p], send[p] * 4, hipMemcpyDeviceToHost, s));
+    }
+    o = 0;
+    for (int p = 0; p < W; ++p) {
+      rd[p] = o * 4;
+      rc[p] = recv[p] * C * 4;
+      o += recv[p] * C;
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    call(c_.alltoallv(c_.ctx, hs.data(), sc.data(), sd.data(), hr.data(), rc.data(), rd.data()), "alltoallv");
+    o = 0;
+    for (int p = 0; p < W; ++p)
+      for (size_t c = 0; c < C; ++c, o += recv[p])
+        if (recv[p]) HIP_OK(hipMemcpyAsync(rbuf[c] + rdispl[p], hr.data() + o, recv[p] * 4, hipMemcpyHostToDevice, s));
+    HIP_OK(hipStreamSynchronize(s));  // (hr is a local)
+  }
+
+ private:
+  void live() const {
+    if (aborted_) fail(OMX_E_EXECUTION, "partitioned MATCH aborted: the communicator was aborted");
+  }
+  void call(int rc, const char *what) {
+    if (rc != 0) fail(OMX_E_EXECUTION, std::string("host collective ") + what + " failed (" + std::to_string(rc) + ")");
+  }
+  int rank_, world_;
+  HostCollectives c_;
+  bool aborted_ = false;
+};
+
 }  // namespace
+
+std::unique_ptr<Transport> make_host_transport(int rank, int world, const HostCollectives &c) {
+  if (world < 1 || rank < 0 || rank >= world) fail(OMX_E_INVALID, "bad communicator rank/world");
+  if (!c.allgather || !c.alltoallv) fail(OMX_E_INVALID, "host collectives without allgather / alltoallv");
+  return std::make_unique<HostTransport>(rank, world, c);
+}
 
 std::unique_ptr<Transport> make_thread_transport(std::shared_ptr<ThreadHub> hub, int rank) {
   return std::make_unique<ThreadTransport>(std::move(hub), rank);

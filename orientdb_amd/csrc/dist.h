@@ -7,12 +7,14 @@
 // every bound column. The reference never distributes MATCH (OMatchStatement.isLocalExecution,
 // P/OMatchStatement.java:1009-1011); this is the MI355X design.
 //
-// Two transports implement the same two collectives:
+// Three transports implement the same two collectives:
 //   * RCCL (one process per GPU, xGMI): ncclAllToAll of the counts, ncclAllToAllv of each column, on
 //     the executor's stream;
 //   * threads of one process (any devices, one shared GPU included): device-to-device copies between
 //     the ranks' buffers behind a barrier — the single-GPU parity tests of the partitioned path run the
-//     same routing code through it.
+//     same routing code through it;
+//   * processes joined by the caller's host collectives (gloo, MPI): counts and rows staged through
+//     host memory — the multi-process partitioned path where the ranks' GPUs have no RCCL between them.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -71,6 +73,14 @@ struct ThreadHub {
 
 std::unique_ptr<Transport> make_thread_transport(std::shared_ptr<ThreadHub> hub, int rank);
 std::unique_ptr<Transport> make_rccl_transport(int rank, int world, int device, const uint8_t *unique_id);
+// processes joined by the caller's host collectives (include/omx/match.h omx_host_collectives)
+struct HostCollectives {
+  void *ctx;
+  int (*allgather)(void *, const void *, uint64_t, void *);
+  int (*alltoallv)(void *, const void *, const uint64_t *, const uint64_t *, void *, const uint64_t *, const uint64_t *);
+  void (*abort)(void *);
+};
+std::unique_ptr<Transport> make_host_transport(int rank, int world, const HostCollectives &c);
 void rccl_unique_id(uint8_t *out);  // 128 bytes (NCCL_UNIQUE_ID_BYTES)
 
 }  // namespace omx

@@ -9,6 +9,8 @@ rank returns its share of the rows.
                                         made on one rank and shared (e.g. torch.distributed over gloo)
   Comm.threads(world)                   `world` ranks that are threads of this process (one GPU is
                                         enough): the exchange is device-to-device copies
+  host_comm(rank, world[, group])       one process per rank joined by torch.distributed host
+                                        collectives (gloo): the exchange staged through host memory
 """
 import ctypes as C
 
@@ -64,3 +66,57 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+# ---- ranks joined by the caller's host collectives (omx_comm_create_host) ----------------------------
+_ALLG = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
+_A2AV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p,
+                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
+_ABRT = C.CFUNCTYPE(None, C.c_void_p)
+
+
+class _HostCollectives(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("allgather", _ALLG), ("alltoallv", _A2AV), ("abort", _ABRT)]
+
+
+def host_comm(rank, world, group=None):
+    """A communicator whose exchange runs over torch.distributed host collectives (gloo: all_gather and
+    all_to_all_single of byte tensors) — one process per rank, any GPUs (one shared GPU included). The
+    process group must be initialised; every rank calls this with the same world."""
+    import torch
+    import torch.distributed as dist
+
+    def _bytes(addr, n):
+        return torch.frombuffer((C.c_uint8 * n).from_address(addr), dtype=torch.uint8) if n else torch.empty(0, dtype=torch.uint8)
+
+    def allgather(_ctx, send, n, recv):
+        try:
+            out = torch.empty(world * n, dtype=torch.uint8)
+            dist.all_gather_into_tensor(out, _bytes(send, n).clone(), group=group)
+            C.memmove(recv, out.data_ptr(), world * n)
+            return 0
+        except Exception:  # an error code, never an exception through the C frames
+            return 1
+
+    def alltoallv(_ctx, send, sc, sd, recv, rc, rd):
+        try:
+            scl = [int(sc[p]) for p in range(world)]
+            rcl = [int(rc[p]) for p in range(world)]
+            ns, nr = sum(scl), sum(rcl)
+            if any(int(sd[p]) != sum(scl[:p]) for p in range(world)) or any(int(rd[p]) != sum(rcl[:p]) for p in range(world)):
+                return 2  # (libomx packs the peers' parts back to back)
+            out = torch.empty(nr, dtype=torch.uint8)
+            dist.all_to_all_single(out, _bytes(send, ns).clone(), rcl, scl, group=group)
+            if nr:
+                C.memmove(recv, out.data_ptr(), nr)
+            return 0
+        except Exception:
+            return 1
+
+    cbs = (_ALLG(allgather), _A2AV(alltoallv), _ABRT(lambda _ctx: None))
+    hc = _HostCollectives(None, *cbs)
+    h = C.c_void_p()
+    N.check(N.lib().omx_comm_create_host(rank, world, C.byref(hc), C.byref(h)))
+    c = Comm(h)
+    c._keep = (cbs, hc)  # the callbacks live as long as the communicator
+    return c

@@ -46,3 +46,20 @@ def test_optional_validation_is_a_parse_error(match_test_db_json):
     st = o.OMatchStatement("match {class:Person, as:a, optional:true}-Friend->{as:b} return a")
     with pytest.raises(o.OmxParseError):
         st.explain(g)
+
+
+def test_host_comm_created_without_a_device():
+    """omx_comm_create_host checks its callbacks and ranks (no device, no collective at creation)."""
+    import ctypes as C
+
+    import orientdb_amd as o
+    from orientdb_amd import dist
+    L = o._native.lib()
+    h = C.c_void_p()
+    hc = dist._HostCollectives(None, dist._ALLG(lambda *a: 0), dist._A2AV(lambda *a: 0), dist._ABRT(lambda c: None))
+    assert L.omx_comm_create_host(1, 2, C.byref(hc), C.byref(h)) == 0
+    assert L.omx_comm_rank(h) == 1 and L.omx_comm_world(h) == 2
+    L.omx_comm_destroy(h)
+    assert L.omx_comm_create_host(2, 2, C.byref(hc), C.byref(h)) == o._native.OMX_E_INVALID
+    bad = dist._HostCollectives(None, dist._ALLG(), dist._A2AV(lambda *a: 0), dist._ABRT())
+    assert L.omx_comm_create_host(0, 2, C.byref(bad), C.byref(h)) == o._native.OMX_E_INVALID
