@@ -1120,10 +1120,12 @@ class Planner {
       // the traversal with the WHERE, $matched included (:468-477 after executeTraversal), so the
       // row-level conjuncts follow the check
       if (!fwd && st.mode != T_FREE) rconds.clear();
+      // (a variable-length or multi-step item: the WHERE selects the walk's outputs and never steers the
+      // walk — the while condition / maxDepth do, P/OMatchPathItem.java:79-105 — so the row-level
+      // conjuncts filter its output rows as they filter a single hop's)
       if (!rconds.empty()) {
-        if (varlen || it.is_multi || st.mode == T_CAND || st.optional)
-          unsupported("$matched in the WHERE of a variable-length, multi-step, bound or prefetched target (" +
-                      nodes_[t].alias + ")");
+        if (st.mode == T_CAND || st.optional)
+          unsupported("$matched in the WHERE of a prefetched or optional target (" + nodes_[t].alias + ")");
         for (auto &rc : rconds) {
           auto ai = alias_idx_.find(rc.first);
           if (ai == alias_idx_.end() || !bound[ai->second] || ai->second == t)
@@ -1135,7 +1137,7 @@ class Planner {
         st.trav.multi = true;
         st.trav.subs = compile_subs(it.multi);
         st.trav.varlen = varlen;
-        st.trav.where_prog = add_prog(where_of(nodes_[t].alias), varlen);  // the rebound alias filter (:185-195)
+        st.trav.where_prog = add_prog(vertex_where_of(nodes_[t].alias), varlen);  // the rebound alias filter (:185-195)
         st.trav.while_prog = add_prog(it.filter.while_, true);
         st.trav.has_max_depth = it.filter.has_max_depth;
         st.trav.max_depth = it.filter.max_depth;
@@ -1143,7 +1145,7 @@ class Planner {
       } else if (varlen) {
         st.kind = S_VARLEN;
         st.adj = adjacency(m, it.labels);
-        st.where_prog = add_prog(where_of(nodes_[t].alias), true);
+        st.where_prog = add_prog(vertex_where_of(nodes_[t].alias), true);
         st.while_prog = add_prog(it.filter.while_, true);
         st.has_max_depth = it.filter.has_max_depth;
         st.max_depth = it.filter.max_depth;

@@ -191,6 +191,13 @@ RMAT_QUERIES = [
      ["a", "b", "c"]),
     ("matched_bound_eq", "MATCH {class:Person,as:a,where:(uid < 200)}-Knows->{as:b}-Knows->{as:c},"
                          "{as:b}-Knows->{as:c, where:($currentMatch = $matched.a)} RETURN a, b, c", ["a", "b", "c"]),
+    # row-level conjuncts on the outputs of a variable-length and of a multi-step item
+    ("matched_varlen", "MATCH {class:Person,as:s,where:(uid < 20)}-Knows->{as:m}-Knows->{as:v, maxDepth: 2, "
+                       "where:($matched.s != $currentMatch and age < 80)} RETURN s, m, v", ["s", "m", "v"]),
+    ("matched_varlen_eq", "MATCH {class:Person,as:s,where:(uid < 60)}-Knows->{as:v, while:($depth < 3), "
+                          "where:($matched.s = $currentMatch)} RETURN s, v", ["s", "v"]),
+    ("matched_multi", "MATCH {class:Person,as:a,where:(uid < 20)}.(out('Knows').out('Knows')){as:c, "
+                      "where:($matched.a <> $currentMatch)} RETURN a, c", ["a", "c"]),
     # b's WHERE declared on another occurrence of the alias: rebindFilters (P/OMatchStatement.java:185-195)
     # gives the forward hop into b the merged filter, so that hop is filtered and set-valued
     ("where_other_occurrence", "MATCH {class:Person,as:a,where:(uid < 60)}-Knows->{as:b}, {as:b,where:(age < 50)} RETURN a,b",
