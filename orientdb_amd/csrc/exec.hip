@@ -257,6 +257,7 @@ class Executor {
     if (const char *pr = std::getenv("OMX_PULL_PROBE")) pull_probe_ = std::strtod(pr, nullptr);
     if (const char *px = std::getenv("OMX_PULL_EXIT")) pull_exit_ = std::strcmp(px, "0") != 0;
     if (const char *pw = std::getenv("OMX_PULL_WAVE")) pull_wave_ = std::strcmp(pw, "0") != 0;
+    if (const char *sp = std::getenv("OMX_SPARSE_PREP")) sparse_prep_ = std::strcmp(sp, "0") != 0;
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
     bound_.assign(p.aliases.size(), 0);
@@ -612,6 +613,7 @@ class Executor {
   // estimate, 0 forces the short-arena re-run in tests)
   double arena_margin_ = 1.25;
   bool factor_ = true;           // factorized expansion of filtered hops (OMX_FACTOR=0: direct)
+  bool sparse_prep_ = true;      // BFS level prologues over a push's touched list (OMX_SPARSE_PREP=0: full sweeps)
   uint64_t factorized_hops_ = 0;
   uint64_t semi_hops_ = 0;  // last hops written as a semi-join (Executor::semi_join)
   uint64_t arena_retries_ = 0;
@@ -3483,8 +3485,26 @@ class Executor {
     const bool carry = bcols.size() <= (size_t)BfsCarry::kMax;
     std::vector<std::vector<DBuf<uint32_t>>> oc(carry ? bcols.size() : 0);
     uint64_t ntotal = 0;
+    // sparse level prologues (bfs.hip k_bfs_prep_sparse): after a push level, the vertices its atomics
+    // touched first are the next level's only candidates; the level's active lists ping-pong between two
+    // slots (the previous level's list clears its bits while this level's is written); lcnt = {touched,
+    // slot 0, slot 1} counts, on the device
+    const bool sparse_ok = sparse_prep_ && !dist_ && vlo == 0 && vhi == V;
+    DBuf<uint32_t> touched, act[2];
+    DBuf<unsigned long long> lcnt;
+    if (sparse_ok) {
+      touched = DBuf<uint32_t>(&pool_, V);
+      act[0] = DBuf<uint32_t>(&pool_, V);
+      act[1] = DBuf<uint32_t>(&pool_, V);
+      lcnt = DBuf<unsigned long long>(&pool_, 3);
+    }
     for (uint64_t row0 = 0; row0 < R; row0 += 64) {
       const int nl = (int)std::min<uint64_t>(64, R - row0);
+      // the previous level: a push with its touched list (t_bound ≥ its length: the push's edges) and its
+      // active list in act[prev_slot] (prev_n vertices)
+      bool t_ok = false;
+      uint64_t t_bound = 0, prev_n = 0;
+      int prev_slot = -1;
       const uint64_t lanes = nl == 64 ? ~0ull : ((1ull << nl) - 1);
       // (one GPU: visited is zeroed by the first level's prologue, which covers every vertex)
       const bool whole = !dist_ && vlo == 0 && vhi == V;
@@ -3496,17 +3516,31 @@ class Executor {
         bool expand = !(st.has_max_depth && d >= st.max_depth);
         if (expand && depth_only_while) expand = !while_never && eval_pred_const(wconst, d);
         HIP_CHECK(hipMemsetAsync(stats.p, 0, 7 * sizeof(unsigned long long), s_));
-        tm_.begin("k_bfs_prep");
         // (one GPU: the prologue zeroes the next level's masks as it streams the frontier, no memset)
         const bool zero_nx = whole;
-        launch_bfs_prep(fr.p, vis.p, vhi, while_bm, expand, adj, stats.p, dist_ ? nullptr : fbm.p, cus(), s_, vlo, hub_bm,
-                        zero_nx ? nx.p : nullptr, whole && d == 0, d == 0);
-        tm_.end(8ull * (vhi - vlo));
+        const bool sparse = sparse_ok && d > 0 && t_ok && prev_slot >= 0 && t_bound * 16 < (uint64_t)V;
+        int cur_slot = -1;  // this level's active list, when the sparse prologue wrote it
+        if (sparse) {
+          cur_slot = prev_slot ^ 1;
+          HIP_CHECK(hipMemsetAsync(lcnt.p + 1 + cur_slot, 0, sizeof(unsigned long long), s_));
+          tm_.begin("k_bfs_prep_sparse");
+          launch_bfs_prep_sparse(act[prev_slot].p, lcnt.p + 1 + prev_slot, touched.p, lcnt.p,
+                                 std::max<uint64_t>(t_bound, prev_n), fr.p, vis.p, while_bm, expand, adj, stats.p, fbm.p,
+                                 hub_bm, nx.p, act[cur_slot].p, lcnt.p + 1 + cur_slot, cus(), s_);
+          tm_.end(12ull * prev_n + 40ull * t_bound);
+        } else {
+          tm_.begin("k_bfs_prep");
+          launch_bfs_prep(fr.p, vis.p, vhi, while_bm, expand, adj, stats.p, dist_ ? nullptr : fbm.p, cus(), s_, vlo, hub_bm,
+                          zero_nx ? nx.p : nullptr, whole && d == 0, d == 0);
+          tm_.end(8ull * (vhi - vlo));
+        }
+        t_ok = false;
         if (!expand) break;
         launch_post_words(stats.p, 6, mail(), s_);
         const uint64_t *hm = wait_mail();
         uint64_t h[6] = {hm[0], hm[1], hm[2], hm[3], hm[4], hm[5]};
-        tm_.amend(8ull * (vhi - vlo) + 24ull * h[2]);  // frontier scan + visited and row_ptr pair of the active vertices
+        // frontier scan + visited and row_ptr pair of the active vertices (sparse: the touched list's)
+        if (!sparse) tm_.amend(8ull * (vhi - vlo) + 24ull * h[2]);
         uint64_t live_or = h[3];
         uint64_t active = h[2];
         std::vector<uint64_t> al;
@@ -3666,23 +3700,52 @@ class Executor {
             edges_iter_ += pe;
           }
         } else {
-          if (!list.p) list = DBuf<uint32_t>(&pool_, V);
-          tm_.begin("k_bfs_list");
-          launch_bfs_list(fr.p, V, list.p, stats.p + 6, cus(), s_);
-          tm_.end(8ull * V + 4ull * h[2]);
+          // the level's active vertices: the sparse prologue's list, or a sweep of the frontier (into the
+          // slot the previous level's list does not hold, with its count on the device for the next clear)
+          const uint32_t *lp;
+          int slot = -1;
+          if (cur_slot >= 0) {
+            slot = cur_slot;
+            lp = act[slot].p;
+          } else if (sparse_ok) {
+            slot = prev_slot == 0 ? 1 : 0;
+            HIP_CHECK(hipMemsetAsync(lcnt.p + 1 + slot, 0, sizeof(unsigned long long), s_));
+            tm_.begin("k_bfs_list");
+            launch_bfs_list(fr.p, V, act[slot].p, lcnt.p + 1 + slot, cus(), s_);
+            tm_.end(8ull * V + 4ull * h[2]);
+            lp = act[slot].p;
+          } else {
+            if (!list.p) list = DBuf<uint32_t>(&pool_, V);
+            tm_.begin("k_bfs_list");
+            launch_bfs_list(fr.p, V, list.p, stats.p + 6, cus(), s_);
+            tm_.end(8ull * V + 4ull * h[2]);
+            lp = list.p;
+          }
           const uint64_t nl_act = h[2];
+          if (sparse_ok) HIP_CHECK(hipMemsetAsync(lcnt.p, 0, sizeof(unsigned long long), s_));
+          uint64_t pushed = 0;
+          bool rec = false;  // this push records its touched list (a small push: the next prologue is sparse)
           DBuf<uint64_t> deg(&pool_, nl_act + 1), loffs(&pool_, nl_act + 1);
           for (int p = 0; p < adj.n; ++p) {
-            launch_bfs_list_deg(list.p, nl_act, adj.p[p].rp, deg.p, s_);
+            launch_bfs_list_deg(lp, nl_act, adj.p[p].rp, deg.p, s_);
             cub([&](void *t, size_t &b) {
               return hipcub::DeviceScan::ExclusiveSum(t, b, deg.p, loffs.p, (int64_t)(nl_act + 1), s_);
             });
             const uint64_t etot = read1(loffs.p + nl_act);
+            rec = sparse_ok && adj.n == 1 && etot * 16 < (uint64_t)V;
             tm_.begin("k_bfs_push");
-            launch_bfs_push(list.p, loffs.p, nl_act, etot, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, cus(), s_);
+            launch_bfs_push(lp, loffs.p, nl_act, etot, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, cus(), s_,
+                            rec ? touched.p : nullptr, rec ? lcnt.p : nullptr);
             // per frontier edge: col + visited + next (+ row_ptr and frontier mask per listed vertex)
             tm_.end(20ull * etot + 24ull * nl_act);
             edges_iter_ += etot;
+            pushed += etot;
+          }
+          if (rec) {  // the next level runs its prologue over what this push touched
+            t_ok = true;
+            t_bound = pushed;
+            prev_slot = slot;
+            prev_n = nl_act;
           }
         }
         std::swap(fr, nx);

@@ -458,9 +458,18 @@ void launch_bfs_frontier_pack(uint32_t *list, uint64_t n, uint32_t vlo, const ui
                               hipStream_t s);
 void launch_bfs_frontier_scatter(const uint32_t *v, const uint32_t *mlo, const uint32_t *mhi, uint64_t n, uint64_t *fr,
                                  hipStream_t s);
+// touched (optional): every vertex whose next mask this push turns non-zero, once (*touched_n counts)
 void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, uint64_t etot, const uint64_t *rp,
                      const uint32_t *col, const uint64_t *frontier, const uint64_t *visited, uint64_t *next,
-                     int cus, hipStream_t s);
+                     int cus, hipStream_t s, uint32_t *touched = nullptr, unsigned long long *touched_n = nullptr);
+// the level prologue over the previous push's touched list (bfs.hip: k_bfs_sparse_clear over the previous
+// level's active list `prev`, then k_bfs_prep_sparse); the level's active list → act (*act_n, zeroed by
+// the caller); bound: an upper bound of both lists' lengths (grid size; the lengths stay on the device)
+void launch_bfs_prep_sparse(const uint32_t *prev, const unsigned long long *prev_n, const uint32_t *touched,
+                            const unsigned long long *touched_n, uint64_t bound, uint64_t *frontier, uint64_t *visited,
+                            const uint64_t *while_bm, bool expand, const DAdj &adj, unsigned long long *stats,
+                            uint64_t *fbm, const uint64_t *hub_bm, uint64_t *zero, uint32_t *act,
+                            unsigned long long *act_n, int cus, hipStream_t s);
 uint64_t bfs_pull_tiles(uint32_t V, uint64_t E);
 void launch_bfs_pull_partition(const uint64_t *rp, uint32_t V, uint64_t E, uint64_t *part, hipStream_t s);
 void launch_bfs_pull(uint32_t V, const uint64_t *rp, const uint32_t *col, const uint64_t *part, uint64_t E,

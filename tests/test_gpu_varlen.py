@@ -42,6 +42,7 @@ MODES = {
     "bfs_pull": dict(_PULL, OMX_PULL_PROBE="0"),  # dense levels: per-vertex early-exit pull
     "bfs_pull_tiles": dict(_PULL, OMX_PULL_PROBE="0", OMX_PULL_EXIT="0"),  # dense levels: in-edge wave tiles
     "bfs_pull_tiles_slow": dict(_PULL, OMX_PULL_PROBE="0", OMX_PULL_EXIT="0", OMX_PULLW_SLOW="1"),  # the long-row path
+    "bfs_full_preps": {"OMX_VARLEN": "bfs", "OMX_SPARSE_PREP": "0"},  # every level prologue a full sweep
     "bfs_pull_probe": dict(_PULL, OMX_PULL_PROBE="2", OMX_HUB_PUSH="0"),
     # sparse levels: the hub entries pulled, the non-hub frontier pushed (every level: OMX_PULL_PROBE=2)
     "bfs_pull_hubs_push": dict(_PULL, OMX_PULL_PROBE="2", OMX_HUB_PUSH="force"),
