@@ -3731,7 +3731,8 @@ class Executor {
             cub([&](void *t, size_t &b) {
               return hipcub::DeviceScan::ExclusiveSum(t, b, deg.p, loffs.p, (int64_t)(nl_act + 1), s_);
             });
-            const uint64_t etot = read1(loffs.p + nl_act);
+            // (one part: the prologue's Σ deg over the active vertices is this scan's total — no read-back)
+            const uint64_t etot = adj.n == 1 ? h[1] : read1(loffs.p + nl_act);
             rec = sparse_ok && adj.n == 1 && etot * 16 < (uint64_t)V;
             tm_.begin("k_bfs_push");
             launch_bfs_push(lp, loffs.p, nl_act, etot, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, cus(), s_,
