@@ -26,6 +26,24 @@
 
 namespace omx {
 namespace {
+// rocPRIM's radix sort takes its merge-sort path up to 2^20 items: at C2's 0.7 M rows that is 21 launches,
+// ≈0.14 ms. With a merge-sort limit of 0 every size above one block runs onesweep (one histogram pass and
+// ⌈bits / 8⌉ scatter passes): C2 0.920 → 0.888 ms, R1 1.573 → 1.495 ms, M1 and C4 unchanged (one box,
+// interleaved, `gpurun_out/rs1`, `rs2`).
+using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+template <class K, class V>
+hipError_t sort_pairs(void *t, size_t &b, const K *ki, K *ko, const V *vi, V *vo, uint64_t n, int bits, hipStream_t s) {
+  return rocprim::radix_sort_pairs<OnesweepSort>(t, b, ki, ko, vi, vo, (size_t)n, 0u, (unsigned)bits, s);
+}
+template <class K>
+hipError_t sort_keys(void *t, size_t &b, const K *ki, K *ko, uint64_t n, int bits, hipStream_t s) {
+  return rocprim::radix_sort_keys<OnesweepSort>(t, b, ki, ko, (size_t)n, 0u, (unsigned)bits, s);
+}
+}  // namespace
+}  // namespace omx
+
+namespace omx {
+namespace {
 
 struct CastU64 {
   __host__ __device__ uint64_t operator()(const uint32_t &x) const { return x; }
@@ -1097,7 +1115,7 @@ class Executor {
       launch_iota(iota.p, R, s_);
       const int bits = std::max(1, bits_for((uint64_t)W - 1));
       cub([&](void *t, size_t &b) {
-        return hipcub::DeviceRadixSort::SortPairs(t, b, dest.p, sdest.p, iota.p, perm.p, (int64_t)R, 0, bits, s_);
+        return sort_pairs(t, b, dest.p, sdest.p, iota.p, perm.p, R, bits, s_);
       });
     }
     std::vector<uint64_t> send, recv;
@@ -2344,7 +2362,7 @@ class Executor {
       // (rocPRIM onesweep configurations of 8-bit digits measured against hipCUB's default: within noise,
       // round 6, gpurun_out/r6i)
       cub([&](void *t, size_t &b) {
-        return hipcub::DeviceRadixSort::SortPairs(t, b, src, ss.p, iota.p, perm_s.p, (int64_t)R, 0, kbits, s_);
+        return sort_pairs(t, b, src, ss.p, iota.p, perm_s.p, R, kbits, s_);
       });
       tm_.end(16ull * R * ((kbits + 7) / 8));
       // the sorted rows' distinct sources (run heads), each row's source index, the sources' degree scan
@@ -3002,7 +3020,7 @@ class Executor {
       DBuf<uint32_t> iota(&pool_, R);
       DBuf<uint8_t> scls(&pool_, R);
       launch_iota(iota.p, R, s_);
-      cub([&](void *t, size_t &b) { return hipcub::DeviceRadixSort::SortPairs(t, b, cls.p, scls.p, iota.p, idx.p, (int64_t)R, 0, 2, s_); });
+      cub([&](void *t, size_t &b) { return sort_pairs(t, b, cls.p, scls.p, iota.p, idx.p, R, 2, s_); });
     }
     const uint64_t nM = nc[1];
     const uint32_t *gi[3] = {idx.p + nc[0], idx.p + nc[0] + nc[1], idx.p + nc[0] + nc[1] + nc[2]};
@@ -3165,7 +3183,7 @@ class Executor {
     dst = std::move(kc[1]);
     DBuf<uint32_t> iota(&pool_, n), perm(&pool_, n);
     launch_iota(iota.p, n, s_);
-    cub([&](void *t, size_t &b) { return hipcub::DeviceRadixSort::SortPairs(t, b, keys.p, skeys.p, iota.p, perm.p, (int64_t)n, 0, 2 * vb, s_); });
+    cub([&](void *t, size_t &b) { return sort_pairs(t, b, keys.p, skeys.p, iota.p, perm.p, n, 2 * vb, s_); });
     DBuf<uint8_t> head(&pool_, n);
     launch_u64_heads(skeys.p, n, head.p, s_);
     DBuf<uint32_t> sel(&pool_, n);
@@ -3296,7 +3314,7 @@ class Executor {
     if (n == 0) return 0;
     DBuf<uint64_t> sorted(&pool_, n), uniq(&pool_, n), nsel(&pool_, 1);
     cub([&](void *t, size_t &b) {
-      return hipcub::DeviceRadixSort::SortKeys(t, b, keys.p, sorted.p, (int64_t)n, 0, end_bit, s_);
+      return sort_keys(t, b, keys.p, sorted.p, n, end_bit, s_);
     });
     cub([&](void *t, size_t &b) { return hipcub::DeviceSelect::Unique(t, b, sorted.p, uniq.p, nsel.p, (int64_t)n, s_); });
     uint64_t m = read1(nsel.p);
@@ -4125,7 +4143,7 @@ class Executor {
       for (int c = k - 1; c >= 0; --c) {
         launch_gather_u32(out[c].p, order.p, R_, kin.p, s_);
         cub([&](void *t, size_t &b) {
-          return hipcub::DeviceRadixSort::SortPairs(t, b, kin.p, kout.p, order.p, order2.p, (int64_t)R_, 0, vbits, s_);
+          return sort_pairs(t, b, kin.p, kout.p, order.p, order2.p, R_, vbits, s_);
         });
         std::swap(order.p, order2.p);
       }
