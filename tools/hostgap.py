@@ -17,6 +17,8 @@ def main():
     g = o.GraphSnapshot.rmat(scale, device=0) if isinstance(scale, int) else o.GraphSnapshot.ldbc_like(device=0)
     st = o.OMatchStatement(query)
     flags = o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_KERNEL_TIMING | o.OMX_FLAG_TIME_HOT
+    if len(sys.argv) > 3 and sys.argv[3] == "untimed":  # no HIP events at all
+        flags = o.OMX_FLAG_KEEP_DEVICE
     for _ in range(3):
         st.execute(g, flags=flags, documents=False)
     L = N.lib()
