@@ -372,6 +372,8 @@ __global__ __launch_bounds__(kB) void k_bfs_push(const uint32_t *list, const uin
                                                  uint32_t *touched, unsigned long long *touched_n) {
   __shared__ uint64_t s_off[kPushStage + 1];
   __shared__ uint64_t s_lo, s_hi;
+  __shared__ uint32_t s_t[kB * kPushIT];  // this range's first touches (LDS appends, one global atomic a range)
+  __shared__ uint32_t s_tn, s_tbase;
   auto search = [&](uint64_t lo, uint64_t hi, uint64_t e) {  // largest i in [lo, hi] with loffs[i] <= e
     while (lo < hi) {
       const uint64_t mid = (lo + hi + 1) >> 1;
@@ -387,6 +389,7 @@ __global__ __launch_bounds__(kB) void k_bfs_push(const uint32_t *list, const uin
       const uint64_t lo = search(0, nl - 1, e0);
       s_lo = lo;
       s_hi = search(lo, nl - 1, e1 - 1);
+      s_tn = 0;
     }
     __syncthreads();
     const uint64_t lo = s_lo, hi = s_hi, n = hi - lo + 1;
@@ -419,19 +422,15 @@ __global__ __launch_bounds__(kB) void k_bfs_push(const uint32_t *list, const uin
         const uint64_t old = atomicOr((unsigned long long *)&next[w], (unsigned long long)m);
         first = old == 0;  // the first bits w receives at this level
       }
-      if (touched) {  // w joins the next level's touched list, once: one counter atomic per wave
-        const uint64_t fm = __ballot(first);
-        if (fm) {
-          const uint64_t live = __ballot(1);
-          const uint32_t leader = (uint32_t)__builtin_ctzll(live);
-          uint32_t base = 0;
-          if ((threadIdx.x & 63) == leader) base = (uint32_t)atomicAdd(touched_n, (unsigned long long)__popcll(fm));
-          base = __shfl(base, leader, 64);
-          if (first) touched[base + lane_prefix(fm)] = w;
-        }
-      }
+      if (touched && first) s_t[atomicAdd(&s_tn, 1u)] = w;  // w joins the next level's touched list, once
     }
-    __syncthreads();  // s_off and s_lo are restaged by the next range
+    __syncthreads();
+    if (touched) {  // the range's touches: one counter atomic, then a coalesced copy
+      if (threadIdx.x == 0 && s_tn) s_tbase = (uint32_t)atomicAdd(touched_n, (unsigned long long)s_tn);
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < s_tn; i += kB) touched[s_tbase + i] = s_t[i];
+    }
+    __syncthreads();  // s_off, s_lo and s_t are restaged by the next range
   }
 }
 void launch_bfs_push(const uint32_t *list, const uint64_t *loffs, uint64_t nl, uint64_t etot, const uint64_t *rp,

@@ -281,7 +281,10 @@ class Executor {
     if (const char *pr = std::getenv("OMX_PULL_PROBE")) pull_probe_ = std::strtod(pr, nullptr);
     if (const char *px = std::getenv("OMX_PULL_EXIT")) pull_exit_ = std::strcmp(px, "0") != 0;
     if (const char *pw = std::getenv("OMX_PULL_WAVE")) pull_wave_ = std::strcmp(pw, "0") != 0;
-    if (const char *sp = std::getenv("OMX_SPARSE_PREP")) sparse_prep_ = std::strcmp(sp, "0") != 0;
+    if (const char *sp = std::getenv("OMX_SPARSE_PREP")) {
+      sparse_prep_ = std::strcmp(sp, "0") != 0;
+      if (std::atoi(sp) > 1) sparse_div_ = (uint64_t)std::atoi(sp);
+    }
     bms_.resize(p.bitmaps.size());
     col_.resize(p.aliases.size());
     bound_.assign(p.aliases.size(), 0);
@@ -647,6 +650,7 @@ class Executor {
   double arena_margin_ = 1.25;
   bool factor_ = true;           // factorized expansion of filtered hops (OMX_FACTOR=0: direct)
   bool sparse_prep_ = true;      // BFS level prologues over a push's touched list (OMX_SPARSE_PREP=0: full sweeps)
+  uint64_t sparse_div_ = 8;      // (OMX_SPARSE_PREP=<n>: the push's edge bound V / n; 1 = every push)
   uint64_t factorized_hops_ = 0;
   uint64_t semi_hops_ = 0;  // last hops written as a semi-join (Executor::semi_join)
   uint64_t arena_retries_ = 0;
@@ -3523,6 +3527,9 @@ class Executor {
     // slots (the previous level's list clears its bits while this level's is written); lcnt = {touched,
     // slot 0, slot 1} counts, on the device
     const bool sparse_ok = sparse_prep_ && !dist_ && vlo == 0 && vhi == V;
+    // a push of fewer than V / kSparsePrepDiv edges records what it touches (at most that many vertices):
+    // the next prologue visits those at a few random words each instead of sweeping V
+    const uint64_t kSparsePrepDiv = sparse_div_;
     DBuf<uint32_t> touched, act[2];
     DBuf<unsigned long long> lcnt;
     if (sparse_ok) {
@@ -3551,7 +3558,7 @@ class Executor {
         HIP_CHECK(hipMemsetAsync(stats.p, 0, 7 * sizeof(unsigned long long), s_));
         // (one GPU: the prologue zeroes the next level's masks as it streams the frontier, no memset)
         const bool zero_nx = whole;
-        const bool sparse = sparse_ok && d > 0 && t_ok && prev_slot >= 0 && t_bound * 16 < (uint64_t)V;
+        const bool sparse = sparse_ok && d > 0 && t_ok && prev_slot >= 0 && t_bound * kSparsePrepDiv < (uint64_t)V;
         int cur_slot = -1;  // this level's active list, when the sparse prologue wrote it
         if (sparse) {
           cur_slot = prev_slot ^ 1;
@@ -3766,7 +3773,7 @@ class Executor {
             });
             // (one part: the prologue's Σ deg over the active vertices is this scan's total — no read-back)
             const uint64_t etot = adj.n == 1 ? h[1] : read1(loffs.p + nl_act);
-            rec = sparse_ok && adj.n == 1 && etot * 16 < (uint64_t)V;
+            rec = sparse_ok && adj.n == 1 && etot * kSparsePrepDiv < (uint64_t)V;
             tm_.begin("k_bfs_push");
             launch_bfs_push(lp, loffs.p, nl_act, etot, adj.p[p].rp, adj.p[p].col, fr.p, vis.p, nx.p, cus(), s_,
                             rec ? touched.p : nullptr, rec ? lcnt.p : nullptr);
