@@ -35,12 +35,19 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
 }  // namespace
 
 // seeds: lane i of the batch starts at src[row0 + i]
-__global__ void k_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier) {
+// touched (optional): each distinct seed vertex once (the first level's sparse prologue)
+__global__ void k_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, uint32_t *touched,
+                           unsigned long long *touched_n) {
   int i = threadIdx.x;
-  if (i < nl) atomicOr((unsigned long long *)&frontier[src[row0 + i]], 1ull << i);
+  if (i < nl) {
+    const uint32_t v = src[row0 + i];
+    const uint64_t old = atomicOr((unsigned long long *)&frontier[v], 1ull << i);
+    if (touched && old == 0) touched[atomicAdd(touched_n, 1ull)] = v;
+  }
 }
-void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, hipStream_t s) {
-  hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(64), 0, s, src, row0, nl, frontier);
+void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, hipStream_t s, uint32_t *touched,
+                     unsigned long long *touched_n) {
+  hipLaunchKernelGGL(k_bfs_seed, dim3(1), dim3(64), 0, s, src, row0, nl, frontier, touched, touched_n);
   KCHECK("k_bfs_seed");
 }
 

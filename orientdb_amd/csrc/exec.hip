@@ -3550,7 +3550,21 @@ class Executor {
       const bool whole = !dist_ && vlo == 0 && vhi == V;
       HIP_CHECK(hipMemsetAsync(fr.p, 0, (size_t)V * 8, s_));
       if (!whole) HIP_CHECK(hipMemsetAsync(vis.p, 0, (size_t)V * 8, s_));
-      launch_bfs_seed(srcc, row0, nl, fr.p, s_);
+      if (sparse_ok) {
+        // the first level's prologue over the distinct seeds: visited, the next masks and the frontier
+        // bitmap zeroed by memsets (write-only streams) instead of the full sweep that also reads the frontier
+        HIP_CHECK(hipMemsetAsync(lcnt.p, 0, 3 * sizeof(unsigned long long), s_));
+        launch_bfs_seed(srcc, row0, nl, fr.p, s_, touched.p, lcnt.p);
+        HIP_CHECK(hipMemsetAsync(vis.p, 0, (size_t)V * 8, s_));
+        HIP_CHECK(hipMemsetAsync(nx.p, 0, (size_t)V * 8, s_));
+        HIP_CHECK(hipMemsetAsync(fbm.p, 0, (size_t)nwords_ * 8, s_));
+        t_ok = true;
+        t_bound = (uint64_t)nl;
+        prev_slot = 0;  // (slot 0's count is 0: nothing to clear)
+        prev_n = 0;
+      } else {
+        launch_bfs_seed(srcc, row0, nl, fr.p, s_);
+      }
       for (int64_t d = 0;; ++d) {
         if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate");
         bool expand = !(st.has_max_depth && d >= st.max_depth);
@@ -3558,7 +3572,7 @@ class Executor {
         HIP_CHECK(hipMemsetAsync(stats.p, 0, 7 * sizeof(unsigned long long), s_));
         // (one GPU: the prologue zeroes the next level's masks as it streams the frontier, no memset)
         const bool zero_nx = whole;
-        const bool sparse = sparse_ok && d > 0 && t_ok && prev_slot >= 0 && t_bound * kSparsePrepDiv < (uint64_t)V;
+        const bool sparse = sparse_ok && t_ok && prev_slot >= 0 && (d == 0 || t_bound * kSparsePrepDiv < (uint64_t)V);
         int cur_slot = -1;  // this level's active list, when the sparse prologue wrote it
         if (sparse) {
           cur_slot = prev_slot ^ 1;

@@ -437,7 +437,8 @@ void launch_digest(int ncols, const uint32_t *const *cols, uint64_t n, const uin
 bool eval_pred_const(const DPred &pred, int64_t depth);
 
 // multi-source BFS (bfs.hip): u64 lane mask per vertex, 64 binding rows per batch
-void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, hipStream_t s);
+void launch_bfs_seed(const uint32_t *src, uint64_t row0, int nl, uint64_t *frontier, hipStream_t s,
+                     uint32_t *touched = nullptr, unsigned long long *touched_n = nullptr);
 // vertices [vlo, V) (a partition's own rows: vlo = part_lo, V = part_hi; fbm only from vertex 0);
 // zero: the next level's mask array — the previous level's frontier array — zeroed where the previous
 // level's frontier bits (fbm, read before this level's overwrite) are set, or everywhere with zero_all (no
