@@ -942,12 +942,25 @@ __global__ void k_pull_partition(const uint64_t *offs, uint64_t R, uint64_t E, u
 }
 
 // Result emission from the visited masks: (row0 + lane, v) for every set lane of v with emit(v).
-__global__ __launch_bounds__(kB) void k_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V,
-                                                       uint32_t *blk) {
+// last: the final level's frontier, not merged into visited by a prologue (a level that does not expand
+// only merges): merged here, so the emission reads visited alone
+__global__ __launch_bounds__(kB) void k_bfs_emit_count(uint64_t *visited, const uint64_t *emit_bm, uint32_t V,
+                                                       uint32_t *blk, const uint64_t *last) {
   __shared__ uint32_t s_w[kB / 64];
   const uint64_t v = (uint64_t)blockIdx.x * kB + threadIdx.x;
   uint32_t c = 0;
-  if (v < V && (!emit_bm || bm_test(emit_bm, (uint32_t)v))) c = (uint32_t)__popcll(visited[v]);
+  uint64_t vis = 0;
+  if (v < V) {
+    vis = visited[v];
+    if (last) {
+      const uint64_t x = last[v];
+      if (x & ~vis) {
+        vis |= x;
+        visited[v] = vis;
+      }
+    }
+  }
+  if (v < V && (!emit_bm || bm_test(emit_bm, (uint32_t)v))) c = (uint32_t)__popcll(vis);
   uint32_t tot;
   block_excl_scan<kB>(c, s_w, &tot);
   if (threadIdx.x == 0) blk[blockIdx.x] = tot;
@@ -1000,8 +1013,9 @@ __global__ __launch_bounds__(kB) void k_bfs_emit_write(const uint64_t *visited, 
     __syncthreads();
   }
 }
-void launch_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, uint32_t *blk, hipStream_t s) {
-  hipLaunchKernelGGL(k_bfs_emit_count, dim3(nblocks(V, kB)), dim3(kB), 0, s, visited, emit_bm, V, blk);
+void launch_bfs_emit_count(uint64_t *visited, const uint64_t *emit_bm, uint32_t V, uint32_t *blk, hipStream_t s,
+                           const uint64_t *last) {
+  hipLaunchKernelGGL(k_bfs_emit_count, dim3(nblocks(V, kB)), dim3(kB), 0, s, visited, emit_bm, V, blk, last);
   KCHECK("k_bfs_emit_count");
 }
 void launch_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, const uint64_t *blk_offs,
@@ -1014,15 +1028,16 @@ unsigned bfs_blocks(uint32_t V) { return nblocks(V, kB); }
 
 // T_BOUND: row r (lane r - row0) keeps its binding iff its bound target was reached and passes emit
 __global__ void k_bfs_bound(const uint32_t *dst, uint64_t row0, int nl, const uint64_t *visited,
-                            const uint64_t *emit_bm, uint8_t *flags) {
+                            const uint64_t *emit_bm, uint8_t *flags, const uint64_t *last) {
   const int i = threadIdx.x;
   if (i >= nl) return;
   const uint32_t t = dst[row0 + i];
-  flags[row0 + i] = ((visited[t] >> i) & 1ull) && (!emit_bm || bm_test(emit_bm, t));
+  const uint64_t vis = visited[t] | (last ? last[t] : 0ull);
+  flags[row0 + i] = ((vis >> i) & 1ull) && (!emit_bm || bm_test(emit_bm, t));
 }
 void launch_bfs_bound(const uint32_t *dst, uint64_t row0, int nl, const uint64_t *visited, const uint64_t *emit_bm,
-                      uint8_t *flags, hipStream_t s) {
-  hipLaunchKernelGGL(k_bfs_bound, dim3(1), dim3(64), 0, s, dst, row0, nl, visited, emit_bm, flags);
+                      uint8_t *flags, hipStream_t s, const uint64_t *last) {
+  hipLaunchKernelGGL(k_bfs_bound, dim3(1), dim3(64), 0, s, dst, row0, nl, visited, emit_bm, flags, last);
   KCHECK("k_bfs_bound");
 }
 

@@ -3565,10 +3565,17 @@ class Executor {
       } else {
         launch_bfs_seed(srcc, row0, nl, fr.p, s_);
       }
+      const uint64_t *last = nullptr;  // a final level left unmerged: the emission merges it into visited
       for (int64_t d = 0;; ++d) {
         if (d > 100000) fail(OMX_E_EXECUTION, "variable-length traversal did not terminate");
         bool expand = !(st.has_max_depth && d >= st.max_depth);
         if (expand && depth_only_while) expand = !while_never && eval_pred_const(wconst, d);
+        // a level that does not expand only merges its frontier into visited: with one GPU the emission's
+        // counting pass does that (one sweep of V fewer); a sparse one still runs over its short list
+        if (!expand && whole && !(sparse_ok && t_ok && prev_slot >= 0 && t_bound * kSparsePrepDiv < (uint64_t)V)) {
+          last = fr.p;
+          break;
+        }
         HIP_CHECK(hipMemsetAsync(stats.p, 0, 7 * sizeof(unsigned long long), s_));
         // (one GPU: the prologue zeroes the next level's masks as it streams the frontier, no memset)
         const bool zero_nx = whole;
@@ -3806,11 +3813,11 @@ class Executor {
         std::swap(fr, nx);
       }
       if (st.mode == T_BOUND) {
-        launch_bfs_bound(col_[st.dst].p, row0, nl, vis.p, emit_bm, bflags.p, s_);
+        launch_bfs_bound(col_[st.dst].p, row0, nl, vis.p, emit_bm, bflags.p, s_, last);
         continue;
       }
       tm_.begin("k_bfs_emit");
-      launch_bfs_emit_count(vis.p, emit_bm, V, blk.p, s_);
+      launch_bfs_emit_count(vis.p, emit_bm, V, blk.p, s_, last);
       HIP_CHECK(hipMemsetAsync(blk_offs.p, 0, 8, s_));
       hipcub::TransformInputIterator<uint64_t, CastU64, const uint32_t *> bit(blk.p, CastU64());
       cub([&](void *t, size_t &b) { return hipcub::DeviceScan::InclusiveSum(t, b, bit, blk_offs.p + 1, (int64_t)nb, s_); });

@@ -498,7 +498,9 @@ uint32_t build_pull_col(const uint64_t *rp_self, const uint64_t *rp_other, const
                         uint32_t *out, int cus, hipStream_t s);
 void launch_hub_gather(const uint32_t *hubs, uint32_t n, const uint64_t *frontier, uint64_t *hub_fr, hipStream_t s);
 unsigned bfs_blocks(uint32_t V);
-void launch_bfs_emit_count(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, uint32_t *blk, hipStream_t s);
+// last (optional): the final level's frontier, merged into visited here (the level skipped its prologue)
+void launch_bfs_emit_count(uint64_t *visited, const uint64_t *emit_bm, uint32_t V, uint32_t *blk, hipStream_t s,
+                           const uint64_t *last = nullptr);
 // binding columns the BFS emission writes directly (row0 + lane → the lane's values); n = 0 → row indices
 struct BfsCarry {
   static constexpr int kMax = 4;
@@ -510,6 +512,6 @@ struct BfsCarry {
 void launch_bfs_emit_write(const uint64_t *visited, const uint64_t *emit_bm, uint32_t V, const uint64_t *blk_offs,
                            uint32_t row0, uint32_t *out_row, uint32_t *out_v, const BfsCarry &cc, hipStream_t s);
 void launch_bfs_bound(const uint32_t *dst, uint64_t row0, int nl, const uint64_t *visited, const uint64_t *emit_bm,
-                      uint8_t *flags, hipStream_t s);
+                      uint8_t *flags, hipStream_t s, const uint64_t *last = nullptr);
 
 }  // namespace omx
