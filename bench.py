@@ -44,6 +44,10 @@ QUERIES = {
            "MATCH {class:Person,as:a,where:(uid < 64)}-Knows->{as:b}-Knows->{as:c}-Knows->{as:d} RETURN a,b,c,d", 26),
     "r1": ("R1: configs[1]'s 2-hop at RMAT-22 returning RETURN expressions (documents by content, evaluated on the device)",
            "MATCH {class:Person,as:a,where:(age < 1)}-Knows->{as:b}-Knows->{as:c,where:(age >= 90)} RETURN a.uid, b.age", 22),
+    # edge nodes (round 6): configs[1]'s shape with the Knows edges as records and a filter on their field w
+    "e1": ("E1: configs[1]'s 2-hop at RMAT-22 through edge nodes, outE('Knows'){as: e, where: (w < 10)}.inV()",
+           "MATCH {class:Person,as:a,where:(age < 1)}.outE('Knows'){as:e, where:(w < 10)}.inV(){as:b,where:(age >= 90)} "
+           "RETURN a, e, b", 22),
     # SURVEY §8(f) rows (not the metric): {hub} = the vertex of highest out-degree
     "t1": ("T1: TRAVERSE out('Knows') STRATEGY BREADTH_FIRST from the highest-degree vertex (its whole reach)",
            "TRAVERSE out('Knows') FROM #11:{hub} STRATEGY BREADTH_FIRST", 24),
@@ -68,7 +72,8 @@ def scaled_query(name, query, world, partitioned):
     return query, "strong"
 
 
-REPLICATED_ONLY = {"c1", "c4", "t1", "s1", "p1"}  # C4 LDBC replica; C1 all-root fof; TRAVERSE / SELECT / shortestPath
+REPLICATED_ONLY = {"c1", "c4", "t1", "s1", "p1", "e1"}
+EDGE_RECORDS = {"e1"}  # snapshots built with the edges as records (GraphSnapshot.rmat(edge_records=True))  # C4 LDBC replica; C1 all-root fof; TRAVERSE / SELECT / shortestPath
 COUNT_MODE = {"c5"}   # the last hop counts its rows (count mode)
 LDBC_SF10 = dict(n_persons=70000, target_edges=2_000_000, seed=10)  # ≈7e4 Person, ≈2e6 Knows
 # kernels that can be the dominant one (pseudo-records like expand_total / dedup are spans, not kernels)
@@ -179,6 +184,30 @@ def cpu_baseline_shortest(g, query, target_s):
                       "1 thread)" % (reps, secs, seen[0])}
 
 
+def cpu_baseline_edges(g, query, target_s):
+    """E1: the edge-node 2-hop restated over the CSR with numpy (oracle/edge_ref.py, one core, pinned to
+    oracle/match_ref.py) on a bounded sample of the roots, doubled until ≈ target_s / 4."""
+    import re
+    import numpy as np
+    from oracle.edge_ref import edge_two_hop
+    rp, col = g.csr
+    amax, wmax, bmin = (int(x) for x in re.search(r"age < (\d+).*w < (\d+).*age >= (\d+)", query).groups())
+    roots = np.nonzero(g.age < amax)[0]
+    emask, bmask = g.w < wmax, g.age >= bmin
+    k = 1024
+    while True:
+        sample = roots[:k]
+        t0 = time.perf_counter()
+        r, edges = edge_two_hop(rp, col, sample, emask, bmask)
+        secs = time.perf_counter() - t0
+        if secs > target_s / 4 or k >= len(roots):
+            break
+        k *= 2
+    return {"value": edges / secs / 1e9, "unit": "GTEPS", "cores": 1, "kind": "port",
+            "sample": "%d of %d roots (%.1f s, %d edges, %d rows; oracle/edge_ref.py, numpy, 1 thread)" % (
+                len(sample), len(roots), secs, edges, len(r[0]))}
+
+
 def cpu_baseline(g, query, target_s=12.0, single_thread_too=False):
     """The oracle's C DFS restatement (oracle/dfs_ref.c) on the host cores, on a bounded sample of
     the same workload's roots; GTEPS over the sampled roots."""
@@ -188,6 +217,8 @@ def cpu_baseline(g, query, target_s=12.0, single_thread_too=False):
         return cpu_baseline_shortest(g, query, target_s)
     if query.startswith(("TRAVERSE", "SELECT")):
         return cpu_baseline_chain(g, query, target_s)
+    if ".outE(" in query:
+        return cpu_baseline_edges(g, query, target_s)
     threads, visible = host_threads()
     if "while:($depth < 4)" in query:
         r = cpu_baseline_varlen(g, 64, 4, target_s, threads)
@@ -374,8 +405,11 @@ def main():
                       "edge_factor": 16, "rows_owned": list(g.part)}
     else:
         args.scale = int(args.scale)
-        g = with_heartbeat("graph build", lambda: o.GraphSnapshot.rmat(args.scale, device=local, keep_csr=keep))
-        graph_desc = {"graph": "RMAT", "scale": args.scale, "edge_factor": 16}
+        erec = args.query in EDGE_RECORDS
+        g = with_heartbeat("graph build", lambda: o.GraphSnapshot.rmat(args.scale, device=local, keep_csr=keep,
+                                                                        edge_records=erec))
+        graph_desc = {"graph": "RMAT" + (" with edge records (field w)" if erec else ""), "scale": args.scale,
+                      "edge_factor": 16}
     t_build = time.perf_counter() - t_build
     if "{hub}" in query:  # the vertex of highest out-degree (lowest id on ties)
         import numpy as np

@@ -787,13 +787,16 @@ class Executor {
     }
   }
 
-  DPred make_pred(int prog, int class_id) const {
+  // records (BitmapSpec::records): the bitmap is kept to that kind's id range afterwards (keep_records)
+  DPred make_pred(int prog, int class_id, int records = 0) const {
     DPred d{};
     d.cols = g_.d_cols;
     d.vclass = g_.d_vclass;
     // (a class whose polymorphic set holds every vertex of the snapshot — configs' class:Person — tests
-    // nothing: the bitmap kernels then read no class ids)
-    if (class_id >= 0 && g_.count(class_id) < (uint64_t)g_.V) {
+    // nothing: the bitmap kernels then read no class ids; nor does one holding every record of the kind
+    // the bitmap is kept to)
+    const uint64_t kind_n = records == 1 ? g_.vertices : records == 2 ? (uint64_t)g_.V - g_.vertices : (uint64_t)g_.V;
+    if (class_id >= 0 && g_.count(class_id) < kind_n) {
       d.use_class = 1;
       g_.class_mask(class_id, d.class_mask);
     }
@@ -803,8 +806,15 @@ class Executor {
       for (size_t i = 0; i < pp.code.size(); ++i) d.code[i] = pp.code[i];
       for (size_t i = 0; i < pp.deg.size(); ++i) d.deg[i] = dist_ ? global_degree_adj(pp.deg[i]) : make_adj(pp.deg[i]);
       match_atoms(pp, d);
+      // a field present on every record of the kind: no presence test (the other kind's bits are cleared)
+      for (int a = 0; a < d.n_atoms && records; ++a)
+        if (!(records == 1 ? g_.props[d.atom_col[a]].nulls_v : g_.props[d.atom_col[a]].nulls_e)) d.atom_c[a].present = nullptr;
     }
     return d;
+  }
+  void keep_records(uint64_t *words, int records) {
+    if (records == 1) launch_bitmap_keep_range(words, nwords_, 0, g_.vertices, s_);
+    else if (records == 2) launch_bitmap_keep_range(words, nwords_, g_.vertices, g_.V, s_);
   }
 
   // [COL c, INT/DBL k, CMP] (AND|OR [COL, INT/DBL, CMP])* → DPred atoms (evaluated without the VM)
@@ -841,12 +851,15 @@ class Executor {
     d.conj = conj < 0 ? 1 : conj;
   }
 
-  void eval_bitmap(int prog, int class_id, int64_t depth, uint64_t *words, uint64_t nwords = 0) {
+  void eval_bitmap(int prog, int class_id, int64_t depth, uint64_t *words, uint64_t nwords = 0, int records = 0) {
     tm_.begin("k_eval_bitmap");
     if (prog >= 0 && p_.progs[prog].const_false) {
       HIP_CHECK(hipMemsetAsync(words, 0, std::max(nwords, nwords_) * 8, s_));
     } else {
-      launch_eval_bitmap(make_pred(prog, class_id), g_.V, depth, words, s_, nwords);
+      // (vertices: the ids [0, vertices) evaluated, the words above written zero; edge records: every id, the
+      // vertices' bits cleared after)
+      launch_eval_bitmap(make_pred(prog, class_id, records), records == 1 ? g_.vertices : g_.V, depth, words, s_, nwords);
+      if (records == 2) keep_records(words, records);
     }
     tm_.end((uint64_t)g_.V * 4 + nwords_ * 8);
     alg_bytes_ += (uint64_t)g_.V * 4;
@@ -866,19 +879,24 @@ class Executor {
       for (size_t j = 0; j < bms_.size() && !cf && b.prog >= 0; ++j) {
         const BitmapSpec &c = p_.bitmaps[j];
         if ((int)j == id || bms_[j].p || c.prog < 0 || p_.progs[c.prog].const_false) continue;
-        const DPred pa = make_pred(b.prog, b.class_id), pb = make_pred(c.prog, c.class_id);
+        const DPred pa = make_pred(b.prog, b.class_id, b.records), pb = make_pred(c.prog, c.class_id, c.records);
         DBuf<uint64_t> other(&pool_, padded_words());
         tm_.begin("k_eval_bitmap");
-        if (!launch_eval_bitmap_pair(pa, pb, g_.V, bms_[id].p, other.p, s_, padded_words())) {
+        const bool verts = b.records == 1 && c.records == 1;
+        if (!launch_eval_bitmap_pair(pa, pb, verts ? g_.vertices : g_.V, bms_[id].p, other.p, s_, padded_words())) {
           tm_.end();
           continue;
+        }
+        if (!verts) {
+          keep_records(bms_[id].p, b.records);
+          keep_records(other.p, c.records);
         }
         tm_.end((uint64_t)g_.V * 4 + 2 * nwords_ * 8);
         alg_bytes_ += (uint64_t)g_.V * 4;
         bms_[j] = std::move(other);
         return bms_[id].p;
       }
-      eval_bitmap(b.prog, b.class_id, 0, bms_[id].p, padded_words());
+      eval_bitmap(b.prog, b.class_id, 0, bms_[id].p, padded_words(), b.records);
     }
     return bms_[id].p;
   }

@@ -156,6 +156,7 @@ void launch_isect_merge(const IsectArgs &a, bool write, int cus, hipStream_t s);
 
 // predicate VM → V-bit bitmap (u64 words); depth = value of $depth
 // nwords > ⌈V/64⌉ zero-fills the padding words (0: no padding)
+void launch_bitmap_keep_range(uint64_t *words, uint64_t nwords, uint64_t lo, uint64_t hi, hipStream_t s);
 void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s,
                         uint64_t nwords = 0);
 // two single-comparison predicates over the same int32 / int64 column (no class test), evaluated in one

@@ -452,6 +452,26 @@ bool launch_eval_bitmap_pair(const DPred &a, const DPred &b, uint32_t V, uint64_
   return true;
 }
 
+// bits outside [lo, hi) cleared (a bitmap of an edge-records snapshot kept to one kind of record)
+__global__ void k_bitmap_keep_range(uint64_t *words, uint64_t nwords, uint64_t lo, uint64_t hi) {
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b0 = w * 64;
+    uint64_t m = 0;
+    if (b0 + 64 > lo && b0 < hi) {
+      m = ~0ull;
+      if (b0 < lo) m &= ~0ull << (lo - b0);
+      if (b0 + 64 > hi) m &= (1ull << (hi - b0)) - 1;
+    }
+    if (m != ~0ull) words[w] &= m;
+  }
+}
+void launch_bitmap_keep_range(uint64_t *words, uint64_t nwords, uint64_t lo, uint64_t hi, hipStream_t s) {
+  if (!nwords) return;
+  hipLaunchKernelGGL(k_bitmap_keep_range, dim3((unsigned)std::min<uint64_t>(nblocks(nwords, 256), 4096)), dim3(256), 0, s,
+                     words, nwords, lo, hi);
+  KCHECK("k_bitmap_keep_range");
+}
+
 void launch_eval_bitmap(const DPred &pred, uint32_t V, int64_t depth, uint64_t *words, hipStream_t s,
                         uint64_t nwords) {
   if (!V) return;

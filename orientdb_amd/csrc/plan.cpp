@@ -1043,6 +1043,7 @@ class Planner {
     auto ai = alias_idx_.find(alias);
     pred_edges_ = ai != alias_idx_.end() && (size_t)ai->second < edge_node_.size() && edge_node_[ai->second];
     s.prog = add_prog(vertex_where_of(alias), false);
+    if (g_.edge_records && ai != alias_idx_.end()) s.records = pred_edges_ ? 2 : 1;
     pred_edges_ = false;
     if (kind == 1) {
       auto c = alias_class_.find(alias);

@@ -36,6 +36,10 @@ struct PredProgram {
 struct BitmapSpec {
   int prog = -1;      // predicate (-1 = none)
   int class_id = -1;  // polymorphic class test (-1 = none)
+  // edge-records snapshots: the records the alias binds (1 vertices, 2 edge records; 0 = any): the bitmap
+  // is evaluated over that id range only (the rest zero), which lets a field present on every record of
+  // that kind take the null-free fast path
+  int records = 0;
 };
 
 // S_ROWCMP: keep the rows where col[src] (=|!=) col[dst]: a WHERE conjunct `$matched.X op $currentMatch`

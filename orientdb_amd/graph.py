@@ -165,11 +165,14 @@ class GraphSnapshot:
         return cls.person_knows(rp, col, seed, device, keep_csr)
 
     @classmethod
-    def rmat(cls, scale, edge_factor=16, seed=None, simple=True, device=0, keep_csr=False, partition=None):
+    def rmat(cls, scale, edge_factor=16, seed=None, simple=True, device=0, keep_csr=False, partition=None,
+             edge_records=False):
         """Synthetic Person/Knows graph: Graph500 RMAT, vertices of class Person
         (one cluster → RID #11:v), edge class Knows, properties uid (int64 = v) and age (int32 uniform
         [0,100) from a seeded splitmix64). partition = (rank, world): the 1-D partition of that rank
-        (rows of the vertices [rank·B, (rank+1)·B), B = ⌈V/world⌉; generated without the other rows)."""
+        (rows of the vertices [rank·B, (rank+1)·B), B = ⌈V/world⌉; generated without the other rows).
+        edge_records: the Knows edges as records — RID #12:i for out-CSR entry i, field `w` (int32 uniform
+        [0,100) from a seeded splitmix64) — so MATCH can bind and filter edge nodes (unpartitioned only)."""
         seed = scale if seed is None else seed
         V = 1 << scale
         part = None
@@ -185,7 +188,16 @@ class GraphSnapshot:
         rids = (np.uint64(11) << np.uint64(RID_POS_BITS)) | np.arange(V, dtype=np.uint64)
         props = [{"name": "uid", "type": N.OMX_PROP_INT64, "values": np.arange(V, dtype=np.int64)},
                  {"name": "age", "type": N.OMX_PROP_INT32, "values": synthetic_int_column(V, seed ^ 0xA9E, 100)}]
-        g = cls(V, classes, vclass, rids, [es], props, [], device, part)
+        eprops = ()
+        if edge_records:
+            if partition is not None:
+                raise ValueError("edge records on a partitioned snapshot are not supported")
+            ne = int(rp[-1])
+            es["edge_rids"] = (np.uint64(12) << np.uint64(RID_POS_BITS)) | np.arange(ne, dtype=np.uint64)
+            eprops = [{"name": "w", "type": N.OMX_PROP_INT32, "values": synthetic_int_column(ne, seed ^ 0xED6E, 100)}]
+        g = cls(V, classes, vclass, rids, [es], props, [], device, part, eprops)
+        if edge_records:
+            g.w = eprops[0]["values"]
         g.scale = scale
         g.n_edges = int(rp[-1])
         if keep_csr:

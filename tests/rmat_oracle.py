@@ -5,7 +5,7 @@ import numpy as np
 from oracle.match_ref import RefDB
 
 
-def refdb_from_csr(rp, col, age):
+def refdb_from_csr(rp, col, age, w=None):
     db = RefDB()
     # clusters as GraphSnapshot.rmat: V 9, E 10, Person 11 (RID #11:v), Knows 12
     db.create_class("V", cluster=9)
@@ -18,5 +18,5 @@ def refdb_from_csr(rp, col, age):
     rp = np.asarray(rp, dtype=np.int64)
     for u in range(V):
         for e in range(rp[u], rp[u + 1]):
-            db.add_edge("Knows", db.vertices[u], db.vertices[int(col[e])])
+            db.add_edge("Knows", db.vertices[u], db.vertices[int(col[e])], None if w is None else {"w": int(w[e])})
     return db

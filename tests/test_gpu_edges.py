@@ -149,3 +149,49 @@ def test_known_db_edge_nodes(refdb, kdb, query):
     reference engine on the lightweight snapshot)."""
     rs = _check(kdb, refdb, query)
     assert rs.info["n_rows"] > 0
+
+
+# ---- RMAT snapshots with edge records (GraphSnapshot.rmat(edge_records=True): RID #12:i, field w) ------
+@pytest.fixture(scope="module")
+def rmat_edges():
+    import orientdb_amd as o
+    from tests.rmat_oracle import refdb_from_csr
+    g = o.GraphSnapshot.rmat(10, device=0, keep_csr=True, edge_records=True)
+    return g, refdb_from_csr(g.csr[0], g.csr[1], g.age, g.w)
+
+
+RMAT_EDGE_QUERIES = [
+    "MATCH {class:Person,as:a,where:(age < 5)}.outE('Knows'){as:e, where:(w < 30)}.inV(){as:b,where:(age >= 50)} RETURN a, e, b",
+    "MATCH {class:Person,as:a,where:(uid < 40)}.inE('Knows'){as:e, where:(w >= 90)}.outV(){as:b} RETURN a, e, b",
+    "MATCH {class:Knows,as:e,where:(w = 7)}.inV(){as:b,where:(age < 50)} RETURN e, b",
+    "MATCH {class:Person,as:a,where:(uid < 30)}.outE('Knows'){as:e, where:(w < 20)}.inV(){as:b}.out('Knows'){as:c,where:(age < 10)} RETURN a, e, b, c",
+    "MATCH {class:Person,as:a,where:(uid < 20)}.outE('Knows'){as:e, where:(w < 50)}.inV(){as:b} RETURN $pathElements",
+    "MATCH {class:Person,as:a,where:(uid < 50)}.bothE('Knows'){as:e, where:(w < 5)}.bothV(){as:b} RETURN a, e, b",
+]
+
+
+@pytest.mark.parametrize("query", RMAT_EDGE_QUERIES, ids=[f"r{i}" for i in range(len(RMAT_EDGE_QUERIES))])
+def test_rmat_edge_nodes(rmat_edges, query):
+    g, db = rmat_edges
+    rs = _check(g, db, query)
+    assert rs.info["n_rows"] > 0
+
+
+def test_e1_rmat20_vs_edge_ref():
+    """The E1 bench line's shape at RMAT-20, whole result: rows, E_t and the digest of the (a, e, b) RID
+    rows against oracle/edge_ref.py (pinned to match_ref.py by tests/test_oracle_edge_ref.py)."""
+    import numpy as np
+    import orientdb_amd as o
+    from oracle.dfs import row_digest
+    from oracle.edge_ref import edge_two_hop
+    g = o.GraphSnapshot.rmat(20, device=0, keep_csr=True, edge_records=True)
+    q = ("MATCH {class:Person,as:a,where:(age < 1)}.outE('Knows'){as:e, where:(w < 10)}.inV(){as:b,where:(age >= 90)} "
+         "RETURN a, e, b")
+    (a, e, b), edges = edge_two_hop(g.csr[0], g.csr[1], np.nonzero(g.age < 1)[0], g.w < 10, g.age >= 90)
+    want = row_digest(np.stack([(np.uint64(11) << np.uint64(48)) | a.astype(np.uint64),
+                                (np.uint64(12) << np.uint64(48)) | e.astype(np.uint64),
+                                (np.uint64(11) << np.uint64(48)) | b.astype(np.uint64)], axis=1))
+    rs = o.OMatchStatement(q).execute(g, flags=o.OMX_FLAG_KEEP_DEVICE | o.OMX_FLAG_DIGEST, documents=False)
+    assert rs.info["n_rows"] == len(a) > 1000
+    assert rs.info["edges_traversed"] == edges
+    assert rs.info["digest"] == want
