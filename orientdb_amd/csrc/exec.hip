@@ -3590,7 +3590,10 @@ class Executor {
         if (expand && depth_only_while) expand = !while_never && eval_pred_const(wconst, d);
         // a level that does not expand only merges its frontier into visited: with one GPU the emission's
         // counting pass does that (one sweep of V fewer); a sparse one still runs over its short list
-        if (!expand && whole && !(sparse_ok && t_ok && prev_slot >= 0 && t_bound * kSparsePrepDiv < (uint64_t)V)) {
+        // (visited must hold something by then: a previous level's prologue, or the sparse first level's
+        // memset — a batch's first full prologue is what writes it)
+        if (!expand && whole && (d > 0 || sparse_ok) &&
+            !(sparse_ok && t_ok && prev_slot >= 0 && t_bound * kSparsePrepDiv < (uint64_t)V)) {
           last = fr.p;
           break;
         }

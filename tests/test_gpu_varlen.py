@@ -173,3 +173,18 @@ def test_c3_shape_rmat16_vs_c_bfs(rmat16, depth, nroots):
     got = np.sort(rs.rows[:, si].astype(np.uint64) << np.uint64(32) | rs.rows[:, vi].astype(np.uint64))
     want = np.sort(ref["pairs"][:, 0].astype(np.uint64) << np.uint64(32) | ref["pairs"][:, 1].astype(np.uint64))
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("mode", ["bfs_auto", "bfs_full_preps", "bfs_push", "bfs_pull_hubs_push"])
+@pytest.mark.parametrize("q", [q for q in VARLEN if q[0] in ("maxdepth0", "two_batches", "while_prop", "where_target")],
+                         ids=lambda q: q[0])
+def test_varlen_poisoned_pool(rmat10, q, mode, monkeypatch):
+    """The BFS levels under OMX_POOL_POISON=1 (every pooled buffer 0xFF-filled first): a level prologue,
+    a touched / active list or an emission that read a word nobody wrote would differ. Round 6 found
+    one this way: maxDepth 0 with full prologues skipped the first level's prologue, the one that writes
+    visited, and emitted from the poisoned words."""
+    monkeypatch.setenv("OMX_POOL_POISON", "1")
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    g, ref = rmat10
+    _parity(g, ref, q[1], _cols(q[1]))
