@@ -188,6 +188,9 @@ struct Graph {
   std::vector<IndexInfo> indexes;
   std::vector<uint16_t> h_vclass;  // kept when indexes exist, or copied on the first RETURN expression
   std::vector<uint64_t> h_rids;    // copied on the first RETURN expression (project.cpp)
+  // edge records: every record's out- / in-vertex (the edge document's `out` / `in` links), copied from
+  // the endpoints set on the first RETURN expression that reads them (project.cpp)
+  std::vector<uint32_t> h_etail, h_ehead;
   uint16_t *d_vclass = nullptr;
   uint64_t *d_rids = nullptr;
   DColumn *d_cols = nullptr;

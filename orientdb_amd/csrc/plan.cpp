@@ -1275,12 +1275,6 @@ class Planner {
       case Expr::CALL: unsupported("function call " + e->name + "() in a RETURN expression");
       case Expr::CHAIN:
         check_return(e->kids[0], refs);
-        if (e->kids[0]->kind == Expr::FIELD && !e->suffixes.empty() && e->suffixes[0].kind == Suffix::FIELD &&
-            (e->suffixes[0].name == "out" || e->suffixes[0].name == "in")) {
-          auto ai = alias_idx_.find(e->kids[0]->name);
-          if (ai != alias_idx_.end() && edge_node_.size() > (size_t)ai->second && edge_node_[ai->second])
-            unsupported("the " + e->suffixes[0].name + " link of an edge record in a RETURN expression");
-        }
         for (size_t si = 0; si < e->suffixes.size(); ++si) {
           const Suffix &s = e->suffixes[si];
           if (s.kind == Suffix::METHOD) {

@@ -115,7 +115,8 @@ struct Compiler {
         }
         const int c = alias_col(e->kids[0]->name);
         const std::string &f = e->suffixes[0].name;
-        if (c < 0 || (!f.empty() && f[0] == '@' && !ieq(f, "@rid"))) {
+        // (an edge record's `out` / `in` link is resolved on the host, project.cpp)
+        if (c < 0 || (!f.empty() && f[0] == '@' && !ieq(f, "@rid")) || (g.edge_records && (f == "out" || f == "in"))) {
           why = "chain " + expr_text(e);
           return false;
         }

@@ -35,6 +35,23 @@ void ensure_vclass(Graph &g) {
   if (g.V) HIP_CHECK(hipMemcpy(c.data(), g.d_vclass, (size_t)g.V * 2, hipMemcpyDeviceToHost));
   g.h_vclass.swap(c);
 }
+// the edge records' `out` / `in` links, from the endpoints set (EdgeSet::pseudo == 2)
+void ensure_links(Graph &g) {
+  const uint64_t E = (uint64_t)g.V - g.vertices;
+  if (g.h_etail.size() == E) return;
+  for (const EdgeSet &es : g.esets)
+    if (es.pseudo == 2) {
+      std::vector<uint32_t> t(E), h(E);
+      if (E) {
+        HIP_CHECK(hipMemcpy(t.data(), es.d_out_col, E * 4, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(h.data(), es.d_in_col, E * 4, hipMemcpyDeviceToHost));
+      }
+      g.h_etail.swap(t);
+      g.h_ehead.swap(h);
+      return;
+    }
+  fail(OMX_E_INVALID, "internal: edge records without an endpoints set");
+}
 void ensure_prop(Graph &g, Property &p) {
   if (!p.h_int.empty() || !p.h_dbl.empty() || g.V == 0) return;
   if (p.type == OMX_PROP_DOUBLE) {
@@ -176,6 +193,11 @@ class Evaluator {
         if (ieq(name, "@class")) {
           ensure_vclass(g_);
           return mk_str(g_.classes[g_.h_vclass[base.v]].name);
+        }
+        // an edge record's `out` / `in` field: the vertex it links (the edge document's LINK fields)
+        if (g_.edge_records && base.v >= g_.vertices && base.v < g_.V && (name == "out" || name == "in")) {
+          ensure_links(g_);
+          return mk_rid((name == "out" ? g_.h_etail : g_.h_ehead)[base.v - g_.vertices]);
         }
         const int pid = g_.prop_id(name);
         if (pid < 0) return HVal();

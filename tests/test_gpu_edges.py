@@ -76,6 +76,10 @@ EDGE_QUERIES = [
     "MATCH {class: Person, as: a, where: (uid < 30)}.outE('Knows'){as: e}.inV(){as: b}.out('Likes'){as: c} RETURN e, c",
     "MATCH {class: Likes, as: f}.inV(){as: b, where: (age < 20)} RETURN f",
     "MATCH {class: E, as: e, where: (since = 2020)} RETURN e",
+    # the edge documents' `out` / `in` links (ODocument fields of a regular edge)
+    "MATCH {class: Person, as: a, where: (uid < 30)}.outE('Knows'){as: e, where: (since > 2015)}.inV(){as: b} "
+    "RETURN e.out AS o, e.in AS i, e.since AS s",
+    "MATCH {class: Knows, as: e, where: (since = 2015)} RETURN e.out.uid AS u, e.in.age AS g, e.w AS w",
 ]
 
 
