@@ -186,7 +186,7 @@ RMAT_QUERIES = [
     ("matched_and_filter", "MATCH {class:Person,as:me,where:(age < 20)}<-Knows-{as:x}-Knows->{as:f, where:($matched.me <> $currentMatch and age < 50)} RETURN me, x, f",
      ["me", "x", "f"]),
     # a bound (cycle-closing) target with a row-level conjunct: the forward check filters with it (:468-477)
-    ("matched_bound", "MATCH {class:Person,as:a,where:(uid < 100)}-Knows->{as:b}-Knows->{as:c},"
+    ("matched_bound", "MATCH {class:Person,as:a,where:(uid < 40)}-Knows->{as:b}-Knows->{as:c},"
                       "{as:a}-Knows->{as:c, where:($matched.b != $currentMatch and age < 70)} RETURN a, b, c",
      ["a", "b", "c"]),
     ("matched_bound_eq", "MATCH {class:Person,as:a,where:(uid < 200)}-Knows->{as:b}-Knows->{as:c},"
