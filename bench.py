@@ -203,9 +203,15 @@ def cpu_baseline_edges(g, query, target_s):
         if secs > target_s / 4 or k >= len(roots):
             break
         k *= 2
-    return {"value": edges / secs / 1e9, "unit": "GTEPS", "cores": 1, "kind": "port",
-            "sample": "%d of %d roots (%.1f s, %d edges, %d rows; oracle/edge_ref.py, numpy, 1 thread)" % (
-                len(sample), len(roots), secs, edges, len(r[0]))}
+    reps = 1
+    while secs < target_s / 4 and reps < 1000:  # the whole root set is a short run: repeat it
+        t0 = time.perf_counter()
+        edge_two_hop(rp, col, sample, emask, bmask)
+        secs += time.perf_counter() - t0
+        reps += 1
+    return {"value": edges * reps / secs / 1e9, "unit": "GTEPS", "cores": 1, "kind": "port",
+            "sample": "%d of %d roots x %d (%.1f s, %d edges and %d rows each; oracle/edge_ref.py, numpy, 1 thread)" % (
+                len(sample), len(roots), reps, secs, edges, len(r[0]))}
 
 
 def cpu_baseline(g, query, target_s=12.0, single_thread_too=False):
